@@ -1,0 +1,258 @@
+"""ptyx ORACLE — CPU restatement of PtyRAD's per-mini-batch hot path.  TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product: only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it.  The product path
+(``ptyrad_amd``) never routes through it and fails loudly without the HIP library.
+
+What it restates (NumPy, written from the equations, not from the reference code):
+
+* patch gather        — ``src/ptyrad/models.py:251-265``  (get_obj_ROI)
+* sub-px probe shift  — ``src/ptyrad/utils/image_proc.py:495-537`` (imshift_batch) with the
+                        grid ``arange(N)/N`` of ``models.py:179``
+* forward model       — ``src/ptyrad/forward.py:20-80`` (multislice_forward_model_vec_all)
+* loss terms          — ``src/ptyrad/losses.py:36-104, 143-155`` (single / poissn / sparse)
+* gradients           — the hand-derived adjoint of all of the above, i.e. what
+                        ``loss.backward()`` (``reconstruction.py:753``) produces by autograd.
+
+Parity pinning: the oracle is checked against golden vectors produced by running the
+reference itself in the build container (``tests/golden/make_golden.py``,
+``tests/test_oracle_golden.py``).
+
+Conventions: F = unnormalised fft2, F^-1 = ifft2, F_o = ortho fft2, S = fftshift2.
+Complex gradients follow torch's real-view convention g = dL/dRe + i dL/dIm.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+LOSS_NAMES = ("loss_single", "loss_poissn", "loss_pacbed", "loss_sparse", "loss_simlar")
+
+
+def _fft2(x):
+    return np.fft.fft2(x, axes=(-2, -1))
+
+
+def _ifft2(x):
+    return np.fft.ifft2(x, axes=(-2, -1))
+
+
+def shift_grid(n: int) -> np.ndarray:
+    """Effective k grid of the probe shift ramp after ifftshift: ((k + N/2) mod N) / N.
+
+    imshift_batch multiplies fftshift2(F P) by exp(-2πi s·g) with g = arange(N)/N
+    (models.py:179, image_proc.py:531), then ifftshifts, so in FFT order the grid is g[(k+N/2)%N].
+    """
+    return ((np.arange(n) + n // 2) % n) / n
+
+
+def shift_ramp(shifts: np.ndarray, n: int, cdt=np.complex128) -> np.ndarray:
+    """W_b[ky,kx] = exp(-2πi (s_y g[ky] + s_x g[kx]))   (image_proc.py:531)."""
+    g = shift_grid(n)
+    sy = shifts[:, 0, None, None].astype(np.float64)
+    sx = shifts[:, 1, None, None].astype(np.float64)
+    return np.exp(-2j * np.pi * (sy * g[None, :, None] + sx * g[None, None, :])).astype(cdt)
+
+
+def get_patches(obja, objp, crop_pos, idx, n):
+    """(B,O,Nz,N,N) amplitude and phase patches at integer crop positions (models.py:251-265)."""
+    B = len(idx)
+    O, Nz = obja.shape[:2]
+    amp = np.empty((B, O, Nz, n, n), obja.dtype)
+    ph = np.empty((B, O, Nz, n, n), objp.dtype)
+    for i, s in enumerate(idx):
+        cy, cx = int(crop_pos[s, 0]), int(crop_pos[s, 1])
+        amp[i] = obja[:, :, cy:cy + n, cx:cx + n]
+        ph[i] = objp[:, :, cy:cy + n, cx:cx + n]
+    return amp, ph
+
+
+def get_probes(probe, shifts_b, shift_probes, cdt=np.complex128):
+    """(B,P,N,N) probes: F^-1(F(P) ⊙ W_b) if shift_probes else broadcast (models.py:286-298)."""
+    n = probe.shape[-1]
+    P = probe.astype(cdt)
+    if not shift_probes:
+        return np.broadcast_to(P, (len(shifts_b),) + P.shape).copy()
+    W = shift_ramp(shifts_b, n, cdt)
+    return _ifft2(_fft2(P)[None] * W[:, None]).astype(cdt)
+
+
+@dataclass
+class ForwardCache:
+    probes: np.ndarray     # (B,P,N,N)
+    O: np.ndarray          # (B,Om,Nz,N,N) complex object patches
+    psis: list             # psis[n] = wave entering slice n, (B,P,Om,N,N)
+    Psi: np.ndarray        # (B,P,Om,N,N) far field, fftshifted
+    dp: np.ndarray         # (B,N,N)
+
+
+def forward(amp, ph, probes, H, occu, eps=1e-10, cdt=np.complex128) -> ForwardCache:
+    """multislice_forward_model_vec_all (forward.py:20-80)."""
+    Ocplx = (amp * np.exp(1j * ph.astype(np.float64))).astype(cdt)   # torch.polar  (forward.py:53)
+    Nz = Ocplx.shape[2]
+    psi = probes[:, :, None].astype(cdt)                               # (B,P,1,N,N)  (forward.py:57)
+    psi = np.broadcast_to(psi, probes.shape[:2] + (Ocplx.shape[1],) + probes.shape[2:]).copy()
+    psis = []
+    Hc = H.astype(cdt)
+    for n in range(Nz - 1):                                            # (forward.py:60-63)
+        psis.append(psi)
+        psi = _ifft2(Hc * _fft2(psi * Ocplx[:, None, :, n])).astype(cdt)
+    psis.append(psi)
+    psi_out = psi * Ocplx[:, None, :, Nz - 1]                          # (forward.py:66-67)
+    nn = psi_out.shape[-1]
+    Psi = np.fft.fftshift(_fft2(psi_out) / nn, axes=(-2, -1)).astype(cdt)   # ortho + fftshift2
+    dp = (np.abs(Psi) ** 2 * occu[None, None, :, None, None]).sum(axis=(1, 2)) + eps   # (forward.py:79)
+    return ForwardCache(probes, Ocplx, psis, Psi, dp)
+
+
+def loss_terms(dp, meas, ph, occu, lp):
+    """CombinedLoss.forward (losses.py:143-155) → [single, poissn, pacbed, sparse, simlar] and dL/dI.
+
+    Returns (terms, dLdI (B,N,N), dL/dφ_patch (B,O,Nz,N,N)).
+    """
+    B = dp.shape[0]
+    K = dp.size
+    terms = np.zeros(5)
+    dLdI = np.zeros_like(dp, dtype=np.float64)
+    I = dp.astype(np.float64)
+    M = meas.astype(np.float64)
+    s = lp["loss_single"]
+    if s["state"]:                                                     # losses.py:36-50
+        q = s.get("dp_pow", 0.5)
+        Iq, Mq = I ** q, M ** q
+        mu = Mq.mean()
+        S = ((Iq - Mq) ** 2).sum()
+        rmse = math.sqrt(S / K)
+        terms[0] = s["weight"] * rmse / mu
+        if rmse > 0:
+            dLdI += s["weight"] / (mu * K * rmse) * (Iq - Mq) * q * I ** (q - 1)
+    p = lp["loss_poissn"]
+    if p["state"]:                                                     # losses.py:52-75
+        q = p.get("dp_pow", 1.0)
+        e = p.get("eps", 1e-6)
+        Iq, Mq = I ** q, M ** q
+        mu = Mq.mean()
+        terms[1] = -p["weight"] * (Mq * np.log(Iq + e) - Iq).mean() / mu
+        dLdI += -p["weight"] / (mu * K) * (Mq / (Iq + e) - 1.0) * q * I ** (q - 1)
+    if lp["loss_pacbed"]["state"] or lp["loss_simlar"]["state"]:
+        raise NotImplementedError("loss_pacbed / loss_simlar are outside the hot-path scope")
+    sp = lp["loss_sparse"]
+    dph = np.zeros(ph.shape, np.float64)
+    if sp["state"]:                                                    # losses.py:91-104
+        nord = sp["ln_order"]
+        a = np.abs(ph.astype(np.float64))
+        cnt = ph.shape[0] * ph.shape[2] * ph.shape[3] * ph.shape[4]
+        m = (a ** nord).sum(axis=(0, 2, 3, 4)) / cnt                  # per object mode
+        terms[3] = sp["weight"] * (m ** (1.0 / nord) * occu).sum()
+        for o in range(ph.shape[1]):
+            coef = sp["weight"] * occu[o] * (m[o] ** (1.0 / nord - 1.0) if m[o] > 0 else 0.0) / cnt
+            dph[:, o] = coef * a[:, o] ** (nord - 1) * np.sign(ph[:, o])
+    return terms, dLdI, dph
+
+
+def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, occu, shift_probes,
+            cdt=np.complex128):
+    """Hand-derived adjoint of forward().
+
+    Returns per-pattern gradients: dA, dφ (B,O,Nz,N,N), dprobe (P,N,N) complex, dshift (B,2).
+    """
+    B, P = cache.probes.shape[:2]
+    Om, Nz = amp.shape[1], amp.shape[2]
+    n = amp.shape[-1]
+    Oc = cache.O
+    Hc = H.astype(cdt)
+    # g_Ψ = 2 occ Ψ ∂L/∂I, un-shift, ortho adjoint = ortho inverse
+    gPsi = 2.0 * occu[None, None, :, None, None] * cache.Psi * dLdI[:, None, None]
+    g = np.fft.ifft2(np.fft.ifftshift(gPsi, axes=(-2, -1)), axes=(-2, -1), norm="ortho").astype(cdt)
+    gO = np.zeros((B, Om, Nz, n, n), cdt)
+    for sl in range(Nz - 1, -1, -1):
+        if sl < Nz - 1:                                 # adjoint of F^-1 H F is F^-1 conj(H) F
+            g = _ifft2(np.conj(Hc) * _fft2(g)).astype(cdt)
+        gO[:, :, sl] = (np.conj(cache.psis[sl]) * g).sum(axis=1)   # Σ_p conj(ψ^n) g
+        g = g * np.conj(Oc[:, None, :, sl])
+    gPb = g.sum(axis=2)                                 # (B,P,N,N): Σ_o
+    # O = A e^{iφ}: dA = Re(g_O e^{-iφ}), dφ = Im(conj(O) g_O)
+    e = np.exp(-1j * ph.astype(np.float64))
+    dA = np.real(gO * e)
+    dP = np.imag(np.conj(Oc) * gO) + dph_sparse
+    if shift_probes:
+        W = shift_ramp(shifts_b, n, cdt)                              # (B,N,N)
+        Fp = _fft2(probe.astype(cdt))                                  # (P,N,N)
+        dprobe = _ifft2(np.conj(W)[:, None] * _fft2(gPb)).sum(axis=0)
+        gg = shift_grid(n)
+        dshift = np.zeros((B, 2))
+        for ax, gvec in ((0, gg[:, None]), (1, gg[None, :])):
+            dPb = _ifft2(Fp[None] * (W[:, None] * (-2j * np.pi) * gvec))     # ∂P_b/∂s
+            dshift[:, ax] = np.real((np.conj(gPb) * dPb).sum(axis=(1, 2, 3)))
+    else:
+        dprobe = gPb.sum(axis=0)
+        dshift = np.zeros((B, 2))
+    return dA, dP, dprobe, dshift
+
+
+def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batches, loss_params,
+                      shift_probes=True, grad_scale=1.0, cdt=np.complex128):
+    """Oracle of ptyx_forward_loss_grad: per-mini-batch losses, gradients accumulated over batches.
+
+    batches: list of index arrays (each its own NRMSE normalisation, losses.py:45-47);
+    grad_scale: the 1/grad_accumulation factor of reconstruction.py:750.
+    Returns (terms (n_batches,5), dp list, grads dict).
+    """
+    if isinstance(loss_params, str):
+        loss_params = json.loads(loss_params)
+    n = probe.shape[-1]
+    g_obja = np.zeros(obja.shape, np.float64)
+    g_objp = np.zeros(objp.shape, np.float64)
+    g_probe = np.zeros(probe.shape, np.complex128)
+    g_shifts = np.zeros(shifts.shape, np.float64)
+    all_terms, dps = [], []
+    for idx in batches:
+        idx = np.asarray(idx)
+        amp, ph = get_patches(obja, objp, crop_pos, idx, n)
+        probes = get_probes(probe, shifts[idx], shift_probes, cdt)
+        cache = forward(amp, ph, probes, H, occu, cdt=cdt)
+        terms, dLdI, dph = loss_terms(cache.dp, meas[idx], ph, occu, loss_params)
+        dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], H, occu,
+                                         shift_probes, cdt)
+        for i, s in enumerate(idx):
+            cy, cx = int(crop_pos[s, 0]), int(crop_pos[s, 1])
+            g_obja[:, :, cy:cy + n, cx:cx + n] += grad_scale * dA[i]
+            g_objp[:, :, cy:cy + n, cx:cx + n] += grad_scale * dP[i]
+            g_shifts[s] += grad_scale * dshift[i]
+        g_probe += grad_scale * dprobe
+        all_terms.append(terms)
+        dps.append(cache.dp)
+    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts)
+    return np.array(all_terms), dps, grads
+
+
+def forward_dp(obja, objp, probe, shifts, crop_pos, H, occu, idx, shift_probes=True, cdt=np.complex128):
+    """Oracle of ptyx_forward (PtychoAD.forward, models.py:422-436): (B,N,N) dp."""
+    n = probe.shape[-1]
+    amp, ph = get_patches(obja, objp, crop_pos, np.asarray(idx), n)
+    probes = get_probes(probe, shifts[np.asarray(idx)], shift_probes, cdt)
+    return forward(amp, ph, probes, H, occu, cdt=cdt).dp
+
+
+def adam_step(params, grads, state, lrs, t, betas=(0.9, 0.999), eps=1e-8):
+    """torch.optim.Adam default update (used at reconstruction.py:759), in the params' dtype.
+
+    Complex parameters are handled through their real view, as PtyRAD's probe is a
+    view_as_real parameter (models.py:103).
+    """
+    b1, b2 = betas
+    for k in params:
+        if grads.get(k) is None or lrs.get(k, 0) == 0:
+            continue
+        g = grads[k].astype(params[k].dtype)
+        m, v = state.get(k, (np.zeros_like(g), np.zeros_like(g)))
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        state[k] = (m, v)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        params[k] = params[k] - (lrs[k] / bc1) * m / (np.sqrt(v) / math.sqrt(bc2) + eps)
+    return params

@@ -1,0 +1,209 @@
+"""Generate golden fixtures for the ptyx hot path by running the PtyRAD reference itself.
+
+Run here (build container) only:  python tests/golden/make_golden.py
+It imports /root/reference/src (read-only) via refimport.py, builds the
+reference ``PtychoAD`` (src/ptyrad/models.py:70) straight from an
+``init_variables`` dict, evaluates ``CombinedLoss`` (src/ptyrad/losses.py:143)
+and ``loss.backward()`` (autograd), and stores inputs + outputs as .npz:
+
+  inputs : obja, objp (O,Nz,Ny,Nx) f32 [the model's own abs/angle of obj],
+           probe (P,N,N) c64, shifts (S,2) f32, crop_pos (S,2) i32, H (N,N) c64,
+           occu (O,) f32, meas (S,N,N) f32 (only batch rows are non-zero),
+           batch (B,) i64, loss_params (json), shift_probes (bool)
+  outputs: dp (B,N,N) f32 (or dp_head + dp_sums for the big case), loss_terms (5,),
+           loss_total, g_obja, g_objp, g_probe (P,N,N,2), g_shifts (S,2)
+
+and a 3-iteration recon_step trajectory (src/ptyrad/reconstruction.py:658)
+with fixed batches, Adam, and a no-op constraint.  The data written are
+inputs and outputs only; no reference source is copied.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from refimport import import_reference  # noqa: E402
+from ptyrad_amd import synthetic as syn  # noqa: E402
+
+models, losses, reconstruction = import_reference()
+
+DEFAULT_LOSS = {
+    "loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+    "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+    "loss_pacbed": {"state": False, "weight": 0.5, "dp_pow": 0.2},
+    "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
+    "loss_simlar": {"state": False, "weight": 0.1, "obj_type": "both",
+                    "scale_factor": [1.0, 1.0, 1.0], "blur_std": 1.0},
+}
+
+
+def model_params(shift_lr=5e-4):
+    up = {
+        "obja": {"start_iter": 1, "lr": 5e-4},
+        "objp": {"start_iter": 1, "lr": 5e-4},
+        "obj_tilts": {"start_iter": None, "lr": 0.0},
+        "slice_thickness": {"start_iter": None, "lr": 0.0},
+        "probe": {"start_iter": 1, "lr": 1e-4},
+        "probe_pos_shifts": {"start_iter": 1 if shift_lr else None, "lr": shift_lr},
+    }
+    return {"detector_blur_std": None, "obj_preblur_std": None, "update_params": up,
+            "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
+
+
+def init_variables(obja, objp, probe, H, occu, crop_pos, shifts, meas, n_slow, n_fast, dz=2.0):
+    lam = syn.electron_wavelength(syn.KV)
+    n = probe.shape[-1]
+    return {
+        "obj": (obja * np.exp(1j * objp)).astype(np.complex64),
+        "obj_tilts": np.zeros((1, 2), np.float32),
+        "slice_thickness": np.float32(dz),
+        "probe": probe.astype(np.complex64),
+        "probe_pos_shifts": shifts.astype(np.float32),
+        "omode_occu": occu.astype(np.float32),
+        "H": H.astype(np.complex64),
+        "measurements": meas.astype(np.float32),
+        "N_scan_slow": n_slow, "N_scan_fast": n_fast,
+        "crop_pos": crop_pos.astype(np.int32),
+        "dx": np.float32(syn.DX_ANG), "dk": np.float32(1.0 / (syn.DX_ANG * n)),
+        "lambd": np.float32(lam), "scan_affine": None,
+    }
+
+
+def build_model(iv, shift_lr):
+    torch.manual_seed(0)
+    return models.PtychoAD(iv, model_params(shift_lr), device="cpu", verbose=False)
+
+
+def make_inputs(n, P, O, Nz, n_slow, n_fast, seed, defocus=40.0, pstd=0.2):
+    rng = np.random.default_rng(seed)
+    scan = syn.raster_scan(n_slow, n_fast, n, seed=seed)
+    probe = syn.mixed_probe(syn.stem_probe(n, defocus=defocus), P)
+    probe = probe * np.float32(np.sqrt(n * n * 0.5))   # intensity scale ~ DP sum
+    H = syn.fresnel_propagator(n, syn.DX_ANG, 2.0)
+    occu = syn.omode_occupancy(O)
+    shape = (O, Nz) + scan.obj_shape
+    obja = (1.0 + 0.05 * rng.standard_normal(shape)).astype(np.float32)
+    objp = (pstd * rng.standard_normal(shape)).astype(np.float32)
+    gta = (1.0 + 0.05 * rng.standard_normal(shape)).astype(np.float32)
+    gtp = (pstd * rng.standard_normal(shape)).astype(np.float32)
+    return scan, probe, H, occu, obja, objp, gta, gtp
+
+
+def simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr):
+    """Measurements = the reference forward model on a different (ground-truth) object."""
+    n = probe.shape[-1]
+    S = scan.crop_pos.shape[0]
+    iv = init_variables(gta, gtp, probe, H, occu, scan.crop_pos, scan.shifts,
+                        np.zeros((S, n, n), np.float32), scan.n_slow, scan.n_fast)
+    m = build_model(iv, shift_lr)
+    with torch.no_grad():
+        dp = m(np.arange(S)).numpy()
+    return dp.astype(np.float32)
+
+
+def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_params=None,
+             big=False):
+    loss_params = loss_params or DEFAULT_LOSS
+    scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
+    meas = simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr)
+    S = scan.crop_pos.shape[0]
+    batch = np.random.default_rng(seed + 100).permutation(S)[:B].astype(np.int64)
+    if big:  # keep the fixture small: only the batch rows of meas, stored as f16 and used as such
+        keep = np.zeros_like(meas)
+        keep[batch] = meas[batch]
+        meas = keep.astype(np.float16).astype(np.float32)
+    iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas,
+                        scan.n_slow, scan.n_fast)
+    model = build_model(iv, shift_lr)
+    loss_fn = losses.CombinedLoss(loss_params, device="cpu")
+    dp = model(batch)
+    mdp = model.get_measurements(batch)
+    total, terms = loss_fn(dp, mdp, model._current_object_patches, model.omode_occu)
+    total.backward()
+
+    def g(t):
+        return None if t.grad is None else t.grad.detach().numpy().copy()
+
+    out = dict(
+        obja=model.opt_obja.detach().numpy(), objp=model.opt_objp.detach().numpy(),
+        probe=torch.view_as_complex(model.opt_probe.detach()).numpy(),
+        shifts=model.opt_probe_pos_shifts.detach().numpy(), crop_pos=scan.crop_pos,
+        H=model.H.numpy(), occu=model.omode_occu.numpy(),
+        batch=batch, loss_params=json.dumps(loss_params), shift_probes=bool(model.shift_probes),
+        loss_terms=np.array([float(t) for t in terms], np.float64),
+        loss_total=np.float64(float(total)),
+        g_obja=g(model.opt_obja), g_objp=g(model.opt_objp), g_probe=g(model.opt_probe),
+    )
+    gs = g(model.opt_probe_pos_shifts)
+    out["g_shifts"] = gs if gs is not None else np.zeros_like(out["shifts"])
+    dpn = dp.detach().numpy()
+    if big:
+        out["meas_f16"] = meas[batch].astype(np.float16)
+        out["dp_head"] = dpn[:4]
+        out["dp_sums"] = dpn.reshape(B, -1).astype(np.float64).sum(1)
+    else:
+        out["meas"] = meas
+        out["dp"] = dpn
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
+
+
+def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumulation, seed):
+    scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
+    meas = simulate_meas(scan, probe, H, occu, gta, gtp, 5e-4)
+    iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas,
+                        scan.n_slow, scan.n_fast)
+    model = build_model(iv, 5e-4)
+    init_state = dict(obja=model.opt_obja.detach().numpy().copy(),
+                      objp=model.opt_objp.detach().numpy().copy(),
+                      probe=torch.view_as_complex(model.opt_probe.detach()).numpy().copy(),
+                      shifts=model.opt_probe_pos_shifts.detach().numpy().copy())
+    S = scan.crop_pos.shape[0]
+    perm = np.random.default_rng(seed + 7).permutation(S)
+    batches = np.array_split(perm, S // bsize)
+    loss_fn = losses.CombinedLoss(DEFAULT_LOSS, device="cpu")
+    opt = reconstruction.create_optimizer(model.optimizer_params, model.optimizable_params,
+                                          verbose=False)
+    hist = []
+    for it in range(1, niter + 1):
+        bl = reconstruction.recon_step(batches, grad_accumulation, model, opt, loss_fn,
+                                       lambda m, i: None, it, verbose=False)
+        hist.append([float(np.mean(v)) for v in bl.values()])
+    np.savez_compressed(
+        os.path.join(HERE, f"{name}.npz"),
+        init_obja=init_state["obja"], init_objp=init_state["objp"],
+        init_probe=init_state["probe"], init_shifts=init_state["shifts"],
+        crop_pos=scan.crop_pos, H=model.H.numpy(), occu=model.omode_occu.numpy(), meas=meas,
+        batches=np.concatenate(batches), batch_sizes=np.array([len(b) for b in batches]),
+        niter=niter, grad_accumulation=grad_accumulation, lrs=json.dumps(model.lr_params),
+        final_obja=model.opt_obja.detach().numpy(), final_objp=model.opt_objp.detach().numpy(),
+        final_probe=torch.view_as_complex(model.opt_probe.detach()).numpy(),
+        final_shifts=model.opt_probe_pos_shifts.detach().numpy(),
+        loss_hist=np.array(hist), loss_params=json.dumps(DEFAULT_LOSS))
+    print(f"{name}: loss_hist={np.array(hist).sum(1)}")
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(4)
+    poisson = json.loads(json.dumps(DEFAULT_LOSS))
+    poisson["loss_poissn"].update(state=True, weight=0.5, dp_pow=1.0, eps=1e-6)
+    poisson["loss_sparse"].update(ln_order=2, weight=0.05)
+    single_q1 = json.loads(json.dumps(DEFAULT_LOSS))
+    single_q1["loss_single"].update(dp_pow=1.0, weight=2.0)
+    single_q1["loss_sparse"].update(state=False)
+
+    run_case("n32_p1o1z1_shift", 32, 1, 1, 1, 4, 4, 6, seed=11)
+    run_case("n32_p2o2z3_shift", 32, 2, 2, 3, 4, 4, 5, seed=12)
+    run_case("n64_p1o1z2_noshift", 64, 1, 1, 2, 3, 3, 5, seed=13, shift_lr=0.0)
+    run_case("n32_p2o1z1_poisson", 32, 2, 1, 1, 4, 4, 7, seed=14, loss_params=poisson)
+    run_case("n32_p1o2z1_q1", 32, 1, 2, 1, 3, 4, 4, seed=15, loss_params=single_q1)
+    run_case("n64_p3o1z1_shift", 64, 3, 1, 1, 3, 3, 9, seed=16)
+    run_case("n128_c1_b32", 128, 1, 1, 1, 8, 8, 32, seed=17, big=True)
+    run_trajectory("traj_n64_b4_ga1", 64, 1, 1, 1, 4, 4, 4, 3, 1, seed=21)
+    run_trajectory("traj_n32_p2_ga2", 32, 2, 1, 2, 4, 4, 4, 3, 2, seed=22)

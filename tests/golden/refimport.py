@@ -1,0 +1,58 @@
+"""Import the read-only PtyRAD reference (/root/reference/src) for fixture generation.
+
+Used ONLY by tests/golden/make_golden.py, in the build container (the reference
+does not exist on the GPU box).  Four optional packages that the reference
+imports at module top level are absent from this image (torchvision, h5py,
+tifffile, optuna); none of them is called on the hot path with blur options
+off and no file I/O, so they are replaced by inert stubs that
+raise if anything actually calls into them.
+"""
+import os
+import sys
+import types
+
+REF_SRC = "/root/reference/src"
+
+
+def _stub(name, **attrs):
+    mod = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(mod, k, v)
+    sys.modules[name] = mod
+    return mod
+
+
+def _raiser(what):
+    def f(*a, **k):
+        raise RuntimeError(f"{what} is stubbed out for fixture generation")
+    return f
+
+
+def import_reference():
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    sys.dont_write_bytecode = True
+    if "torchvision" not in sys.modules:
+        tv = _stub("torchvision")
+        tr = _stub("torchvision.transforms")
+        fn = _stub("torchvision.transforms.functional", gaussian_blur=_raiser("gaussian_blur"))
+        tv.transforms = tr
+        tr.functional = fn
+    if "h5py" not in sys.modules:
+        class _Placeholder:  # noqa: D401 - inert placeholder type
+            def __init__(self, *a, **k):
+                raise RuntimeError("h5py is stubbed out for fixture generation")
+        _stub("h5py", File=_Placeholder, Group=_Placeholder, Dataset=_Placeholder)
+    if "tifffile" not in sys.modules:
+        _stub("tifffile", imread=None, imwrite=None)
+    if "optuna" not in sys.modules:
+        op = _stub("optuna")
+        op.samplers = _stub("optuna.samplers")
+        op.pruners = _stub("optuna.pruners")
+        op.trial = _stub("optuna.trial", Trial=object)
+        op.Trial = object
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    import ptyrad.models as models
+    import ptyrad.losses as losses
+    import ptyrad.reconstruction as reconstruction
+    return models, losses, reconstruction

@@ -1,0 +1,103 @@
+"""Pin the oracle (oracle/ptyx_oracle.py) to golden vectors produced by the PtyRAD reference.
+
+Fixtures: tests/golden/*.npz, made by tests/golden/make_golden.py (reference autograd,
+fp32, CPU).  Tolerance: the reference itself runs in fp32, so the fp64 oracle is compared
+with relative-L2 error ≤ 2e-6 on dp, ≤ 1e-6 relative on loss terms, ≤ 5e-5 on the object /
+probe gradients and ≤ 1e-4 on the position gradient (a sum of cancelling terms, where the
+reference's own fp32 rounding is largest).
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ptyx_oracle as orc
+
+CASES = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*.npz")))
+
+
+def rel(a, b):
+    a = np.asarray(a, np.complex128 if np.iscomplexobj(a) or np.iscomplexobj(b) else np.float64)
+    b = np.asarray(b, a.dtype)
+    return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
+
+
+def load_case(path):
+    z = np.load(path, allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    if "meas_f16" in d:
+        S, n = d["shifts"].shape[0], d["probe"].shape[-1]
+        meas = np.zeros((S, n, n), np.float32)
+        meas[d["batch"]] = d["meas_f16"].astype(np.float32)
+        d["meas"] = meas
+    d["loss_params"] = json.loads(str(d["loss_params"]))
+    return d
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(p)[:-4] for p in CASES])
+def test_oracle_matches_reference(path):
+    d = load_case(path)
+    terms, dps, g = orc.forward_loss_grad(
+        d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"],
+        d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]))
+    dp = dps[0]
+    if "dp" in d:
+        assert rel(dp, d["dp"]) < 2e-6
+    else:
+        assert rel(dp[:4], d["dp_head"]) < 2e-6
+        assert rel(dp.reshape(len(dp), -1).sum(1), d["dp_sums"]) < 2e-6
+    np.testing.assert_allclose(terms[0], d["loss_terms"], rtol=1e-6, atol=1e-8)
+    assert rel(g["obja"], d["g_obja"]) < 5e-5
+    assert rel(g["objp"], d["g_objp"]) < 5e-5
+    gp = d["g_probe"][..., 0] + 1j * d["g_probe"][..., 1]
+    assert rel(g["probe"], gp) < 5e-5
+    if d["shift_probes"]:
+        assert rel(g["shifts"], d["g_shifts"]) < 1e-4
+
+
+TRAJ = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "traj_*.npz")))
+
+
+def oracle_trajectory(z, grad_fn=None):
+    """Replays reference recon_step (reconstruction.py:658-781, Adam branch) with oracle grads."""
+    lp = json.loads(str(z["loss_params"]))
+    lrs = json.loads(str(z["lrs"]))
+    sizes = z["batch_sizes"]
+    flat = z["batches"]
+    batches = np.split(flat, np.cumsum(sizes)[:-1])
+    ga = int(z["grad_accumulation"])
+    params = {"obja": z["init_obja"].copy(), "objp": z["init_objp"].copy(),
+              "probe": np.stack([z["init_probe"].real, z["init_probe"].imag], -1).astype(np.float32),
+              "probe_pos_shifts": z["init_shifts"].copy()}
+    state, t = {}, 0
+    grad_fn = grad_fn or (lambda prm, b, scale: orc.forward_loss_grad(
+        prm["obja"], prm["objp"], prm["probe"][..., 0] + 1j * prm["probe"][..., 1],
+        prm["probe_pos_shifts"], z["crop_pos"], z["H"], z["occu"], z["meas"], [b], lp,
+        shift_probes=True, grad_scale=scale)[2])
+    for _ in range(int(z["niter"])):
+        acc = None
+        for bi, b in enumerate(batches):
+            g = grad_fn(params, b, 1.0 / ga)
+            g = {"obja": g["obja"], "objp": g["objp"],
+                 "probe": np.stack([g["probe"].real, g["probe"].imag], -1),
+                 "probe_pos_shifts": g["shifts"]}
+            acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
+            if (bi + 1) % ga == 0 or bi + 1 == len(batches):
+                t += 1
+                orc.adam_step(params, {k: v.astype(np.float32) for k, v in acc.items()}, state, lrs, t)
+                acc = None
+    return params
+
+
+@pytest.mark.parametrize("path", TRAJ, ids=[os.path.basename(p)[:-4] for p in TRAJ])
+def test_oracle_trajectory_matches_reference(path):
+    """3 reference iterations (Adam, fixed batches): object RMS error vs reference < 1e-5."""
+    z = np.load(path, allow_pickle=False)
+    p = oracle_trajectory(z)
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        rms = float(np.sqrt(np.mean((p[k].astype(np.float64) - ref) ** 2)))
+        assert rms < 1e-5, (k, rms)
+    prb = p["probe"][..., 0] + 1j * p["probe"][..., 1]
+    assert rel(prb, z["final_probe"]) < 1e-5
