@@ -1,0 +1,123 @@
+/* ptyx.h — C ABI of the MI355X-native ptychographic forward/adjoint engine (libptyx.so).
+ *
+ * Drop-in boundary for PtyRAD's per-mini-batch hot path.  PtyRAD has no
+ * FFI of its own; the interfaces each entry point replaces are:
+ *
+ *   ptyx_forward            PtychoAD.forward(indices) -> dp_fwd      src/ptyrad/models.py:422-436
+ *                           (get_obj_ROI :251-265, get_probes :286-298, get_propagators case 4
+ *                            :358-360, multislice_forward_model_vec_all src/ptyrad/forward.py:20-80)
+ *   ptyx_forward_loss_grad  compute_loss + loss_batch.backward()      src/ptyrad/reconstruction.py:792-806, :750-753
+ *                           (CombinedLoss.forward src/ptyrad/losses.py:143-155: loss_single :36-50,
+ *                            loss_poissn :52-75, loss_sparse :91-104; autograd adjoint of all of the above)
+ *   ptyx_adjoint_dldi       the autograd backward of PtychoAD.forward for an arbitrary downstream
+ *                           loss that supplies dL/d(dp_fwd)            src/ptyrad/models.py:422-436
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (HBM), caller-owned, contiguous, row-major, in the
+ *    reference's layouts.  They are borrowed for the duration of the call only.
+ *  - Complex arrays are interleaved (re, im) float32, i.e. torch.view_as_real layout.
+ *  - Every call is asynchronous on `stream` (a hipStream_t; NULL = default stream) and performs
+ *    no host<->device synchronisation, no allocation and no host copies, so it can be captured
+ *    in a hipGraph.  Loss terms stay on the device.
+ *  - Gradients are ACCUMULATED (+=) into caller-zeroed buffers; a NULL gradient pointer means
+ *    "not required" (requires_grad False, reconstruction.py:783-790) and its work is skipped.
+ *  - Status: 0 on success, a PTYX_E* code otherwise; ptyx_last_error() gives a thread-local
+ *    message.  No C++ exception crosses the ABI.
+ *  - A plan is bound to one device and one geometry and must not be used by two host threads
+ *    concurrently.
+ */
+#ifndef PTYX_H
+#define PTYX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTYX_OK 0
+#define PTYX_EINVAL 1
+#define PTYX_ENOMEM 2
+#define PTYX_EHIP 3
+#define PTYX_EUNSUPPORTED 4
+
+/* dims.flags */
+#define PTYX_SHIFT_PROBES 1u /* sub-px Fourier-shifted probes (PtychoAD.shift_probes, models.py:120) */
+#define PTYX_MEAS_F16 2u     /* measurements stored as IEEE half (fp16 storage / fp32 accumulate)   */
+
+typedef struct ptyx_plan ptyx_plan;
+
+typedef struct ptyx_dims {
+  int32_t N;            /* probe / DP side, power of two, 16..256                         */
+  int32_t P;            /* probe modes  (opt_probe.shape[0])                               */
+  int32_t O;            /* object modes (opt_obja.shape[0])                                */
+  int32_t Nz;           /* object slices (opt_obja.shape[1])                               */
+  int32_t Ny, Nx;       /* object extent                                                   */
+  int32_t n_scans;      /* number of probe positions (crop_pos.shape[0])                   */
+  int32_t max_patterns; /* largest number of patterns per call (sizes the workspace)       */
+  uint32_t flags;       /* PTYX_SHIFT_PROBES | PTYX_MEAS_F16                               */
+} ptyx_dims;
+
+typedef struct ptyx_inputs {
+  const float *obja;       /* (O,Nz,Ny,Nx) f32  PtychoAD.opt_obja                            */
+  const float *objp;       /* (O,Nz,Ny,Nx) f32  PtychoAD.opt_objp                            */
+  const float *probe;      /* (P,N,N,2)    f32  PtychoAD.opt_probe (view_as_real)            */
+  const float *shifts;     /* (n_scans,2)  f32  PtychoAD.opt_probe_pos_shifts (y,x) px       */
+  const float *H;          /* (N,N,2)      f32  PtychoAD.H, zero frequency at the corner      */
+  const float *omode_occu; /* (O,)         f32                                               */
+  const int32_t *crop_pos; /* (n_scans,2)  i32  integer top-left (y,x) of each patch          */
+  const void *meas;        /* (n_scans,N,N) f32 (or f16 with PTYX_MEAS_F16), fftshifted DPs  */
+} ptyx_inputs;
+
+typedef struct ptyx_grads {
+  float *d_obja;   /* (O,Nz,Ny,Nx)  += dL/dobja                 or NULL */
+  float *d_objp;   /* (O,Nz,Ny,Nx)  += dL/dobjp                 or NULL */
+  float *d_probe;  /* (P,N,N,2)     += dL/dRe + i dL/dIm probe  or NULL */
+  float *d_shifts; /* (n_scans,2)   += dL/dshift                or NULL */
+} ptyx_grads;
+
+/* CombinedLoss terms on the hot path (params/loss_params.py defaults in brackets). */
+typedef struct ptyx_loss_cfg {
+  int32_t single_on;  float single_w, single_q;              /* loss_single [1, 1.0, 0.5]       */
+  int32_t poissn_on;  float poissn_w, poissn_q, poissn_eps;  /* loss_poissn [0, 1.0, 1.0, 1e-6] */
+  int32_t sparse_on;  float sparse_w; int32_t sparse_n;      /* loss_sparse [1, 0.1, 1]         */
+  float grad_scale;   /* multiplies every gradient: 1/grad_accumulation, reconstruction.py:750 */
+} ptyx_loss_cfg;
+
+/* Create a plan: validates dims, allocates the device workspace and twiddle tables.
+ * device: HIP device ordinal the plan (and every pointer passed to it) lives on. */
+int ptyx_plan_create(ptyx_plan **out, const ptyx_dims *dims, int device);
+int ptyx_plan_destroy(ptyx_plan *plan);
+
+/* dp_out (n_idx,N,N) f32 = PtychoAD.forward(idx) for the positions idx[0..n_idx). */
+int ptyx_forward(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
+                 int32_t n_idx, float *dp_out);
+
+/* Fused forward + loss + adjoint over n_batches mini-batches.
+ * idx[batch_offsets[b] .. batch_offsets[b+1]) are the scan indices of mini-batch b (each with its
+ * own NRMSE normalisation, losses.py:45-47); gradients of all mini-batches are summed (i.e. the
+ * reference's grad_accumulation over these batches, scaled by cfg->grad_scale).
+ * loss_terms (n_batches,5) f32 device: [single, poissn, pacbed(=0), sparse, simlar(=0)] per batch,
+ * unscaled (the values CombinedLoss returns). dp_out (n_idx,N,N) optional (NULL to skip). */
+int ptyx_forward_loss_grad(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
+                           const int32_t *batch_offsets, int32_t n_batches, int32_t n_idx,
+                           const ptyx_loss_cfg *cfg, float *loss_terms, float *dp_out,
+                           const ptyx_grads *grads);
+
+/* Adjoint for an external loss: given dLdI (n_idx,N,N) = dL/d(dp_fwd) for the patterns idx,
+ * accumulate the object / probe / position gradients (autograd of PtychoAD.forward). */
+int ptyx_adjoint_dldi(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
+                      int32_t n_idx, const float *dLdI, float grad_scale, const ptyx_grads *grads);
+
+/* Bytes of device workspace the plan holds. */
+size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
+/* Last error message of the calling thread ("" if none). */
+const char *ptyx_last_error(void);
+/* ABI version (major*100 + minor). */
+int ptyx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTYX_H */

@@ -1,0 +1,94 @@
+"""ctypes binding of libptyx.so (include/ptyx.h).  The HIP library is REQUIRED.
+
+There is no CPU fallback: if the shared library is missing or fails to load, every entry
+point raises.  torch is imported first so that its HIP runtime (libamdhip64.so.7) is the one
+that libptyx.so binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
+
+PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
+PTYX_SHIFT_PROBES = 1
+PTYX_MEAS_F16 = 2
+
+_ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
+
+# every symbol include/ptyx.h declares (checked by tests/test_abi.py)
+EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+           "ptyx_adjoint_dldi", "ptyx_plan_workspace_bytes", "ptyx_last_error", "ptyx_version")
+
+
+class PtyxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"ptyx {_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int32), ("P", ctypes.c_int32), ("O", ctypes.c_int32),
+                ("Nz", ctypes.c_int32), ("Ny", ctypes.c_int32), ("Nx", ctypes.c_int32),
+                ("n_scans", ctypes.c_int32), ("max_patterns", ctypes.c_int32),
+                ("flags", ctypes.c_uint32)]
+
+
+class Inputs(ctypes.Structure):
+    _fields_ = [("obja", ctypes.c_void_p), ("objp", ctypes.c_void_p), ("probe", ctypes.c_void_p),
+                ("shifts", ctypes.c_void_p), ("H", ctypes.c_void_p), ("omode_occu", ctypes.c_void_p),
+                ("crop_pos", ctypes.c_void_p), ("meas", ctypes.c_void_p)]
+
+
+class Grads(ctypes.Structure):
+    _fields_ = [("d_obja", ctypes.c_void_p), ("d_objp", ctypes.c_void_p),
+                ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p)]
+
+
+class LossCfg(ctypes.Structure):
+    _fields_ = [("single_on", ctypes.c_int32), ("single_w", ctypes.c_float), ("single_q", ctypes.c_float),
+                ("poissn_on", ctypes.c_int32), ("poissn_w", ctypes.c_float), ("poissn_q", ctypes.c_float),
+                ("poissn_eps", ctypes.c_float),
+                ("sparse_on", ctypes.c_int32), ("sparse_w", ctypes.c_float), ("sparse_n", ctypes.c_int32),
+                ("grad_scale", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libptyx.so once and declare the prototypes.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"libptyx.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(there is no CPU fallback)")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+    lib.ptyx_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Dims), ctypes.c_int]
+    lib.ptyx_plan_destroy.argtypes = [vp]
+    lib.ptyx_forward.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, i32, vp]
+    lib.ptyx_forward_loss_grad.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, vp, i32, i32,
+                                           ctypes.POINTER(LossCfg), vp, vp, ctypes.POINTER(Grads)]
+    lib.ptyx_adjoint_dldi.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, i32, vp, f32,
+                                      ctypes.POINTER(Grads)]
+    lib.ptyx_plan_workspace_bytes.argtypes = [vp]
+    lib.ptyx_plan_workspace_bytes.restype = ctypes.c_size_t
+    lib.ptyx_last_error.restype = ctypes.c_char_p
+    lib.ptyx_version.restype = ctypes.c_int
+    for name in ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+                 "ptyx_adjoint_dldi"):
+        getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != PTYX_OK:
+        raise PtyxError(rc, _lib.ptyx_last_error().decode(errors="replace"))

@@ -1,0 +1,310 @@
+// ptyx_fft.hpp — workgroup-resident 2-D complex FFTs for gfx950 (CDNA4), fp32.
+//
+// One workgroup transforms one N×N complex64 array.  The array lives either in LDS
+// (N ≤ 128: 128·136·8 B = 136 KiB, in place) or in a per-workgroup global scratch pair
+// (N = 256, ping-pong).  Each 1-D pass is a Stockham radix-R iteration (natural order in
+// and out; Govindaraju et al. 2008 indexing, checked against numpy in tests): every thread
+// loads R points of one line, applies the stage twiddles (fp64-rounded table in LDS),
+// runs an in-register DFT_R and stores R points.  Rows are transformed first, then
+// columns.  Point-wise work that sits between FFTs in the ptychography model (probe
+// shift ramps, object multiply, propagator, |·|², loss gradient, scatter-add) is fused
+// into the first stage's loads ("pre") and the last stage's stores ("post"), so data
+// makes one trip through LDS per stage and none through HBM.
+//
+// Replaces the torch.fft calls of src/ptyrad/forward.py:63,79 and
+// src/ptyrad/utils/image_proc.py:532 (pocketfft on CPU / hipFFT on GPU in the reference).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <type_traits>
+
+namespace ptyx {
+
+// ---------------------------------------------------------------- complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float cabs2(float2 a) { return fmaf(a.x, a.x, a.y * a.y); }
+
+// cos/sin(2πk/16), correctly rounded to fp32
+__device__ constexpr float kCos16[16] = {
+    1.0f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
+    0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f,
+    -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f,
+    0.0f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128674f};
+__device__ constexpr float kSin16[16] = {
+    0.0f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128674f,
+    1.0f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
+    0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f,
+    -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f};
+
+// v · exp(DIR·2πi·K/R), trivial rotations without multiplies (DIR = -1 forward, +1 inverse)
+template <int R, int K, int DIR>
+__device__ __forceinline__ float2 twmul(float2 v) {
+  constexpr int k16 = (K * (16 / R)) & 15;
+  if constexpr (k16 == 0) {
+    return v;
+  } else if constexpr (k16 == 4) {  // DIR·i
+    return DIR < 0 ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+  } else if constexpr (k16 == 8) {
+    return make_float2(-v.x, -v.y);
+  } else if constexpr (k16 == 12) {  // -DIR·i
+    return DIR < 0 ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+  } else {
+    return cmul(v, make_float2(kCos16[k16], DIR * kSin16[k16]));
+  }
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// In-register DFT of size R ∈ {2,4,8,16}, natural order in and out, radix-2 DIT recursion.
+template <int R, int DIR>
+struct DFT {
+  __device__ __forceinline__ static void run(float2 (&v)[R]) {
+    float2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    DFT<R / 2, DIR>::run(e);
+    DFT<R / 2, DIR>::run(o);
+    static_for<0, R / 2>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      const float2 t = twmul<R, k, DIR>(o[k]);
+      v[k] = cadd(e[k], t);
+      v[k + R / 2] = csub(e[k], t);
+    });
+  }
+};
+template <int DIR>
+struct DFT<2, DIR> {
+  __device__ __forceinline__ static void run(float2 (&v)[2]) {
+    const float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+template <int DIR>
+struct DFT<4, DIR> {
+  __device__ __forceinline__ static void run(float2 (&v)[4]) {
+    const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
+    const float2 a2 = cadd(v[1], v[3]), a3 = twmul<4, 1, DIR>(csub(v[1], v[3]));
+    v[0] = cadd(a0, a2);
+    v[2] = csub(a0, a2);
+    v[1] = cadd(a1, a3);
+    v[3] = csub(a1, a3);
+  }
+};
+
+// ---------------------------------------------------------------- radix plans
+// Per-dimension Stockham radices: N = R1·R2 (R2 = 1 ⇒ one pass per dimension).
+template <int N> struct Plan1D;
+template <> struct Plan1D<16>  { static constexpr int R1 = 16, R2 = 1; };
+template <> struct Plan1D<32>  { static constexpr int R1 = 8,  R2 = 4; };
+template <> struct Plan1D<64>  { static constexpr int R1 = 8,  R2 = 8; };
+template <> struct Plan1D<128> { static constexpr int R1 = 16, R2 = 8; };
+template <> struct Plan1D<256> { static constexpr int R1 = 16, R2 = 16; };
+
+// ---------------------------------------------------------------- array views
+// LDS view, in place.  Row stride N + N/16 and one pad point per 16 spreads the
+// strided Stockham accesses over the banks (ds_read_b64 / ds_write_b64).
+template <int N>
+struct LdsArray {
+  static constexpr bool kInPlace = true;
+  static constexpr int kRowStride = N + N / 16;
+  static constexpr int kElems = N * kRowStride;
+  float2* p;
+  __device__ __forceinline__ int off(int y, int x) const { return y * kRowStride + x + (x >> 4); }
+  __device__ __forceinline__ float2 ld(int y, int x) const { return p[off(y, x)]; }
+  __device__ __forceinline__ void st(int y, int x, float2 v) const { p[off(y, x)] = v; }
+};
+
+// Global scratch pair for arrays that do not fit LDS (N = 256); ping-pong between a and b.
+template <int N>
+struct GlobalPair {
+  static constexpr bool kInPlace = false;
+  float2* a;
+  float2* b;
+  __device__ __forceinline__ float2 ld(int y, int x) const { return a[y * N + x]; }
+  __device__ __forceinline__ void st(int y, int x, float2 v) const { a[y * N + x] = v; }
+};
+template <int N>
+struct GlobalView {
+  float2* p;
+  __device__ __forceinline__ float2 ld(int y, int x) const { return p[y * N + x]; }
+  __device__ __forceinline__ void st(int y, int x, float2 v) const { p[y * N + x] = v; }
+};
+
+// stage kinds
+enum : int { kMid = 0, kFirst = 1, kLast = 2 };
+
+// Fused pre/post element group size between scheduling barriers (0 = let the compiler
+// schedule freely).  Without it hipcc hoists every element's global loads of a 16-point
+// epilogue ahead of the arithmetic and spills at 128 VGPRs (1024-thread workgroups).
+#ifndef PTYX_FUSE_GROUP
+#define PTYX_FUSE_GROUP 4
+#endif
+constexpr int kFuseGroup = PTYX_FUSE_GROUP;
+
+// twiddle table tw[m] = exp(-2πi m / N) (fp64 rounded), conj for inverse
+template <int DIR>
+__device__ __forceinline__ float2 twiddle(const float2* tw, int m) {
+  const float2 w = tw[m];
+  return DIR < 0 ? w : make_float2(w.x, -w.y);
+}
+
+// One Stockham pass of radix R over all N lines.  ROW: lines are rows (x varies).
+//  PRELOAD (first pass only): whether to load the source before calling pre(y,x,v).
+//  post(y,x,v) (last pass only) may modify v and returns true if v must be stored.
+template <int N, int NT, int R, int NS, bool ROW, int DIR, int KIND, bool PRELOAD, bool INPLACE, class Src,
+          class Dst, class Pre, class Post>
+__device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, const float2* tw, Pre& pre,
+                                              Post& post) {
+  constexpr int NB = N * N / R;           // butterflies in this pass
+  constexpr int L = N / R;                // butterflies per line
+  constexpr int TWS = N / (NS * R);       // twiddle table stride
+  // Opaque copy of threadIdx.x: keeps hipcc from hoisting every pass's per-element LDS
+  // addresses out of the persistent pattern loop (loop-invariant code motion of ~300 address
+  // registers, all spilled at the 128-VGPR cap).  Recomputing them is a few VALU ops per point.
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  if constexpr (INPLACE) {
+    constexpr int KB = (NB + NT - 1) / NT;
+    float2 v[KB][R];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int bf = tid + kb * NT;
+      if ((NB % NT) == 0 || bf < NB) {
+        const int line = ROW ? bf / L : bf % N;
+        const int j = ROW ? bf % L : bf / N;
+        const int k = j % NS;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int e = j + r * L;
+          const int y = ROW ? line : e, x = ROW ? e : line;
+          float2 val;
+          if constexpr (KIND & kFirst) {
+            if constexpr (PRELOAD) val = pre(y, x, src.ld(y, x));
+            else val = pre(y, x, make_float2(0.f, 0.f));
+            if constexpr (kFuseGroup > 0) {
+              if ((r + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
+            }
+          } else {
+            val = src.ld(y, x);
+          }
+          if constexpr (NS > 1) {
+            if (r > 0) val = cmul(val, twiddle<DIR>(tw, k * r * TWS));
+          }
+          v[kb][r] = val;
+        }
+        DFT<R, DIR>::run(v[kb]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int bf = tid + kb * NT;
+      if ((NB % NT) == 0 || bf < NB) {
+        const int line = ROW ? bf / L : bf % N;
+        const int j = ROW ? bf % L : bf / N;
+        const int k = j % NS;
+        const int d0 = (j / NS) * NS * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int e = d0 + r * NS;
+          const int y = ROW ? line : e, x = ROW ? e : line;
+          float2 val = v[kb][r];
+          if constexpr (KIND & kLast) {
+            if (post(y, x, val)) dst.st(y, x, val);
+            // bound the compiler's hoisting of the fused epilogue's global loads
+            if constexpr (kFuseGroup > 0) {
+              if ((r + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
+            }
+          } else {
+            dst.st(y, x, val);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  } else {
+    for (int bf = tid; bf < NB; bf += NT) {
+      const int line = ROW ? bf / L : bf % N;
+      const int j = ROW ? bf % L : bf / N;
+      const int k = j % NS;
+      float2 v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = j + r * L;
+        const int y = ROW ? line : e, x = ROW ? e : line;
+        float2 val;
+        if constexpr (KIND & kFirst) {
+          if constexpr (PRELOAD) val = pre(y, x, src.ld(y, x));
+          else val = pre(y, x, make_float2(0.f, 0.f));
+        } else {
+          val = src.ld(y, x);
+        }
+        if constexpr (NS > 1) {
+          if (r > 0) val = cmul(val, twiddle<DIR>(tw, k * r * TWS));
+        }
+        v[r] = val;
+      }
+      DFT<R, DIR>::run(v);
+      const int d0 = (j / NS) * NS * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = d0 + r * NS;
+        const int y = ROW ? line : e, x = ROW ? e : line;
+        float2 val = v[r];
+        if constexpr (KIND & kLast) {
+          if (post(y, x, val)) dst.st(y, x, val);
+        } else {
+          dst.st(y, x, val);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Unnormalised 2-D DFT of the array (DIR = -1 forward, +1 inverse), rows then columns.
+// Result left in the array (for GlobalPair: in .a after an even number of passes).
+template <int N, int NT, int DIR, bool PRELOAD, class Arr, class Pre, class Post>
+__device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pre, Post&& post) {
+  using P1 = Plan1D<N>;
+  constexpr int R1 = P1::R1, R2 = P1::R2;
+  if constexpr (Arr::kInPlace) {
+    if constexpr (R2 == 1) {
+      stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, true>(arr, arr, tw, pre, post);
+      stockham_pass<N, NT, R1, 1, false, DIR, kLast, false, true>(arr, arr, tw, pre, post);
+    } else {
+      stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, true>(arr, arr, tw, pre, post);
+      stockham_pass<N, NT, R2, R1, true, DIR, kMid, false, true>(arr, arr, tw, pre, post);
+      stockham_pass<N, NT, R1, 1, false, DIR, kMid, false, true>(arr, arr, tw, pre, post);
+      stockham_pass<N, NT, R2, R1, false, DIR, kLast, false, true>(arr, arr, tw, pre, post);
+    }
+  } else {
+    static_assert(R2 != 1, "global ping-pong needs two passes per dimension");
+    const GlobalView<N> A{arr.a}, B{arr.b};
+    stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, false>(A, B, tw, pre, post);
+    stockham_pass<N, NT, R2, R1, true, DIR, kMid, false, false>(B, A, tw, pre, post);
+    stockham_pass<N, NT, R1, 1, false, DIR, kMid, false, false>(A, B, tw, pre, post);
+    stockham_pass<N, NT, R2, R1, false, DIR, kLast, false, false>(B, A, tw, pre, post);
+  }
+}
+
+}  // namespace ptyx

@@ -1,0 +1,974 @@
+// ptyx_kernels.hip — HIP kernels (gfx950) and C ABI for the PtyRAD forward/loss/adjoint hot path.
+//
+// Per call (one group of mini-batches, include/ptyx.h):
+//   k_probe_spectrum  F(P_p) once per call                       (image_proc.py:532, fft2(img))
+//   k_forward         per pattern: shifted probe, object multiply, multislice, far field,
+//                     Σ occ|Ψ|² + 1e-10, per-pattern loss partial sums      (models.py:422-436,
+//                     forward.py:20-80, losses.py:45-46,70-71,101)
+//   k_finalize        per mini-batch: loss terms + adjoint coefficients (losses.py:36-104)
+//   k_adjoint         per pattern: recompute forward, dL/dI, back through the FFTs, object
+//                     gradient scatter-add (fp32 atomics), probe-gradient partial (per-workgroup
+//                     slab in k space), position gradient (Parseval, no extra FFT)  
+//   k_slab_reduce     Σ over workgroup slabs in fixed order (deterministic)
+//   k_probe_finalize  F^-1 of the k-space probe gradient → d_probe  (+=)
+//
+// One workgroup owns one pattern at a time and keeps the N×N wave in LDS (N ≤ 128) or in a
+// per-workgroup global scratch pair (N = 256).  The grid is persistent (≈ one workgroup per CU
+// for N = 128) and walks the patterns with a grid stride.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ptyx.h"
+#include "ptyx_fft.hpp"
+
+namespace ptyx {
+
+constexpr int kMaxModesO = 8;
+constexpr int kSumBase = 4;                    // [S_single, ΣM^q1, S_poissn, ΣM^q2] then O sparse sums
+constexpr int kNSum = kSumBase + kMaxModesO;
+constexpr int kNCoef = 2 + kMaxModesO;         // [c_single, c_poissn, c_sparse[o]...]
+constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
+
+template <int N> struct Geo;
+template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true; };
+template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true; };
+template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true; };
+template <> struct Geo<256> { static constexpr int NT = 1024; static constexpr bool kLds = false; };
+
+struct KArgs {
+  int P, O, Nz, Ny, Nx, n_scans;
+  int shift, meas_f16;
+  const float* obja;
+  const float* objp;
+  const float2* probe;
+  const float2* Fp;
+  const float* shifts;
+  const int* crop;
+  const float2* H;
+  const float* occu;
+  const void* meas;
+  const int* idx;
+  int n_idx;
+  const int* boff;
+  int n_batches;
+  int single_on, pois_on, sparse_on, sparse_n;
+  float q1, q2, eps2;
+  const float* coef;
+  float* psums;
+  float* Ibuf;
+  float* dp_out;
+  const float* dLdI_ext;
+  float ext_scale;
+  float* d_obja;
+  float* d_objp;
+  float* d_shifts;
+  int need_probe;
+  float2* slab;
+  float2* scratch;
+  long long scratch_stride;
+  const float2* twg;
+};
+
+// ---------------------------------------------------------------- small helpers
+// threadIdx.x behind an empty asm: per-pattern address arithmetic stays inside the pattern
+// loop instead of being hoisted (and spilled) by loop-invariant code motion.
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// x^q for x >= 0 (DP intensities): exact forms for the schema values 0.5 / 1, otherwise
+// exp2(q·log2 x) on the v_exp_f32 / v_log_f32 units (no libm slow path in the fused epilogues).
+__device__ __forceinline__ float powq(float x, float q) {
+  if (q == 0.5f) return sqrtf(x);
+  if (q == 1.0f) return x;
+  if (!(x > 0.f)) return q > 0.f ? 0.f : __builtin_inff();
+  return __builtin_amdgcn_exp2f(q * __builtin_amdgcn_logf(x));
+}
+
+__device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+
+// sin/cos of an object phase: reduce to revolutions in [-1/2, 1/2], then v_sin_f32 / v_cos_f32
+// (which take revolutions).  Absolute error ≈ |φ|·6e-8 + 1 ulp, far inside the parity budget.
+__device__ __forceinline__ void phase_sincos(float ph, float* sn, float* cs) {
+  float r = ph * 0.15915494309189535f;
+  r = r - rintf(r);
+  *sn = __builtin_amdgcn_sinf(r);
+  *cs = __builtin_amdgcn_cosf(r);
+}
+
+__device__ __forceinline__ float meas_at(const KArgs& a, int s, int e, int N2) {
+  const size_t off = (size_t)s * N2 + e;
+  if (a.meas_f16) return __half2float(reinterpret_cast<const __half*>(a.meas)[off]);
+  return reinterpret_cast<const float*>(a.meas)[off];
+}
+
+__device__ __forceinline__ size_t obj_off(const KArgs& a, int o, int n, int yy, int xx) {
+  return ((size_t)(o * a.Nz + n) * a.Ny + yy) * a.Nx + xx;
+}
+
+// wave64 + workgroup sum of NV floats, fixed order (deterministic); result valid in thread 0.
+template <int NT, int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v[i] += __shfl_xor(v[i], m, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[wv * NV + i] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float t = 0.f;
+      for (int w = 0; w < NT / 64; ++w) t += red[w * NV + i];
+      v[i] = t;
+    }
+  }
+  __syncthreads();
+}
+
+struct PatternGeom {
+  int s, cy, cx;
+  float sy, sx;
+};
+
+__device__ __forceinline__ PatternGeom pattern_geom(const KArgs& a, int pat, int N) {
+  PatternGeom g;
+  int s = a.idx[pat];
+  s = min(max(s, 0), a.n_scans - 1);  // defensive clamp; the host validates indices
+  g.s = s;
+  g.cy = min(max(a.crop[2 * s], 0), a.Ny - N);
+  g.cx = min(max(a.crop[2 * s + 1], 0), a.Nx - N);
+  g.sy = a.shifts[2 * s];
+  g.sx = a.shifts[2 * s + 1];
+  return g;
+}
+
+// W_b ramps along y and x: exp(-2πi s g[k]), g[k] = ((k + N/2) mod N)/N  (image_proc.py:531,
+// models.py:179 grid arange(N)/N after ifftshift).
+template <int N, int NT>
+__device__ __forceinline__ void build_ramps(const PatternGeom& g, float2* wy, float2* wx) {
+  for (int k = opaque_tid(); k < 2 * N; k += NT) {
+    const int kk = k % N;
+    const float gr = (float)((kk + N / 2) % N) / (float)N;
+    const float s = k < N ? g.sy : g.sx;
+    float sn, cs;
+    sincospif(-2.0f * s * gr, &sn, &cs);
+    (k < N ? wy : wx)[kk] = make_float2(cs, sn);
+  }
+  __syncthreads();
+}
+
+template <int N>
+__device__ __forceinline__ float shift_g(int k) {
+  return (float)((k + N / 2) % N) / (float)N;
+}
+
+template <int N, bool LDS>
+struct ArrayFor;
+template <int N>
+struct ArrayFor<N, true> {
+  using type = LdsArray<N>;
+};
+template <int N>
+struct ArrayFor<N, false> {
+  using type = GlobalPair<N>;
+};
+
+// Scratch layout per workgroup (float2 units): [fft a, fft b (N=256 only)] [psi: Nz·N²] [gacc: N²]
+template <int N>
+__device__ __forceinline__ float2* scratch_psi(const KArgs& a) {
+  return a.scratch + (long long)blockIdx.x * a.scratch_stride + (Geo<N>::kLds ? 0 : 2 * N * N);
+}
+
+// =====================================================================================
+// Forward chain for one (pattern, p, o): leaves ψ_out = ψ^{Nz-1} ⊙ O_{Nz-1} in the array.
+// STORE_PSI: store every ψ^n (n = 0..Nz-1, the wave ENTERING slice n) to psi[n·N²].
+// SPARSE: accumulate Σ|φ|^n of every object pixel touched (once per pattern: caller gates).
+template <int N, int NT, bool STORE_PSI, class Arr>
+__device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, const float2* tw,
+                                              const float2* wy, const float2* wx,
+                                              const PatternGeom& g, int p, int o, float2* psi,
+                                              bool sparse, float& sp_acc) {
+  constexpr int N2 = N * N;
+  constexpr float inv_n2 = 1.0f / (float)N2;
+  auto mul_obj = [&](int n, int y, int x, float2 w) -> float2 {
+    const size_t off = obj_off(a, o, n, g.cy + y, g.cx + x);
+    const float A = a.obja[off], ph = a.objp[off];
+    float sn, cs;
+    phase_sincos(ph, &sn, &cs);
+    if (sparse) {
+      const float ap = fabsf(ph);
+      sp_acc += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
+    }
+    return cmul(w, make_float2(A * cs, A * sn));
+  };
+  const float2* Fp = a.Fp + (size_t)p * N2;
+  const float2* P0 = a.probe + (size_t)p * N2;
+  // ψ^0: shifted probe F^-1(F(P) ⊙ W_b)   (image_proc.py:532) or the broadcast probe
+  if (a.shift) {
+    fft2d<N, NT, +1, false>(
+        arr, tw,
+        [&](int y, int x, float2) { return cmul(cmul(Fp[y * N + x], wy[y]), wx[x]); },
+        [&](int y, int x, float2& v) {
+          const float2 w = cscale(v, inv_n2);
+          if (STORE_PSI) psi[y * N + x] = w;
+          v = mul_obj(0, y, x, w);
+          return true;
+        });
+  } else {
+    for (int e = opaque_tid(); e < N2; e += NT) {
+      const int y = e / N, x = e % N;
+      const float2 w = P0[e];
+      if (STORE_PSI) psi[e] = w;
+      arr.st(y, x, mul_obj(0, y, x, w));
+    }
+    __syncthreads();
+  }
+  // multislice: ψ^{n} = F^-1(H ⊙ F(ψ^{n-1} ⊙ O_{n-1}))   (forward.py:60-63)
+  for (int n = 1; n < a.Nz; ++n) {
+    fft2d<N, NT, -1, true>(
+        arr, tw, [&](int, int, float2 v) { return v; },
+        [&](int y, int x, float2& v) {
+          v = cmul(v, a.H[y * N + x]);
+          return true;
+        });
+    fft2d<N, NT, +1, true>(
+        arr, tw, [&](int, int, float2 v) { return v; },
+        [&](int y, int x, float2& v) {
+          const float2 w = cscale(v, inv_n2);
+          if (STORE_PSI) psi[(size_t)n * N2 + y * N + x] = w;
+          v = mul_obj(n, y, x, w);
+          return true;
+        });
+  }
+}
+
+// =====================================================================================
+// k_probe_spectrum: Fp[p] = F(P_p)
+template <int N>
+__global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* Fp_out) {
+  constexpr int NT = Geo<N>::NT;
+  constexpr bool LDS = Geo<N>::kLds;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
+  __syncthreads();
+  const int p = blockIdx.x;
+  typename ArrayFor<N, LDS>::type arr;
+  if constexpr (LDS) arr.p = s_buf;
+  else {
+    arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
+    arr.b = arr.a + N * N;
+  }
+  const float2* P0 = a.probe + (size_t)p * N * N;
+  float2* out = Fp_out + (size_t)p * N * N;
+  fft2d<N, NT, -1, false>(
+      arr, s_tw, [&](int y, int x, float2) { return P0[y * N + x]; },
+      [&](int y, int x, float2& v) {
+        out[y * N + x] = v;
+        return false;
+      });
+}
+
+// =====================================================================================
+// k_forward: I = Σ_{p,o} occ_o |S F_o ψ_out|² + eps per pattern; dp_out; loss partial sums.
+// SINGLE: P·O == 1, the loss sums are taken straight from the far-field pass.
+template <int N, bool SINGLE>
+__global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
+  constexpr int NT = Geo<N>::NT;
+  constexpr bool LDS = Geo<N>::kLds;
+  constexpr int N2 = N * N;
+  constexpr float inv_n = 1.0f / (float)N;
+  __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
+  __shared__ float s_red[(NT / 64) * 4];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
+  typename ArrayFor<N, LDS>::type arr;
+  if constexpr (LDS) arr.p = s_buf;
+  else {
+    arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
+    arr.b = arr.a + N2;
+  }
+  __syncthreads();
+  const bool want_sums = a.psums != nullptr;
+
+  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
+    const PatternGeom g = pattern_geom(a, pat, N);
+    if (a.shift) build_ramps<N, NT>(g, s_wy, s_wx);
+    float sums[4] = {0.f, 0.f, 0.f, 0.f};
+    auto add_sums = [&](float I, float M) {
+      if (a.single_on) {
+        const float Iq = powq(I, a.q1), Mq = powq(M, a.q1), d = Iq - Mq;
+        sums[0] = fmaf(d, d, sums[0]);
+        sums[1] += Mq;
+      }
+      if (a.pois_on) {
+        const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
+        sums[2] += Mq * fast_ln(Iq + a.eps2) - Iq;
+        sums[3] += Mq;
+      }
+    };
+    float* Ip = SINGLE ? nullptr : a.Ibuf + (size_t)pat * N2;
+    for (int p = 0; p < a.P; ++p) {
+      for (int o = 0; o < a.O; ++o) {
+        const bool sparse = want_sums && a.sparse_on && p == 0;
+        float sp = 0.f;
+        forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp);
+        const float occ = a.occu[o];
+        const bool first = (p == 0 && o == 0);
+        // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
+        fft2d<N, NT, -1, true>(
+            arr, s_tw, [&](int, int, float2 v) { return v; },
+            [&](int y, int x, float2& v) {
+              const float2 Psi = cscale(v, inv_n);
+              const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
+              const float c = occ * cabs2(Psi);
+              if constexpr (SINGLE) {
+                const float I = c + kDpEps;
+                if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
+                if (want_sums) add_sums(I, meas_at(a, g.s, e, N2));
+              } else {
+                Ip[e] = first ? c : Ip[e] + c;
+              }
+              return false;
+            });
+        if (sparse) {
+          float v1[1] = {sp};
+          block_sum<NT, 1>(v1, s_red);
+          if (threadIdx.x == 0) a.psums[(size_t)pat * kNSum + kSumBase + o] = v1[0];
+        }
+      }
+    }
+    if constexpr (!SINGLE) {
+      // epilogue: + eps, dp_out, loss sums (Ip was written by this workgroup; barrier above)
+      for (int e = opaque_tid(); e < N2; e += NT) {
+        const float I = Ip[e] + kDpEps;
+        Ip[e] = I;
+        if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
+        if (want_sums) add_sums(I, meas_at(a, g.s, e, N2));
+      }
+    }
+    if (want_sums) {
+      block_sum<NT, 4>(sums, s_red);
+      if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.psums[(size_t)pat * kNSum + i] = sums[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// =====================================================================================
+// k_finalize: one thread per mini-batch — loss terms and adjoint coefficients.
+struct FinArgs {
+  const int* boff;
+  int n_batches, N, Nz, O;
+  const float* psums;
+  const float* occu;
+  int single_on, pois_on, sparse_on, sparse_n;
+  float w1, w2, ws, grad_scale;
+  float* coef;
+  float* loss_terms;
+};
+
+__global__ void k_finalize(FinArgs f) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= f.n_batches) return;
+  const int b0 = f.boff[m], b1 = f.boff[m + 1];
+  const double B = (double)(b1 - b0);
+  const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
+  double S1 = 0, M1 = 0, S2 = 0, M2 = 0, sp[kMaxModesO] = {0};
+  for (int t = b0; t < b1; ++t) {
+    const float* ps = f.psums + (size_t)t * kNSum;
+    S1 += ps[0];
+    M1 += ps[1];
+    S2 += ps[2];
+    M2 += ps[3];
+    for (int o = 0; o < f.O; ++o) sp[o] += ps[kSumBase + o];
+  }
+  float terms[5] = {0, 0, 0, 0, 0};
+  float c1 = 0.f, c2 = 0.f;
+  if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
+    const double mu = M1 / K, rmse = sqrt(S1 / K);
+    terms[0] = (float)(f.w1 * rmse / mu);
+    c1 = rmse > 0 ? (float)(f.w1 / (mu * K * rmse) * f.grad_scale) : 0.f;
+  }
+  if (f.pois_on && B > 0) {  // -w·mean(M^q log(I^q+eps) - I^q) / mean(M^q)   losses.py:70-72
+    const double mu = M2 / K;
+    terms[1] = (float)(-f.w2 * (S2 / K) / mu);
+    c2 = (float)(-f.w2 / (mu * K) * f.grad_scale);
+  }
+  float* cf = f.coef + (size_t)m * kNCoef;
+  cf[0] = c1;
+  cf[1] = c2;
+  if (f.sparse_on && B > 0) {  // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
+    const double cnt = B * f.Nz * f.N * f.N;
+    double t = 0;
+    for (int o = 0; o < f.O; ++o) {
+      const double mo = sp[o] / cnt;
+      const double inv = 1.0 / f.sparse_n;
+      t += f.occu[o] * pow(mo, inv);
+      const double dm = (f.sparse_n == 1) ? 1.0 : (mo > 0 ? pow(mo, inv - 1.0) : 0.0);
+      cf[2 + o] = (float)(f.ws * f.occu[o] * dm / cnt * f.grad_scale);
+    }
+    terms[3] = (float)(f.ws * t);
+  } else {
+    for (int o = 0; o < f.O; ++o) cf[2 + o] = 0.f;
+  }
+  if (f.loss_terms)
+    for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
+}
+
+// =====================================================================================
+// k_adjoint: gradients.  EXT: dL/dI supplied by the caller (ptyx_adjoint_dldi).
+template <int N, bool SINGLE, bool EXT>
+__global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
+  constexpr int NT = Geo<N>::NT;
+  constexpr bool LDS = Geo<N>::kLds;
+  constexpr int N2 = N * N;
+  constexpr float inv_n = 1.0f / (float)N;
+  constexpr float inv_n2 = 1.0f / (float)N2;
+  __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
+  __shared__ float s_red[(NT / 64) * 2];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
+  typename ArrayFor<N, LDS>::type arr;
+  if constexpr (LDS) arr.p = s_buf;
+  else {
+    arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
+    arr.b = arr.a + N2;
+  }
+  float2* psi = scratch_psi<N>(a);
+  float2* gacc = psi + (size_t)a.Nz * N2;
+  float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
+  if (a.need_probe)
+    for (int e = threadIdx.x; e < a.P * N2; e += NT) slab[e] = make_float2(0.f, 0.f);
+  __syncthreads();
+
+  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
+    const PatternGeom g = pattern_geom(a, pat, N);
+    float c1 = 0.f, c2 = 0.f;
+    int m = 0;
+    if constexpr (!EXT) {
+      int lo = 0, hi = a.n_batches;  // batch containing pat: boff[m] <= pat < boff[m+1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.boff[mid] <= pat) lo = mid;
+        else hi = mid;
+      }
+      m = lo;
+      c1 = a.coef[(size_t)m * kNCoef + 0];
+      c2 = a.coef[(size_t)m * kNCoef + 1];
+    }
+    if (a.shift) build_ramps<N, NT>(g, s_wy, s_wx);
+    float ds[2] = {0.f, 0.f};
+    const float* Ip = (SINGLE || EXT) ? nullptr : a.Ibuf + (size_t)pat * N2;
+
+    for (int p = 0; p < a.P; ++p) {
+      for (int o = 0; o < a.O; ++o) {
+        const float occ = a.occu[o];
+        const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
+        float dummy = 0.f;
+        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy);
+        // far field → g_Ψ = 2 occ Ψ ∂L/∂I  (left in natural FFT order)
+        fft2d<N, NT, -1, true>(
+            arr, s_tw, [&](int, int, float2 v) { return v; },
+            [&](int y, int x, float2& v) {
+              const float2 Psi = cscale(v, inv_n);
+              const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
+              float dLdI;
+              if constexpr (EXT) {
+                dLdI = a.ext_scale * a.dLdI_ext[(size_t)pat * N2 + e];
+              } else {
+                const float I = SINGLE ? fmaf(occ, cabs2(Psi), kDpEps) : Ip[e];
+                const float M = meas_at(a, g.s, e, N2);
+                const float rI = 1.0f / I;
+                dLdI = 0.f;
+                if (a.single_on) {
+                  const float Iq = powq(I, a.q1), Mq = powq(M, a.q1);
+                  dLdI = c1 * (Iq - Mq) * a.q1 * Iq * rI;
+                }
+                if (a.pois_on) {
+                  const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
+                  dLdI += c2 * (Mq / (Iq + a.eps2) - 1.0f) * a.q2 * Iq * rI;
+                }
+              }
+              v = cscale(Psi, 2.0f * occ * dLdI);
+              return true;
+            });
+        // adjoint of slice n: g_O += conj(ψ^n) g → dA, dφ; g ← g ⊙ conj(O_n)
+        auto slice_adj = [&](int n, int y, int x, float2 gv) -> float2 {
+          const size_t off = obj_off(a, o, n, g.cy + y, g.cx + x);
+          const float A = a.obja[off], ph = a.objp[off];
+          float sn, cs;
+          phase_sincos(ph, &sn, &cs);
+          const float2 Ov = make_float2(A * cs, A * sn);
+          const float2 gO = cmulc(gv, psi[(size_t)n * N2 + y * N + x]);
+          if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));   // Re(g_O e^{-iφ})
+          if (a.d_objp) {
+            float dph = fmaf(gO.y, Ov.x, -gO.x * Ov.y);                          // Im(conj(O) g_O)
+            if (csp != 0.f) {
+              const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
+              dph += a.sparse_n == 1 ? csp * sg : csp * powq(fabsf(ph), (float)(a.sparse_n - 1)) * sg;
+            }
+            atomicAdd(a.d_objp + off, dph);
+          }
+          return cmulc(gv, Ov);
+        };
+        auto acc_probe = [&](int y, int x, float2 gv) {
+          const int e = y * N + x;
+          gacc[e] = (o == 0) ? gv : cadd(gacc[e], gv);
+        };
+        const int Nz = a.Nz;
+        // F_o^-1 (ortho adjoint of F_o, fftshift undone by the index map above)
+        fft2d<N, NT, +1, true>(
+            arr, s_tw, [&](int, int, float2 v) { return v; },
+            [&](int y, int x, float2& v) {
+              const float2 gv = slice_adj(Nz - 1, y, x, cscale(v, inv_n));
+              if (Nz == 1) {
+                acc_probe(y, x, gv);
+                return false;
+              }
+              v = gv;
+              return true;
+            });
+        for (int n = Nz - 2; n >= 0; --n) {  // adjoint of F^-1 H F is F^-1 conj(H) F
+          fft2d<N, NT, -1, true>(
+              arr, s_tw, [&](int, int, float2 v) { return v; },
+              [&](int y, int x, float2& v) {
+                v = cmulc(v, a.H[y * N + x]);
+                return true;
+              });
+          fft2d<N, NT, +1, true>(
+              arr, s_tw, [&](int, int, float2 v) { return v; },
+              [&](int y, int x, float2& v) {
+                const float2 gv = slice_adj(n, y, x, cscale(v, inv_n2));
+                if (n == 0) {
+                  acc_probe(y, x, gv);
+                  return false;
+                }
+                v = gv;
+                return true;
+              });
+        }
+      }
+      // probe mode p: g_{P_b} = Σ_o g (in gacc)
+      if (a.shift) {
+        if (a.need_probe || a.d_shifts) {
+          const float2* Fp = a.Fp + (size_t)p * N2;
+          float2* sl = slab + (size_t)p * N2;
+          fft2d<N, NT, -1, false>(
+              arr, s_tw, [&](int y, int x, float2) { return gacc[y * N + x]; },
+              [&](int y, int x, float2& G) {
+                const int e = y * N + x;
+                const float2 W = cmul(s_wy[y], s_wx[x]);
+                const float2 FW = cmul(Fp[e], W);
+                const float im = cmulc(FW, G).y;  // Im(conj(G) F(P) W)
+                ds[0] = fmaf(6.283185307179586f * shift_g<N>(y), im, ds[0]);
+                ds[1] = fmaf(6.283185307179586f * shift_g<N>(x), im, ds[1]);
+                if (a.need_probe) sl[e] = cadd(sl[e], cmulc(G, W));  // Σ_b conj(W_b) F(g_Pb)
+                return false;
+              });
+        }
+      } else if (a.need_probe) {
+        float2* sl = slab + (size_t)p * N2;
+        for (int e = opaque_tid(); e < N2; e += NT) sl[e] = cadd(sl[e], gacc[e]);
+        __syncthreads();
+      }
+    }
+    if (a.shift && a.d_shifts) {
+      block_sum<NT, 2>(ds, s_red);
+      if (threadIdx.x == 0) {
+        atomicAdd(a.d_shifts + 2 * g.s, ds[0] * inv_n2);
+        atomicAdd(a.d_shifts + 2 * g.s + 1, ds[1] * inv_n2);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Σ over workgroup slabs, fixed order.
+__global__ void k_slab_reduce(const float2* slab, int nwg, long long per, float2* out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= per) return;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int w = 0; w < nwg; ++w) acc = cadd(acc, slab[(long long)w * per + e]);
+  out[e] = acc;
+}
+
+// d_probe[p] += F^-1(G_p) (shift) or G_p (no shift)
+template <int N>
+__global__ __launch_bounds__(Geo<N>::NT) void k_probe_finalize(KArgs a, const float2* G, float2* d_probe) {
+  constexpr int NT = Geo<N>::NT;
+  constexpr bool LDS = Geo<N>::kLds;
+  constexpr int N2 = N * N;
+  constexpr float inv_n2 = 1.0f / (float)N2;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
+  __syncthreads();
+  const int p = blockIdx.x;
+  const float2* Gp = G + (size_t)p * N2;
+  float2* dp = d_probe + (size_t)p * N2;
+  if (!a.shift) {
+    for (int e = opaque_tid(); e < N2; e += NT) dp[e] = cadd(dp[e], Gp[e]);
+    return;
+  }
+  typename ArrayFor<N, LDS>::type arr;
+  if constexpr (LDS) arr.p = s_buf;
+  else {
+    arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
+    arr.b = arr.a + N2;
+  }
+  fft2d<N, NT, +1, false>(
+      arr, s_tw, [&](int y, int x, float2) { return Gp[y * N + x]; },
+      [&](int y, int x, float2& v) {
+        const int e = y * N + x;
+        dp[e] = cadd(dp[e], cscale(v, inv_n2));
+        return false;
+      });
+}
+
+}  // namespace ptyx
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+using namespace ptyx;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(PTYX_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+  int prev = -1, want;
+  explicit DeviceGuard(int d) : want(d) {
+    (void)hipGetDevice(&prev);
+    if (prev != want) (void)hipSetDevice(want);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
+
+struct ptyx_plan {
+  ptyx_dims d;
+  int device = 0;
+  int n_cu = 0;
+  int nwg = 0;  // persistent workgroups for k_forward / k_adjoint
+  float2* twg = nullptr;
+  float2* Fp = nullptr;
+  float* psums = nullptr;
+  float* coef = nullptr;
+  float* Ibuf = nullptr;
+  float2* slab = nullptr;
+  float2* Gsum = nullptr;
+  float2* scratch = nullptr;
+  long long scratch_stride = 0;
+  size_t ws_bytes = 0;
+  std::vector<void*> allocs;
+};
+
+static bool is_supported_n(int n) { return n == 32 || n == 64 || n == 128 || n == 256; }
+
+static int blocks_per_cu(int N) {
+  // LDS-limited residency (160 KiB per CU) of the workgroup-resident FFT kernels
+  switch (N) {
+    case 32: return 8;
+    case 64: return 4;
+    case 128: return 1;
+    default: return 1;
+  }
+}
+
+template <class T>
+static int dalloc(ptyx_plan* pl, T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) return PTYX_OK;
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) return fail(PTYX_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  pl->allocs.push_back(q);
+  pl->ws_bytes += count * sizeof(T);
+  *p = static_cast<T*>(q);
+  return PTYX_OK;
+}
+
+static void free_plan(ptyx_plan* pl) {
+  for (void* q : pl->allocs) (void)hipFree(q);
+  delete pl;
+}
+
+extern "C" int ptyx_version(void) { return 100; }
+
+extern "C" const char* ptyx_last_error(void) { return g_err.c_str(); }
+
+extern "C" size_t ptyx_plan_workspace_bytes(const ptyx_plan* plan) { return plan ? plan->ws_bytes : 0; }
+
+extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int device) {
+  g_err.clear();
+  if (!out || !dims) return fail(PTYX_EINVAL, "null argument");
+  *out = nullptr;
+  const ptyx_dims& d = *dims;
+  if (!is_supported_n(d.N)) return fail(PTYX_EUNSUPPORTED, "N must be one of 32, 64, 128, 256");
+  if (d.P < 1 || d.O < 1 || d.Nz < 1 || d.n_scans < 1 || d.max_patterns < 1)
+    return fail(PTYX_EINVAL, "P, O, Nz, n_scans, max_patterns must be >= 1");
+  if (d.O > kMaxModesO) return fail(PTYX_EUNSUPPORTED, "at most 8 object modes");
+  if (d.Ny < d.N || d.Nx < d.N) return fail(PTYX_EINVAL, "object smaller than the probe window");
+  DeviceGuard dg(device);
+  int cu = 0;
+  hipError_t e = hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+  auto* pl = new ptyx_plan();
+  pl->d = d;
+  pl->device = device;
+  pl->n_cu = cu;
+  pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * blocks_per_cu(d.N)));
+  const size_t N2 = (size_t)d.N * d.N;
+  const bool lds = d.N <= 128;
+  pl->scratch_stride = (long long)((lds ? 0 : 2 * N2) + (size_t)d.Nz * N2 + N2);
+  int rc = PTYX_OK;
+  const bool multi = (d.P * d.O) > 1;
+  if ((rc = dalloc(pl, &pl->twg, d.N)) || (rc = dalloc(pl, &pl->Fp, d.P * N2)) ||
+      (rc = dalloc(pl, &pl->psums, (size_t)d.max_patterns * kNSum)) ||
+      (rc = dalloc(pl, &pl->coef, (size_t)d.max_patterns * kNCoef)) ||
+      (rc = dalloc(pl, &pl->Ibuf, multi ? (size_t)d.max_patterns * N2 : 0)) ||
+      (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
+      (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
+      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride))) {
+    free_plan(pl);
+    return rc;
+  }
+  // fp64 twiddles rounded once to fp32: tw[m] = exp(-2πi m/N)
+  std::vector<float2> tw(d.N);
+  for (int m = 0; m < d.N; ++m) {
+    const double ang = -2.0 * M_PI * (double)m / (double)d.N;
+    tw[m] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  }
+  e = hipMemcpy(pl->twg, tw.data(), sizeof(float2) * d.N, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    free_plan(pl);
+    return hip_fail(e, "hipMemcpy twiddles");
+  }
+  *out = pl;
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_plan_destroy(ptyx_plan* plan) {
+  if (!plan) return PTYX_OK;
+  DeviceGuard dg(plan->device);
+  free_plan(plan);
+  return PTYX_OK;
+}
+
+static int check_inputs(const ptyx_plan* pl, const ptyx_inputs* in, bool need_meas) {
+  if (!in) return fail(PTYX_EINVAL, "inputs is null");
+  if (!in->obja || !in->objp || !in->probe || !in->shifts || !in->omode_occu || !in->crop_pos)
+    return fail(PTYX_EINVAL, "a required input pointer is null");
+  if (pl->d.Nz > 1 && !in->H) return fail(PTYX_EINVAL, "H is required for Nz > 1");
+  if (need_meas && !in->meas) return fail(PTYX_EINVAL, "meas is null");
+  return PTYX_OK;
+}
+
+static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, int n_idx) {
+  KArgs a{};
+  const ptyx_dims& d = pl->d;
+  a.P = d.P; a.O = d.O; a.Nz = d.Nz; a.Ny = d.Ny; a.Nx = d.Nx; a.n_scans = d.n_scans;
+  a.shift = (d.flags & PTYX_SHIFT_PROBES) ? 1 : 0;
+  a.meas_f16 = (d.flags & PTYX_MEAS_F16) ? 1 : 0;
+  a.obja = in->obja; a.objp = in->objp;
+  a.probe = reinterpret_cast<const float2*>(in->probe);
+  a.Fp = pl->Fp;
+  a.shifts = in->shifts; a.crop = in->crop_pos;
+  a.H = reinterpret_cast<const float2*>(in->H);
+  a.occu = in->omode_occu; a.meas = in->meas;
+  a.idx = idx; a.n_idx = n_idx;
+  a.Ibuf = pl->Ibuf;
+  a.slab = pl->slab; a.scratch = pl->scratch; a.scratch_stride = pl->scratch_stride;
+  a.twg = pl->twg;
+  return a;
+}
+
+template <int N>
+static void launch_spectrum(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_probe_spectrum<N>, dim3(pl->d.P), dim3(Geo<N>::NT), 0, st, a, pl->Fp);
+}
+template <int N>
+static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  const int grid = std::max(1, std::min(a.n_idx, pl->nwg));
+  if (pl->d.P * pl->d.O == 1)
+    hipLaunchKernelGGL((k_forward<N, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_forward<N, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+}
+template <int N>
+static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, bool ext) {
+  const int grid = pl->nwg;  // every workgroup zeroes its slab, so launch all of them
+  const bool single = pl->d.P * pl->d.O == 1;
+  if (ext)
+    hipLaunchKernelGGL((k_adjoint<N, false, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+  else if (single)
+    hipLaunchKernelGGL((k_adjoint<N, true, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_adjoint<N, false, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+}
+template <int N>
+static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe) {
+  const long long per = (long long)pl->d.P * N * N;
+  const int tb = 256;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + tb - 1) / tb)), dim3(tb), 0, st, pl->slab, pl->nwg,
+                     per, pl->Gsum);
+  hipLaunchKernelGGL(k_probe_finalize<N>, dim3(pl->d.P), dim3(Geo<N>::NT), 0, st, a, pl->Gsum,
+                     reinterpret_cast<float2*>(d_probe));
+}
+
+// PTYX_ONLY_N=<n> builds a single size (kernel experiments); the shipped library has all four.
+#ifdef PTYX_ONLY_N
+#define PTYX_DISPATCH_N(N_, FN, ...) \
+  if ((N_) == PTYX_ONLY_N) FN<PTYX_ONLY_N>(__VA_ARGS__);
+#else
+#define PTYX_DISPATCH_N(N_, FN, ...)                     \
+  switch (N_) {                                          \
+    case 32: FN<32>(__VA_ARGS__); break;                 \
+    case 64: FN<64>(__VA_ARGS__); break;                 \
+    case 128: FN<128>(__VA_ARGS__); break;               \
+    case 256: FN<256>(__VA_ARGS__); break;               \
+  }
+#endif
+
+static int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, what);
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx, int32_t n_idx,
+                            float* dp_out) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  int rc = check_inputs(pl, in, false);
+  if (rc) return rc;
+  if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
+  if (n_idx == 0) return PTYX_OK;
+  if (!idx || !dp_out) return fail(PTYX_EINVAL, "idx / dp_out is null");
+  DeviceGuard dg(pl->device);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  KArgs a = make_args(pl, in, idx, n_idx);
+  a.dp_out = dp_out;
+  a.psums = nullptr;
+  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+  return launch_status("ptyx_forward launch");
+}
+
+extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
+                                      const int32_t* boff, int32_t n_batches, int32_t n_idx,
+                                      const ptyx_loss_cfg* cfg, float* loss_terms, float* dp_out,
+                                      const ptyx_grads* grads) {
+  g_err.clear();
+  if (!pl || !cfg) return fail(PTYX_EINVAL, "plan / cfg is null");
+  int rc = check_inputs(pl, in, true);
+  if (rc) return rc;
+  if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
+  if (n_batches < 1 || n_batches > n_idx) return fail(PTYX_EINVAL, "need 1 <= n_batches <= n_idx");
+  if (!idx || !boff) return fail(PTYX_EINVAL, "idx / batch_offsets is null");
+  if (!cfg->single_on && !cfg->poissn_on)
+    return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
+  if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
+  DeviceGuard dg(pl->device);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  KArgs a = make_args(pl, in, idx, n_idx);
+  a.boff = boff;
+  a.n_batches = n_batches;
+  a.single_on = cfg->single_on;
+  a.pois_on = cfg->poissn_on;
+  a.sparse_on = cfg->sparse_on;
+  a.sparse_n = cfg->sparse_n;
+  a.q1 = cfg->single_q;
+  a.q2 = cfg->poissn_q;
+  a.eps2 = cfg->poissn_eps;
+  a.psums = pl->psums;
+  a.coef = pl->coef;
+  a.dp_out = dp_out;
+  ptyx_grads gz{};
+  if (grads) gz = *grads;
+  a.d_obja = gz.d_obja;
+  a.d_objp = gz.d_objp;
+  a.d_shifts = gz.d_shifts;
+  a.need_probe = gz.d_probe != nullptr;
+
+  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+  if ((rc = launch_status("k_forward launch"))) return rc;
+  FinArgs f{};
+  f.boff = boff; f.n_batches = n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
+  f.psums = pl->psums; f.occu = in->omode_occu;
+  f.single_on = cfg->single_on; f.pois_on = cfg->poissn_on; f.sparse_on = cfg->sparse_on;
+  f.sparse_n = cfg->sparse_n; f.w1 = cfg->single_w; f.w2 = cfg->poissn_w; f.ws = cfg->sparse_w;
+  f.grad_scale = cfg->grad_scale; f.coef = pl->coef; f.loss_terms = loss_terms;
+  hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
+  if ((rc = launch_status("k_finalize launch"))) return rc;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
+  if (!any_grad) return PTYX_OK;
+  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
+  if ((rc = launch_status("k_adjoint launch"))) return rc;
+  if (gz.d_probe) {
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe);
+    if ((rc = launch_status("probe finalize launch"))) return rc;
+  }
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
+                                 int32_t n_idx, const float* dLdI, float grad_scale, const ptyx_grads* grads) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  int rc = check_inputs(pl, in, false);
+  if (rc) return rc;
+  if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
+  if (n_idx == 0 || !grads) return PTYX_OK;
+  if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
+  const ptyx_grads gz = *grads;
+  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts)) return PTYX_OK;
+  DeviceGuard dg(pl->device);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  KArgs a = make_args(pl, in, idx, n_idx);
+  a.dLdI_ext = dLdI;
+  a.ext_scale = grad_scale;
+  a.d_obja = gz.d_obja;
+  a.d_objp = gz.d_objp;
+  a.d_shifts = gz.d_shifts;
+  a.need_probe = gz.d_probe != nullptr;
+  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, true);
+  if ((rc = launch_status("k_adjoint(ext) launch"))) return rc;
+  if (gz.d_probe) {
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe);
+    if ((rc = launch_status("probe finalize launch"))) return rc;
+  }
+  return PTYX_OK;
+}

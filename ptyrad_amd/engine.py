@@ -1,0 +1,195 @@
+"""Torch-tensor front end of the C ABI (include/ptyx.h): plans, argument marshalling, streams.
+
+All tensors passed here must already live on the plan's device (HBM-resident inputs); the
+engine never copies data between host and device and never synchronises the stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+LOSS_TERM_NAMES = ("loss_single", "loss_poissn", "loss_pacbed", "loss_sparse", "loss_simlar")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _need(t, dtype, name, device):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+@dataclass
+class LossConfig:
+    """Hot-path subset of PtyRAD's loss_params (src/ptyrad/params/loss_params.py)."""
+    single_on: bool = True
+    single_w: float = 1.0
+    single_q: float = 0.5
+    poissn_on: bool = False
+    poissn_w: float = 1.0
+    poissn_q: float = 1.0
+    poissn_eps: float = 1e-6
+    sparse_on: bool = True
+    sparse_w: float = 0.1
+    sparse_n: int = 1
+
+    @classmethod
+    def from_loss_params(cls, lp: dict) -> "LossConfig":
+        for k in ("loss_pacbed", "loss_simlar"):
+            if lp.get(k, {}).get("state", False):
+                raise NotImplementedError(f"{k} is not on the fused HIP path; use the generic "
+                                          "(autograd) path of ptyrad_amd.losses.CombinedLoss")
+        s, p, sp = lp["loss_single"], lp["loss_poissn"], lp["loss_sparse"]
+        return cls(bool(s["state"]), float(s.get("weight", 1.0)), float(s.get("dp_pow", 0.5)),
+                   bool(p["state"]), float(p.get("weight", 1.0)), float(p.get("dp_pow", 1.0)),
+                   float(p.get("eps", 1e-6)),
+                   bool(sp["state"]), float(sp.get("weight", 0.1)), int(sp.get("ln_order", 1)))
+
+    def to_c(self, grad_scale: float) -> _lib.LossCfg:
+        return _lib.LossCfg(int(self.single_on), self.single_w, self.single_q,
+                            int(self.poissn_on), self.poissn_w, self.poissn_q, self.poissn_eps,
+                            int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale))
+
+
+class Plan:
+    """One ptyx_plan: fixed device and geometry (N, P, O, Nz, object extent, n_scans)."""
+
+    def __init__(self, N, P, O, Nz, Ny, Nx, n_scans, max_patterns, shift_probes=True,
+                 meas_f16=False, device=None):
+        self.lib = _lib.load()
+        device = torch.device(device if device is not None else "cuda")
+        if device.type != "cuda":
+            raise ValueError("ptyx plans need a HIP device (torch 'cuda' device on ROCm)")
+        self.device = torch.device("cuda", device.index if device.index is not None
+                                   else torch.cuda.current_device())
+        flags = (_lib.PTYX_SHIFT_PROBES if shift_probes else 0) | (_lib.PTYX_MEAS_F16 if meas_f16 else 0)
+        self.dims = _lib.Dims(int(N), int(P), int(O), int(Nz), int(Ny), int(Nx), int(n_scans),
+                              int(max_patterns), flags)
+        self.shift_probes = bool(shift_probes)
+        self.meas_f16 = bool(meas_f16)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(self.dims), self.device.index))
+        self._h = h
+
+    @property
+    def workspace_bytes(self) -> int:
+        return int(self.lib.ptyx_plan_workspace_bytes(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.ptyx_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ marshalling
+    def _inputs(self, obja, objp, probe_rv, shifts, H, occu, crop_pos, meas):
+        d, dev = self.dims, self.device
+        _need(obja, torch.float32, "obja", dev)
+        _need(objp, torch.float32, "objp", dev)
+        _need(probe_rv, torch.float32, "probe", dev)
+        _need(shifts, torch.float32, "shifts", dev)
+        _need(occu, torch.float32, "omode_occu", dev)
+        _need(crop_pos, torch.int32, "crop_pos", dev)
+        if tuple(obja.shape) != (d.O, d.Nz, d.Ny, d.Nx) or obja.shape != objp.shape:
+            raise ValueError(f"object shape {tuple(obja.shape)} != {(d.O, d.Nz, d.Ny, d.Nx)}")
+        if tuple(probe_rv.shape) != (d.P, d.N, d.N, 2):
+            raise ValueError(f"probe shape {tuple(probe_rv.shape)} != {(d.P, d.N, d.N, 2)}")
+        if tuple(shifts.shape) != (d.n_scans, 2) or tuple(crop_pos.shape) != (d.n_scans, 2):
+            raise ValueError("shifts / crop_pos must be (n_scans, 2)")
+        if H is not None:
+            if H.dtype == torch.complex64:
+                H = torch.view_as_real(H)
+            _need(H, torch.float32, "H", dev)
+            if tuple(H.shape) != (d.N, d.N, 2):
+                raise ValueError("H must be (N, N) complex64")
+        if meas is not None:
+            _need(meas, torch.float16 if self.meas_f16 else torch.float32, "meas", dev)
+            if tuple(meas.shape) != (d.n_scans, d.N, d.N):
+                raise ValueError(f"meas shape {tuple(meas.shape)} != {(d.n_scans, d.N, d.N)}")
+        inp = _lib.Inputs(_ptr(obja), _ptr(objp), _ptr(probe_rv), _ptr(shifts), _ptr(H), _ptr(occu),
+                          _ptr(crop_pos), _ptr(meas))
+        return inp, H
+
+    def _idx(self, idx):
+        if isinstance(idx, torch.Tensor) and idx.device == self.device and idx.dtype == torch.int32:
+            return idx.contiguous()
+        return torch.as_tensor(np.asarray(idx.cpu() if isinstance(idx, torch.Tensor) else idx),
+                               dtype=torch.int32).to(self.device, non_blocking=True)
+
+    def _grads(self, grads: dict | None):
+        grads = grads or {}
+        d, dev = self.dims, self.device
+        for k, shape in (("obja", (d.O, d.Nz, d.Ny, d.Nx)), ("objp", (d.O, d.Nz, d.Ny, d.Nx)),
+                         ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2))):
+            g = grads.get(k)
+            if g is not None:
+                _need(g, torch.float32, f"grad {k}", dev)
+                if tuple(g.shape) != shape:
+                    raise ValueError(f"grad {k} shape {tuple(g.shape)} != {shape}")
+        return _lib.Grads(_ptr(grads.get("obja")), _ptr(grads.get("objp")), _ptr(grads.get("probe")),
+                          _ptr(grads.get("shifts")))
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ entry points
+    def forward(self, t: dict, idx, dp_out=None):
+        """ptyx_forward: dp (n, N, N) f32 = PtychoAD.forward(idx)."""
+        idx_t = self._idx(idx)
+        n = int(idx_t.numel())
+        if dp_out is None:
+            dp_out = torch.empty((n, self.dims.N, self.dims.N), dtype=torch.float32, device=self.device)
+        inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
+                                  t["crop_pos"], None)
+        _lib.check(self.lib.ptyx_forward(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t), n,
+                                         _ptr(dp_out)))
+        return dp_out
+
+    def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
+                          grad_scale: float = 1.0, loss_terms=None, dp_out=None):
+        """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5)."""
+        idx_t = self._idx(idx)
+        off_t = self._idx(batch_offsets)
+        n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
+        if loss_terms is None:
+            loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
+        inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
+                                  t["crop_pos"], t["meas"])
+        cfg = loss_cfg.to_c(grad_scale)
+        g = self._grads(grads)
+        _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
+                                                   _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
+                                                   _ptr(dp_out), ctypes.byref(g)))
+        return loss_terms
+
+    def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):
+        """ptyx_adjoint_dldi: accumulate gradients for an external dL/d(dp)."""
+        idx_t = self._idx(idx)
+        n = int(idx_t.numel())
+        _need(dLdI, torch.float32, "dLdI", self.device)
+        inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
+                                  t["crop_pos"], None)
+        g = self._grads(grads)
+        _lib.check(self.lib.ptyx_adjoint_dldi(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t), n,
+                                              _ptr(dLdI), float(grad_scale), ctypes.byref(g)))
+
+
+def batch_offsets(batches) -> np.ndarray:
+    """[0, len(b0), len(b0)+len(b1), ...] for a list of index arrays (reference make_batches output)."""
+    sizes = [len(b) for b in batches]
+    return np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)

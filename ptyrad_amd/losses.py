@@ -1,0 +1,119 @@
+"""CombinedLoss — drop-in for PtyRAD's ``CombinedLoss`` (src/ptyrad/losses.py:17-155).
+
+``forward(model_DP, measured_DP, object_patches, omode_occu) -> (total, [5 terms])`` keeps the
+reference signature and runs in torch on the engine's dp (generic path; the dp's backward runs
+the HIP adjoint).  ``fused(model, batches)`` is the hot path: one ptyx_forward_loss_grad call
+computes dp, the loss terms of every mini-batch and all gradients on the GPU, and returns a
+loss tensor whose backward hands those gradients to autograd.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .engine import LOSS_TERM_NAMES, LossConfig, batch_offsets
+
+
+class _FusedLoss(torch.autograd.Function):
+    """Σ_m loss_m over mini-batches; backward = cached engine gradients × grad_output."""
+
+    @staticmethod
+    def forward(ctx, obja, objp, probe_rv, shifts, model, idx_t, off_t, cfg):
+        want = {"obja": obja.requires_grad, "objp": objp.requires_grad, "probe": probe_rv.requires_grad,
+                "shifts": shifts.requires_grad and model.shift_probes}
+        grads = {}
+        for k, p in (("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts)):
+            if want[k]:
+                grads[k] = torch.zeros_like(p)
+        terms = model.plan.forward_loss_grad(model._engine_tensors(), idx_t, off_t, cfg, grads, grad_scale=1.0)
+        ctx.grads = grads
+        ctx.shift_req = shifts.requires_grad
+        total = terms.sum()
+        ctx.mark_non_differentiable(terms)
+        return total, terms
+
+    @staticmethod
+    def backward(ctx, g_total, g_terms):
+        out = []
+        for k in ("obja", "objp", "probe", "shifts"):
+            g = ctx.grads.get(k)
+            out.append(None if g is None else g * g_total)
+        ctx.grads = None
+        return out[0], out[1], out[2], out[3], None, None, None, None
+
+
+class CombinedLoss(torch.nn.Module):
+    """Same loss_params dict and call signature as the reference CombinedLoss."""
+
+    def __init__(self, loss_params, device="cuda"):
+        super().__init__()
+        self.device = device
+        self.loss_params = loss_params
+
+    # ---------------------------------------------------------------- generic (torch) path
+    def get_loss_single(self, model_DP, measured_DP):           # losses.py:36-50
+        p = self.loss_params["loss_single"]
+        if not p["state"]:
+            return torch.tensor(0.0, device=model_DP.device)
+        q = p.get("dp_pow", 0.5)
+        mq = measured_DP.pow(q)
+        return p["weight"] * torch.sqrt(torch.mean((model_DP.pow(q) - mq) ** 2)) / mq.mean()
+
+    def get_loss_poissn(self, model_DP, measured_DP):           # losses.py:52-75
+        p = self.loss_params["loss_poissn"]
+        if not p["state"]:
+            return torch.tensor(0.0, device=model_DP.device)
+        q, eps = p.get("dp_pow", 1.0), p.get("eps", 1e-6)
+        mq, iq = measured_DP.pow(q), model_DP.pow(q)
+        return -p["weight"] * torch.mean(mq * torch.log(iq + eps) - iq) / mq.mean()
+
+    def get_loss_pacbed(self, model_DP, measured_DP):           # losses.py:77-89
+        p = self.loss_params["loss_pacbed"]
+        if not p["state"]:
+            return torch.tensor(0.0, device=model_DP.device)
+        q = p.get("dp_pow", 0.2)
+        d = model_DP.mean(0).pow(q) - measured_DP.mean(0).pow(q)
+        return p["weight"] * torch.sqrt(torch.mean(d * d)) / measured_DP.pow(q).mean()
+
+    def get_loss_sparse(self, objp_patches, omode_occu):        # losses.py:91-104
+        p = self.loss_params["loss_sparse"]
+        if not p["state"]:
+            return torch.tensor(0.0, device=objp_patches.device)
+        n = p["ln_order"]
+        m = torch.mean(objp_patches.abs().pow(n), dim=(0, 2, 3, 4))
+        return p["weight"] * (m.pow(1.0 / n) * omode_occu).sum()
+
+    def get_loss_simlar(self, object_patches, omode_occu):      # losses.py:106-141
+        p = self.loss_params.get("loss_simlar", {"state": False})
+        if not p["state"]:
+            return torch.tensor(0.0, device=object_patches.device)
+        raise NotImplementedError("loss_simlar (needs torchvision gaussian_blur) is outside the hot path")
+
+    def forward(self, model_DP, measured_DP, object_patches, omode_occu):
+        losses = [self.get_loss_single(model_DP, measured_DP),
+                  self.get_loss_poissn(model_DP, measured_DP),
+                  self.get_loss_pacbed(model_DP, measured_DP),
+                  self.get_loss_sparse(object_patches[..., 1], omode_occu),
+                  self.get_loss_simlar(object_patches, omode_occu)]
+        return sum(losses), losses
+
+    # ---------------------------------------------------------------- fused HIP path
+    def fused(self, model, batches):
+        """Forward + loss + adjoint of every mini-batch in ``batches`` in one engine call.
+
+        Returns (Σ_m total_m as a differentiable scalar, terms (n_batches, 5) tensor).
+        ``(loss / grad_accumulation).backward()`` then leaves exactly the reference's accumulated
+        gradients (reconstruction.py:741-760) in ``.grad``.
+        """
+        cfg = LossConfig.from_loss_params(self.loss_params)
+        flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
+        model._check_indices(flat)
+        dev = model.opt_obja.device
+        idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
+        off_t = torch.as_tensor(batch_offsets(batches)).to(dev, non_blocking=True)
+        total, terms = _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe,
+                                        model.opt_probe_pos_shifts, model, idx_t, off_t, cfg)
+        return total, terms
+
+
+__all__ = ["CombinedLoss", "LOSS_TERM_NAMES"]

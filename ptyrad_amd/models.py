@@ -1,0 +1,233 @@
+"""PtychoHIP — drop-in for PtyRAD's ``PtychoAD`` (src/ptyrad/models.py:30-436) on the HIP engine.
+
+Same constructor (``init_variables``, ``model_params``, ``device``, ``verbose``), same
+optimisable parameters (``opt_obja``, ``opt_objp``, ``opt_probe`` as a real view,
+``opt_probe_pos_shifts``, ``opt_obj_tilts``, ``opt_slice_thickness``), buffers and bookkeeping
+lists, so ``recon_step``, ``CombinedConstraint``, ``make_save_dict`` and the plotting code that
+read a PtychoAD find what they expect.  The forward model and its gradients run in
+``libptyx.so`` (include/ptyx.h); there is no torch fallback for them.
+
+Two ways to get gradients:
+* generic   — ``dp = model(indices)`` is differentiable: its backward runs ptyx_adjoint_dldi with
+              whatever dL/d(dp) a downstream torch loss produced (any loss, incl. pacbed/simlar);
+* fused     — ``ptyrad_amd.losses.CombinedLoss.fused(model, batches)`` runs forward + loss +
+              adjoint in one engine call (ptyx_forward_loss_grad), the hot path.
+
+Out of scope on the HIP path (raise NotImplementedError when enabled): tilted / optimised-dz
+propagators (models.py:339-356), detector blur (:379-380), object pre-blur (:275-284),
+on-the-fly measurement padding / resampling (:392-409).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .engine import Plan
+
+_PARAM_NAMES = ("obja", "objp", "obj_tilts", "slice_thickness", "probe", "probe_pos_shifts")
+
+
+class _EngineForward(torch.autograd.Function):
+    """dp = PtychoAD.forward(idx); backward = ptyx_adjoint_dldi (autograd of models.py:422-436)."""
+
+    @staticmethod
+    def forward(ctx, obja, objp, probe_rv, shifts, model, idx_t):
+        ctx.model = model
+        ctx.save_for_backward(idx_t)
+        with torch.no_grad():
+            return model.plan.forward(model._engine_tensors(), idx_t)
+
+    @staticmethod
+    def backward(ctx, grad_dp):
+        (idx_t,) = ctx.saved_tensors
+        m = ctx.model
+        want = ctx.needs_input_grad
+        grads = {}
+        outs = [None] * 4
+        for i, (k, p) in enumerate((("obja", m.opt_obja), ("objp", m.opt_objp),
+                                    ("probe", m.opt_probe), ("shifts", m.opt_probe_pos_shifts))):
+            if want[i]:
+                outs[i] = torch.zeros_like(p)
+                grads[k] = outs[i]
+        if not m.shift_probes:
+            grads.pop("shifts", None)
+            if want[3]:
+                outs[3] = torch.zeros_like(m.opt_probe_pos_shifts)
+        if grads:
+            m.plan.adjoint_dldi(m._engine_tensors(), idx_t, grad_dp.contiguous().float(), grads)
+        return outs[0], outs[1], outs[2], outs[3], None, None
+
+
+class PtychoHIP(nn.Module):
+    """Optimisable ptychography model whose forward/adjoint run on the MI355X engine."""
+
+    def __init__(self, init_variables, model_params, device="cuda", verbose=True, max_patterns=None):
+        super().__init__()
+        with torch.no_grad():
+            self.device = device
+            self.verbose = verbose
+            self.detector_blur_std = model_params.get("detector_blur_std")
+            self.obj_preblur_std = model_params.get("obj_preblur_std")
+            if self.detector_blur_std not in (None, 0) or self.obj_preblur_std not in (None, 0):
+                raise NotImplementedError("detector_blur_std / obj_preblur_std are not on the HIP path")
+            if init_variables.get("on_the_fly_meas_padded") is not None or \
+                    init_variables.get("on_the_fly_meas_scale_factors") is not None:
+                raise NotImplementedError("on-the-fly measurement padding/resampling is not on the HIP path")
+            self.meas_padded = None
+            self.meas_scale_factors = None
+            start_iter, lrs = {}, {}
+            for k, p in model_params["update_params"].items():
+                start_iter[k] = p["start_iter"]
+                lrs[k] = p["lr"]
+            self.optimizer_params = model_params.get("optimizer_params", {"name": "Adam", "configs": {}})
+            self.start_iter = start_iter
+            self.lr_params = lrs
+
+            obj = np.asarray(init_variables["obj"])
+            if "obja" in init_variables:          # exact amplitude / phase (fixtures, resume)
+                obja = np.asarray(init_variables["obja"], np.float32)
+                objp = np.asarray(init_variables["objp"], np.float32)
+            else:                                  # models.py:99-100 (abs / angle of complex64)
+                o = torch.tensor(obj.astype(np.complex64))
+                obja, objp = o.abs().numpy(), o.angle().numpy()
+            self.opt_obja = nn.Parameter(torch.tensor(obja, dtype=torch.float32, device=device))
+            self.opt_objp = nn.Parameter(torch.tensor(objp, dtype=torch.float32, device=device))
+            self.opt_obj_tilts = nn.Parameter(torch.tensor(np.asarray(init_variables.get("obj_tilts", [[0.0, 0.0]])),
+                                                           dtype=torch.float32, device=device))
+            self.opt_slice_thickness = nn.Parameter(torch.tensor(init_variables.get("slice_thickness", 1.0),
+                                                                 dtype=torch.float32, device=device))
+            probe = torch.tensor(np.asarray(init_variables["probe"]).astype(np.complex64), device=device)
+            self.opt_probe = nn.Parameter(torch.view_as_real(probe).contiguous())
+            self.opt_probe_pos_shifts = nn.Parameter(torch.tensor(np.asarray(init_variables["probe_pos_shifts"]),
+                                                                  dtype=torch.float32, device=device))
+            self.register_buffer("omode_occu", torch.tensor(np.asarray(init_variables["omode_occu"]),
+                                                            dtype=torch.float32, device=device))
+            self.register_buffer("H", torch.tensor(np.asarray(init_variables["H"]).astype(np.complex64), device=device))
+            meas = init_variables.get("measurements")
+            meas_dtype = torch.float16 if (meas is not None and np.asarray(meas).dtype == np.float16) else torch.float32
+            self.register_buffer("measurements", None if meas is None else
+                                 torch.as_tensor(np.asarray(meas)).to(device=device, dtype=meas_dtype))
+            for k, dt in (("N_scan_slow", torch.int32), ("N_scan_fast", torch.int32)):
+                self.register_buffer(k, torch.tensor(init_variables.get(k, 0), dtype=dt, device=device))
+            self.register_buffer("crop_pos", torch.tensor(np.asarray(init_variables["crop_pos"]), dtype=torch.int32,
+                                                          device=device))
+            for k in ("slice_thickness", "dx", "dk", "lambd"):
+                self.register_buffer(k, torch.tensor(float(init_variables.get(k, 0.0)), dtype=torch.float32,
+                                                     device=device))
+            self.scan_affine = init_variables.get("scan_affine")
+            self.tilt_obj = bool(self.lr_params.get("obj_tilts", 0) != 0 or torch.any(self.opt_obj_tilts))
+            self.shift_probes = bool(self.lr_params.get("probe_pos_shifts", 0) != 0)   # models.py:120
+            self.change_thickness = bool(self.lr_params.get("slice_thickness", 0) != 0)
+            if self.tilt_obj or self.change_thickness:
+                raise NotImplementedError("tilted / optimised-thickness propagators are not on the HIP path")
+            self.probe_int_sum = self.get_complex_probe_view().abs().pow(2).sum()
+            self.loss_iters, self.iter_times, self.dz_iters, self.avg_tilt_iters = [], [], [], []
+            self._current_object_patches = None
+            self.optimizable_tensors = {
+                "obja": self.opt_obja, "objp": self.opt_objp, "obj_tilts": self.opt_obj_tilts,
+                "slice_thickness": self.opt_slice_thickness, "probe": self.opt_probe,
+                "probe_pos_shifts": self.opt_probe_pos_shifts}
+            self.create_optimizable_params_dict(self.lr_params, verbose)
+            self._validate_geometry()
+            O, Nz, Ny, Nx = self.opt_obja.shape
+            P, N = self.opt_probe.shape[0], self.opt_probe.shape[1]
+            n_scans = self.crop_pos.shape[0]
+            self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or n_scans,
+                             shift_probes=self.shift_probes, meas_f16=(meas_dtype == torch.float16),
+                             device=device)
+
+    # ------------------------------------------------------------------ reference API
+    def get_complex_probe_view(self):
+        return torch.view_as_complex(self.opt_probe)
+
+    def create_optimizable_params_dict(self, lr_params, verbose=True):
+        """models.py:187-208: requires_grad from lr, Adam param groups with per-tensor lr."""
+        self.lr_params = lr_params
+        self.optimizable_params = []
+        for name, lr in lr_params.items():
+            if name not in self.optimizable_tensors:
+                raise ValueError(f"'{name}' is not a valid parameter name; choose from {list(_PARAM_NAMES)}")
+            self.optimizable_tensors[name].requires_grad = (lr != 0)
+            if lr != 0:
+                self.optimizable_params.append({"params": [self.optimizable_tensors[name]], "lr": lr})
+
+    def _validate_geometry(self):
+        N = self.opt_probe.shape[1]
+        Ny, Nx = self.opt_obja.shape[-2:]
+        cp = self.crop_pos.detach().cpu().numpy()
+        if cp.size and (cp.min() < 0 or cp[:, 0].max() > Ny - N or cp[:, 1].max() > Nx - N):
+            raise ValueError("crop_pos places a probe window outside the object")
+
+    def _check_indices(self, indices):
+        idx = np.asarray(indices.cpu() if isinstance(indices, torch.Tensor) else indices).reshape(-1)
+        if idx.size and (idx.min() < 0 or idx.max() >= self.crop_pos.shape[0]):
+            raise IndexError("scan index out of range")
+        return idx
+
+    def _engine_tensors(self):
+        return {"obja": self.opt_obja.detach(), "objp": self.opt_objp.detach(),
+                "probe": self.opt_probe.detach(), "shifts": self.opt_probe_pos_shifts.detach(),
+                "H": self.H, "occu": self.omode_occu, "crop_pos": self.crop_pos,
+                "meas": self.measurements}
+
+    def get_obj_patches(self, indices):
+        """models.py:251-273 (torch gather, for losses that need the patches themselves)."""
+        idx = torch.as_tensor(self._check_indices(indices), device=self.opt_obja.device, dtype=torch.long)
+        N = self.opt_probe.shape[1]
+        r = torch.arange(N, device=self.opt_obja.device)
+        cp = self.crop_pos[idx].long()
+        gy = (cp[:, 0, None, None] + r[None, :, None]).expand(-1, N, N)
+        gx = (cp[:, 1, None, None] + r[None, None, :]).expand(-1, N, N)
+        a = self.opt_obja[:, :, gy, gx].permute(2, 0, 1, 3, 4)
+        p = self.opt_objp[:, :, gy, gx].permute(2, 0, 1, 3, 4)
+        return torch.stack([a, p], dim=-1)
+
+    def get_probes(self, indices):
+        """models.py:286-298 (torch restatement; not on the hot path)."""
+        probe = self.get_complex_probe_view()
+        idx = self._check_indices(indices)
+        if not self.shift_probes:
+            return torch.broadcast_to(probe, (len(idx), *probe.shape))
+        N = probe.shape[-1]
+        g = torch.remainder(torch.arange(N, device=probe.device) + N // 2, N).float() / N
+        s = self.opt_probe_pos_shifts[torch.as_tensor(idx, device=probe.device)]
+        w = torch.exp(-2j * torch.pi * (s[:, 0, None, None] * g[None, :, None] + s[:, 1, None, None] * g[None, None, :]))
+        return torch.fft.ifft2(torch.fft.fft2(probe)[None] * w[:, None])
+
+    def get_propagators(self, indices):
+        return self.H[None,]
+
+    def get_propagated_probe(self, index):
+        probe = self.get_probes(index)[0].detach()
+        H = self.H[None]
+        n_slices = self.opt_objp.shape[1]
+        out = torch.zeros((n_slices, *probe.shape), dtype=probe.dtype, device=probe.device)
+        psi = probe
+        for n in range(n_slices):
+            out[n] = psi
+            psi = torch.fft.ifft2(H[None] * torch.fft.fft2(psi))
+        return out
+
+    def get_measurements(self, indices=None):
+        """models.py:384-416 (no on-the-fly padding / resampling)."""
+        if indices is None:
+            return self.measurements
+        idx = torch.as_tensor(self._check_indices(indices), device=self.measurements.device, dtype=torch.long)
+        return self.measurements[idx].float()
+
+    def clear_cache(self):
+        self._current_object_patches = None
+
+    def forward(self, indices):
+        """models.py:422-436: dp_fwd (B,N,N) f32 from the HIP engine, differentiable."""
+        idx = self._check_indices(indices)
+        idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device, non_blocking=True)
+        dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
+                                  self, idx_t)
+        # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
+        self._current_object_patches = self.get_obj_patches(idx)
+        return dp
+
+
+PtychoAD = PtychoHIP   # name the reference's callers import

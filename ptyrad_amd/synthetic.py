@@ -193,8 +193,10 @@ def random_problem(n: int, n_slow: int, n_fast: int, P: int = 1, O: int = 1, Nz:
     objp = (0.1 * rng.standard_normal((O, Nz) + scan.obj_shape)).astype(np.float32)
     n_scans = n_slow * n_fast
     if meas == "uniform":
-        m = rng.random((n_scans, n, n), dtype=np.float32)
-    else:
-        m = np.zeros((n_scans, n, n), np.float32)
+        m = rng.random((n_scans, n, n), dtype=np.float32).astype(meas_dtype)
+    elif meas == "zeros":
+        m = np.zeros((n_scans, n, n), meas_dtype)
+    else:                      # "none": caller provides measurements (e.g. generated on the GPU)
+        m = None
     return Problem(obja, objp, probe, H, omode_occupancy(O), scan.crop_pos, scan.shifts,
-                   m.astype(meas_dtype), n_slow, n_fast)
+                   m, n_slow, n_fast)

@@ -1,0 +1,49 @@
+"""The C-ABI library loads and exports every symbol include/ptyx.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from ptyrad_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "ptyx.h")).read()
+    return sorted(set(re.findall(r"\b(ptyx_[a-z_]+)\s*\(", src)))
+
+
+def test_header_matches_python_exports():
+    assert sorted(_lib.EXPORTS) == header_symbols()
+
+
+def test_library_loads_and_exports_all_symbols():
+    lib = _lib.load()
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    assert lib.ptyx_version() >= 100
+    assert lib.ptyx_last_error() == b""
+
+
+def test_struct_layouts_match_header():
+    # sizes of the C structs (all 4-byte fields / 8-byte pointers, no padding surprises)
+    assert ctypes.sizeof(_lib.Dims) == 9 * 4
+    assert ctypes.sizeof(_lib.Inputs) == 8 * 8
+    assert ctypes.sizeof(_lib.Grads) == 4 * 8
+    assert ctypes.sizeof(_lib.LossCfg) == 11 * 4
+
+
+def test_plan_create_rejects_bad_dims_without_gpu():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    d = _lib.Dims(100, 1, 1, 1, 200, 200, 4, 4, 0)   # N=100 unsupported -> checked before any HIP call
+    rc = lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0)
+    assert rc == _lib.PTYX_EUNSUPPORTED
+    assert b"N must be" in lib.ptyx_last_error()
+    d = _lib.Dims(128, 1, 9, 1, 200, 200, 4, 4, 0)   # too many object modes
+    assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EUNSUPPORTED
+    d = _lib.Dims(128, 1, 1, 1, 100, 200, 4, 4, 0)   # object smaller than the window
+    assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EINVAL
+    assert lib.ptyx_plan_create(None, ctypes.byref(d), 0) == _lib.PTYX_EINVAL

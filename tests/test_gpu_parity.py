@@ -1,0 +1,221 @@
+"""HIP path (libptyx.so through the C ABI) vs the reference's golden vectors and the oracle.
+
+Tolerances (fp32 engine vs fp32 reference / fp64 oracle, relative L2 over the array):
+  dp and loss terms          ≤ 1e-5
+  object / probe gradients   ≤ 5e-5
+  position gradients         ≤ 2e-4   (a sum of cancelling terms; the reference's own fp32
+                                       rounding is ~6e-5 here, tests/test_oracle_golden.py)
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptyx_oracle as orc
+from tests.test_oracle_golden import CASES, load_case, rel
+
+pytestmark = pytest.mark.gpu
+
+TOL_DP, TOL_TERMS, TOL_G, TOL_SH = 1e-5, 1e-5, 5e-5, 2e-4
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def tensors(d, device, meas_dtype=torch.float32):
+    t = {
+        "obja": torch.tensor(d["obja"], device=device),
+        "objp": torch.tensor(d["objp"], device=device),
+        "probe": torch.view_as_real(torch.tensor(d["probe"].astype(np.complex64), device=device)).contiguous(),
+        "shifts": torch.tensor(d["shifts"], device=device),
+        "H": torch.tensor(d["H"].astype(np.complex64), device=device),
+        "occu": torch.tensor(d["occu"], device=device),
+        "crop_pos": torch.tensor(d["crop_pos"].astype(np.int32), device=device),
+        "meas": torch.tensor(d["meas"], device=device).to(meas_dtype),
+    }
+    return t
+
+
+def make_plan(d, device, max_patterns=None, meas_f16=False):
+    from ptyrad_amd.engine import Plan
+    O, Nz, Ny, Nx = d["obja"].shape
+    P, N = d["probe"].shape[:2]
+    return Plan(N, P, O, Nz, Ny, Nx, d["shifts"].shape[0], max_patterns or d["shifts"].shape[0],
+                shift_probes=bool(d["shift_probes"]), meas_f16=meas_f16, device=device)
+
+
+def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", "objp", "probe", "shifts")):
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    plan = make_plan(d, device, meas_f16=meas_f16)
+    t = tensors(d, device, torch.float16 if meas_f16 else torch.float32)
+    grads = {k: torch.zeros_like(t[k if k != "shifts" else "shifts"]) for k in want}
+    if not d["shift_probes"]:
+        grads.pop("shifts", None)
+    flat = np.concatenate(batches).astype(np.int32)
+    N = d["probe"].shape[-1]
+    dp = torch.zeros((len(flat), N, N), device=device)
+    terms = plan.forward_loss_grad(t, flat, batch_offsets(batches), LossConfig.from_loss_params(d["loss_params"]),
+                                   grads, grad_scale=grad_scale, dp_out=dp)
+    torch.cuda.synchronize()
+    g = {k: v.cpu().numpy() for k, v in grads.items()}
+    if "probe" in g:
+        g["probe"] = g["probe"][..., 0] + 1j * g["probe"][..., 1]
+    return terms.cpu().numpy(), dp.cpu().numpy(), g, plan
+
+
+@pytest.mark.parametrize("path", CASES, ids=[p.split("/")[-1][:-4] for p in CASES])
+def test_fused_matches_reference_golden(path):
+    device = dev()
+    d = load_case(path)
+    terms, dp, g, _ = run_fused(d, device, [d["batch"]])
+    if "dp" in d:
+        assert rel(dp, d["dp"]) < TOL_DP
+    else:
+        assert rel(dp[:4], d["dp_head"]) < TOL_DP
+        assert rel(dp.reshape(len(dp), -1).astype(np.float64).sum(1), d["dp_sums"]) < TOL_DP
+    np.testing.assert_allclose(terms[0], d["loss_terms"], rtol=TOL_TERMS, atol=1e-7)
+    assert rel(g["obja"], d["g_obja"]) < TOL_G
+    assert rel(g["objp"], d["g_objp"]) < TOL_G
+    assert rel(g["probe"], d["g_probe"][..., 0] + 1j * d["g_probe"][..., 1]) < TOL_G
+    if d["shift_probes"]:
+        assert rel(g["shifts"], d["g_shifts"]) < TOL_SH
+
+
+@pytest.mark.parametrize("path", CASES[:4], ids=[p.split("/")[-1][:-4] for p in CASES[:4]])
+def test_forward_only_matches_oracle(path):
+    device = dev()
+    d = load_case(path)
+    plan = make_plan(d, device)
+    t = tensors(d, device)
+    dp = plan.forward(t, d["batch"].astype(np.int32))
+    ref = orc.forward_dp(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"],
+                         d["batch"], shift_probes=bool(d["shift_probes"]))
+    assert rel(dp.cpu().numpy(), ref) < TOL_DP
+
+
+def test_multibatch_call_equals_sum_of_batches():
+    """Several mini-batches in one call: per-batch NRMSE normalisation, gradients summed."""
+    device = dev()
+    d = load_case([c for c in CASES if "n32_p2o2z3" in c][0])
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(5).permutation(S)
+    batches = np.array_split(perm, 3)
+    terms, _, g, _ = run_fused(d, device, batches, grad_scale=0.5)
+    oterms, _, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                          d["occu"], d["meas"], batches, d["loss_params"],
+                                          shift_probes=True, grad_scale=0.5)
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_meas_fp16_storage():
+    device = dev()
+    d = load_case([c for c in CASES if "n32_p1o1z1" in c][0])
+    d16 = dict(d)
+    d16["meas"] = d["meas"].astype(np.float16).astype(np.float32)
+    terms, _, g, _ = run_fused(d16, device, [d["batch"]], meas_f16=True)
+    oterms, _, og = orc.forward_loss_grad(d16["obja"], d16["objp"], d16["probe"], d16["shifts"], d16["crop_pos"],
+                                          d16["H"], d16["occu"], d16["meas"], [d["batch"]], d["loss_params"])
+    np.testing.assert_allclose(terms[0], oterms[0], rtol=TOL_TERMS, atol=1e-7)
+    assert rel(g["objp"], og["objp"]) < TOL_G
+
+
+def test_null_gradients_skip_work_and_others_unchanged():
+    device = dev()
+    d = load_case([c for c in CASES if "n32_p1o1z1" in c][0])
+    terms, _, g, _ = run_fused(d, device, [d["batch"]], want=("objp",))
+    assert set(g) == {"objp"}
+    assert rel(g["objp"], d["g_objp"]) < TOL_G
+    np.testing.assert_allclose(terms[0], d["loss_terms"], rtol=TOL_TERMS, atol=1e-7)
+
+
+def test_external_dldi_adjoint_matches_oracle():
+    """ptyx_adjoint_dldi with dL/dI from the oracle loss == oracle adjoint (no sparse term)."""
+    device = dev()
+    d = load_case([c for c in CASES if "n32_p2o2z3" in c][0])
+    b = d["batch"]
+    n = d["probe"].shape[-1]
+    amp, ph = orc.get_patches(d["obja"], d["objp"], d["crop_pos"], b, n)
+    probes = orc.get_probes(d["probe"], d["shifts"][b], True)
+    cache = orc.forward(amp, ph, probes, d["H"], d["occu"])
+    _, dLdI, _ = orc.loss_terms(cache.dp, d["meas"][b], ph, d["occu"], d["loss_params"])
+    dA, dP, dprobe, dshift = orc.adjoint(cache, dLdI, np.zeros_like(ph, np.float64), amp, ph, d["probe"],
+                                         d["shifts"][b], d["H"], d["occu"], True)
+    gA = np.zeros(d["obja"].shape)
+    gP = np.zeros(d["objp"].shape)
+    for i, s in enumerate(b):
+        cy, cx = d["crop_pos"][s]
+        gA[:, :, cy:cy + n, cx:cx + n] += dA[i]
+        gP[:, :, cy:cy + n, cx:cx + n] += dP[i]
+    plan = make_plan(d, device)
+    t = tensors(d, device)
+    grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+    plan.adjoint_dldi(t, b.astype(np.int32), torch.tensor(dLdI, dtype=torch.float32, device=device), grads)
+    torch.cuda.synchronize()
+    assert rel(grads["obja"].cpu().numpy(), gA) < TOL_G
+    assert rel(grads["objp"].cpu().numpy(), gP) < TOL_G
+    gp = grads["probe"].cpu().numpy()
+    assert rel(gp[..., 0] + 1j * gp[..., 1], dprobe) < TOL_G
+
+
+def test_loss_terms_deterministic():
+    device = dev()
+    d = load_case([c for c in CASES if "n64_p3o1z1" in c][0])
+    t1, _, g1, _ = run_fused(d, device, [d["batch"]])
+    t2, _, g2, _ = run_fused(d, device, [d["batch"]])
+    assert np.array_equal(t1, t2)
+    assert np.array_equal(g1["probe"], g2["probe"])   # slab reduction in fixed order
+
+
+def test_n256_mixed_state_vs_oracle():
+    """c3-shaped (N=256, P=2, O=2) small problem through the global-scratch FFT path."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(256, 2, 2, P=2, O=2, Nz=1, seed=3)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True,
+             loss_params=json.loads(json.dumps(orc_default_loss())))
+    b = np.array([0, 3, 1])
+    terms, dp, g, _ = run_fused(d, device, [b])
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], [b], d["loss_params"])
+    assert rel(dp, odps[0]) < TOL_DP
+    np.testing.assert_allclose(terms[0], oterms[0], rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+def orc_default_loss():
+    return {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+            "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+            "loss_pacbed": {"state": False}, "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
+            "loss_simlar": {"state": False}}
+
+
+def test_bench_config_sample_vs_oracle():
+    """The bench workload (c2: 256x256 scan, N=128, object 1033^2): one mini-batch of 32 vs oracle."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(128, 256, 256, seed=0, meas="none")
+    rng = np.random.default_rng(9)
+    sel = rng.choice(256 * 256, 32, replace=False)      # 32 scan positions of the full scan
+    meas = rng.random((32, 128, 128), dtype=np.float32)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(60.0), shifts=pr.shifts[sel],
+             crop_pos=pr.crop_pos[sel], H=pr.H, occu=pr.occu, meas=meas, shift_probes=True,
+             loss_params=orc_default_loss())
+    b = rng.permutation(32)
+    terms, dp, g, _ = run_fused(d, device, [b])
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], [b], d["loss_params"])
+    assert rel(dp, odps[0]) < TOL_DP
+    np.testing.assert_allclose(terms[0], oterms[0], rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
