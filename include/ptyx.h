@@ -110,6 +110,18 @@ int ptyx_forward_loss_grad(ptyx_plan *plan, void *stream, const ptyx_inputs *in,
 int ptyx_adjoint_dldi(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
                       int32_t n_idx, const float *dLdI, float grad_scale, const ptyx_grads *grads);
 
+/* Per-kernel timing for roofline reporting: while profiling is on, every kernel the plan
+ * launches is bracketed by HIP events on its stream.  ptyx_profile_end waits for the recorded
+ * events, writes up to `cap` {kernel name, launches, total milliseconds} rows and turns
+ * profiling off.  (Not for graph capture: it creates events.) */
+typedef struct ptyx_kernel_stat {
+  char name[32];
+  int32_t launches;
+  float total_ms;
+} ptyx_kernel_stat;
+int ptyx_profile_begin(ptyx_plan *plan);
+int ptyx_profile_end(ptyx_plan *plan, ptyx_kernel_stat *out, int32_t cap, int32_t *n_out);
+
 /* Bytes of device workspace the plan holds. */
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
 /* Last error message of the calling thread ("" if none). */

@@ -22,7 +22,8 @@ _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 
 # every symbol include/ptyx.h declares (checked by tests/test_abi.py)
 EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
-           "ptyx_adjoint_dldi", "ptyx_plan_workspace_bytes", "ptyx_last_error", "ptyx_version")
+           "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
+           "ptyx_last_error", "ptyx_version")
 
 
 class PtyxError(RuntimeError):
@@ -57,6 +58,10 @@ class LossCfg(ctypes.Structure):
                 ("grad_scale", ctypes.c_float)]
 
 
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int32), ("total_ms", ctypes.c_float)]
+
+
 _lib = None
 
 
@@ -78,6 +83,10 @@ def load(path: str | None = None):
                                            ctypes.POINTER(LossCfg), vp, vp, ctypes.POINTER(Grads)]
     lib.ptyx_adjoint_dldi.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, i32, vp, f32,
                                       ctypes.POINTER(Grads)]
+    lib.ptyx_profile_begin.argtypes = [vp]
+    lib.ptyx_profile_end.argtypes = [vp, ctypes.POINTER(KernelStat), i32, ctypes.POINTER(i32)]
+    lib.ptyx_profile_begin.restype = ctypes.c_int
+    lib.ptyx_profile_end.restype = ctypes.c_int
     lib.ptyx_plan_workspace_bytes.argtypes = [vp]
     lib.ptyx_plan_workspace_bytes.restype = ctypes.c_size_t
     lib.ptyx_last_error.restype = ctypes.c_char_p

@@ -691,6 +691,35 @@ struct ptyx_plan {
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
+  // ptyx_profile_begin/end: HIP events around every launch (kind, start, stop)
+  bool prof = false;
+  struct ProfRec {
+    int kind;
+    hipEvent_t a, b;
+  };
+  mutable std::vector<ProfRec> recs;
+};
+
+enum KernelKind { kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKCount };
+static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",     "k_finalize",
+                                                  "k_adjoint",        "k_slab_reduce", "k_probe_finalize"};
+
+// Brackets one launch with HIP events on its stream while the plan is profiling.
+struct ProfScope {
+  const ptyx_plan* pl;
+  int kind;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(const ptyx_plan* p, int k, hipStream_t s) : pl(p), kind(k), st(s) {
+    if (pl->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+      (void)hipEventRecord(a, st);
+  }
+  ~ProfScope() {
+    if (pl->prof && a && b) {
+      (void)hipEventRecord(b, st);
+      pl->recs.push_back({kind, a, b});
+    }
+  }
 };
 
 static bool is_supported_n(int n) { return n == 32 || n == 64 || n == 128 || n == 256; }
@@ -815,10 +844,12 @@ static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t
 
 template <int N>
 static void launch_spectrum(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  ProfScope ps(pl, kKSpectrum, st);
   hipLaunchKernelGGL(k_probe_spectrum<N>, dim3(pl->d.P), dim3(Geo<N>::NT), 0, st, a, pl->Fp);
 }
 template <int N>
 static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  ProfScope ps(pl, kKForward, st);
   const int grid = std::max(1, std::min(a.n_idx, pl->nwg));
   if (pl->d.P * pl->d.O == 1)
     hipLaunchKernelGGL((k_forward<N, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
@@ -827,6 +858,7 @@ static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) 
 }
 template <int N>
 static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, bool ext) {
+  ProfScope ps(pl, kKAdjoint, st);
   const int grid = pl->nwg;  // every workgroup zeroes its slab, so launch all of them
   const bool single = pl->d.P * pl->d.O == 1;
   if (ext)
@@ -840,10 +872,54 @@ template <int N>
 static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe) {
   const long long per = (long long)pl->d.P * N * N;
   const int tb = 256;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + tb - 1) / tb)), dim3(tb), 0, st, pl->slab, pl->nwg,
-                     per, pl->Gsum);
+  {
+    ProfScope ps(pl, kKSlabReduce, st);
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + tb - 1) / tb)), dim3(tb), 0, st, pl->slab, pl->nwg,
+                       per, pl->Gsum);
+  }
+  ProfScope ps(pl, kKProbeFinalize, st);
   hipLaunchKernelGGL(k_probe_finalize<N>, dim3(pl->d.P), dim3(Geo<N>::NT), 0, st, a, pl->Gsum,
                      reinterpret_cast<float2*>(d_probe));
+}
+
+extern "C" int ptyx_profile_begin(ptyx_plan* pl) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  pl->prof = true;
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_profile_end(ptyx_plan* pl, ptyx_kernel_stat* out, int32_t cap, int32_t* n_out) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  DeviceGuard dg(pl->device);
+  int launches[kKCount] = {0};
+  double ms[kKCount] = {0};
+  int rc = PTYX_OK;
+  for (auto& r : pl->recs) {
+    float t = 0.f;
+    hipError_t e = hipEventSynchronize(r.b);
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, r.a, r.b);
+    if (e != hipSuccess && rc == PTYX_OK) rc = hip_fail(e, "hipEventElapsedTime");
+    launches[r.kind] += 1;
+    ms[r.kind] += t;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  pl->recs.clear();
+  pl->prof = false;
+  int n = 0;
+  for (int k = 0; k < kKCount; ++k) {
+    if (!launches[k]) continue;
+    if (out && n < cap) {
+      std::snprintf(out[n].name, sizeof(out[n].name), "%s", kKernelNames[k]);
+      out[n].launches = launches[k];
+      out[n].total_ms = (float)ms[k];
+    }
+    ++n;
+  }
+  if (n_out) *n_out = n;
+  return rc;
 }
 
 // PTYX_ONLY_N=<n> builds a single size (kernel experiments); the shipped library has all four.
@@ -930,7 +1006,10 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   f.single_on = cfg->single_on; f.pois_on = cfg->poissn_on; f.sparse_on = cfg->sparse_on;
   f.sparse_n = cfg->sparse_n; f.w1 = cfg->single_w; f.w2 = cfg->poissn_w; f.ws = cfg->sparse_w;
   f.grad_scale = cfg->grad_scale; f.coef = pl->coef; f.loss_terms = loss_terms;
-  hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
+  {
+    ProfScope ps(pl, kKFinalize, st);
+    hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
+  }
   if ((rc = launch_status("k_finalize launch"))) return rc;
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
   if (!any_grad) return PTYX_OK;

@@ -147,6 +147,19 @@ class Plan:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    # ------------------------------------------------------------------ per-kernel timing
+    def profile_begin(self):
+        _lib.check(self.lib.ptyx_profile_begin(self._h))
+
+    def profile_end(self) -> dict:
+        """{kernel name: (launches, total_ms)} from HIP events recorded on the launch stream."""
+        cap = 16
+        arr = (_lib.KernelStat * cap)()
+        n = ctypes.c_int32(0)
+        _lib.check(self.lib.ptyx_profile_end(self._h, arr, cap, ctypes.byref(n)))
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms))
+                for i in range(min(n.value, cap))}
+
     # ------------------------------------------------------------------ entry points
     def forward(self, t: dict, idx, dp_out=None):
         """ptyx_forward: dp (n, N, N) f32 = PtychoAD.forward(idx)."""
