@@ -1,0 +1,61 @@
+"""Host-side logic that needs no GPU: batching, index selection, loss-config mapping."""
+import numpy as np
+import pytest
+
+from ptyrad_amd.engine import LossConfig, batch_offsets
+from ptyrad_amd.reconstruction import make_batches, select_scan_indices, toggle_grad_requires
+
+
+def test_batch_offsets():
+    b = [np.arange(3), np.arange(3, 5), np.arange(5, 9)]
+    assert batch_offsets(b).tolist() == [0, 3, 5, 9]
+    assert batch_offsets(b).dtype == np.int32
+
+
+def test_make_batches_random_is_a_partition():
+    idx = np.arange(100)
+    bs = make_batches(idx, None, 32, rng=np.random.default_rng(0))
+    assert len(bs) == 3                               # len // batch_size groups (array_split)
+    flat = np.sort(np.concatenate(bs))
+    assert np.array_equal(flat, idx)
+    assert sorted(len(b) for b in bs) == [33, 33, 34]
+
+
+def test_select_scan_indices_modes():
+    assert np.array_equal(select_scan_indices(4, 5), np.arange(20))
+    c = select_scan_indices(4, 4, 2, 2, mode="center")
+    assert sorted(c.tolist()) == [5, 6, 9, 10]
+    s = select_scan_indices(4, 4, 2, 2, mode="sub")
+    assert sorted(s.tolist()) == [0, 3, 12, 15]
+    with pytest.raises(ValueError):
+        select_scan_indices(4, 4, mode="bogus")
+
+
+def test_loss_config_mapping_and_out_of_scope_terms():
+    lp = {"loss_single": {"state": True, "weight": 2.0, "dp_pow": 0.4},
+          "loss_poissn": {"state": True, "weight": 0.5, "dp_pow": 1.0, "eps": 1e-5},
+          "loss_pacbed": {"state": False}, "loss_sparse": {"state": True, "weight": 0.2, "ln_order": 2},
+          "loss_simlar": {"state": False}}
+    c = LossConfig.from_loss_params(lp)
+    assert (c.single_on, c.single_w, c.single_q) == (True, 2.0, 0.4)
+    assert (c.poissn_on, c.poissn_w, c.poissn_eps) == (True, 0.5, 1e-5)
+    assert (c.sparse_on, c.sparse_n) == (True, 2)
+    cs = c.to_c(0.25)
+    assert abs(cs.grad_scale - 0.25) < 1e-9
+    lp["loss_pacbed"]["state"] = True
+    with pytest.raises(NotImplementedError):
+        LossConfig.from_loss_params(lp)
+
+
+def test_toggle_grad_requires_follows_start_iter():
+    import torch
+
+    class M:
+        pass
+    m = M()
+    m.start_iter = {"obja": 1, "probe": 3, "obj_tilts": None}
+    m.optimizable_tensors = {k: torch.zeros(1, requires_grad=False) for k in m.start_iter}
+    toggle_grad_requires(m, 2)
+    assert [m.optimizable_tensors[k].requires_grad for k in ("obja", "probe", "obj_tilts")] == [True, False, False]
+    toggle_grad_requires(m, 3)
+    assert m.optimizable_tensors["probe"].requires_grad
