@@ -167,6 +167,59 @@ __device__ __forceinline__ float2 twiddle(const float2* tw, int m) {
   return DIR < 0 ? w : make_float2(w.x, -w.y);
 }
 
+// pre/post hooks come in two forms: (y, x, v) and slot-aware (y, x, v, slot), where slot =
+// kb·R + r enumerates a thread's points of the pass (see PassMap).  Slot-aware hooks read
+// values the caller prefetched into registers for exactly those points, so they carry no
+// global-memory latency and are scheduled freely.
+template <class F>
+constexpr bool kSlotPre = std::is_invocable_v<F&, int, int, float2, int>;
+template <class F>
+constexpr bool kSlotPost = std::is_invocable_v<F&, int, int, float2&, int>;
+
+template <class F>
+__device__ __forceinline__ float2 call_pre(F& f, int y, int x, float2 v, int slot) {
+  if constexpr (kSlotPre<F>) return f(y, x, v, slot);
+  else return f(y, x, v);
+}
+template <class F>
+__device__ __forceinline__ bool call_post(F& f, int y, int x, float2& v, int slot) {
+  if constexpr (kSlotPost<F>) return f(y, x, v, slot);
+  else return f(y, x, v);
+}
+
+// Points (y, x) a thread owns in the first (row, radix R1) and last (column) pass of fft2d on
+// an LDS array: the same formulas as stockham_pass, for register prefetch outside the FFT.
+template <int N, int NT>
+struct PassMap {
+  using P1 = Plan1D<N>;
+  static constexpr int R1 = P1::R1;
+  static constexpr int RL = P1::R2 == 1 ? P1::R1 : P1::R2;   // radix of the last pass
+  static constexpr int NSL = P1::R2 == 1 ? 1 : P1::R1;        // its Stockham span
+  static constexpr int KBF = (N * N / R1 + NT - 1) / NT;
+  static constexpr int KBL = (N * N / RL + NT - 1) / NT;
+  static constexpr int kFirstSlots = KBF * R1;
+  static constexpr int kLastSlots = KBL * RL;
+  // Idle slots (only when NT does not divide the butterfly count) are clamped onto a valid
+  // point so that register prefetches can be unconditional: a conditionally written register
+  // array becomes loop-carried and stays live across the whole pattern loop.
+  __device__ __forceinline__ static void first(int tid, int slot, int& y, int& x) {
+    const int kb = slot / R1, r = slot % R1;
+    const int bf = min(tid + kb * NT, N * N / R1 - 1);
+    y = bf / (N / R1);
+    x = bf % (N / R1) + r * (N / R1);
+  }
+  __device__ __forceinline__ static void last(int tid, int slot, int& y, int& x) {
+    const int kb = slot / RL, r = slot % RL;
+    const int bf = min(tid + kb * NT, N * N / RL - 1);
+    const int j = bf / N;
+    x = bf % N;
+    y = (j / NSL) * NSL * RL + (j % NSL) + r * NSL;
+  }
+  __device__ __forceinline__ static bool last_active(int tid, int slot) {
+    return tid + (slot / RL) * NT < N * N / RL;
+  }
+};
+
 // One Stockham pass of radix R over all N lines.  ROW: lines are rows (x varies).
 //  PRELOAD (first pass only): whether to load the source before calling pre(y,x,v).
 //  post(y,x,v) (last pass only) may modify v and returns true if v must be stored.
@@ -198,9 +251,9 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
           const int y = ROW ? line : e, x = ROW ? e : line;
           float2 val;
           if constexpr (KIND & kFirst) {
-            if constexpr (PRELOAD) val = pre(y, x, src.ld(y, x));
-            else val = pre(y, x, make_float2(0.f, 0.f));
-            if constexpr (kFuseGroup > 0) {
+            if constexpr (PRELOAD) val = call_pre(pre, y, x, src.ld(y, x), kb * R + r);
+            else val = call_pre(pre, y, x, make_float2(0.f, 0.f), kb * R + r);
+            if constexpr (kFuseGroup > 0 && !kSlotPre<Pre>) {
               if ((r + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
             }
           } else {
@@ -229,9 +282,9 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
           const int y = ROW ? line : e, x = ROW ? e : line;
           float2 val = v[kb][r];
           if constexpr (KIND & kLast) {
-            if (post(y, x, val)) dst.st(y, x, val);
+            if (call_post(post, y, x, val, kb * R + r)) dst.st(y, x, val);
             // bound the compiler's hoisting of the fused epilogue's global loads
-            if constexpr (kFuseGroup > 0) {
+            if constexpr (kFuseGroup > 0 && !kSlotPost<Post>) {
               if ((r + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
             }
           } else {
@@ -253,8 +306,8 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
         const int y = ROW ? line : e, x = ROW ? e : line;
         float2 val;
         if constexpr (KIND & kFirst) {
-          if constexpr (PRELOAD) val = pre(y, x, src.ld(y, x));
-          else val = pre(y, x, make_float2(0.f, 0.f));
+          if constexpr (PRELOAD) val = call_pre(pre, y, x, src.ld(y, x), r);
+          else val = call_pre(pre, y, x, make_float2(0.f, 0.f), r);
         } else {
           val = src.ld(y, x);
         }
@@ -271,7 +324,7 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
         const int y = ROW ? line : e, x = ROW ? e : line;
         float2 val = v[r];
         if constexpr (KIND & kLast) {
-          if (post(y, x, val)) dst.st(y, x, val);
+          if (call_post(post, y, x, val, r)) dst.st(y, x, val);
         } else {
           dst.st(y, x, val);
         }

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <cstdlib>
 
 #include "ptyx.h"
 #include "ptyx_fft.hpp"
@@ -602,6 +603,8 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   }
 }
 
+#include "ptyx_single.hpp"
+
 // Σ over workgroup slabs, fixed order.
 __global__ void k_slab_reduce(const float2* slab, int nwg, long long per, float2* out) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -691,6 +694,8 @@ struct ptyx_plan {
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
+  // single-mode fast kernels (P = O = Nz = 1, N <= 128); PTYX_GENERIC=1 forces the general ones
+  bool fast = true;
   // ptyx_profile_begin/end: HIP events around every launch (kind, start, stop)
   bool prof = false;
   struct ProfRec {
@@ -776,7 +781,11 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->d = d;
   pl->device = device;
   pl->n_cu = cu;
-  pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * blocks_per_cu(d.N)));
+  {
+    const char* gen = std::getenv("PTYX_GENERIC");
+    pl->fast = !(gen && gen[0] == '1');
+  }
+  pl->nwg =std::max(d.P, std::min(d.max_patterns, cu * blocks_per_cu(d.N)));
   const size_t N2 = (size_t)d.N * d.N;
   const bool lds = d.N <= 128;
   pl->scratch_stride = (long long)((lds ? 0 : 2 * N2) + (size_t)d.Nz * N2 + N2);
@@ -851,6 +860,16 @@ template <int N>
 static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
   ProfScope ps(pl, kKForward, st);
   const int grid = std::max(1, std::min(a.n_idx, pl->nwg));
+  if constexpr (Geo<N>::kLds) {
+    if (pl->d.P * pl->d.O * pl->d.Nz == 1 && pl->fast) {
+      const bool sums = a.psums != nullptr;
+      if (a.shift && sums) hipLaunchKernelGGL((k_forward1<N, true, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+      else if (a.shift) hipLaunchKernelGGL((k_forward1<N, true, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+      else if (sums) hipLaunchKernelGGL((k_forward1<N, false, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+      else hipLaunchKernelGGL((k_forward1<N, false, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+      return;
+    }
+  }
   if (pl->d.P * pl->d.O == 1)
     hipLaunchKernelGGL((k_forward<N, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
   else
@@ -861,6 +880,16 @@ static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, 
   ProfScope ps(pl, kKAdjoint, st);
   const int grid = pl->nwg;  // every workgroup zeroes its slab, so launch all of them
   const bool single = pl->d.P * pl->d.O == 1;
+  if constexpr (Geo<N>::kLds) {
+    if (single && pl->d.Nz == 1 && pl->fast) {
+      const dim3 gr(grid), bl(Geo<N>::NT);
+      if (a.shift && ext) hipLaunchKernelGGL((k_adjoint1<N, true, true>), gr, bl, 0, st, a);
+      else if (a.shift) hipLaunchKernelGGL((k_adjoint1<N, true, false>), gr, bl, 0, st, a);
+      else if (ext) hipLaunchKernelGGL((k_adjoint1<N, false, true>), gr, bl, 0, st, a);
+      else hipLaunchKernelGGL((k_adjoint1<N, false, false>), gr, bl, 0, st, a);
+      return;
+    }
+  }
   if (ext)
     hipLaunchKernelGGL((k_adjoint<N, false, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
   else if (single)
