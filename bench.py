@@ -126,6 +126,7 @@ def main():
     idx_t = torch.as_tensor(np.concatenate(batches), dtype=torch.int32, device=dev)
     off_t = torch.as_tensor(batch_offsets(batches), device=dev)
     nb = len(batches)
+    max_batch = max(len(b) for b in batches)
     cfg = LossConfig()
     n_obj = obja.numel()
     flat = torch.zeros(2 * n_obj + probe.numel(), device=dev)     # one all-reduce buffer
@@ -136,7 +137,8 @@ def main():
     def step():
         flat.zero_()
         grads["shifts"].zero_()
-        plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0 / nb, loss_terms=terms)
+        plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0 / nb, loss_terms=terms,
+                               max_batch=max_batch)
         if world > 1:
             dist.all_reduce(flat)          # object + probe gradients; positions are rank-local
 

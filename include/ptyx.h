@@ -83,6 +83,9 @@ typedef struct ptyx_loss_cfg {
   int32_t poissn_on;  float poissn_w, poissn_q, poissn_eps;  /* loss_poissn [0, 1.0, 1.0, 1e-6] */
   int32_t sparse_on;  float sparse_w; int32_t sparse_n;      /* loss_sparse [1, 0.1, 1]         */
   float grad_scale;   /* multiplies every gradient: 1/grad_accumulation, reconstruction.py:750 */
+  int32_t max_batch;  /* largest mini-batch of the call, 0 = unknown.  When it fits the resident
+                         grid, single-mode calls run forward, loss and adjoint in ONE pass per
+                         pattern (per-mini-batch arrival counter instead of a second forward). */
 } ptyx_loss_cfg;
 
 /* Create a plan: validates dims, allocates the device workspace and twiddle tables.

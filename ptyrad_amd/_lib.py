@@ -55,7 +55,7 @@ class LossCfg(ctypes.Structure):
                 ("poissn_on", ctypes.c_int32), ("poissn_w", ctypes.c_float), ("poissn_q", ctypes.c_float),
                 ("poissn_eps", ctypes.c_float),
                 ("sparse_on", ctypes.c_int32), ("sparse_w", ctypes.c_float), ("sparse_n", ctypes.c_int32),
-                ("grad_scale", ctypes.c_float)]
+                ("grad_scale", ctypes.c_float), ("max_batch", ctypes.c_int32)]
 
 
 class KernelStat(ctypes.Structure):

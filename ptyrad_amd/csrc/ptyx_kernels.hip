@@ -75,6 +75,11 @@ struct KArgs {
   float2* scratch;
   long long scratch_stride;
   const float2* twg;
+  // one-pass fused kernel: loss weights and the per-call sync words
+  // sync[0] = dequeue head, sync[1] = error flag (spin timeout), sync[2 + m] = arrivals of batch m
+  float w1, w2, ws, grad_scale;
+  unsigned* sync;
+  int debug_nowait;   // PTYX_DEBUG_NOWAIT=1: skip the batch wait (timing experiments only; wrong gradients)
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -691,6 +696,7 @@ struct ptyx_plan {
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* scratch = nullptr;
+  unsigned* sync = nullptr;   // k_fused1: dequeue head, error flag, per-batch arrivals
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
@@ -705,9 +711,9 @@ struct ptyx_plan {
   mutable std::vector<ProfRec> recs;
 };
 
-enum KernelKind { kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKCount };
-static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",     "k_finalize",
-                                                  "k_adjoint",        "k_slab_reduce", "k_probe_finalize"};
+enum KernelKind { kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKCount };
+static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize", "k_adjoint",
+                                                  "k_slab_reduce",    "k_probe_finalize", "k_fused"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -797,7 +803,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->Ibuf, multi ? (size_t)d.max_patterns * N2 : 0)) ||
       (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
       (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
-      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride))) {
+      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride)) ||
+      (rc = dalloc(pl, &pl->sync, ((size_t)d.max_patterns + 2 + 3) / 4 * 4))) {
     free_plan(pl);
     return rc;
   }
@@ -896,6 +903,15 @@ static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, 
     hipLaunchKernelGGL((k_adjoint<N, true, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
   else
     hipLaunchKernelGGL((k_adjoint<N, false, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+}
+template <int N>
+static void launch_fused(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  if constexpr (Geo<N>::kLds) {
+    ProfScope ps(pl, kKFused, st);
+    const dim3 gr(pl->nwg), bl(Geo<N>::NT);   // persistent: every workgroup resident (1 per CU at N = 128)
+    if (a.shift) hipLaunchKernelGGL((k_fused1<N, true>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_fused1<N, false>), gr, bl, 0, st, a);
+  }
 }
 template <int N>
 static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe) {
@@ -1026,9 +1042,31 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.d_shifts = gz.d_shifts;
   a.need_probe = gz.d_probe != nullptr;
 
+  a.w1 = cfg->single_w;
+  a.w2 = cfg->poissn_w;
+  a.ws = cfg->sparse_w;
+  a.grad_scale = cfg->grad_scale;
+  a.sync = pl->sync;
+  {
+    const char* dbg = std::getenv("PTYX_DEBUG_NOWAIT");
+    a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
+  }
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
+  // one pass per pattern when the resident grid can hold every mini-batch (see k_fused1)
+  const bool fused = any_grad && pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1 &&
+                     cfg->max_batch > 0 && cfg->max_batch <= pl->nwg && !std::getenv("PTYX_TWO_PASS");
+
   if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
-  PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
-  if ((rc = launch_status("k_forward launch"))) return rc;
+  if (fused) {
+    const size_t sync_bytes = ((size_t)(2 + n_batches) * sizeof(unsigned) + 15) / 16 * 16;
+    hipError_t e = hipMemsetAsync(pl->sync, 0, sync_bytes, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(sync)");
+    PTYX_DISPATCH_N(pl->d.N, launch_fused, pl, a, st);
+    if ((rc = launch_status("k_fused launch"))) return rc;
+  } else {
+    PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+    if ((rc = launch_status("k_forward launch"))) return rc;
+  }
   FinArgs f{};
   f.boff = boff; f.n_batches = n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
   f.psums = pl->psums; f.occu = in->omode_occu;
@@ -1040,10 +1078,11 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
   }
   if ((rc = launch_status("k_finalize launch"))) return rc;
-  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
   if (!any_grad) return PTYX_OK;
-  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
-  if ((rc = launch_status("k_adjoint launch"))) return rc;
+  if (!fused) {
+    PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
+    if ((rc = launch_status("k_adjoint launch"))) return rc;
+  }
   if (gz.d_probe) {
     PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe);
     if ((rc = launch_status("probe finalize launch"))) return rc;

@@ -55,10 +55,11 @@ class LossConfig:
                    float(p.get("eps", 1e-6)),
                    bool(sp["state"]), float(sp.get("weight", 0.1)), int(sp.get("ln_order", 1)))
 
-    def to_c(self, grad_scale: float) -> _lib.LossCfg:
+    def to_c(self, grad_scale: float, max_batch: int = 0) -> _lib.LossCfg:
         return _lib.LossCfg(int(self.single_on), self.single_w, self.single_q,
                             int(self.poissn_on), self.poissn_w, self.poissn_q, self.poissn_eps,
-                            int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale))
+                            int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale),
+                            int(max_batch))
 
 
 class Plan:
@@ -174,8 +175,18 @@ class Plan:
         return dp_out
 
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
-                          grad_scale: float = 1.0, loss_terms=None, dp_out=None):
-        """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5)."""
+                          grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None):
+        """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5).
+
+        max_batch: largest mini-batch size (enables the one-pass fused kernel); derived from
+        host-side offsets when not given, 0 (= two-pass) for device-only offsets.
+        """
+        if max_batch is None:
+            if isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu":
+                max_batch = 0
+            else:
+                off = np.asarray(batch_offsets)
+                max_batch = int(np.max(np.diff(off))) if off.size > 1 else 0
         idx_t = self._idx(idx)
         off_t = self._idx(batch_offsets)
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
@@ -183,7 +194,7 @@ class Plan:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
                                   t["crop_pos"], t["meas"])
-        cfg = loss_cfg.to_c(grad_scale)
+        cfg = loss_cfg.to_c(grad_scale, max_batch)
         g = self._grads(grads)
         _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),

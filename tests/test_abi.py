@@ -32,7 +32,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Dims) == 9 * 4
     assert ctypes.sizeof(_lib.Inputs) == 8 * 8
     assert ctypes.sizeof(_lib.Grads) == 4 * 8
-    assert ctypes.sizeof(_lib.LossCfg) == 11 * 4
+    assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
 
 
 def test_plan_create_rejects_bad_dims_without_gpu():
