@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="reference mini-batch size (BATCH_SIZE.size)")
     ap.add_argument("--scan", type=int, default=256, help="scan positions per side per GPU shard")
     ap.add_argument("--N", type=int, default=128)
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="patterns for the CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=40960, help="patterns for the CPU baseline (about 10 s on 16 cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
@@ -166,23 +166,33 @@ def main():
     value = total_patterns / elapsed
     ms_per_step = 1e3 * elapsed / a.steps
 
-    # roofline of the dominant kernel (k_adjoint): SURVEY §8d B_alg = N^2 (s_m + 16 O Nz) per pattern
+    # roofline of the dominant kernel (k_fused: forward + loss + adjoint in one pass; k_adjoint on
+    # the two-pass path).  SURVEY §8d per pattern: B_alg = N^2 (s_m + 16 O Nz) bytes,
+    # F_alg = n_fft 5 N^2 log2 N^2 flops (n_fft = 2 P O (2 Nz - 1) + 2P with shifts).
     b_alg = N * N * (4 + 16 * 1 * 1)
-    launches, adj_ms = kstats.get("k_adjoint", (0, 0.0))
-    roof = None
-    if launches:
-        avg_s = adj_ms / launches / 1e3
-        achieved = b_alg * n_local / avg_s / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_c2_adjoint.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        roof = {"kernel": "k_adjoint", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": b_alg * n_local, "avg_launch_ms": round(avg_s * 1e3, 4)}
     n_fft = 2 * 1 * 1 * (2 * 1 - 1) + 2
     flops = n_fft * 5 * N * N * math.log2(N * N)
+    dom = "k_fused" if "k_fused" in kstats else "k_adjoint"
+    launches, dom_ms = kstats.get(dom, (0, 0.0))
+    roof = None
+    if launches:
+        avg_s = dom_ms / launches / 1e3
+        achieved = b_alg * n_local / avg_s / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_c2.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch", {}).get(dom)
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": b_alg * n_local, "avg_launch_ms": round(avg_s * 1e3, 4),
+                "fft_fp32_frac": round(flops * n_local / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        g_launches, g_ms = kstats.get("k_obj_gather", (0, 0.0))
+        if g_launches:
+            # gather reads one N^2 complex g_O slot per pattern (+ the object tile, negligible)
+            g_s = g_ms / g_launches / 1e3
+            roof["gather"] = {"avg_launch_ms": round(g_s * 1e3, 4),
+                              "achieved_GBps": round(8 * N * N * n_local / g_s / 1e9, 1)}
     out = {
         "metric": "diffraction-patterns/sec/iter (fwd+bwd), 256x256 probe positions, 128x128 DP",
         "value": round(value, 1), "unit": "patterns/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

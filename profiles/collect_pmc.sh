@@ -14,7 +14,7 @@ i=0
 for pass in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES" \
             "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" \
-            "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum" \
+            "TCC_HIT_sum TCC_MISS_sum" \
             "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i + 1))
   timeout -k 10 300 rocprofv3 --pmc $pass --output-format csv -d "$OUT/pass$i" -o pmc -- \

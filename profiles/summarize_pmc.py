@@ -51,10 +51,12 @@ if __name__ == "__main__":
         for c in sorted(m):
             print(f"    {c:28s} {m[c]:.5g}")
     if len(sys.argv) > 2:
-        adj = [k for k in res if "k_adjoint" in k]
-        payload = {"source": sys.argv[1], "kernels": res}
-        if adj:
-            payload["hbm_bytes_per_launch"] = res[adj[0]]["hbm_bytes_per_launch"]
-            payload["kernel"] = adj[0]
+        # short kernel name (k_fused, k_obj_gather, ...) -> HBM bytes per launch, for bench.py
+        short = {}
+        for k, m in res.items():
+            base = k.split("<")[0].split("::")[-1]
+            short[{"k_fused2": "k_fused", "k_fused1": "k_fused", "k_adjoint1": "k_adjoint",
+                   "k_forward1": "k_forward"}.get(base, base)] = m["hbm_bytes_per_launch"]
+        payload = {"source": sys.argv[1], "hbm_bytes_per_launch": short, "kernels": res}
         with open(sys.argv[2], "w") as f:
             json.dump(payload, f, indent=1)

@@ -80,6 +80,9 @@ struct KArgs {
   float w1, w2, ws, grad_scale;
   unsigned* sync;
   int debug_nowait;   // PTYX_DEBUG_NOWAIT=1: skip the batch wait (timing experiments only; wrong gradients)
+  // k_fused2: pattern → mini-batch table and the per-pattern object-gradient slots
+  const int* bid;
+  float2* ogscr;
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -390,6 +393,8 @@ struct FinArgs {
   float w1, w2, ws, grad_scale;
   float* coef;
   float* loss_terms;
+  float2* pcoef;   // optional, per pattern: (coef[ci], c_sparse) of its mini-batch (k_obj_gather)
+  int ci;
 };
 
 __global__ void k_finalize(FinArgs f) {
@@ -438,6 +443,10 @@ __global__ void k_finalize(FinArgs f) {
   }
   if (f.loss_terms)
     for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
+  if (f.pcoef) {
+    const float2 pc = make_float2(cf[f.ci], cf[2]);
+    for (int t = b0; t < b1; ++t) f.pcoef[t] = pc;
+  }
 }
 
 // =====================================================================================
@@ -609,6 +618,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
 }
 
 #include "ptyx_single.hpp"
+#include "ptyx_fused.hpp"
 
 // Σ over workgroup slabs, fixed order.
 __global__ void k_slab_reduce(const float2* slab, int nwg, long long per, float2* out) {
@@ -696,7 +706,14 @@ struct ptyx_plan {
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* scratch = nullptr;
-  unsigned* sync = nullptr;   // k_fused1: dequeue head, error flag, per-batch arrivals
+  unsigned* sync = nullptr;   // k_fused1/2: dequeue head, error flag, per-batch arrivals
+  // k_fused2 (single mode, N <= 128): co-resident grid, per-pattern object-gradient slots
+  int nwg_fused = 0;
+  long long og_cap = 0;       // patterns per call the slots can hold (0: path unavailable)
+  float2* ogscr = nullptr;
+  int* bid = nullptr;
+  int2* geo = nullptr;
+  float2* pcoef = nullptr;
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
@@ -711,9 +728,12 @@ struct ptyx_plan {
   mutable std::vector<ProfRec> recs;
 };
 
-enum KernelKind { kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKCount };
-static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize", "k_adjoint",
-                                                  "k_slab_reduce",    "k_probe_finalize", "k_fused"};
+enum KernelKind {
+  kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather, kKCount
+};
+static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize",
+                                                  "k_adjoint",        "k_slab_reduce",    "k_probe_finalize",
+                                                  "k_fused",          "k_pattern_table",  "k_obj_gather"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -745,6 +765,20 @@ static int blocks_per_cu(int N) {
   }
 }
 
+// PTYX_ONLY_N=<n> builds a single size (kernel experiments); the shipped library has all four.
+#ifdef PTYX_ONLY_N
+#define PTYX_DISPATCH_N(N_, FN, ...) \
+  if ((N_) == PTYX_ONLY_N) FN<PTYX_ONLY_N>(__VA_ARGS__);
+#else
+#define PTYX_DISPATCH_N(N_, FN, ...)                     \
+  switch (N_) {                                          \
+    case 32: FN<32>(__VA_ARGS__); break;                 \
+    case 64: FN<64>(__VA_ARGS__); break;                 \
+    case 128: FN<128>(__VA_ARGS__); break;               \
+    case 256: FN<256>(__VA_ARGS__); break;               \
+  }
+#endif
+
 template <class T>
 static int dalloc(ptyx_plan* pl, T** p, size_t count) {
   *p = nullptr;
@@ -756,6 +790,23 @@ static int dalloc(ptyx_plan* pl, T** p, size_t count) {
   pl->ws_bytes += count * sizeof(T);
   *p = static_cast<T*>(q);
   return PTYX_OK;
+}
+
+// Workgroups of k_fused2<N> that are co-resident on the whole device (its batch wait relies
+// on every workgroup running at once); 0 when N has no fused kernel.
+template <int N>
+static int fused_resident(int cu) {
+  if constexpr (N <= 128) {
+    constexpr int NT = FusedKit<N>::NT;
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_fused2<N, true>, NT, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_fused2<N, false>, NT, 0) != hipSuccess)
+      return 0;
+    return cu * std::min(a, b);
+  } else {
+    (void)cu;
+    return 0;
+  }
 }
 
 static void free_plan(ptyx_plan* pl) {
@@ -807,6 +858,24 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->sync, ((size_t)d.max_patterns + 2 + 3) / 4 * 4))) {
     free_plan(pl);
     return rc;
+  }
+  if (lds && d.P * d.O * d.Nz == 1 && pl->fast) {
+    // one-pass path: g_O slot per pattern of a call (N² float2), bounded by PTYX_OBJ_SCRATCH_MB
+    long long mb = 16384;
+    if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
+    const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2));
+    int res = 0;
+    PTYX_DISPATCH_N(d.N, res = fused_resident, cu);
+    pl->nwg_fused = std::min(res, pl->nwg);
+    if (cap > 0 && pl->nwg_fused > 0) {
+      if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns))) {
+        free_plan(pl);
+        return rc;
+      }
+      pl->og_cap = cap;
+    }
   }
   // fp64 twiddles rounded once to fp32: tw[m] = exp(-2πi m/N)
   std::vector<float2> tw(d.N);
@@ -914,12 +983,40 @@ static void launch_fused(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
   }
 }
 template <int N>
-static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe) {
+static void launch_fused2(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
+  if constexpr (N <= 128) {
+    constexpr int NT = FusedKit<N>::NT;
+    {
+      ProfScope ps(pl, kKTable, st);
+      hipLaunchKernelGGL(k_pattern_table, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
+                         a.n_batches, a.crop, a.n_scans, a.Ny, a.Nx, N, pl->bid, pl->geo);
+    }
+    ProfScope ps(pl, kKFused, st);
+    const dim3 gr(pl->nwg_fused), bl(NT);   // every workgroup co-resident (fused_resident)
+    if (a.shift) hipLaunchKernelGGL((k_fused2<N, true>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_fused2<N, false>), gr, bl, 0, st, a);
+  }
+}
+template <int N>
+static void launch_gather(const ptyx_plan* pl, const KArgs& a, hipStream_t st, int sparse_n) {
+  if constexpr (N <= 128) {
+    GatherArgs g{};
+    g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
+    g.Ny = a.Ny; g.Nx = a.Nx; g.tiles_x = (a.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse_n;
+    g.obja = a.obja; g.objp = a.objp; g.d_obja = a.d_obja; g.d_objp = a.d_objp;
+    const int tiles = g.tiles_x * ((a.Ny + kGTY - 1) / kGTY);
+    ProfScope ps(pl, kKGather, st);
+    hipLaunchKernelGGL(k_obj_gather<N>, dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+  }
+}
+template <int N>
+static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe,
+                                  int n_slabs) {
   const long long per = (long long)pl->d.P * N * N;
   const int tb = 256;
   {
     ProfScope ps(pl, kKSlabReduce, st);
-    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + tb - 1) / tb)), dim3(tb), 0, st, pl->slab, pl->nwg,
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + tb - 1) / tb)), dim3(tb), 0, st, pl->slab, n_slabs,
                        per, pl->Gsum);
   }
   ProfScope ps(pl, kKProbeFinalize, st);
@@ -966,20 +1063,6 @@ extern "C" int ptyx_profile_end(ptyx_plan* pl, ptyx_kernel_stat* out, int32_t ca
   if (n_out) *n_out = n;
   return rc;
 }
-
-// PTYX_ONLY_N=<n> builds a single size (kernel experiments); the shipped library has all four.
-#ifdef PTYX_ONLY_N
-#define PTYX_DISPATCH_N(N_, FN, ...) \
-  if ((N_) == PTYX_ONLY_N) FN<PTYX_ONLY_N>(__VA_ARGS__);
-#else
-#define PTYX_DISPATCH_N(N_, FN, ...)                     \
-  switch (N_) {                                          \
-    case 32: FN<32>(__VA_ARGS__); break;                 \
-    case 64: FN<64>(__VA_ARGS__); break;                 \
-    case 128: FN<128>(__VA_ARGS__); break;               \
-    case 256: FN<256>(__VA_ARGS__); break;               \
-  }
-#endif
 
 static int launch_status(const char* what) {
   hipError_t e = hipGetLastError();
@@ -1052,16 +1135,30 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
   }
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
-  // one pass per pattern when the resident grid can hold every mini-batch (see k_fused1)
-  const bool fused = any_grad && pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1 &&
-                     cfg->max_batch > 0 && cfg->max_batch <= pl->nwg && !std::getenv("PTYX_TWO_PASS");
+  const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
+  // one pass per pattern (k_fused2) when every mini-batch fits the co-resident grid, the call
+  // fits the object-gradient slots and exactly one data term is on (its coefficient factors out)
+  const bool fused2 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && !std::getenv("PTYX_FUSED_V1") &&
+                      cfg->max_batch > 0 && cfg->max_batch <= pl->nwg_fused && n_idx <= pl->og_cap &&
+                      (cfg->single_on != 0) != (cfg->poissn_on != 0);
+  // earlier one-pass variant (atomics, dynamic dequeue): both data terms on, or PTYX_FUSED_V1=1
+  const bool fused = !fused2 && any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && cfg->max_batch > 0 &&
+                     cfg->max_batch <= pl->nwg;
+  if (fused2) {
+    a.bid = pl->bid;
+    a.ogscr = pl->ogscr;
+  }
 
   if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
-  if (fused) {
+  if (fused || fused2) {
     const size_t sync_bytes = ((size_t)(2 + n_batches) * sizeof(unsigned) + 15) / 16 * 16;
     hipError_t e = hipMemsetAsync(pl->sync, 0, sync_bytes, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(sync)");
-    PTYX_DISPATCH_N(pl->d.N, launch_fused, pl, a, st);
+    if (fused2) {
+      PTYX_DISPATCH_N(pl->d.N, launch_fused2, pl, a, st);
+    } else {
+      PTYX_DISPATCH_N(pl->d.N, launch_fused, pl, a, st);
+    }
     if ((rc = launch_status("k_fused launch"))) return rc;
   } else {
     PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
@@ -1073,18 +1170,27 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   f.single_on = cfg->single_on; f.pois_on = cfg->poissn_on; f.sparse_on = cfg->sparse_on;
   f.sparse_n = cfg->sparse_n; f.w1 = cfg->single_w; f.w2 = cfg->poissn_w; f.ws = cfg->sparse_w;
   f.grad_scale = cfg->grad_scale; f.coef = pl->coef; f.loss_terms = loss_terms;
+  if (fused2 && (gz.d_obja || gz.d_objp)) {
+    f.pcoef = pl->pcoef;
+    f.ci = cfg->single_on ? 0 : 1;
+  }
   {
     ProfScope ps(pl, kKFinalize, st);
     hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
   }
   if ((rc = launch_status("k_finalize launch"))) return rc;
   if (!any_grad) return PTYX_OK;
-  if (!fused) {
+  if (fused2) {
+    if (gz.d_obja || gz.d_objp) {
+      PTYX_DISPATCH_N(pl->d.N, launch_gather, pl, a, st, cfg->sparse_on ? cfg->sparse_n : 1);
+      if ((rc = launch_status("k_obj_gather launch"))) return rc;
+    }
+  } else if (!fused) {
     PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
     if ((rc = launch_status("k_adjoint launch"))) return rc;
   }
   if (gz.d_probe) {
-    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe);
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, fused2 ? pl->nwg_fused : pl->nwg);
     if ((rc = launch_status("probe finalize launch"))) return rc;
   }
   return PTYX_OK;
@@ -1114,7 +1220,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, true);
   if ((rc = launch_status("k_adjoint(ext) launch"))) return rc;
   if (gz.d_probe) {
-    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe);
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, pl->nwg);
     if ((rc = launch_status("probe finalize launch"))) return rc;
   }
   return PTYX_OK;

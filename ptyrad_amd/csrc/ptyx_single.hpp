@@ -17,6 +17,32 @@
 #ifndef PTYX_ADJ_PREFETCH_SLAB
 #define PTYX_ADJ_PREFETCH_SLAB 0
 #endif
+// Cost-attribution knobs (experiments only, results are wrong with them set): drop the object
+// gradient atomics / the probe slab update from the fused kernel.
+#ifndef PTYX_EXP_NO_OBJ_ATOMIC
+#define PTYX_EXP_NO_OBJ_ATOMIC 0
+#endif
+#ifndef PTYX_EXP_NO_SLAB
+#define PTYX_EXP_NO_SLAB 0
+#endif
+// PTYX_EXP_PHASE_TIMES=1: barrier + s_memrealtime stamp at every phase boundary of k_fused1;
+// workgroups 0 and 128 printf their per-phase totals (µs) at exit.
+#ifndef PTYX_EXP_PHASE_TIMES
+#define PTYX_EXP_PHASE_TIMES 0
+#endif
+#if PTYX_EXP_PHASE_TIMES
+#define PTYX_PHASE(k)                            \
+  do {                                           \
+    __syncthreads();                             \
+    const unsigned long long _t = wall_clock64(); \
+    ph_acc[k] += _t - ph_prev;                   \
+    ph_prev = _t;                                \
+  } while (0)
+#else
+#define PTYX_PHASE(k) \
+  do {                \
+  } while (0)
+#endif
 //
 // All prefetches are unconditional and every switch that decides whether a register array is
 // written is a template parameter: a conditionally written array is loop-carried by the
@@ -387,10 +413,18 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
   const float occ = a.occu[0];
   if (threadIdx.x == 0) s_pat = (int)atomicAdd(head, 1u);
   __syncthreads();
+#if PTYX_EXP_PHASE_TIMES
+  unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph_prev = wall_clock64();
+  int ph_n = 0;
+#endif
 
   for (;;) {
     const int pat = s_pat;
     if (pat >= a.n_idx) break;
+#if PTYX_EXP_PHASE_TIMES
+    ++ph_n;
+#endif
     int m;
     {
       int lo = 0, hi = a.n_batches;
@@ -417,8 +451,10 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
         sp += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
       }
     }
+    PTYX_PHASE(0);
     float2 pb[SL];   // ψ⁰
     exit_wave<N, NT, SHIFT>(a, arr, s_tw, s_wy, s_wx, tid, fp, oa, op, [&](float2 w, int s) { pb[s] = w; });
+    PTYX_PHASE(1);
     float mv[SL];
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
@@ -447,6 +483,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
           }
           return true;
         });
+    PTYX_PHASE(2);
     {
       float v5[5] = {sums[0], sums[1], sums[2], sums[3], sp};
       block_sum<NT, 5>(v5, s_red);
@@ -476,6 +513,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
       }
       __syncthreads();
     }
+    PTYX_PHASE(3);
     // batch coefficients (wave 0, after the barrier its polling lane joined; sc1 loads, as the
     // sums were stored sc1; identical fixed-order reduction in every workgroup)
     if (threadIdx.x < 64) {
@@ -515,6 +553,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
       }
     }
     __syncthreads();
+    PTYX_PHASE(4);
     const float c1 = s_coef[0], c2 = s_coef[1], csp = s_coef[2];
     // g_Ψ = 2 occ Ψ ∂L/∂I into LDS (the far-field pass's own point order)
 #pragma unroll
@@ -535,6 +574,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
       if (PM::last_active(tid, s)) arr.st(y, x, cscale(Psi, 2.0f * occ * dLdI));
     }
     __syncthreads();
+    PTYX_PHASE(5);
     // back to real space; object gradient (scatter-add); g ⊙ conj(O) into LDS
     fft2d<N, NT, +1, true>(
         arr, s_tw, [&](int, int, float2 v, int) { return v; },
@@ -545,6 +585,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
           float sn, cs;
           phase_sincos(ph, &sn, &cs);
           const float2 gO = cmulc(gv, pb[s]);
+#if !PTYX_EXP_NO_OBJ_ATOMIC
           if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));
           if (a.d_objp) {
             float dph = A * fmaf(gO.y, cs, -gO.x * sn);
@@ -554,9 +595,13 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
             }
             atomicAdd(a.d_objp + off, dph);
           }
+#else
+          if (gO.x == 1234.5f) a.d_obja[off] = gO.y;   // keep gO live
+#endif
           v = cmulc(gv, make_float2(A * cs, A * sn));
           return true;
         });
+    PTYX_PHASE(6);
     if constexpr (SHIFT) {
       if (a.need_probe || a.d_shifts) {
         float ds[2] = {0.f, 0.f};
@@ -567,7 +612,9 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
               const float im = cmulc(cmul(a.Fp[y * N + x], W), G).y;
               ds[0] = fmaf(6.283185307179586f * shift_g<N>(y), im, ds[0]);
               ds[1] = fmaf(6.283185307179586f * shift_g<N>(x), im, ds[1]);
+#if !PTYX_EXP_NO_SLAB
               if (a.need_probe) slab[y * N + x] = cadd(slab[y * N + x], cmulc(G, W));
+#endif
               return false;
             });
         if (a.d_shifts) {
@@ -589,5 +636,12 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
       }
     }
     __syncthreads();
+    PTYX_PHASE(7);
   }
+#if PTYX_EXP_PHASE_TIMES
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 128))
+    printf("PHASES wg %d n %d us: pre %.1f ifft1 %.1f fft2 %.1f wait %.1f coef %.1f gpsi %.1f ifft3 %.1f fft4 %.1f\n",
+           (int)blockIdx.x, ph_n, ph_acc[0] * 0.01, ph_acc[1] * 0.01, ph_acc[2] * 0.01, ph_acc[3] * 0.01,
+           ph_acc[4] * 0.01, ph_acc[5] * 0.01, ph_acc[6] * 0.01, ph_acc[7] * 0.01);
+#endif
 }

@@ -38,6 +38,26 @@ struct Impl<N, 1> {
   }
 };
 
+// V2 / V3: the V0 Stockham transform with 1/2 and 1/4 of the threads (more registers per thread)
+template <int N>
+struct Impl<N, 2> {
+  static constexpr int NT = Impl<N, 0>::NT / 2;
+  using Arr = LdsArray<N>;
+  template <int DIR, class Post>
+  __device__ static void fft(const Arr& a, const float2* tw, Post&& post) {
+    fft2d<N, NT, DIR, true>(a, tw, [](int, int, float2 v) { return v; }, post);
+  }
+};
+template <int N>
+struct Impl<N, 3> {
+  static constexpr int NT = Impl<N, 0>::NT / 4;
+  using Arr = LdsArray<N>;
+  template <int DIR, class Post>
+  __device__ static void fft(const Arr& a, const float2* tw, Post&& post) {
+    fft2d<N, NT, DIR, true>(a, tw, [](int, int, float2 v) { return v; }, post);
+  }
+};
+
 template <int N, int V>
 __global__ __launch_bounds__((Impl<N, V>::NT)) void fft_loop(const float2* in, float2* out, const float2* twg,
                                                             int iters, int forward_only) {
@@ -139,6 +159,8 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(dtw, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice);
     rc |= run<N, 0>(iters, grid, h, din, dout, dtw);
     rc |= run<N, 1>(iters, grid, h, din, dout, dtw);
+    rc |= run<N, 2>(iters, grid, h, din, dout, dtw);
+    rc |= run<N, 3>(iters, grid, h, din, dout, dtw);
     (void)hipFree(din);
     (void)hipFree(dout);
     (void)hipFree(dtw);
