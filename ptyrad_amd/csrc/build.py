@@ -38,7 +38,7 @@ def build(force: bool = False, only_n: int | None = None, out: str = OUT, extra=
     if not force and only_n is None and up_to_date(out):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", *SOURCES]
     if only_n:
         cmd.insert(2, f"-DPTYX_ONLY_N={only_n}")

@@ -1,0 +1,185 @@
+// ptyx_common.hpp — constants, kernel argument block and small device helpers shared by every
+// ptyx kernel (ptyx_kernels.hip and the per-engine headers it includes).
+#pragma once
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include "ptyx_fft.hpp"
+
+namespace ptyx {
+
+constexpr int kMaxModesO = 8;
+constexpr int kSumBase = 4;                    // [S_single, ΣM^q1, S_poissn, ΣM^q2] then O sparse sums
+constexpr int kNSum = kSumBase + kMaxModesO;
+constexpr int kNCoef = 2 + kMaxModesO;         // [c_single, c_poissn, c_sparse[o]...]
+constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
+
+template <int N> struct Geo;
+template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true; };
+template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true; };
+template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true; };
+template <> struct Geo<256> { static constexpr int NT = 1024; static constexpr bool kLds = false; };
+
+struct KArgs {
+  int P, O, Nz, Ny, Nx, n_scans;
+  int shift, meas_f16;
+  const float* obja;
+  const float* objp;
+  const float2* probe;
+  const float2* Fp;
+  const float* shifts;
+  const int* crop;
+  const float2* H;
+  const float* occu;
+  const void* meas;
+  const int* idx;
+  int n_idx;
+  const int* boff;
+  int n_batches;
+  int single_on, pois_on, sparse_on, sparse_n;
+  float q1, q2, eps2;
+  const float* coef;
+  float* psums;
+  float* Ibuf;
+  float* dp_out;
+  const float* dLdI_ext;
+  float ext_scale;
+  float* d_obja;
+  float* d_objp;
+  float* d_shifts;
+  int need_probe;
+  float2* slab;
+  float2* scratch;
+  long long scratch_stride;
+  const float2* twg;
+  // one-pass fused kernel: loss weights and the per-call sync words
+  // sync[0] = dequeue head, sync[1] = error flag (spin timeout), sync[2 + m] = arrivals of batch m
+  float w1, w2, ws, grad_scale;
+  unsigned* sync;
+  int debug_nowait;   // PTYX_DEBUG_NOWAIT=1: skip the batch wait (timing experiments only; wrong gradients)
+  // k_fused2: pattern → mini-batch table and the per-pattern object-gradient slots
+  const int* bid;
+  float2* ogscr;
+};
+
+// ---------------------------------------------------------------- small helpers
+// threadIdx.x behind an empty asm: per-pattern address arithmetic stays inside the pattern
+// loop instead of being hoisted (and spilled) by loop-invariant code motion.
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// x^q for x >= 0 (DP intensities): exact forms for the schema values 0.5 / 1, otherwise
+// exp2(q·log2 x) on the v_exp_f32 / v_log_f32 units (no libm slow path in the fused epilogues).
+__device__ __forceinline__ float powq(float x, float q) {
+  if (q == 0.5f) return sqrtf(x);
+  if (q == 1.0f) return x;
+  if (!(x > 0.f)) return q > 0.f ? 0.f : __builtin_inff();
+  return __builtin_amdgcn_exp2f(q * __builtin_amdgcn_logf(x));
+}
+
+__device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+
+// sin/cos of an object phase: reduce to revolutions in [-1/2, 1/2], then v_sin_f32 / v_cos_f32
+// (which take revolutions).  Absolute error ≈ |φ|·6e-8 + 1 ulp, far inside the parity budget.
+__device__ __forceinline__ void phase_sincos(float ph, float* sn, float* cs) {
+  float r = ph * 0.15915494309189535f;
+  r = r - rintf(r);
+  *sn = __builtin_amdgcn_sinf(r);
+  *cs = __builtin_amdgcn_cosf(r);
+}
+
+__device__ __forceinline__ float meas_at(const KArgs& a, int s, int e, int N2) {
+  const size_t off = (size_t)s * N2 + e;
+  if (a.meas_f16) return __half2float(reinterpret_cast<const __half*>(a.meas)[off]);
+  return reinterpret_cast<const float*>(a.meas)[off];
+}
+
+__device__ __forceinline__ size_t obj_off(const KArgs& a, int o, int n, int yy, int xx) {
+  return ((size_t)(o * a.Nz + n) * a.Ny + yy) * a.Nx + xx;
+}
+
+// wave64 + workgroup sum of NV floats, fixed order (deterministic); result valid in thread 0.
+template <int NT, int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v[i] += __shfl_xor(v[i], m, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[wv * NV + i] = v[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float t = 0.f;
+      for (int w = 0; w < NT / 64; ++w) t += red[w * NV + i];
+      v[i] = t;
+    }
+  }
+  __syncthreads();
+}
+
+struct PatternGeom {
+  int s, cy, cx;
+  float sy, sx;
+};
+
+__device__ __forceinline__ PatternGeom pattern_geom(const KArgs& a, int pat, int N) {
+  PatternGeom g;
+  int s = a.idx[pat];
+  s = min(max(s, 0), a.n_scans - 1);  // defensive clamp; the host validates indices
+  g.s = s;
+  g.cy = min(max(a.crop[2 * s], 0), a.Ny - N);
+  g.cx = min(max(a.crop[2 * s + 1], 0), a.Nx - N);
+  g.sy = a.shifts[2 * s];
+  g.sx = a.shifts[2 * s + 1];
+  return g;
+}
+
+// W_b ramps along y and x: exp(-2πi s g[k]), g[k] = ((k + N/2) mod N)/N  (image_proc.py:531,
+// models.py:179 grid arange(N)/N after ifftshift).
+template <int N, int NT>
+__device__ __forceinline__ void build_ramps(const PatternGeom& g, float2* wy, float2* wx) {
+  for (int k = opaque_tid(); k < 2 * N; k += NT) {
+    const int kk = k % N;
+    const float gr = (float)((kk + N / 2) % N) / (float)N;
+    const float s = k < N ? g.sy : g.sx;
+    float sn, cs;
+    sincospif(-2.0f * s * gr, &sn, &cs);
+    (k < N ? wy : wx)[kk] = make_float2(cs, sn);
+  }
+  __syncthreads();
+}
+
+template <int N>
+__device__ __forceinline__ float shift_g(int k) {
+  return (float)((k + N / 2) % N) / (float)N;
+}
+
+template <int N, bool LDS>
+struct ArrayFor;
+template <int N>
+struct ArrayFor<N, true> {
+  using type = LdsArray<N>;
+};
+template <int N>
+struct ArrayFor<N, false> {
+  using type = GlobalPair<N>;
+};
+
+// Scratch layout per workgroup (float2 units): [fft a, fft b (N=256 only)] [psi: Nz·N²] [gacc: N²]
+template <int N>
+__device__ __forceinline__ float2* scratch_psi(const KArgs& a) {
+  return a.scratch + (long long)blockIdx.x * a.scratch_stride + (Geo<N>::kLds ? 0 : 2 * N * N);
+}
+
+constexpr unsigned kMaxSpins = 1u << 24;   // ≈1 s of s_sleep polling (bounded batch waits)
+
+}  // namespace ptyx

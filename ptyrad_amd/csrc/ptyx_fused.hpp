@@ -344,7 +344,8 @@ struct GatherArgs {
 };
 constexpr int kGTX = 64, kGTY = 16, kGWaves = 4;
 
-template <int N>
+// ROWPERM: slots written by k_fused3 (N = 128), row y stored at row 2(y & 63) + (y >> 6).
+template <int N, bool ROWPERM = false>
 __global__ __launch_bounds__(64 * kGWaves) void k_obj_gather(GatherArgs ga) {
   constexpr int N2 = N * N;
   __shared__ float2 s_acc[kGTY * kGTX];
@@ -381,7 +382,8 @@ __global__ __launch_bounds__(64 * kGWaves) void k_obj_gather(GatherArgs ga) {
 #pragma unroll
       for (int r = 0; r < kGTY; ++r) {
         const int row = ty + r - cy;
-        v[r] = (colok && row >= 0 && row < N) ? src[row * N + col] : make_float2(0.f, 0.f);
+        const int srow = ROWPERM ? 2 * (row & (N / 2 - 1)) + (row >> 6) : row;
+        v[r] = (colok && row >= 0 && row < N) ? src[srow * N + col] : make_float2(0.f, 0.f);
       }
 #pragma unroll
       for (int r = 0; r < kGTY; ++r) {

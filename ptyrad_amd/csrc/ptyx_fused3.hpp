@@ -1,0 +1,604 @@
+// ptyx_fused3.hpp — one-pass forward / loss / adjoint for N = 128, P = O = Nz = 1 (the bench
+// configuration c2, and c1) on the register-resident FFT of ptyx_regfft.hpp.  Included by
+// ptyx_kernels.hip.
+//
+// One 256-thread workgroup owns one pattern; two workgroups per CU (64 KiB LDS, ≤ 256 VGPRs
+// each), so two patterns are in flight per CU and one hides the other's barrier and memory
+// waits.  Per pattern (reference forward.py:20-80, losses.py:36-104, autograd):
+//
+//   K layout  v = F(P)·W_b                     F(P) K-packed, W_b = exp(-2πi s_b·g) (image_proc.py:531)
+//   IFFT  →   ψ⁰ = F⁻¹(v)/N²                   R layout; ψ⁰ parked in this pattern's slot
+//             ψ  = ψ⁰·O                        O = A e^{iφ} precomputed per call (k_obj_prep)
+//   FFT   →   Ψ  = F(ψ)/N                      the DP streams HBM → LDS (LDS-DMA) meanwhile
+//             I  = occ|Ψ|² + 1e-10, loss partial sums, g_Ψ/c_m = 2 occ Ψ ∂ℓ/∂I (unit coefficient)
+//   IFFT  →   g  = F⁻¹(g_Ψ)/N                  R layout
+//             slot = g·conj(ψ⁰)   (object gradient per unit c_m; k_obj_gather reduces the slots)
+//             h    = g·conj(O)
+//   wait for mini-batch m (arrival counter), c_m from its partial sums (k_finalize arithmetic)
+//   FFT   →   G  = F(h)                        K layout
+//             slab += c_m G conj(W_b);  d_shift += c_m 2π/N² Σ g·Im(F(P) W_b conj(G))
+//
+// Every global operand is laid out so that one register's access is contiguous across lanes:
+// F(P) and the slab are K-packed ([k][thread]); slots are stored row-permuted
+// (row' = 2(y & 63) + (y >> 6)); object rows are read 2 × 256 B per wave instruction; the DP
+// lands in LDS through 1 KiB global_load_lds_dwordx4 instructions with an XOR-swizzled source
+// so that the K-layout ds_read_b128 of it are bank-conflict free.
+// The sparse loss needs no per-pattern FFT work: its window sums come from per-row prefix
+// sums (k_obj_prep, k_pattern_table3).
+#pragma once
+#include "ptyx_common.hpp"
+#include "ptyx_regfft.hpp"
+
+namespace ptyx {
+namespace f3 {
+
+constexpr int kN = 128, kN2 = kN * kN;
+
+__device__ __forceinline__ int fixed_of(int t) { return ((t & 63) >> 1) | ((t >> 6) << 5); }
+
+// (cos 2πx, sin 2πx) for x in revolutions (v_cos_f32 / v_sin_f32 after reduction to [-1/2, 1/2])
+__device__ __forceinline__ float2 cis_rev(float x) {
+  const float r = x - rintf(x);
+  return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
+}
+
+struct F3Args {
+  int n_idx, n_scans, Ny, Nx;
+  const int* idx;          // scan index per pattern
+  const int* bid;          // mini-batch per pattern
+  const int2* geo;         // clamped window origin (cy, cx) per pattern
+  const int* boff;         // mini-batch offsets
+  const float* shifts;     // (n_scans, 2)
+  const float2* fpk;       // SHIFT: F(probe) K-packed; else the probe R-packed
+  const float2* oc;        // A e^{iφ}, (Ny, Nx)
+  const float* meas;       // (n_scans, 128, 128) f32, fftshifted
+  const float* occp;       // omode_occu (device), occ = occp[0]
+  float q, eps2, w, grad_scale;
+  float* psums;
+  unsigned* sync;          // [dequeue head (unused), error flag, arrivals per mini-batch]
+  int debug_nowait;
+  float2* slots;           // per-pattern object-gradient slots (row-permuted)
+  float2* slab;            // per-workgroup probe-gradient partials (K-packed / R-packed)
+  float* d_shifts;
+  int need_probe;
+  float* dp_out;
+};
+
+// Packed layouts (thread t = 0..255, register i = 0..63):
+//   K: (row, col) = (ky, kx) = (fixed(t), i + 64·(t & 1))
+//   R: (row, col) = (y, x)   = (i + 64·(t & 1), fixed(t))
+template <bool KL>
+__device__ __forceinline__ int packed_rc(int t, int i) {
+  const int f = fixed_of(t), o = i + 64 * (t & 1);
+  return KL ? f * kN + o : o * kN + f;
+}
+
+// natural (N×N complex) → packed, one element per thread
+template <bool KL>
+__global__ void k_pack128(const float2* src, float2* dst) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kN2) return;
+  const int i = e >> 8, t = e & 255;
+  dst[e] = src[packed_rc<KL>(t, i)];
+}
+
+// Σ over workgroup slabs (packed, fixed order) → natural Gsum
+template <bool KL>
+__global__ void k_slab_reduce3(const float2* slab, int nwg, float2* out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kN2) return;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int w = 0; w < nwg; ++w) acc = cadd(acc, slab[(size_t)w * kN2 + e]);
+  out[packed_rc<KL>(e & 255, e >> 8)] = acc;
+}
+
+// Per call: complex object O = A e^{iφ} (the fused kernel then needs no transcendental per
+// object point), and — for loss_sparse — per-row fp64 prefix sums of |φ|^n:
+// pref[y][x] = Σ_{x' < x} |φ(y, x')|^n, x = 0..Nx.  One workgroup per object row.
+__global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx, float2* oc, double* pref,
+                           int sparse_n) {
+  __shared__ double s_part[256];
+  const int y = blockIdx.x;
+  const float* ar = obja + (size_t)y * Nx;
+  const float* pr = objp + (size_t)y * Nx;
+  float2* orow = oc + (size_t)y * Nx;
+  for (int x = threadIdx.x; x < Nx; x += blockDim.x) {
+    float sn, cs;
+    phase_sincos(pr[x], &sn, &cs);
+    orow[x] = make_float2(ar[x] * cs, ar[x] * sn);
+  }
+  if (!pref) return;
+  // contiguous chunk per thread, exclusive scan of the chunk sums in thread order (fixed order)
+  const int per = (Nx + blockDim.x - 1) / blockDim.x;
+  const int x0 = threadIdx.x * per, x1 = min(Nx, x0 + per);
+  double sum = 0;
+  for (int x = x0; x < x1; ++x) {
+    const float ap = fabsf(pr[x]);
+    sum += sparse_n == 1 ? (double)ap : (double)powq(ap, (float)sparse_n);
+  }
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double run = 0;
+    for (int i = 0; i < (int)blockDim.x; ++i) {
+      const double t = s_part[i];
+      s_part[i] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+  double* prow = pref + (size_t)y * (Nx + 1);
+  double run = s_part[threadIdx.x];
+  for (int x = x0; x < x1; ++x) {
+    prow[x] = run;
+    const float ap = fabsf(pr[x]);
+    run += sparse_n == 1 ? (double)ap : (double)powq(ap, (float)sparse_n);
+  }
+  if (x1 == Nx && x0 < x1) prow[Nx] = run;
+  if (Nx == 0 && threadIdx.x == 0) prow[0] = 0;
+}
+
+// pattern → (mini-batch, clamped window origin) and, with pref, the loss_sparse window sum
+// Σ_{window} |φ|^n into psums[kSumBase] (fp64 over rows, fixed order).  One wave per pattern.
+__global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_batches, const int* crop,
+                                 int n_scans, int Ny, int Nx, int* bid, int2* geo, const double* pref,
+                                 float* psums) {
+  const int j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n) return;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
+  if (lane == 0) {
+    int lo = 0, hi = n_batches;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (boff[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    bid[j] = lo;
+    geo[j] = make_int2(cy, cx);
+  }
+  if (!pref) return;
+  double acc = 0;
+  for (int r = lane; r < kN; r += 64) {
+    const double* prow = pref + (size_t)(cy + r) * (Nx + 1);
+    acc += prow[cx + kN] - prow[cx];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) psums[(size_t)j * kNSum + kSumBase] = (float)acc;
+}
+
+// Far-field loss at one point, branch-free.  Returns u = ∂ℓ/∂I per unit mini-batch coefficient
+// and accumulates the partial sums (S, ΣM^q):
+//   SINGLE: ℓ ∝ Σ(I^q − M^q)²          (losses.py:45-47),  u = (I^q − M^q)·q·I^q/I
+//   else:   ℓ ∝ Σ(M^q ln(I^q+ε) − I^q) (losses.py:70-72),  u = (M^q/(I^q+ε) − 1)·q·I^q/I
+// QM: 0 → q = 1/2 (sqrt / rsqrt), 1 → q = 1, 2 → general q (exp2(q·log2 x)); I ≥ 1e-10 > 0.
+// (The kernel is instantiated for QM 0 and 2 only: q = 1 runs the general form.)
+template <int QM, bool SINGLE>
+__device__ __forceinline__ float loss_point(float I, float M, float q, float eps2, float& S, float& Ms) {
+  float Iq, Mq, qIqI;   // qIqI = q·I^q/I
+  if constexpr (QM == 0) {
+    const float r = __builtin_amdgcn_rsqf(I);
+    Iq = I * r;
+    Mq = __builtin_amdgcn_sqrtf(M);
+    qIqI = 0.5f * r;
+  } else if constexpr (QM == 1) {
+    Iq = I;
+    Mq = M;
+    qIqI = 1.0f;
+  } else {
+    Iq = __builtin_amdgcn_exp2f(q * __builtin_amdgcn_logf(I));
+    Mq = M > 0.f ? __builtin_amdgcn_exp2f(q * __builtin_amdgcn_logf(M)) : (q > 0.f ? 0.f : __builtin_inff());
+    qIqI = q * Iq * __builtin_amdgcn_rcpf(I);
+  }
+  Ms += Mq;
+  if constexpr (SINGLE) {
+    const float d = Iq - Mq;
+    S = fmaf(d, d, S);
+    return d * qIqI;
+  } else {
+    const float ip = Iq + eps2;
+    S += Mq * fast_ln(ip) - Iq;
+    return fmaf(Mq, __builtin_amdgcn_rcpf(ip), -1.0f) * qIqI;
+  }
+}
+
+// Buffer-resource access with 32-bit VGPR offsets (base + per-register constant, one v_add each;
+// soffset 0).  Plain global loads would need a 64-bit address VGPR pair per register once the
+// offsets pass the 4 KiB immediate range, and per-register SGPR soffsets get hoisted out of the
+// pattern loop by MachineLICM (≈200 SGPRs, spilled).
+using Rsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ Rsrc rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float2 ld2(Rsrc r, int voff, int off) {
+  const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, voff + off, 0, 0);
+  return make_float2(__uint_as_float(u[0]), __uint_as_float(u[1]));
+}
+__device__ __forceinline__ void st2(float2 v, Rsrc r, int voff, int off) {
+  const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v.x), __float_as_uint(v.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, 0);
+}
+
+// Wave sum in a fixed order, result in every lane: DPP adds within each 16-lane row
+// (pairs, quads, half-rows, rows), then the four row sums via v_readlane.  No ds_bpermute,
+// no per-step lane-index arithmetic (which spills beside 128 live data VGPRs).
+template <int CTRL>
+__device__ __forceinline__ float dppmov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  x += dppmov<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dppmov<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dppmov<0x141>(x);   // row_half_mirror
+  x += dppmov<0x140>(x);   // row_mirror
+  const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+  const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+  const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+  const float a3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+  return (a0 + a1) + (a2 + a3);
+}
+// Workgroup (4 waves) sum of NV floats in a fixed order; result valid in every thread.
+template <int NV>
+__device__ __forceinline__ void block_sum4(float (&v)[NV], float* red) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[wv * NV + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = (red[i] + red[NV + i]) + (red[2 * NV + i] + red[3 * NV + i]);
+  __syncthreads();
+}
+
+// Pin a value at this point of the program (empty volatile asm that "redefines" it): the
+// compiler can no longer sink its computation towards a later use, which otherwise keeps every
+// intermediate of a 64-register pass live across barriers and spills.
+__device__ __forceinline__ void pin(float2& v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
+
+// Software-pipelined pass over the 64 registers in NC chunks: chunk c+1's global loads are
+// issued before chunk c is consumed, and a scheduling barrier after every chunk keeps the
+// compiler from hoisting all 64 loads at once (which would need 128+ extra VGPRs and spill).
+template <int NC, class Ld, class Use>
+__device__ __forceinline__ void pipeline(Ld&& ld, Use&& use) {
+  auto cur = ld(std::integral_constant<int, 0>{});
+  rf::sfor<0, NC>([&](auto C) {
+    constexpr int c = decltype(C)::value;
+    if constexpr (c + 1 < NC) {
+      auto nxt = ld(std::integral_constant<int, c + 1>{});
+      use(C, cur);
+      __builtin_amdgcn_sched_barrier(0);
+      cur = nxt;
+    } else {
+      use(C, cur);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+}
+struct Ch8 {
+  float2 x[8];
+};
+struct Ch4x2 {
+  float2 x[4], y[4];
+};
+
+// QM: 0 → dp_pow q = 1/2 (sqrt / rsqrt), 2 → general q (see loss_point)
+template <bool SHIFT, bool SINGLE, int QM>
+__global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
+  using namespace rf;
+  __shared__ float2 buf[kLdsElems];
+  __shared__ float s_red[4 * 2];
+  __shared__ float s_c;
+  const Coord cd = coord(threadIdx.x);
+  const LaneCtx lc = lane_ctx(cd.lane);
+  constexpr float inv_n = 1.0f / kN, inv_n2 = 1.0f / kN2;
+  {
+    // the slab is always updated (branch-free passes); without a probe gradient it is not reduced
+    float2* slab = a.slab + (size_t)blockIdx.x * kN2 + threadIdx.x;
+    for (int k = 0; k < 64; ++k) slab[k * 256] = make_float2(0.f, 0.f);   // own entries only
+  }
+  unsigned* err = a.sync + 1;
+  unsigned* arrive = a.sync + 2;
+  const float occ = a.occp[0], q = a.q;
+  const bool tail = a.need_probe || a.d_shifts;   // (uniform)
+  const int Nx = a.Nx;
+
+  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
+    // per-thread bases re-derived from an opaque thread id each pattern: keeps LICM from hoisting
+    // 64 per-register addresses out of the pattern loop (they would spill)
+    asm volatile("" ::: "memory");   // no memory operation of one pattern moves into another
+    const int tid = rf::opaque(threadIdx.x);
+    const int fx = fixed_of(tid);
+    const int l0 = tid & 1;
+    const int m = a.bid[pat];
+    const int2 g = a.geo[pat];
+    // packed arrays ([register][thread]): voff = 8·tid, soff = 2048·register
+    const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
+    const Rsrc r_slab = rsrc(a.slab + (size_t)blockIdx.x * kN2, kN2 * 8);
+    // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → soff = 2048·j
+    const Rsrc r_slot = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
+    const int vslot0 = 8 * (l0 * kN + fx);
+    // object window: element (j + 64 l0, fx) → soff = 8·Nx·j
+    const Rsrc r_obj = rsrc(a.oc + (size_t)g.x * Nx + g.y, (unsigned)(((kN - 1) * Nx + kN) * 8));
+    const int vobj0 = 8 * (64 * l0 * Nx + fx);
+    const int ostr0 = 8 * Nx;   // register j's object offset is vobj + j·ostr
+    const int sidx = min(max(a.idx[pat], 0), a.n_scans - 1);
+    float sy0 = 0.f, sx0 = 0.f;
+    if constexpr (SHIFT) {
+      sy0 = a.shifts[2 * sidx];
+      sx0 = a.shifts[2 * sidx + 1];
+    }
+    const float sy = sy0, sx = sx0;
+    const float gy = (float)((fx + 64) & 127) * inv_n;   // ifftshifted grid of this thread's ky
+    // W(ky, kx = 4qq + r + 64 l0) = A(qq)·B(r): exp(-2πi(sy gy + sx gx)), g = ((k + 64) mod 128)/128
+    auto ramp_a = [&](int qq) { return cis_rev(-fmaf(sy, gy, sx * (float)(4 * qq + 64 * (1 - l0)) * inv_n)); };
+    float2 v[64];
+    // Every pass below re-derives its per-register offsets / ramp arguments from opaque copies
+    // (rf::opaque): otherwise CSE shares them between passes that are an FFT or two apart and
+    // keeps ~64-128 extra values live across the transforms (spilled).
+    // ------------------------------------------------ ψ⁰ = F⁻¹(F(P)·W_b)  (R layout)
+    if constexpr (SHIFT) {
+      const int vpk = rf::opaque(8 * tid);
+      const int l0 = rf::opaque(tid) & 1;
+      float2 B[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) B[r] = cis_rev(-sx * (float)r * inv_n);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = ramp_a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[4 * C + r] = cmul(t.x[r], cmul(A, B[r]));
+              pin(v[4 * C + r]);
+            }
+          });
+      fft_inv(v, buf, lc, cd.wsign);
+#pragma unroll
+      for (int j = 0; j < 64; ++j) v[j] = cscale(v[j], inv_n2);
+    } else {
+      const int vpk = rf::opaque(8 * tid);
+      pipeline<8>(
+          [&](auto C) {
+            Ch8 t;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (8 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch8& t) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[8 * C + r] = t.x[r];
+          });
+    }
+    // ------------------------------------------------ park ψ⁰; ψ = ψ⁰·O
+    {
+    const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+    pipeline<8>(
+        [&](auto C) {
+          Ch8 t;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch8& t) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int j = 8 * C + r;
+            st2(v[j], r_slot, vslot, 2048 * j);
+            v[j] = cmul(v[j], t.x[r]);
+            pin(v[j]);
+          }
+        });
+    }
+    // ------------------------------------------------ far field; DP → LDS during the row DFTs
+    const float* dp = a.meas + (size_t)sidx * kN2;
+    fft_fwd(v, buf, lc, cd.wsign, [&] {
+      const int lane = cd.lane;
+      const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int gi = wv * 16 + i;                // rows 2gi, 2gi+1 (1 KiB)
+        const int r = 2 * gi + (lane >> 5);
+        const int sl = lane & 31;
+        const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
+        __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
+                                         (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
+                                         0);
+      }
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float S = 0.f, Ms = 0.f;
+    {
+      const int r = (fx + 64) & 127;               // fftshifted DP row of ky
+      const int b = 1 - l0;                        // fftshifted column half of kx = k + 64 l0
+      const float4* row4 = reinterpret_cast<const float4*>(buf) + r * 32;
+      // dp_out through a buffer resource with num_records 0 when not requested: the stores are
+      // dropped by the hardware bounds check, so the loop has no branch
+      const Rsrc r_dp = rsrc(a.dp_out ? a.dp_out + (size_t)pat * kN2 : a.psums, a.dp_out ? kN2 * 4 : 0);
+      const int vdp = 4 * (r * kN + 64 * b);
+#pragma unroll
+      for (int kq = 0; kq < 16; ++kq) {
+        const float4 M4 = row4[(kq + 16 * b) ^ ((r & 7) | (b << 3))];
+        const float Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+        float Iv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * kq + e;
+          const float2 Psi = cscale(v[k], inv_n);
+          Iv[e] = fmaf(occ, cabs2(Psi), kDpEps);
+          const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+          v[k] = cscale(Psi, 2.0f * occ * u);
+          pin(v[k]);
+        }
+        {
+          const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, i4),
+                                                 r_dp, vdp + 16 * kq, 0, 0);
+        }
+        if (kq & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    {
+      // (block_sum's first barrier also retires every wave's DP reads before the next exchange)
+      float v2[2] = {S, Ms};
+      block_sum4<2>(v2, s_red);
+      if (tid == 0) {
+        float* ps = a.psums + (size_t)pat * kNSum;
+        const int base = SINGLE ? 0 : 2;
+        __hip_atomic_store(ps + base, v2[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ps + base + 1, v2[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ps + (2 - base), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ps + (3 - base), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(arrive + m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // ------------------------------------------------ back to real space
+    fft_inv(v, buf, lc, cd.wsign);
+    {
+    const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = 4 * C + r;
+            t.x[r] = ld2(r_slot, vslot, 2048 * j);
+            t.y[r] = ld2(r_obj, vobj, ostr * j);
+          }
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = 4 * C + r;
+            const float2 gv = cscale(v[j], inv_n);
+            st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+            v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
+            pin(v[j]);
+          }
+        });
+    }
+    if (!tail) continue;
+    // ------------------------------------------------ c_m of this mini-batch
+    // Wave 0 only (scalar branch) and no lane divergence inside: every lane polls the same
+    // arrival word, loads one pattern's partial sums (clamped index, masked value) and forms the
+    // same fixed-order fp64 sums, so the 128 live data VGPRs see no divergent region.
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+      const int lane = cd.lane;
+      const int b0 = a.boff[m], b1 = a.boff[m + 1];
+      const unsigned want = (unsigned)(b1 - b0);
+      unsigned spins = 0;
+      while (!a.debug_nowait && __hip_atomic_load(arrive + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kMaxSpins) {
+          atomicOr(err, 1u);
+          break;
+        }
+      }
+      const int base = SINGLE ? 0 : 2;
+      double Sb = 0, Mb = 0;
+      for (int t0 = b0; t0 < b1; t0 += 64) {
+        const bool ok = t0 + lane < b1;
+        const float* pq = a.psums + (size_t)min(t0 + lane, b1 - 1) * kNSum + base;
+        float vs = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float vm = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vs = ok ? vs : 0.f;
+        vm = ok ? vm : 0.f;
+        const int cnt = min(64, b1 - t0);
+        for (int i = 0; i < cnt; ++i) {
+          Sb += (double)__shfl(vs, i, 64);
+          Mb += (double)__shfl(vm, i, 64);
+        }
+      }
+      const double K = (double)(b1 - b0) * kN2;
+      float c = 0.f;
+      if constexpr (SINGLE) {
+        const double mu = Mb / K, rmse = sqrt(Sb / K);
+        c = rmse > 0 ? (float)(a.w / (mu * K * rmse) * a.grad_scale) : 0.f;
+      } else {
+        c = (float)(-a.w / ((Mb / K) * K) * a.grad_scale);
+      }
+      s_c = c;   // every lane stores the same value
+    }
+    __syncthreads();
+    const float c = s_c;
+    // ------------------------------------------------ probe / position gradient
+    if constexpr (SHIFT) {
+      fft_fwd(v, buf, lc, cd.wsign);                  // G = F(h), K layout
+      const int vpk = rf::opaque(8 * tid);
+      const int l0 = rf::opaque(tid) & 1;
+      const float sx = rf::opaquef(sx0), sy = rf::opaquef(sy0);
+      auto ramp_a = [&](int qq) { return cis_rev(-fmaf(sy, gy, sx * (float)(4 * qq + 64 * (1 - l0)) * inv_n)); };
+      float2 B[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) B[r] = cis_rev(-sx * (float)r * inv_n);
+      float sim = 0.f, kim = 0.f;
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              t.x[r] = ld2(r_fpk, vpk, 2048 * k);
+              t.y[r] = ld2(r_slab, vpk, 2048 * k);
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = ramp_a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              const float2 W = cmul(A, B[r]);
+              const float2 FW = cmul(t.x[r], W);
+              const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
+              sim += im;
+              kim = fmaf((float)k, im, kim);                         // Σ k·im (k literal)
+              st2(cadd(t.y[r], cscale(cmulc(v[k], W), c)), r_slab, vpk, 2048 * k);   // + c_m conj(W) G
+            }
+          });
+      {
+        // Always reduced (only the atomics are conditional): a conditional consumer lets the
+        // compiler sink all 64 im products into the branch and keep F(P)·W and G live (spills).
+        // Σ g_x·im with g_x = (k + 64(1 − l0))/128
+        float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0) * sim)};
+        block_sum4<2>(ds, s_red);
+        if (tid == 0 && a.d_shifts) {
+          const float kk = 6.283185307179586f * c * inv_n2;
+          atomicAdd(a.d_shifts + 2 * sidx, ds[0] * kk);
+          atomicAdd(a.d_shifts + 2 * sidx + 1, ds[1] * kk);
+        }
+      }
+    } else {
+      {
+        const int vpk = rf::opaque(8 * tid);
+        pipeline<8>(
+            [&](auto C) {
+              Ch8 t;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_slab, vpk, 2048 * (8 * C + r));
+              return t;
+            },
+            [&](auto C, const Ch8& t) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r)
+                st2(cadd(t.x[r], cscale(v[8 * C + r], c)), r_slab, vpk, 2048 * (8 * C + r));
+            });
+      }
+    }
+  }
+}
+
+}  // namespace f3
+}  // namespace ptyx

@@ -28,180 +28,12 @@
 
 #include "ptyx.h"
 #include "ptyx_fft.hpp"
+#include "ptyx_regfft.hpp"
+
+#include "ptyx_common.hpp"
+#include "ptyx_fused3.hpp"
 
 namespace ptyx {
-
-constexpr int kMaxModesO = 8;
-constexpr int kSumBase = 4;                    // [S_single, ΣM^q1, S_poissn, ΣM^q2] then O sparse sums
-constexpr int kNSum = kSumBase + kMaxModesO;
-constexpr int kNCoef = 2 + kMaxModesO;         // [c_single, c_poissn, c_sparse[o]...]
-constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
-
-template <int N> struct Geo;
-template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true; };
-template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true; };
-template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true; };
-template <> struct Geo<256> { static constexpr int NT = 1024; static constexpr bool kLds = false; };
-
-struct KArgs {
-  int P, O, Nz, Ny, Nx, n_scans;
-  int shift, meas_f16;
-  const float* obja;
-  const float* objp;
-  const float2* probe;
-  const float2* Fp;
-  const float* shifts;
-  const int* crop;
-  const float2* H;
-  const float* occu;
-  const void* meas;
-  const int* idx;
-  int n_idx;
-  const int* boff;
-  int n_batches;
-  int single_on, pois_on, sparse_on, sparse_n;
-  float q1, q2, eps2;
-  const float* coef;
-  float* psums;
-  float* Ibuf;
-  float* dp_out;
-  const float* dLdI_ext;
-  float ext_scale;
-  float* d_obja;
-  float* d_objp;
-  float* d_shifts;
-  int need_probe;
-  float2* slab;
-  float2* scratch;
-  long long scratch_stride;
-  const float2* twg;
-  // one-pass fused kernel: loss weights and the per-call sync words
-  // sync[0] = dequeue head, sync[1] = error flag (spin timeout), sync[2 + m] = arrivals of batch m
-  float w1, w2, ws, grad_scale;
-  unsigned* sync;
-  int debug_nowait;   // PTYX_DEBUG_NOWAIT=1: skip the batch wait (timing experiments only; wrong gradients)
-  // k_fused2: pattern → mini-batch table and the per-pattern object-gradient slots
-  const int* bid;
-  float2* ogscr;
-};
-
-// ---------------------------------------------------------------- small helpers
-// threadIdx.x behind an empty asm: per-pattern address arithmetic stays inside the pattern
-// loop instead of being hoisted (and spilled) by loop-invariant code motion.
-__device__ __forceinline__ int opaque_tid() {
-  int t = threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
-// x^q for x >= 0 (DP intensities): exact forms for the schema values 0.5 / 1, otherwise
-// exp2(q·log2 x) on the v_exp_f32 / v_log_f32 units (no libm slow path in the fused epilogues).
-__device__ __forceinline__ float powq(float x, float q) {
-  if (q == 0.5f) return sqrtf(x);
-  if (q == 1.0f) return x;
-  if (!(x > 0.f)) return q > 0.f ? 0.f : __builtin_inff();
-  return __builtin_amdgcn_exp2f(q * __builtin_amdgcn_logf(x));
-}
-
-__device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
-
-// sin/cos of an object phase: reduce to revolutions in [-1/2, 1/2], then v_sin_f32 / v_cos_f32
-// (which take revolutions).  Absolute error ≈ |φ|·6e-8 + 1 ulp, far inside the parity budget.
-__device__ __forceinline__ void phase_sincos(float ph, float* sn, float* cs) {
-  float r = ph * 0.15915494309189535f;
-  r = r - rintf(r);
-  *sn = __builtin_amdgcn_sinf(r);
-  *cs = __builtin_amdgcn_cosf(r);
-}
-
-__device__ __forceinline__ float meas_at(const KArgs& a, int s, int e, int N2) {
-  const size_t off = (size_t)s * N2 + e;
-  if (a.meas_f16) return __half2float(reinterpret_cast<const __half*>(a.meas)[off]);
-  return reinterpret_cast<const float*>(a.meas)[off];
-}
-
-__device__ __forceinline__ size_t obj_off(const KArgs& a, int o, int n, int yy, int xx) {
-  return ((size_t)(o * a.Nz + n) * a.Ny + yy) * a.Nx + xx;
-}
-
-// wave64 + workgroup sum of NV floats, fixed order (deterministic); result valid in thread 0.
-template <int NT, int NV>
-__device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v[i] += __shfl_xor(v[i], m, 64);
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) red[wv * NV + i] = v[i];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      float t = 0.f;
-      for (int w = 0; w < NT / 64; ++w) t += red[w * NV + i];
-      v[i] = t;
-    }
-  }
-  __syncthreads();
-}
-
-struct PatternGeom {
-  int s, cy, cx;
-  float sy, sx;
-};
-
-__device__ __forceinline__ PatternGeom pattern_geom(const KArgs& a, int pat, int N) {
-  PatternGeom g;
-  int s = a.idx[pat];
-  s = min(max(s, 0), a.n_scans - 1);  // defensive clamp; the host validates indices
-  g.s = s;
-  g.cy = min(max(a.crop[2 * s], 0), a.Ny - N);
-  g.cx = min(max(a.crop[2 * s + 1], 0), a.Nx - N);
-  g.sy = a.shifts[2 * s];
-  g.sx = a.shifts[2 * s + 1];
-  return g;
-}
-
-// W_b ramps along y and x: exp(-2πi s g[k]), g[k] = ((k + N/2) mod N)/N  (image_proc.py:531,
-// models.py:179 grid arange(N)/N after ifftshift).
-template <int N, int NT>
-__device__ __forceinline__ void build_ramps(const PatternGeom& g, float2* wy, float2* wx) {
-  for (int k = opaque_tid(); k < 2 * N; k += NT) {
-    const int kk = k % N;
-    const float gr = (float)((kk + N / 2) % N) / (float)N;
-    const float s = k < N ? g.sy : g.sx;
-    float sn, cs;
-    sincospif(-2.0f * s * gr, &sn, &cs);
-    (k < N ? wy : wx)[kk] = make_float2(cs, sn);
-  }
-  __syncthreads();
-}
-
-template <int N>
-__device__ __forceinline__ float shift_g(int k) {
-  return (float)((k + N / 2) % N) / (float)N;
-}
-
-template <int N, bool LDS>
-struct ArrayFor;
-template <int N>
-struct ArrayFor<N, true> {
-  using type = LdsArray<N>;
-};
-template <int N>
-struct ArrayFor<N, false> {
-  using type = GlobalPair<N>;
-};
-
-// Scratch layout per workgroup (float2 units): [fft a, fft b (N=256 only)] [psi: Nz·N²] [gacc: N²]
-template <int N>
-__device__ __forceinline__ float2* scratch_psi(const KArgs& a) {
-  return a.scratch + (long long)blockIdx.x * a.scratch_stride + (Geo<N>::kLds ? 0 : 2 * N * N);
-}
 
 // =====================================================================================
 // Forward chain for one (pattern, p, o): leaves ψ_out = ψ^{Nz-1} ⊙ O_{Nz-1} in the array.
@@ -714,6 +546,12 @@ struct ptyx_plan {
   int* bid = nullptr;
   int2* geo = nullptr;
   float2* pcoef = nullptr;
+  // k_fused3 (N = 128, single mode, f32 DPs): register-resident FFT, 2 workgroups per CU
+  int nwg3 = 0;
+  float2* fpk = nullptr;      // packed probe spectrum / probe
+  float2* oc = nullptr;       // A e^{iφ}
+  double* pref = nullptr;     // per-row prefix sums of |φ|^n (loss_sparse)
+  float2* slab3 = nullptr;    // per-workgroup probe-gradient partials, packed
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
@@ -729,11 +567,13 @@ struct ptyx_plan {
 };
 
 enum KernelKind {
-  kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather, kKCount
+  kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather,
+  kKObjPrep, kKPack, kKCount
 };
 static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize",
                                                   "k_adjoint",        "k_slab_reduce",    "k_probe_finalize",
-                                                  "k_fused",          "k_pattern_table",  "k_obj_gather"};
+                                                  "k_fused",          "k_pattern_table",  "k_obj_gather",
+                                                  "k_obj_prep",       "k_pack"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -875,6 +715,25 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
         return rc;
       }
       pl->og_cap = cap;
+    }
+  }
+  if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast && pl->og_cap > 0) {
+    const char* f3 = std::getenv("PTYX_FUSED3");
+    int occ3 = 0;
+    if (!(f3 && f3[0] == '0') &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, 0) == hipSuccess &&
+        occ3 > 0) {
+      int o2 = 0;
+      for (auto kf : {f3::k_fused3<true, true, 2>, f3::k_fused3<true, false, 2>, f3::k_fused3<false, true, 0>,
+                      f3::k_fused3<false, true, 2>, f3::k_fused3<false, false, 2>})
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
+      pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
+      if ((rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
+          (rc = dalloc(pl, &pl->pref, (size_t)d.Ny * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->slab3, (size_t)pl->nwg3 * N2))) {
+        free_plan(pl);
+        return rc;
+      }
     }
   }
   // fp64 twiddles rounded once to fp32: tw[m] = exp(-2πi m/N)
@@ -1024,6 +883,113 @@ static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream
                      reinterpret_cast<float2*>(d_probe));
 }
 
+static int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, what);
+  return PTYX_OK;
+}
+
+// ---------------------------------------------------------------- k_fused3 path (N = 128)
+// Launch sequence of one ptyx_forward_loss_grad call on the register-resident engine.
+static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                      const ptyx_grads& gz, hipStream_t st, float* loss_terms) {
+  constexpr int N = 128, N2 = N * N;
+  const ptyx_dims& d = pl->d;
+  const bool sparse = cfg->sparse_on != 0;
+  if (a.shift) {
+    launch_spectrum<N>(pl, a, st);
+    ProfScope ps(pl, kKPack, st);
+    hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, pl->Fp, pl->fpk);
+  } else {
+    ProfScope ps(pl, kKPack, st);
+    hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256), dim3(256), 0, st,
+                       reinterpret_cast<const float2*>(in->probe), pl->fpk);
+  }
+  {
+    ProfScope ps(pl, kKObjPrep, st);
+    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny), dim3(256), 0, st, a.obja, a.objp, d.Ny, d.Nx, pl->oc,
+                       sparse ? pl->pref : nullptr, cfg->sparse_n);
+  }
+  {
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
+                       a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo,
+                       sparse ? pl->pref : nullptr, pl->psums);
+  }
+  const size_t sync_bytes = ((size_t)(2 + a.n_batches) * sizeof(unsigned) + 15) / 16 * 16;
+  hipError_t e = hipMemsetAsync(pl->sync, 0, sync_bytes, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(sync)");
+  f3::F3Args f{};
+  f.n_idx = a.n_idx; f.n_scans = a.n_scans; f.Ny = d.Ny; f.Nx = d.Nx;
+  f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.boff = a.boff; f.shifts = a.shifts;
+  f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas);
+  const bool single = cfg->single_on != 0;
+  f.q = single ? cfg->single_q : cfg->poissn_q;
+  f.eps2 = cfg->poissn_eps;
+  f.w = single ? cfg->single_w : cfg->poissn_w;
+  f.grad_scale = cfg->grad_scale;
+  f.psums = pl->psums; f.sync = pl->sync; f.debug_nowait = a.debug_nowait;
+  f.slots = pl->ogscr; f.slab = pl->slab3; f.d_shifts = a.shift ? gz.d_shifts : nullptr;
+  f.need_probe = gz.d_probe != nullptr;
+  f.dp_out = a.dp_out;
+  f.occp = in->omode_occu;
+  {
+    ProfScope ps(pl, kKFused, st);
+    const dim3 gr(pl->nwg3), bl(256);
+    const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
+    if (a.shift) {
+      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, 0, st, f);
+    } else {
+      if (half) hipLaunchKernelGGL((f3::k_fused3<false, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<false, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<false, false, 2>), gr, bl, 0, st, f);
+    }
+  }
+  int rc = launch_status("k_fused3 launch");
+  if (rc) return rc;
+  FinArgs fa{};
+  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = 1; fa.O = 1;
+  fa.psums = pl->psums; fa.occu = in->omode_occu;
+  fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
+  fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
+  fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  if (gz.d_obja || gz.d_objp) {
+    fa.pcoef = pl->pcoef;
+    fa.ci = single ? 0 : 1;
+  }
+  {
+    ProfScope ps(pl, kKFinalize, st);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
+  }
+  if ((rc = launch_status("k_finalize launch"))) return rc;
+  if (gz.d_obja || gz.d_objp) {
+    GatherArgs g{};
+    g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
+    g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse ? cfg->sparse_n : 1;
+    g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
+    const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    ProfScope ps(pl, kKGather, st);
+    hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+  }
+  if ((rc = launch_status("k_obj_gather launch"))) return rc;
+  if (gz.d_probe) {
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      if (a.shift)
+        hipLaunchKernelGGL(f3::k_slab_reduce3<true>, dim3(N2 / 256), dim3(256), 0, st, pl->slab3, pl->nwg3, pl->Gsum);
+      else
+        hipLaunchKernelGGL(f3::k_slab_reduce3<false>, dim3(N2 / 256), dim3(256), 0, st, pl->slab3, pl->nwg3, pl->Gsum);
+    }
+    ProfScope ps(pl, kKProbeFinalize, st);
+    hipLaunchKernelGGL(k_probe_finalize<N>, dim3(1), dim3(Geo<N>::NT), 0, st, a, pl->Gsum,
+                       reinterpret_cast<float2*>(gz.d_probe));
+    if ((rc = launch_status("probe finalize launch"))) return rc;
+  }
+  return PTYX_OK;
+}
+
 extern "C" int ptyx_profile_begin(ptyx_plan* pl) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
@@ -1064,11 +1030,6 @@ extern "C" int ptyx_profile_end(ptyx_plan* pl, ptyx_kernel_stat* out, int32_t ca
   return rc;
 }
 
-static int launch_status(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, what);
-  return PTYX_OK;
-}
 
 extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx, int32_t n_idx,
                             float* dp_out) {
@@ -1147,6 +1108,14 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   if (fused2) {
     a.bid = pl->bid;
     a.ogscr = pl->ogscr;
+  }
+  // register-resident engine (k_fused3): N = 128, f32 DPs, same conditions as k_fused2
+  if (fused2 && pl->nwg3 > 0 && cfg->max_batch <= pl->nwg3 && pl->d.N == 128 && !a.meas_f16) {
+#ifndef PTYX_ONLY_N
+    return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
+#else
+    if (PTYX_ONLY_N == 128) return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
+#endif
   }
 
   if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);

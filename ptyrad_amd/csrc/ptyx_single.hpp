@@ -388,7 +388,6 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
 // Hand-off per MI355X_MICROARCH.md "Valid forms": plain stores → fence(release, agent) →
 // vmcnt(0) → relaxed agent atomic add; consumer: relaxed poll → fence(acquire, agent) →
 // vmcnt(0) → barrier → plain loads.
-constexpr unsigned kMaxSpins = 1u << 24;   // ≈1 s of s_sleep polling
 
 template <int N, bool SHIFT>
 __global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
