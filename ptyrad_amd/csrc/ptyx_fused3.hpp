@@ -47,20 +47,18 @@ struct F3Args {
   const int* idx;          // scan index per pattern
   const int* bid;          // mini-batch per pattern
   const int2* geo;         // clamped window origin (cy, cx) per pattern
-  const int* boff;         // mini-batch offsets
   const float* shifts;     // (n_scans, 2)
   const float2* fpk;       // SHIFT: F(probe) K-packed; else the probe R-packed
   const float2* oc;        // A e^{iφ}, (Ny, Nx)
   const float* meas;       // (n_scans, 128, 128) f32, fftshifted
   const float* occp;       // omode_occu (device), occ = occp[0]
-  float q, eps2, w, grad_scale;
-  float* psums;
-  unsigned* sync;          // [dequeue head (unused), error flag, arrivals per mini-batch]
-  int debug_nowait;
-  float2* slots;           // per-pattern object-gradient slots (row-permuted)
-  float2* slab;            // per-workgroup probe-gradient partials (K-packed / R-packed)
-  float* d_shifts;
-  int need_probe;
+  float q, eps2;
+  float* psums;            // per-pattern loss partial sums (k_finalize)
+  float2* slots;           // per-pattern object-gradient slots, unit coefficient (row-permuted)
+  float2* segslab;         // per-segment probe-gradient spectra, unit coefficient (K- / R-packed)
+  int* segbid;             // mini-batch of each segment (-1: unused id)
+  float* dsu;              // per-pattern position-gradient sums, unit coefficient (2 floats)
+  int tail;                // probe or position gradient wanted
   float* dp_out;
 };
 
@@ -82,14 +80,42 @@ __global__ void k_pack128(const float2* src, float2* dst) {
   dst[e] = src[packed_rc<KL>(t, i)];
 }
 
-// Σ over workgroup slabs (packed, fixed order) → natural Gsum
-template <bool KL>
-__global__ void k_slab_reduce3(const float2* slab, int nwg, float2* out) {
+// Probe-gradient spectrum: Σ over segments (fixed order) of c_{m(seg)} × the segment's unit
+// slab.  Two levels for parallelism: block (x, y) sums segments y, y + SPL, ... of 256 elements
+// into part[y]; k_segslab_final adds the SPL partials in order and unpacks to natural order.
+constexpr int kSegSplit = 32;
+__global__ void k_segslab_reduce(const float2* segslab, const int* segbid, int nseg, const float* coef, int ci,
+                                 float2* part) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= kN2) return;
+  const int y = blockIdx.y;
   float2 acc = make_float2(0.f, 0.f);
-  for (int w = 0; w < nwg; ++w) acc = cadd(acc, slab[(size_t)w * kN2 + e]);
+  for (int g = y; g < nseg; g += kSegSplit) {
+    const int m = segbid[g];
+    if (m < 0) continue;
+    const float c = coef[(size_t)m * kNCoef + ci];
+    const float2 u = segslab[(size_t)g * kN2 + e];
+    acc.x = fmaf(c, u.x, acc.x);
+    acc.y = fmaf(c, u.y, acc.y);
+  }
+  part[(size_t)y * kN2 + e] = acc;
+}
+template <bool KL>
+__global__ void k_segslab_final(const float2* part, float2* out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[(size_t)y * kN2 + e]);
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
+}
+
+// d_shifts[s] += c_{m(pat)} · 2π/N² · dsu[pat]   (position gradient, image_proc.py:531 adjoint)
+__global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid, const float* coef, int ci,
+                              const float* dsu, float* d_shifts) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  const float k = 6.283185307179586f * coef[(size_t)bid[j] * kNCoef + ci] * (1.0f / kN2);
+  atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
+  atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
 }
 
 // Per call: complex object O = A e^{iφ} (the fused kernel then needs no transcendental per
@@ -286,121 +312,170 @@ struct Ch4x2 {
   float2 x[4], y[4];
 };
 
+// PTYX_F3_PHASES=1 (diagnostic builds only): s_memtime stamps at the phase boundaries of wave 0;
+// workgroups 0 and 1 printf their per-phase cycle totals at exit.
+#ifndef PTYX_F3_PHASES
+#define PTYX_F3_PHASES 0
+#endif
+#if PTYX_F3_PHASES
+#define F3PH(i)                                                  \
+  do {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - ph_prev;                                       \
+    ph_prev = t_;                                                \
+  } while (0)
+#elif defined(PTYX_F3_MARK)
+#define F3PH(i) asm volatile("; MARK " #i)
+#else
+#define F3PH(i) \
+  do {          \
+  } while (0)
+#endif
+
+// Per-pattern scalars.
+struct PatInfo {
+  int m, cy, cx, sidx;
+  float sy, sx;
+};
+template <bool SHIFT>
+__device__ __forceinline__ PatInfo pat_info(const F3Args& a, int pat) {
+  PatInfo p;
+  const int pp = min(pat, a.n_idx - 1);   // (a past-the-end "next" pattern reads a valid slot)
+  p.m = a.bid[pp];
+  const int2 g = a.geo[pp];
+  p.cy = g.x;
+  p.cx = g.y;
+  p.sidx = min(max(a.idx[pp], 0), a.n_scans - 1);
+  p.sy = SHIFT ? a.shifts[2 * p.sidx] : 0.f;
+  p.sx = SHIFT ? a.shifts[2 * p.sidx + 1] : 0.f;
+  return p;
+}
+
+// W_b(ky, kx) = exp(-2πi (sy gy + sx gx)), g = ((k + 64) mod 128)/128 (image_proc.py:531 on the
+// ifftshifted grid of models.py:179).  K layout: ky = this thread's row, kx = 4qq + r + 64 l0,
+// factored as A(qq)·B(r) so a 64-register pass needs 16 + 4 sin/cos pairs.
+struct Ramp {
+  float2 B[4];
+  float sy, sx, gy;
+  int l0;
+  __device__ __forceinline__ void init(float sy_, float sx_, float gy_, int l0_) {
+    sy = rf::opaquef(sy_);
+    sx = rf::opaquef(sx_);
+    gy = gy_;
+    l0 = l0_;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) B[r] = cis_rev(-sx * (float)r * (1.0f / kN));
+  }
+  __device__ __forceinline__ float2 a(int qq) const {
+    return cis_rev(-fmaf(sy, gy, sx * (float)(4 * qq + 64 * (1 - l0)) * (1.0f / kN)));
+  }
+};
+
 // QM: 0 → dp_pow q = 1/2 (sqrt / rsqrt), 2 → general q (see loss_point)
+//
+// Work split: workgroup w owns the contiguous pattern range [w·n/G, (w+1)·n/G).  Everything that
+// depends on a mini-batch's NRMSE coefficient c_m (losses.py:45-47) is accumulated with a unit
+// coefficient and scaled after k_finalize: the object-gradient slots (k_obj_gather), the
+// position-gradient sums (k_shift_apply) and the probe-gradient spectrum, which is kept per
+// SEGMENT = maximal run of the range inside one mini-batch (id m + w, unique because every
+// segment boundary advances m or w), reduced by k_segslab_reduce.  So no workgroup ever waits
+// for another: no arrival counters, no co-residency requirement, any grid size.
+//
+// Per pattern: IFFT · park ψ⁰, ×O · FFT (DP → LDS meanwhile) · loss partial sums, g_Ψ ·
+// IFFT · slot, ×conj(O) · FFT (probe-gradient spectrum) · one pass: segment slab += conj(W) G,
+// position-gradient sums, and v = F(P)·W for the next pattern (F(P) read once per pattern).
 template <bool SHIFT, bool SINGLE, int QM>
 __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
   __shared__ float s_red[4 * 2];
-  __shared__ float s_c;
   const Coord cd = coord(threadIdx.x);
   const LaneCtx lc = lane_ctx(cd.lane);
+#if PTYX_F3_PHASES
+  unsigned long long ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph_prev = __builtin_amdgcn_s_memtime();
+  int ph_n = 0;
+#endif
   constexpr float inv_n = 1.0f / kN, inv_n2 = 1.0f / kN2;
-  {
-    // the slab is always updated (branch-free passes); without a probe gradient it is not reduced
-    float2* slab = a.slab + (size_t)blockIdx.x * kN2 + threadIdx.x;
-    for (int k = 0; k < 64; ++k) slab[k * 256] = make_float2(0.f, 0.f);   // own entries only
-  }
-  unsigned* err = a.sync + 1;
-  unsigned* arrive = a.sync + 2;
+  const int w = blockIdx.x, G = gridDim.x;
+  const int p0 = (int)((long long)w * a.n_idx / G), p1 = (int)((long long)(w + 1) * a.n_idx / G);
+  if (p0 >= p1) return;
   const float occ = a.occp[0], q = a.q;
-  const bool tail = a.need_probe || a.d_shifts;   // (uniform)
+  const bool tail = a.tail != 0;   // (uniform)
   const int Nx = a.Nx;
+  const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
+  const float gy = (float)((cd.fixed + 64) & 127) * inv_n;   // ifftshifted grid of this thread's ky
 
-  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
-    // per-thread bases re-derived from an opaque thread id each pattern: keeps LICM from hoisting
-    // 64 per-register addresses out of the pattern loop (they would spill)
-    asm volatile("" ::: "memory");   // no memory operation of one pattern moves into another
+  // ---------------------------------------------------------------- prologue: v for the first pattern
+  float2 v[64];
+  {
+    const int tid = rf::opaque(threadIdx.x);
+    const int vpk = 8 * tid;
+    const PatInfo pi0 = pat_info<SHIFT>(a, p0);
+    Ramp rp;
+    rp.init(pi0.sy, pi0.sx, gy, tid & 1);
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+          const float2 A = rp.a(C);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
+            pin(v[4 * C + r]);
+          }
+        });
+  }
+
+  for (int pat = p0; pat < p1; ++pat) {
+    // per-thread bases re-derived from an opaque thread id each pattern and pass: keeps LICM /
+    // CSE from holding 64 per-register offsets live across the transforms (they would spill)
     const int tid = rf::opaque(threadIdx.x);
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
-    const int m = a.bid[pat];
-    const int2 g = a.geo[pat];
-    // packed arrays ([register][thread]): voff = 8·tid, soff = 2048·register
-    const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
-    const Rsrc r_slab = rsrc(a.slab + (size_t)blockIdx.x * kN2, kN2 * 8);
-    // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → soff = 2048·j
+    const PatInfo p = pat_info<SHIFT>(a, pat);
+    // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → offset 2048·j
     const Rsrc r_slot = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
     const int vslot0 = 8 * (l0 * kN + fx);
-    // object window: element (j + 64 l0, fx) → soff = 8·Nx·j
-    const Rsrc r_obj = rsrc(a.oc + (size_t)g.x * Nx + g.y, (unsigned)(((kN - 1) * Nx + kN) * 8));
+    // object window: element (j + 64 l0, fx) → offset vobj + 8·Nx·j
+    const Rsrc r_obj = rsrc(a.oc + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
     const int vobj0 = 8 * (64 * l0 * Nx + fx);
-    const int ostr0 = 8 * Nx;   // register j's object offset is vobj + j·ostr
-    const int sidx = min(max(a.idx[pat], 0), a.n_scans - 1);
-    float sy0 = 0.f, sx0 = 0.f;
-    if constexpr (SHIFT) {
-      sy0 = a.shifts[2 * sidx];
-      sx0 = a.shifts[2 * sidx + 1];
-    }
-    const float sy = sy0, sx = sx0;
-    const float gy = (float)((fx + 64) & 127) * inv_n;   // ifftshifted grid of this thread's ky
-    // W(ky, kx = 4qq + r + 64 l0) = A(qq)·B(r): exp(-2πi(sy gy + sx gx)), g = ((k + 64) mod 128)/128
-    auto ramp_a = [&](int qq) { return cis_rev(-fmaf(sy, gy, sx * (float)(4 * qq + 64 * (1 - l0)) * inv_n)); };
-    float2 v[64];
-    // Every pass below re-derives its per-register offsets / ramp arguments from opaque copies
-    // (rf::opaque): otherwise CSE shares them between passes that are an FFT or two apart and
-    // keeps ~64-128 extra values live across the transforms (spilled).
+    const int ostr0 = 8 * Nx;
     // ------------------------------------------------ ψ⁰ = F⁻¹(F(P)·W_b)  (R layout)
+    F3PH(0);
     if constexpr (SHIFT) {
-      const int vpk = rf::opaque(8 * tid);
-      const int l0 = rf::opaque(tid) & 1;
-      float2 B[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) B[r] = cis_rev(-sx * (float)r * inv_n);
-      pipeline<16>(
-          [&](auto C) {
-            Ch4x2 t;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
-            return t;
-          },
-          [&](auto C, const Ch4x2& t) {
-            const float2 A = ramp_a(C);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              v[4 * C + r] = cmul(t.x[r], cmul(A, B[r]));
-              pin(v[4 * C + r]);
-            }
-          });
       fft_inv(v, buf, lc, cd.wsign);
 #pragma unroll
       for (int j = 0; j < 64; ++j) v[j] = cscale(v[j], inv_n2);
-    } else {
-      const int vpk = rf::opaque(8 * tid);
+    }
+    F3PH(1);
+    // ------------------------------------------------ park ψ⁰; ψ = ψ⁰·O
+    {
+      const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
       pipeline<8>(
           [&](auto C) {
             Ch8 t;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (8 * C + r));
+            for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
             return t;
           },
           [&](auto C, const Ch8& t) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[8 * C + r] = t.x[r];
+            for (int r = 0; r < 8; ++r) {
+              const int j = 8 * C + r;
+              st2(v[j], r_slot, vslot, 2048 * j);
+              v[j] = cmul(v[j], t.x[r]);
+              pin(v[j]);
+            }
           });
     }
-    // ------------------------------------------------ park ψ⁰; ψ = ψ⁰·O
-    {
-    const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
-    pipeline<8>(
-        [&](auto C) {
-          Ch8 t;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
-          return t;
-        },
-        [&](auto C, const Ch8& t) {
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const int j = 8 * C + r;
-            st2(v[j], r_slot, vslot, 2048 * j);
-            v[j] = cmul(v[j], t.x[r]);
-            pin(v[j]);
-          }
-        });
-    }
+    F3PH(2);
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
-    const float* dp = a.meas + (size_t)sidx * kN2;
+    const float* dp = a.meas + (size_t)p.sidx * kN2;
     fft_fwd(v, buf, lc, cd.wsign, [&] {
       const int lane = cd.lane;
       const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
@@ -415,8 +490,10 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
                                          0);
       }
     });
+    F3PH(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    F3PH(4);
     float S = 0.f, Ms = 0.f;
     {
       const int r = (fx + 64) & 127;               // fftshifted DP row of ky
@@ -448,101 +525,69 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
         if (kq & 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
+    F3PH(5);
     {
-      // (block_sum's first barrier also retires every wave's DP reads before the next exchange)
+      // (block_sum4's first barrier also retires every wave's DP reads before the next exchange)
       float v2[2] = {S, Ms};
       block_sum4<2>(v2, s_red);
-      if (tid == 0) {
+      if (threadIdx.x == 0) {
         float* ps = a.psums + (size_t)pat * kNSum;
         const int base = SINGLE ? 0 : 2;
-        __hip_atomic_store(ps + base, v2[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ps + base + 1, v2[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ps + (2 - base), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ps + (3 - base), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(arrive + m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ps[base] = v2[0];
+        ps[base + 1] = v2[1];
+        ps[2 - base] = 0.f;
+        ps[3 - base] = 0.f;
       }
     }
+    F3PH(6);
     // ------------------------------------------------ back to real space
     fft_inv(v, buf, lc, cd.wsign);
+    F3PH(7);
     {
-    const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
-    pipeline<16>(
-        [&](auto C) {
-          Ch4x2 t;
+      const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = 4 * C + r;
-            t.x[r] = ld2(r_slot, vslot, 2048 * j);
-            t.y[r] = ld2(r_obj, vobj, ostr * j);
-          }
-          return t;
-        },
-        [&](auto C, const Ch4x2& t) {
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * C + r;
+              t.x[r] = ld2(r_slot, vslot, 2048 * j);
+              t.y[r] = ld2(r_obj, vobj, ostr * j);
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int j = 4 * C + r;
-            const float2 gv = cscale(v[j], inv_n);
-            st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
-            v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
-            pin(v[j]);
-          }
-        });
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * C + r;
+              const float2 gv = cscale(v[j], inv_n);
+              st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+              v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
+              pin(v[j]);
+            }
+          });
     }
-    if (!tail) continue;
-    // ------------------------------------------------ c_m of this mini-batch
-    // Wave 0 only (scalar branch) and no lane divergence inside: every lane polls the same
-    // arrival word, loads one pattern's partial sums (clamped index, masked value) and forms the
-    // same fixed-order fp64 sums, so the 128 live data VGPRs see no divergent region.
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
-      const int lane = cd.lane;
-      const int b0 = a.boff[m], b1 = a.boff[m + 1];
-      const unsigned want = (unsigned)(b1 - b0);
-      unsigned spins = 0;
-      while (!a.debug_nowait && __hip_atomic_load(arrive + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kMaxSpins) {
-          atomicOr(err, 1u);
-          break;
-        }
-      }
-      const int base = SINGLE ? 0 : 2;
-      double Sb = 0, Mb = 0;
-      for (int t0 = b0; t0 < b1; t0 += 64) {
-        const bool ok = t0 + lane < b1;
-        const float* pq = a.psums + (size_t)min(t0 + lane, b1 - 1) * kNSum + base;
-        float vs = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        float vm = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vs = ok ? vs : 0.f;
-        vm = ok ? vm : 0.f;
-        const int cnt = min(64, b1 - t0);
-        for (int i = 0; i < cnt; ++i) {
-          Sb += (double)__shfl(vs, i, 64);
-          Mb += (double)__shfl(vm, i, 64);
-        }
-      }
-      const double K = (double)(b1 - b0) * kN2;
-      float c = 0.f;
-      if constexpr (SINGLE) {
-        const double mu = Mb / K, rmse = sqrt(Sb / K);
-        c = rmse > 0 ? (float)(a.w / (mu * K * rmse) * a.grad_scale) : 0.f;
-      } else {
-        c = (float)(-a.w / ((Mb / K) * K) * a.grad_scale);
-      }
-      s_c = c;   // every lane stores the same value
-    }
-    __syncthreads();
-    const float c = s_c;
-    // ------------------------------------------------ probe / position gradient
+    F3PH(8);
+    // ------------------------------------------------ probe / position gradient, next pattern's v
+    // Segment of this pattern: the run of the range inside mini-batch m, id m + w.  The first
+    // pattern of a segment reads its slab through a zero-length buffer resource (loads return 0)
+    // and so initialises it; later patterns accumulate.  Without probe/position gradients (tail
+    // false) the same pass runs without the FFT and its slab / sums are never used.
+    const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
+    const bool first = pat == p0 || a.bid[pat - 1] != p.m;   // (uniform)
+    const int seg = p.m + w;
+    float2* segs = a.segslab + (size_t)seg * kN2;
+    const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
+    const Rsrc r_slab_st = rsrc(segs, kN2 * 8);
+    if (first && threadIdx.x == 0) a.segbid[seg] = p.m;
     if constexpr (SHIFT) {
-      fft_fwd(v, buf, lc, cd.wsign);                  // G = F(h), K layout
+      if (tail) fft_fwd(v, buf, lc, cd.wsign);        // G = F(h), K layout
+      F3PH(9);
       const int vpk = rf::opaque(8 * tid);
-      const int l0 = rf::opaque(tid) & 1;
-      const float sx = rf::opaquef(sx0), sy = rf::opaquef(sy0);
-      auto ramp_a = [&](int qq) { return cis_rev(-fmaf(sy, gy, sx * (float)(4 * qq + 64 * (1 - l0)) * inv_n)); };
-      float2 B[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) B[r] = cis_rev(-sx * (float)r * inv_n);
+      const int l0b = rf::opaque(tid) & 1;
+      Ramp rc, rn;
+      rc.init(p.sy, p.sx, gy, l0b);
+      rn.init(pn.sy, pn.sx, gy, l0b);
       float sim = 0.f, kim = 0.f;
       pipeline<16>(
           [&](auto C) {
@@ -551,53 +596,71 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
               t.x[r] = ld2(r_fpk, vpk, 2048 * k);
-              t.y[r] = ld2(r_slab, vpk, 2048 * k);
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * k);
             }
             return t;
           },
           [&](auto C, const Ch4x2& t) {
-            const float2 A = ramp_a(C);
+            const float2 A = rc.a(C), An = rn.a(C);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
-              const float2 W = cmul(A, B[r]);
+              const float2 W = cmul(A, rc.B[r]);
               const float2 FW = cmul(t.x[r], W);
               const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
               sim += im;
-              kim = fmaf((float)k, im, kim);                         // Σ k·im (k literal)
-              st2(cadd(t.y[r], cscale(cmulc(v[k], W), c)), r_slab, vpk, 2048 * k);   // + c_m conj(W) G
+              kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
+              st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
+              v[k] = cmul(t.x[r], cmul(An, rn.B[r]));                 // next pattern: F(P)·W_next
+              pin(v[k]);
             }
           });
+      F3PH(10);
       {
-        // Always reduced (only the atomics are conditional): a conditional consumer lets the
-        // compiler sink all 64 im products into the branch and keep F(P)·W and G live (spills).
-        // Σ g_x·im with g_x = (k + 64(1 − l0))/128
-        float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0) * sim)};
+        // Always reduced (a conditional consumer lets the compiler sink all 64 im products into
+        // the branch and keep F(P)·W and G live, which spills).
+        // Σ g_y·im and Σ g_x·im with g_x = (k + 64(1 − l0))/128
+        float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0b) * sim)};
         block_sum4<2>(ds, s_red);
-        if (tid == 0 && a.d_shifts) {
-          const float kk = 6.283185307179586f * c * inv_n2;
-          atomicAdd(a.d_shifts + 2 * sidx, ds[0] * kk);
-          atomicAdd(a.d_shifts + 2 * sidx + 1, ds[1] * kk);
+        if (threadIdx.x == 0) {
+          a.dsu[2 * pat] = ds[0];
+          a.dsu[2 * pat + 1] = ds[1];
         }
       }
     } else {
-      {
-        const int vpk = rf::opaque(8 * tid);
-        pipeline<8>(
-            [&](auto C) {
-              Ch8 t;
+      const int vpk = rf::opaque(8 * tid);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
 #pragma unroll
-              for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_slab, vpk, 2048 * (8 * C + r));
-              return t;
-            },
-            [&](auto C, const Ch8& t) {
+            for (int r = 0; r < 4; ++r) {
+              t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
 #pragma unroll
-              for (int r = 0; r < 8; ++r)
-                st2(cadd(t.x[r], cscale(v[8 * C + r], c)), r_slab, vpk, 2048 * (8 * C + r));
-            });
-      }
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * C + r;
+              st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (unit, R layout)
+              v[j] = t.x[r];                                       // next pattern: the probe
+              pin(v[j]);
+            }
+          });
     }
+    F3PH(11);
+#if PTYX_F3_PHASES
+    ++ph_n;
+#endif
   }
+#if PTYX_F3_PHASES
+  if (threadIdx.x == 0 && blockIdx.x < 2)
+    printf("F3PHASES wg %d n %d cyc/pattern: top %llu ifft1 %llu post1 %llu fft2 %llu dpwait %llu loss %llu "
+           "publish %llu ifft3 %llu post3 %llu fft4 %llu post4+pre %llu ds %llu\n",
+           (int)blockIdx.x, ph_n, ph[0] / ph_n, ph[1] / ph_n, ph[2] / ph_n, ph[3] / ph_n, ph[4] / ph_n, ph[5] / ph_n,
+           ph[6] / ph_n, ph[7] / ph_n, ph[8] / ph_n, ph[9] / ph_n, ph[10] / ph_n, ph[11] / ph_n);
+#endif
 }
 
 }  // namespace f3

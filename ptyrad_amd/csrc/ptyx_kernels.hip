@@ -551,7 +551,11 @@ struct ptyx_plan {
   float2* fpk = nullptr;      // packed probe spectrum / probe
   float2* oc = nullptr;       // A e^{iφ}
   double* pref = nullptr;     // per-row prefix sums of |φ|^n (loss_sparse)
-  float2* slab3 = nullptr;    // per-workgroup probe-gradient partials, packed
+  float2* segslab = nullptr;  // per-segment unit probe-gradient spectra, packed
+  int* segbid = nullptr;      // batch of each segment id (-1 unused)
+  float* dsu = nullptr;       // per-pattern unit position-gradient sums
+  float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
+  long long seg_cap = 0;      // segment ids the segslab holds
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
@@ -728,9 +732,17 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
                       f3::k_fused3<false, true, 2>, f3::k_fused3<false, false, 2>})
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
+      // segment ids = mini-batches + workgroups of a call; sized for a mean mini-batch of ≥ 8
+      // patterns (PTYX_SEG_DIV); calls with more segments take the k_fused2 path
+      long long div = 8;
+      if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
+      pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
       if ((rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Ny * (d.Nx + 1))) ||
-          (rc = dalloc(pl, &pl->slab3, (size_t)pl->nwg3 * N2))) {
+          (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
+          (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
+          (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
+          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2))) {
         free_plan(pl);
         return rc;
       }
@@ -916,26 +928,26 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
                        a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo,
                        sparse ? pl->pref : nullptr, pl->psums);
   }
-  const size_t sync_bytes = ((size_t)(2 + a.n_batches) * sizeof(unsigned) + 15) / 16 * 16;
-  hipError_t e = hipMemsetAsync(pl->sync, 0, sync_bytes, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(sync)");
+  const bool single = cfg->single_on != 0;
+  const int ci = single ? 0 : 1;
+  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int nseg = a.n_batches + G;
+  hipError_t e = hipMemsetAsync(pl->segbid, 0xFF, sizeof(int) * (size_t)nseg, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(segbid)");
   f3::F3Args f{};
   f.n_idx = a.n_idx; f.n_scans = a.n_scans; f.Ny = d.Ny; f.Nx = d.Nx;
-  f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.boff = a.boff; f.shifts = a.shifts;
+  f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.shifts = a.shifts;
   f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas);
-  const bool single = cfg->single_on != 0;
+  f.occp = in->omode_occu;
   f.q = single ? cfg->single_q : cfg->poissn_q;
   f.eps2 = cfg->poissn_eps;
-  f.w = single ? cfg->single_w : cfg->poissn_w;
-  f.grad_scale = cfg->grad_scale;
-  f.psums = pl->psums; f.sync = pl->sync; f.debug_nowait = a.debug_nowait;
-  f.slots = pl->ogscr; f.slab = pl->slab3; f.d_shifts = a.shift ? gz.d_shifts : nullptr;
-  f.need_probe = gz.d_probe != nullptr;
+  f.psums = pl->psums;
+  f.slots = pl->ogscr; f.segslab = pl->segslab; f.segbid = pl->segbid; f.dsu = pl->dsu;
+  f.tail = (gz.d_probe != nullptr || (a.shift && gz.d_shifts != nullptr)) ? 1 : 0;
   f.dp_out = a.dp_out;
-  f.occp = in->omode_occu;
   {
     ProfScope ps(pl, kKFused, st);
-    const dim3 gr(pl->nwg3), bl(256);
+    const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
     if (a.shift) {
       if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
@@ -957,7 +969,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
   if (gz.d_obja || gz.d_objp) {
     fa.pcoef = pl->pcoef;
-    fa.ci = single ? 0 : 1;
+    fa.ci = ci;
   }
   {
     ProfScope ps(pl, kKFinalize, st);
@@ -974,19 +986,26 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
+  if (a.shift && gz.d_shifts) {
+    ProfScope ps(pl, kKSlabReduce, st);
+    hipLaunchKernelGGL(f3::k_shift_apply, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.n_scans,
+                       pl->bid, pl->coef, ci, pl->dsu, gz.d_shifts);
+  }
   if (gz.d_probe) {
     {
       ProfScope ps(pl, kKSlabReduce, st);
+      hipLaunchKernelGGL(f3::k_segslab_reduce, dim3(N2 / 256, f3::kSegSplit), dim3(256), 0, st, pl->segslab,
+                         pl->segbid, nseg, pl->coef, ci, pl->segpart);
       if (a.shift)
-        hipLaunchKernelGGL(f3::k_slab_reduce3<true>, dim3(N2 / 256), dim3(256), 0, st, pl->slab3, pl->nwg3, pl->Gsum);
+        hipLaunchKernelGGL(f3::k_segslab_final<true>, dim3(N2 / 256), dim3(256), 0, st, pl->segpart, pl->Gsum);
       else
-        hipLaunchKernelGGL(f3::k_slab_reduce3<false>, dim3(N2 / 256), dim3(256), 0, st, pl->slab3, pl->nwg3, pl->Gsum);
+        hipLaunchKernelGGL(f3::k_segslab_final<false>, dim3(N2 / 256), dim3(256), 0, st, pl->segpart, pl->Gsum);
     }
     ProfScope ps(pl, kKProbeFinalize, st);
     hipLaunchKernelGGL(k_probe_finalize<N>, dim3(1), dim3(Geo<N>::NT), 0, st, a, pl->Gsum,
                        reinterpret_cast<float2*>(gz.d_probe));
-    if ((rc = launch_status("probe finalize launch"))) return rc;
   }
+  if ((rc = launch_status("probe finalize launch"))) return rc;
   return PTYX_OK;
 }
 
@@ -1109,8 +1128,12 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     a.bid = pl->bid;
     a.ogscr = pl->ogscr;
   }
-  // register-resident engine (k_fused3): N = 128, f32 DPs, same conditions as k_fused2
-  if (fused2 && pl->nwg3 > 0 && cfg->max_batch <= pl->nwg3 && pl->d.N == 128 && !a.meas_f16) {
+  // register-resident engine (k_fused3): N = 128, f32 DPs, one data term, slots and segment
+  // slabs large enough for the call (no co-residency or max_batch condition: it never waits)
+  const bool fused3 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 &&
+                      n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
+                      (cfg->single_on != 0) != (cfg->poissn_on != 0);
+  if (fused3) {
 #ifndef PTYX_ONLY_N
     return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
 #else
