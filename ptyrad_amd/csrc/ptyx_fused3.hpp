@@ -371,6 +371,22 @@ struct Ramp {
   }
 };
 
+// Cost-attribution knobs for diagnostic builds (results are WRONG with any of them set):
+//   PTYX_F3_EXP_NOPARK  no ψ⁰ park store / reload      PTYX_F3_EXP_NOSLAB  no segment-slab load/store
+//   PTYX_F3_EXP_NOOBJ   no object loads (O = 1)          PTYX_F3_EXP_NOSLOT  no final slot store
+#ifndef PTYX_F3_EXP_NOPARK
+#define PTYX_F3_EXP_NOPARK 0
+#endif
+#ifndef PTYX_F3_EXP_NOSLAB
+#define PTYX_F3_EXP_NOSLAB 0
+#endif
+#ifndef PTYX_F3_EXP_NOOBJ
+#define PTYX_F3_EXP_NOOBJ 0
+#endif
+#ifndef PTYX_F3_EXP_NOSLOT
+#define PTYX_F3_EXP_NOSLOT 0
+#endif
+
 // QM: 0 → dp_pow q = 1/2 (sqrt / rsqrt), 2 → general q (see loss_point)
 //
 // Work split: workgroup w owns the contiguous pattern range [w·n/G, (w+1)·n/G).  Everything that
@@ -460,14 +476,15 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
           [&](auto C) {
             Ch8 t;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
+            for (int r = 0; r < 8; ++r)
+              t.x[r] = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : ld2(r_obj, vobj, ostr * (8 * C + r));
             return t;
           },
           [&](auto C, const Ch8& t) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const int j = 8 * C + r;
-              st2(v[j], r_slot, vslot, 2048 * j);
+              if (!PTYX_F3_EXP_NOPARK) st2(v[j], r_slot, vslot, 2048 * j);
               v[j] = cmul(v[j], t.x[r]);
               pin(v[j]);
             }
@@ -551,8 +568,8 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
-              t.x[r] = ld2(r_slot, vslot, 2048 * j);
-              t.y[r] = ld2(r_obj, vobj, ostr * j);
+              t.x[r] = PTYX_F3_EXP_NOPARK ? make_float2(1.f, 0.f) : ld2(r_slot, vslot, 2048 * j);
+              t.y[r] = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : ld2(r_obj, vobj, ostr * j);
             }
             return t;
           },
@@ -561,7 +578,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
               const float2 gv = cscale(v[j], inv_n);
-              st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+              if (!PTYX_F3_EXP_NOSLOT) st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
               v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
               pin(v[j]);
             }
@@ -596,7 +613,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
               t.x[r] = ld2(r_fpk, vpk, 2048 * k);
-              t.y[r] = ld2(r_slab_ld, vpk, 2048 * k);
+              t.y[r] = PTYX_F3_EXP_NOSLAB ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * k);
             }
             return t;
           },
@@ -610,7 +627,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
               const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
               sim += im;
               kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
-              st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
+              if (!PTYX_F3_EXP_NOSLAB) st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
               v[k] = cmul(t.x[r], cmul(An, rn.B[r]));                 // next pattern: F(P)·W_next
               pin(v[k]);
             }
