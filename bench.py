@@ -181,8 +181,12 @@ def main():
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_c2.json")
         if os.path.exists(pmc):
+            # PMC summary of the same workload (profiles/collect_pmc.sh → summarize_pmc.py); its
+            # kernel names are the HIP symbols: k_fused3 (register engine) or k_fused2
+            engine = "k_fused3" if "k_obj_prep" in kstats else "k_fused2"
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch", {}).get(dom)
+                tb = json.load(f).get("hbm_bytes_per_launch", {})
+            traffic = tb.get(engine) if dom == "k_fused" else tb.get(dom)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "alg_bytes_per_launch": b_alg * n_local, "avg_launch_ms": round(avg_s * 1e3, 4),

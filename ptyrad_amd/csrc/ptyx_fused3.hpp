@@ -246,6 +246,16 @@ __device__ __forceinline__ void st2(float2 v, Rsrc r, int voff, int off) {
   const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v.x), __float_as_uint(v.y)};
   __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, 0);
 }
+// PTYX_F3_NT: non-temporal (aux = 2, "nt") for the streams read once much later or never again
+// in this kernel (final slot stores, the DP), so they do not evict the park / slab / object /
+// F(P) lines the next passes re-read from L2.
+#ifndef PTYX_F3_NT
+#define PTYX_F3_NT 1
+#endif
+__device__ __forceinline__ void st2_stream(float2 v, Rsrc r, int voff, int off) {
+  const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v.x), __float_as_uint(v.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, PTYX_F3_NT ? 2 : 0);
+}
 
 // Wave sum in a fixed order, result in every lane: DPP adds within each 16-lane row
 // (pairs, quads, half-rows, rows), then the four row sums via v_readlane.  No ds_bpermute,
@@ -504,7 +514,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
         const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
         __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
                                          (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
-                                         0);
+                                         PTYX_F3_NT ? 2 : 0);
       }
     });
     F3PH(3);
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
               const float2 gv = cscale(v[j], inv_n);
-              if (!PTYX_F3_EXP_NOSLOT) st2(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+              if (!PTYX_F3_EXP_NOSLOT) st2_stream(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
               v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
               pin(v[j]);
             }
