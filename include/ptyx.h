@@ -125,6 +125,44 @@ typedef struct ptyx_kernel_stat {
 int ptyx_profile_begin(ptyx_plan *plan);
 int ptyx_profile_end(ptyx_plan *plan, ptyx_kernel_stat *out, int32_t cap, int32_t *n_out);
 
+/* ---------------------------------------------------------------------------------------------
+ * Iteration-wise constraints on the device, replacing the object / probe
+ * updates of CombinedConstraint.forward (src/ptyrad/constraints.py:227-246).  Same conventions
+ * as above: device pointers, asynchronous on `stream`, no host synchronisation; `ws` is a
+ * caller-allocated device workspace of ptyx_constraints_ws_bytes() bytes (8-byte aligned).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct ptyx_obj_constraints {
+  int32_t zblur_a, zblur_p, zblur_ks; float zblur_std;     /* obj_zblur      constraints.py:100-114 */
+  int32_t cr_a, cr_p; float cr_alpha1, cr_alpha2;           /* complex_ratio  constraints.py:147-163 */
+  int32_t mir_on; float mir_relax, mir_scale, mir_power;     /* mirrored_amp   constraints.py:165-179 */
+  int32_t thr_on; float thr_relax, thr_lo, thr_hi;           /* obja_thresh    constraints.py:181-190 */
+  int32_t pos_on, pos_subtract_min; float pos_relax;         /* objp_postiv    constraints.py:192-208 */
+} ptyx_obj_constraints;
+
+size_t ptyx_constraints_ws_bytes(void);
+
+/* obj_rblur (constraints.py:83-98): torchvision gaussian_blur over the last two axes of
+ * n_planes contiguous (Ny, Nx) f32 planes, reflect padding, kernel_size odd ≤ 15, out of place. */
+int ptyx_obj_rblur(void *stream, const float *in, float *out, int32_t n_planes, int32_t Ny, int32_t Nx,
+                   int32_t kernel_size, float sigma);
+
+/* obj_zblur → complex_ratio → mirrored_amp → obja_thresh → objp_postiv on (O,Nz,Ny,Nx) f32
+ * obja / objp, in place, in CombinedConstraint.forward order (kr/kz filters, which sit between
+ * zblur and complex_ratio, are the caller's: call once with only zblur, filter, call again). */
+int ptyx_obj_constrain(void *stream, float *obja, float *objp, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
+                       const ptyx_obj_constraints *c, void *ws);
+
+/* fix_probe_int (constraints.py:70-81): probe (P,N,N,2) *= sqrt(*probe_int_sum / Σ|probe|²);
+ * probe_int_sum is a device f32 scalar (PtychoAD.probe_int_sum, models.py:122). */
+int ptyx_probe_fix_int(void *stream, float *probe, int32_t P, int32_t N, const float *probe_int_sum, void *ws);
+
+/* ortho_pmode (constraints.py:34-41 → orthogonalize_modes_vec :255-291, sort=True): probe modes
+ * (P,N,N,2), 1 ≤ P ≤ 16, replaced in place by V^H M sorted by descending power, V the
+ * eigenvectors of M M^H (LAPACK geev normalisation).  Eigenvalues (P f64) land in
+ * ws + ptyx_constraints_evals_offset(). */
+int ptyx_probe_ortho(void *stream, float *probe, int32_t P, int32_t N, void *ws);
+size_t ptyx_constraints_evals_offset(void);
+
 /* Bytes of device workspace the plan holds. */
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
 /* Last error message of the calling thread ("" if none). */

@@ -23,7 +23,8 @@ _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 # every symbol include/ptyx.h declares (checked by tests/test_abi.py)
 EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
-           "ptyx_last_error", "ptyx_version")
+           "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
+           "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho")
 
 
 class PtyxError(RuntimeError):
@@ -56,6 +57,18 @@ class LossCfg(ctypes.Structure):
                 ("poissn_eps", ctypes.c_float),
                 ("sparse_on", ctypes.c_int32), ("sparse_w", ctypes.c_float), ("sparse_n", ctypes.c_int32),
                 ("grad_scale", ctypes.c_float), ("max_batch", ctypes.c_int32)]
+
+
+class ObjConstraints(ctypes.Structure):
+    _fields_ = [("zblur_a", ctypes.c_int32), ("zblur_p", ctypes.c_int32), ("zblur_ks", ctypes.c_int32),
+                ("zblur_std", ctypes.c_float),
+                ("cr_a", ctypes.c_int32), ("cr_p", ctypes.c_int32), ("cr_alpha1", ctypes.c_float),
+                ("cr_alpha2", ctypes.c_float),
+                ("mir_on", ctypes.c_int32), ("mir_relax", ctypes.c_float), ("mir_scale", ctypes.c_float),
+                ("mir_power", ctypes.c_float),
+                ("thr_on", ctypes.c_int32), ("thr_relax", ctypes.c_float), ("thr_lo", ctypes.c_float),
+                ("thr_hi", ctypes.c_float),
+                ("pos_on", ctypes.c_int32), ("pos_subtract_min", ctypes.c_int32), ("pos_relax", ctypes.c_float)]
 
 
 class KernelStat(ctypes.Structure):
@@ -91,8 +104,15 @@ def load(path: str | None = None):
     lib.ptyx_plan_workspace_bytes.restype = ctypes.c_size_t
     lib.ptyx_last_error.restype = ctypes.c_char_p
     lib.ptyx_version.restype = ctypes.c_int
+    lib.ptyx_constraints_ws_bytes.restype = ctypes.c_size_t
+    lib.ptyx_constraints_evals_offset.restype = ctypes.c_size_t
+    lib.ptyx_obj_rblur.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32]
+    lib.ptyx_obj_constrain.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(ObjConstraints), vp]
+    lib.ptyx_probe_fix_int.argtypes = [vp, vp, i32, i32, vp, vp]
+    lib.ptyx_probe_ortho.argtypes = [vp, vp, i32, i32, vp]
     for name in ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
-                 "ptyx_adjoint_dldi"):
+                 "ptyx_adjoint_dldi", "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int",
+                 "ptyx_probe_ortho"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

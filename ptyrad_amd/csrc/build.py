@@ -1,23 +1,31 @@
 """Build libptyx.so for gfx950 with hipcc (in-tree, so the .so travels with the repo snapshot).
 
     python -m ptyrad_amd.csrc.build [--force] [--only-n 128]
+
+Each translation unit compiles to its own object under build/obj/ (in parallel, and only when
+it or a header is newer than its object), then one hipcc -shared link.
 """
 from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "lib", "libptyx.so")
-SOURCES = [os.path.join(HERE, "ptyx_kernels.hip")]
-DEPS = SOURCES + glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
+OBJ = os.path.join(ROOT, "build", "obj")
+SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_constraints.hip")]
+HEADERS = glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
+DEPS = SOURCES + HEADERS
 ARCH = os.environ.get("PTYX_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC"]
 
 
 def hipcc() -> str:
@@ -34,16 +42,45 @@ def up_to_date(out: str = OUT) -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
+def _headers_of(src: str):
+    """Headers a translation unit depends on (the constraints unit includes only its own)."""
+    if os.path.basename(src) == "ptyx_constraints.hip":
+        return [os.path.join(HERE, "ptyx_constraints.hpp"), os.path.join(HERE, "ptyx_abi.hpp"),
+                os.path.join(ROOT, "include", "ptyx.h")]
+    return HEADERS
+
+
+def _stale(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + _headers_of(src))
+
+
 def build(force: bool = False, only_n: int | None = None, out: str = OUT, extra=None, verbose=True) -> str:
-    if not force and only_n is None and up_to_date(out):
+    if not force and only_n is None and not extra and up_to_date(out):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", *SOURCES]
-    if only_n:
-        cmd.insert(2, f"-DPTYX_ONLY_N={only_n}")
-    if extra:
-        cmd[2:2] = list(extra)
+    defs = ([f"-DPTYX_ONLY_N={only_n}"] if only_n else []) + list(extra or [])
+    tag = "default" if not defs else "v" + hashlib.sha1(" ".join(defs).encode()).hexdigest()[:10]
+    odir = os.path.join(OBJ, tag)
+    os.makedirs(odir, exist_ok=True)
+    cc = hipcc()
+
+    def compile_one(src):
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
+        if force or _stale(obj, src):
+            cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, *defs, "-I", os.path.join(ROOT, "include"), "-c", src,
+                   "-o", obj + ".tmp"]
+            if verbose:
+                print("[ptyx build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(obj + ".tmp", obj)
+        return obj
+
+    with ThreadPoolExecutor(len(SOURCES)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print("[ptyx build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,208 @@
+// ptyx_constraints.hip — C ABI of the on-device constraints (include/ptyx.h), a translation unit
+// of libptyx.so of its own (kernels in ptyx_constraints.hpp).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "ptyx.h"
+#include "ptyx_abi.hpp"
+#include "ptyx_constraints.hpp"
+
+using namespace ptyx;
+
+namespace {
+using cons::kMaxHalf;
+using cons::kMaxModes;
+using cons::kRedBlocks;
+constexpr int kGramChunks = 64;
+// workspace layout (doubles): stats[8] | partials[2·kRedBlocks] | gram[2·pairs·chunks] | evals[16]
+// | U (kMaxModes² float2)
+constexpr size_t kWsStats = 0, kWsPart = 8, kWsGram = kWsPart + 2 * kRedBlocks,
+                 kWsEvals = kWsGram + 2 * (kMaxModes * (kMaxModes + 1) / 2) * kGramChunks, kWsU = kWsEvals + kMaxModes;
+constexpr size_t kWsBytes = kWsU * sizeof(double) + kMaxModes * kMaxModes * sizeof(float2);
+
+// scipy.signal.windows.gaussian(k, std) / sum, f64 then f32 (utils/image_proc.py:435-449)
+cons::Taps scipy_taps(int ks, double std) {
+  cons::Taps t{};
+  t.half = ks / 2;
+  double w[cons::kMaxTaps], sum = 0;
+  for (int i = 0; i < ks; ++i) {
+    const double n = i - (ks - 1) / 2.0;
+    w[i] = std::exp(-0.5 * (n / std) * (n / std));
+    sum += w[i];
+  }
+  for (int i = 0; i < ks; ++i) t.w[i] = (float)(w[i] / sum);
+  return t;
+}
+// torchvision _get_gaussian_kernel1d: f32 linspace, exp, normalise in f32
+cons::Taps torchvision_taps(int ks, float sigma) {
+  cons::Taps t{};
+  t.half = ks / 2;
+  const float half = (ks - 1) * 0.5f;
+  float sum = 0.f;
+  for (int i = 0; i < ks; ++i) {
+    const float x = ks > 1 ? -half + i * ((2 * half) / (float)(ks - 1)) : 0.f;
+    t.w[i] = std::exp(-0.5f * (x / sigma) * (x / sigma));
+    sum += t.w[i];
+  }
+  for (int i = 0; i < ks; ++i) t.w[i] /= sum;
+  return t;
+}
+
+template <int H>
+void launch_column(hipStream_t st, float* a, float* p, const cons::ObjCfg& c, int pointwise_on) {
+  const long long cols = (long long)c.O * c.Ny * c.Nx;
+  hipLaunchKernelGGL(cons::k_obj_column<H>, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, a, p, c,
+                     pointwise_on);
+}
+void launch_column_h(int h, hipStream_t st, float* a, float* p, const cons::ObjCfg& c, int pw) {
+  switch (h) {
+    case 0: launch_column<0>(st, a, p, c, pw); break;
+    case 1: launch_column<1>(st, a, p, c, pw); break;
+    case 2: launch_column<2>(st, a, p, c, pw); break;
+    case 3: launch_column<3>(st, a, p, c, pw); break;
+    case 4: launch_column<4>(st, a, p, c, pw); break;
+    case 5: launch_column<5>(st, a, p, c, pw); break;
+    case 6: launch_column<6>(st, a, p, c, pw); break;
+    default: launch_column<7>(st, a, p, c, pw); break;
+  }
+}
+template <int P>
+void launch_ortho_apply(hipStream_t st, float2* M, long long n2, const float2* U) {
+  hipLaunchKernelGGL(cons::k_ortho_apply<P>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, M, n2, U);
+}
+}  // namespace
+
+extern "C" size_t ptyx_constraints_ws_bytes(void) { return kWsBytes; }
+extern "C" size_t ptyx_constraints_evals_offset(void) { return kWsEvals * sizeof(double); }
+
+extern "C" int ptyx_obj_rblur(void* stream, const float* in, float* out, int32_t n_planes, int32_t Ny, int32_t Nx,
+                              int32_t kernel_size, float sigma) {
+  abi::clear_error();
+  if (n_planes < 0 || Ny <= 0 || Nx <= 0) return abi::fail(PTYX_EINVAL, "obj_rblur: bad shape");
+  if (kernel_size < 1 || kernel_size % 2 == 0 || kernel_size / 2 > kMaxHalf)
+    return abi::fail(PTYX_EUNSUPPORTED, "obj_rblur: kernel_size must be odd and <= 15");
+  if (!(sigma > 0.f)) return abi::fail(PTYX_EINVAL, "obj_rblur: sigma must be > 0");
+  if (kernel_size / 2 >= Ny || kernel_size / 2 >= Nx)
+    return abi::fail(PTYX_EINVAL, "obj_rblur: reflect padding needs kernel_size/2 < Ny, Nx");
+  if (n_planes == 0) return PTYX_OK;
+  if (!in || !out || in == out) return abi::fail(PTYX_EINVAL, "obj_rblur: in / out null or aliased");
+  const cons::Taps t = torchvision_taps(kernel_size, sigma);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(cons::k_rblur, dim3((Nx + cons::kTX - 1) / cons::kTX, (Ny + cons::kTY - 1) / cons::kTY, n_planes),
+                     dim3(256), 0, st, in, out, Ny, Nx, t);
+  return abi::launch_status("k_rblur launch");
+}
+
+extern "C" int ptyx_obj_constrain(void* stream, float* obja, float* objp, int32_t O, int32_t Nz, int32_t Ny,
+                                  int32_t Nx, const ptyx_obj_constraints* cc, void* ws) {
+  abi::clear_error();
+  if (!cc) return abi::fail(PTYX_EINVAL, "obj_constrain: config is null");
+  if (O <= 0 || Nz <= 0 || Ny <= 0 || Nx <= 0) return abi::fail(PTYX_EINVAL, "obj_constrain: bad shape");
+  if (!obja || !objp) return abi::fail(PTYX_EINVAL, "obj_constrain: obja / objp null");
+  const bool zb = (cc->zblur_a || cc->zblur_p) && cc->zblur_std != 0.f;
+  if (zb && (cc->zblur_ks < 1 || cc->zblur_ks % 2 == 0 || cc->zblur_ks / 2 > kMaxHalf))
+    return abi::fail(PTYX_EUNSUPPORTED, "obj_zblur: kernel_size must be odd and <= 15");
+  const bool cr = cc->cr_a || cc->cr_p, submin = cc->pos_on && cc->pos_subtract_min;
+  if ((cr || submin) && !ws) return abi::fail(PTYX_EINVAL, "obj_constrain: workspace needed for complex_ratio / subtract_min");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* wsd = reinterpret_cast<double*>(ws);
+  cons::ObjCfg c{};
+  c.O = O;
+  c.Nz = Nz;
+  c.Ny = Ny;
+  c.Nx = Nx;
+  c.zb_a = zb && cc->zblur_a;
+  c.zb_p = zb && cc->zblur_p;
+  if (zb) c.zt = scipy_taps(cc->zblur_ks, cc->zblur_std);
+  c.cr_a = cc->cr_a;
+  c.cr_p = cc->cr_p;
+  c.alpha1 = cc->cr_alpha1;
+  c.alpha2 = cc->cr_alpha2;
+  c.mir = cc->mir_on;
+  c.mir_relax = cc->mir_relax;
+  c.mir_scale = cc->mir_scale;
+  c.mir_power = cc->mir_power;
+  c.thr = cc->thr_on;
+  c.thr_relax = cc->thr_relax;
+  c.thr_lo = cc->thr_lo;
+  c.thr_hi = cc->thr_hi;
+  c.pos = cc->pos_on;
+  c.pos_submin = submin;
+  c.pos_relax = cc->pos_relax;
+  c.stats = wsd ? wsd + kWsStats : nullptr;
+  const int h = zb ? cc->zblur_ks / 2 : 0;
+  const bool pw = cr || c.mir || c.thr || c.pos;
+  if (!cr && !submin) {              // the default chain: ONE pass over the object
+    if (zb || pw) launch_column_h(h, st, obja, objp, c, pw ? 1 : 0);
+    return abi::launch_status("k_obj_column launch");
+  }
+  // options needing global scalars: z-blur pass, reductions, then the point-wise pass
+  if (zb) {
+    cons::ObjCfg z = c;
+    launch_column_h(h, st, obja, objp, z, 0);
+  }
+  const long long n = (long long)O * Nz * Ny * Nx;
+  if (cr) {
+    hipLaunchKernelGGL(cons::k_obj_reduce<0>, dim3(kRedBlocks), dim3(256), 0, st, obja, objp, n, c, wsd + kWsPart);
+    hipLaunchKernelGGL(cons::k_reduce_final<0>, dim3(1), dim3(64), 0, st, wsd + kWsPart, kRedBlocks, wsd + kWsStats);
+  }
+  if (submin) {
+    hipLaunchKernelGGL(cons::k_obj_reduce<1>, dim3(kRedBlocks), dim3(256), 0, st, obja, objp, n, c, wsd + kWsPart);
+    hipLaunchKernelGGL(cons::k_reduce_final<1>, dim3(1), dim3(64), 0, st, wsd + kWsPart, kRedBlocks, wsd + kWsStats);
+  }
+  cons::ObjCfg q = c;
+  q.zb_a = q.zb_p = 0;
+  launch_column_h(0, st, obja, objp, q, 1);
+  return abi::launch_status("obj_constrain launch");
+}
+
+extern "C" int ptyx_probe_fix_int(void* stream, float* probe, int32_t P, int32_t N, const float* probe_int_sum,
+                                  void* ws) {
+  abi::clear_error();
+  if (P <= 0 || N <= 0) return abi::fail(PTYX_EINVAL, "fix_probe_int: bad shape");
+  if (!probe || !probe_int_sum || !ws) return abi::fail(PTYX_EINVAL, "fix_probe_int: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* wsd = reinterpret_cast<double*>(ws);
+  const long long n = (long long)P * N * N;
+  float2* x = reinterpret_cast<float2*>(probe);
+  hipLaunchKernelGGL(cons::k_sumsq, dim3(kRedBlocks), dim3(256), 0, st, x, n, wsd + kWsPart);
+  hipLaunchKernelGGL(cons::k_fix_int_final, dim3(1), dim3(64), 0, st, wsd + kWsPart, kRedBlocks, probe_int_sum,
+                     wsd + kWsStats);
+  hipLaunchKernelGGL(cons::k_cscale, dim3(256), dim3(256), 0, st, x, n, wsd + kWsStats);
+  return abi::launch_status("fix_probe_int launch");
+}
+
+extern "C" int ptyx_probe_ortho(void* stream, float* probe, int32_t P, int32_t N, void* ws) {
+  abi::clear_error();
+  if (P <= 0 || N <= 0) return abi::fail(PTYX_EINVAL, "ortho_pmode: bad shape");
+  if (P > kMaxModes) return abi::fail(PTYX_EUNSUPPORTED, "ortho_pmode: at most 16 probe modes");
+  if (!probe || !ws) return abi::fail(PTYX_EINVAL, "ortho_pmode: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* wsd = reinterpret_cast<double*>(ws);
+  float2* M = reinterpret_cast<float2*>(probe);
+  const long long n2 = (long long)N * N;
+  const int npair = P * (P + 1) / 2;
+  float2* U = reinterpret_cast<float2*>(wsd + kWsU);
+  hipLaunchKernelGGL(cons::k_gram, dim3(kGramChunks, npair), dim3(256), 0, st, M, P, n2, kGramChunks, wsd + kWsGram);
+  hipLaunchKernelGGL(cons::k_ortho_eig, dim3(1), dim3(256), 0, st, wsd + kWsGram, P, kGramChunks, U, wsd + kWsEvals);
+  switch (P) {
+    case 1: launch_ortho_apply<1>(st, M, n2, U); break;
+    case 2: launch_ortho_apply<2>(st, M, n2, U); break;
+    case 3: launch_ortho_apply<3>(st, M, n2, U); break;
+    case 4: launch_ortho_apply<4>(st, M, n2, U); break;
+    case 5: launch_ortho_apply<5>(st, M, n2, U); break;
+    case 6: launch_ortho_apply<6>(st, M, n2, U); break;
+    case 7: launch_ortho_apply<7>(st, M, n2, U); break;
+    case 8: launch_ortho_apply<8>(st, M, n2, U); break;
+    case 9: launch_ortho_apply<9>(st, M, n2, U); break;
+    case 10: launch_ortho_apply<10>(st, M, n2, U); break;
+    case 11: launch_ortho_apply<11>(st, M, n2, U); break;
+    case 12: launch_ortho_apply<12>(st, M, n2, U); break;
+    case 13: launch_ortho_apply<13>(st, M, n2, U); break;
+    case 14: launch_ortho_apply<14>(st, M, n2, U); break;
+    case 15: launch_ortho_apply<15>(st, M, n2, U); break;
+    default: launch_ortho_apply<16>(st, M, n2, U); break;
+  }
+  return abi::launch_status("ortho_pmode launch");
+}

@@ -1,0 +1,433 @@
+// ptyx_constraints.hpp — PtyRAD's iteration-wise constraints on the device.
+// Included by ptyx_kernels.hip; the C ABI is ptyx_obj_rblur / ptyx_obj_constrain /
+// ptyx_probe_fix_int / ptyx_probe_ortho (include/ptyx.h).
+//
+// Object constraints are HBM-bound streams over (O, Nz, Ny, Nx) f32, so they are fused:
+//   k_rblur       obj_rblur   (constraints.py:83-98, torchvision gaussian_blur): separable 2-D
+//                 Gaussian, reflect padding, one LDS tile (TY + 2h) × (TX + 2h) per workgroup;
+//                 each voxel read once from HBM and written once (out of place).
+//   k_obj_column  obj_zblur (:100-114, gaussian_blur_1d: conv1d 'same', replicate padding) +
+//                 complex_ratio (:147-163, :333-358) + mirrored_amp (:165-179) + obja_thresh
+//                 (:181-190) + objp_postiv (:192-208) in ONE pass: one thread per (o, y, x)
+//                 column walks z with a register window of 2h + 1 slices, so the z-blur needs no
+//                 second read and works in place; lanes run along x, so every z-slice access of
+//                 a wave is one contiguous 256-B segment.
+//   k_obj_reduce / k_reduce_final   the global scalars some options need (complex_ratio's Cbar,
+//                 objp_postiv 'subtract_min''s minimum): fp64 per-block partials summed in a
+//                 fixed order (deterministic), kept on the device — no host round trip.
+// Probe constraints (P ≤ 16 modes of N × N):
+//   fix_probe_int (:70-81): k_sumsq partials → k_fix_int_final (scale) → k_cscale.
+//   ortho_pmode (:34-41, orthogonalize_modes_vec :255-291): k_gram (A = M M^H, one block column
+//   per mode pair, fp64) → k_ortho_eig (one workgroup: fixed-order partial sums, cyclic complex
+//   Jacobi in fp64, LAPACK geev eigenvector normalisation — unit norm, largest component real
+//   positive — and the descending-eigenvalue order that sort_by_mode_int produces) →
+//   k_ortho_apply (ortho = V^H M per pixel, in place).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ptyx {
+namespace cons {
+
+constexpr int kMaxHalf = 7;        // kernel_size ≤ 15
+constexpr int kMaxTaps = 2 * kMaxHalf + 1;
+constexpr int kMaxModes = 16;
+constexpr int kRedBlocks = 512;    // fixed reduction grid (deterministic partials)
+
+struct Taps {
+  float w[kMaxTaps];
+  int half;
+};
+
+// ------------------------------------------------------------------ obj_rblur
+constexpr int kTX = 64, kTY = 16;
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
+}
+// grid (ceil(Nx/64), ceil(Ny/16), planes); block 256
+__global__ __launch_bounds__(256) void k_rblur(const float* __restrict__ in, float* __restrict__ out, int Ny, int Nx,
+                                               Taps t) {
+  __shared__ float s_in[kTY + 2 * kMaxHalf][kTX + 2 * kMaxHalf + 1];
+  __shared__ float s_mid[kTY + 2 * kMaxHalf][kTX + 1];
+  const int h = t.half;
+  const size_t plane = (size_t)blockIdx.z * Ny * Nx;
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const int rows = kTY + 2 * h, cols = kTX + 2 * h;
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int r = e / cols, c = e - r * cols;
+    const int gy = reflect_idx(min(y0 + r - h, Ny - 1 + h), Ny);
+    const int gx = reflect_idx(min(x0 + c - h, Nx - 1 + h), Nx);
+    s_in[r][c] = in[plane + (size_t)gy * Nx + gx];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < rows * kTX; e += blockDim.x) {
+    const int r = e / kTX, c = e - r * kTX;
+    float acc = 0.f;
+    for (int j = 0; j <= 2 * h; ++j) acc = fmaf(t.w[j], s_in[r][c + j], acc);
+    s_mid[r][c] = acc;
+  }
+  __syncthreads();
+  const int c = threadIdx.x & (kTX - 1);
+  for (int r = threadIdx.x >> 6; r < kTY; r += blockDim.x >> 6) {
+    const int gy = y0 + r, gx = x0 + c;
+    if (gy >= Ny || gx >= Nx) continue;
+    float acc = 0.f;
+    for (int i = 0; i <= 2 * h; ++i) acc = fmaf(t.w[i], s_mid[r + i][c], acc);
+    out[plane + (size_t)gy * Nx + gx] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ object column pass
+struct ObjCfg {
+  int O, Nz, Ny, Nx;
+  int zb_a, zb_p;            // obj_zblur on amplitude / phase
+  Taps zt;
+  int cr_a, cr_p;            // complex_ratio writes amplitude / phase
+  float alpha1, alpha2;
+  int mir;
+  float mir_relax, mir_scale, mir_power;
+  int thr;
+  float thr_relax, thr_lo, thr_hi;
+  int pos, pos_submin;
+  float pos_relax;
+  const double* stats;       // [Σ|ln a|, Σ|p|, Cbar, min p'] (device), when cr / submin are on
+};
+
+__device__ __forceinline__ float powf_pos(float x, float e) {
+  // x ≥ 0; torch.pow(x, e) for float e (x = 0 → 0 for e > 0, 1 for e = 0)
+  if (e == 4.0f) { const float x2 = x * x; return x2 * x2; }
+  if (e == 2.0f) return x * x;
+  if (e == 1.0f) return x;
+  if (x == 0.f) return e == 0.f ? 1.f : 0.f;
+  return exp2f(e * log2f(x));
+}
+
+// complex_ratio (both outputs from the pre-constraint a, p), then mirrored_amp, obja_thresh,
+// objp_postiv, in the order of CombinedConstraint.forward (constraints.py:227-246)
+__device__ __forceinline__ void pointwise(const ObjCfg& c, float cbar, float pmin, float& a, float& p) {
+  if (c.cr_a | c.cr_p) {
+    const float la = logf(a);
+    const float an = expf((1.f - c.alpha1) * la - c.alpha1 * cbar * p);
+    const float pn = (1.f - c.alpha2) * p - c.alpha2 / (cbar + 1e-8f) * la;
+    if (c.cr_a) a = an;
+    if (c.cr_p) p = pn;
+  }
+  if (c.mir) a = c.mir_relax * a + (1.f - c.mir_relax) * (1.f - c.mir_scale * powf_pos(fmaxf(p, 0.f), c.mir_power));
+  if (c.thr) a = c.thr_relax * a + (1.f - c.thr_relax) * fminf(fmaxf(a, c.thr_lo), c.thr_hi);
+  if (c.pos) p = c.pos_relax * p + (1.f - c.pos_relax) * (c.pos_submin ? p - pmin : fmaxf(p, 0.f));
+}
+
+// One thread per (o, y, x); register window over z.  In place: slice z is written after every
+// read that needs its original value (the window holds z − h .. z + h; the only later read of
+// an already-written slice would be the clamped index Nz − 1, which is written last).
+template <int H>
+__global__ __launch_bounds__(256) void k_obj_column(float* __restrict__ A, float* __restrict__ Pp, ObjCfg c, int pointwise_on) {
+  const long long col = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long plane = (long long)c.Ny * c.Nx;
+  if (col >= (long long)c.O * plane) return;
+  const long long o = col / plane, yx = col - o * plane;
+  float* a = A + o * c.Nz * plane + yx;
+  float* p = Pp + o * c.Nz * plane + yx;
+  const float cbar = (c.cr_a | c.cr_p) ? (float)c.stats[2] : 0.f;
+  const float pmin = c.pos_submin ? (float)c.stats[3] : 0.f;
+  const int nz = c.Nz;
+  float wa[2 * H + 1], wp[2 * H + 1];
+#pragma unroll
+  for (int j = 0; j <= 2 * H; ++j) {
+    const int z = min(max(j - H, 0), nz - 1);
+    wa[j] = a[z * plane];
+    wp[j] = p[z * plane];
+  }
+  for (int z = 0; z < nz; ++z) {
+    float va = wa[H], vp = wp[H];
+    if (H > 0) {
+      if (c.zb_a) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j <= 2 * H; ++j) s = fmaf(c.zt.w[j], wa[j], s);
+        va = s;
+      }
+      if (c.zb_p) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j <= 2 * H; ++j) s = fmaf(c.zt.w[j], wp[j], s);
+        vp = s;
+      }
+    }
+    // advance the window before slice z is overwritten
+    const int zn = min(z + 1 + H, nz - 1);
+    const float na = a[zn * plane], np_ = p[zn * plane];
+#pragma unroll
+    for (int j = 0; j < 2 * H; ++j) {
+      wa[j] = wa[j + 1];
+      wp[j] = wp[j + 1];
+    }
+    wa[2 * H] = na;
+    wp[2 * H] = np_;
+    if (pointwise_on) pointwise(c, cbar, pmin, va, vp);
+    a[z * plane] = va;
+    p[z * plane] = vp;
+  }
+}
+
+// Block partials (fp64) for the global scalars:
+//   MODE 0: Σ|ln a|, Σ|p|                 (complex_ratio Cbar, constraints.py:344)
+//   MODE 1: min over p after complex_ratio (objp_postiv 'subtract_min', constraints.py:200)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_obj_reduce(const float* __restrict__ A, const float* __restrict__ Pp, long long n,
+                                                    ObjCfg c, double* part) {
+  __shared__ double s0[256], s1[256];
+  double v0 = MODE == 0 ? 0.0 : __builtin_huge_val(), v1 = 0.0;
+  const float cbar = MODE == 1 && (c.cr_p) ? (float)c.stats[2] : 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float a = A[i], p = Pp[i];
+    if (MODE == 0) {
+      v0 += fabs((double)logf(a));
+      v1 += fabs((double)p);
+    } else {
+      float pv = p;
+      if (c.cr_p) pv = (1.f - c.alpha2) * p - c.alpha2 / (cbar + 1e-8f) * logf(a);
+      v0 = fmin(v0, (double)pv);
+    }
+  }
+  s0[threadIdx.x] = v0;
+  s1[threadIdx.x] = v1;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      s0[threadIdx.x] = MODE == 0 ? s0[threadIdx.x] + s0[threadIdx.x + s] : fmin(s0[threadIdx.x], s0[threadIdx.x + s]);
+      s1[threadIdx.x] += s1[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s0[0];
+    part[2 * blockIdx.x + 1] = s1[0];
+  }
+}
+// one block: fixed-order sum of the partials → stats
+template <int MODE>
+__global__ void k_reduce_final(const double* part, int nblk, double* stats) {
+  if (threadIdx.x != 0) return;
+  if (MODE == 0) {
+    double s0 = 0, s1 = 0;
+    for (int b = 0; b < nblk; ++b) {
+      s0 += part[2 * b];
+      s1 += part[2 * b + 1];
+    }
+    stats[0] = s0;
+    stats[1] = s1;
+    // Cbar in f32 arithmetic as the reference (sums are f32 tensors there)
+    stats[2] = (double)((float)s0 / ((float)s1 + 1e-8f));
+  } else {
+    double m = __builtin_huge_val();
+    for (int b = 0; b < nblk; ++b) m = fmin(m, part[2 * b]);
+    stats[3] = m;
+  }
+}
+
+// ------------------------------------------------------------------ probe: fix_probe_int
+__global__ __launch_bounds__(256) void k_sumsq(const float2* __restrict__ x, long long n, double* part) {
+  __shared__ double s[256];
+  double v = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float2 u = x[i];
+    v += (double)u.x * u.x + (double)u.y * u.y;
+  }
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) s[threadIdx.x] += s[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+// scale = sqrt(target) / sqrt(Σ|P|²)   (constraints.py:76-79)
+__global__ void k_fix_int_final(const double* part, int nblk, const float* target, double* stats) {
+  if (threadIdx.x != 0) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += part[b];
+  stats[4] = s;
+  stats[5] = sqrt((double)target[0]) / sqrt(s);
+}
+__global__ __launch_bounds__(256) void k_cscale(float2* x, long long n, const double* stats) {
+  const float k = (float)stats[5];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float2 u = x[i];
+    x[i] = make_float2(u.x * k, u.y * k);
+  }
+}
+
+// ------------------------------------------------------------------ probe: ortho_pmode
+struct Cd {
+  double x, y;
+};
+__device__ __forceinline__ Cd cd_mul(Cd a, Cd b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ Cd cd_conj(Cd a) { return {a.x, -a.y}; }
+__device__ __forceinline__ Cd cd_add(Cd a, Cd b) { return {a.x + b.x, a.y + b.y}; }
+
+// grid (nchunk, npairs): pair (i ≤ j) → partial Σ_n M_i[n] conj(M_j[n]) over chunk, fp64
+__global__ __launch_bounds__(256) void k_gram(const float2* __restrict__ M, int P, long long n2, int nchunk, double* part) {
+  __shared__ double sx[256], sy[256];
+  int pr = blockIdx.y, i = 0;
+  while (pr >= P - i) {
+    pr -= P - i;
+    ++i;
+  }
+  const int j = i + pr;
+  const float2* mi = M + (size_t)i * n2;
+  const float2* mj = M + (size_t)j * n2;
+  const long long per = (n2 + nchunk - 1) / nchunk;
+  const long long b = blockIdx.x * per, e = min(n2, b + per);
+  double ax = 0, ay = 0;
+  for (long long k = b + threadIdx.x; k < e; k += blockDim.x) {
+    const float2 u = mi[k], v = mj[k];
+    ax += (double)u.x * v.x + (double)u.y * v.y;     // u conj(v)
+    ay += (double)u.y * v.x - (double)u.x * v.y;
+  }
+  sx[threadIdx.x] = ax;
+  sy[threadIdx.x] = ay;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sx[threadIdx.x] += sx[threadIdx.x + s];
+      sy[threadIdx.x] += sy[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * ((size_t)blockIdx.y * nchunk + blockIdx.x)] = sx[0];
+    part[2 * ((size_t)blockIdx.y * nchunk + blockIdx.x) + 1] = sy[0];
+  }
+}
+
+// one workgroup: Gram matrix from the partials (fixed order), Hermitian eigendecomposition by
+// cyclic complex Jacobi (fp64), geev normalisation, descending order; writes U (P × P, f32
+// complex, U[p][q] = conj(V[q][perm[p]]) so that ortho_p = Σ_q U[p][q] M_q).
+__global__ __launch_bounds__(256) void k_ortho_eig(const double* part, int P, int nchunk, float2* U, double* evals) {
+  __shared__ Cd A[kMaxModes][kMaxModes];
+  __shared__ Cd V[kMaxModes][kMaxModes];
+  const int npair = P * (P + 1) / 2;
+  for (int pr = threadIdx.x; pr < npair; pr += blockDim.x) {
+    int r = pr, i = 0;
+    while (r >= P - i) {
+      r -= P - i;
+      ++i;
+    }
+    const int j = i + r;
+    double sx = 0, sy = 0;
+    for (int c = 0; c < nchunk; ++c) {
+      sx += part[2 * ((size_t)pr * nchunk + c)];
+      sy += part[2 * ((size_t)pr * nchunk + c) + 1];
+    }
+    A[i][j] = {sx, sy};
+    A[j][i] = {sx, -sy};
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < P; ++i) {
+    A[i][i].y = 0;
+    for (int j = 0; j < P; ++j) V[i][j] = {i == j ? 1.0 : 0.0, 0.0};
+  }
+  double scale = 0;
+  for (int i = 0; i < P; ++i) scale += A[i][i].x;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double off = 0;
+    for (int i = 0; i < P; ++i)
+      for (int j = i + 1; j < P; ++j) off += A[i][j].x * A[i][j].x + A[i][j].y * A[i][j].y;
+    if (off <= 1e-30 * scale * scale) break;
+    for (int p = 0; p < P; ++p)
+      for (int q = p + 1; q < P; ++q) {
+        const double g = sqrt(A[p][q].x * A[p][q].x + A[p][q].y * A[p][q].y);
+        if (g <= 1e-300) continue;
+        const Cd e = {A[p][q].x / g, A[p][q].y / g};            // phase of A_pq
+        const double tau = (A[q][q].x - A[p][p].x) / (2 * g);
+        const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1 + tau * tau));
+        const double cs = 1 / sqrt(1 + t * t), sn = t * cs;
+        // U = diag(1, conj(e)) · [[c, s], [-s, c]] on (p, q)
+        const Cd upp = {cs, 0}, upq = {sn, 0};
+        const Cd uqp = cd_mul({-sn, 0}, cd_conj(e)), uqq = cd_mul({cs, 0}, cd_conj(e));
+        for (int k = 0; k < P; ++k) {   // A ← A U, V ← V U (columns p, q)
+          const Cd akp = A[k][p], akq = A[k][q];
+          A[k][p] = cd_add(cd_mul(akp, upp), cd_mul(akq, uqp));
+          A[k][q] = cd_add(cd_mul(akp, upq), cd_mul(akq, uqq));
+          const Cd vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = cd_add(cd_mul(vkp, upp), cd_mul(vkq, uqp));
+          V[k][q] = cd_add(cd_mul(vkp, upq), cd_mul(vkq, uqq));
+        }
+        for (int k = 0; k < P; ++k) {   // A ← U^H A (rows p, q)
+          const Cd apk = A[p][k], aqk = A[q][k];
+          A[p][k] = cd_add(cd_mul(cd_conj(upp), apk), cd_mul(cd_conj(uqp), aqk));
+          A[q][k] = cd_add(cd_mul(cd_conj(upq), apk), cd_mul(cd_conj(uqq), aqk));
+        }
+        A[p][q] = {0, 0};
+        A[q][p] = {0, 0};
+        A[p][p].y = 0;
+        A[q][q].y = 0;
+      }
+  }
+  // geev normalisation: unit norm, largest-modulus component (first on ties) real positive
+  for (int j = 0; j < P; ++j) {
+    double nrm = 0;
+    for (int k = 0; k < P; ++k) nrm += V[k][j].x * V[k][j].x + V[k][j].y * V[k][j].y;
+    nrm = sqrt(nrm);
+    int km = 0;
+    double best = -1;
+    for (int k = 0; k < P; ++k) {
+      V[k][j] = {V[k][j].x / nrm, V[k][j].y / nrm};
+      const double m2 = V[k][j].x * V[k][j].x + V[k][j].y * V[k][j].y;
+      if (m2 > best) {
+        best = m2;
+        km = k;
+      }
+    }
+    const double am = sqrt(best);
+    const Cd ph = {V[km][j].x / am, -V[km][j].y / am};
+    for (int k = 0; k < P; ++k) V[k][j] = cd_mul(V[k][j], ph);
+    V[km][j].y = 0;
+  }
+  // descending eigenvalue order (stable)
+  int perm[kMaxModes];
+  for (int i = 0; i < P; ++i) perm[i] = i;
+  for (int i = 1; i < P; ++i) {
+    const int pi = perm[i];
+    int k = i - 1;
+    while (k >= 0 && A[perm[k]][perm[k]].x < A[pi][pi].x) {
+      perm[k + 1] = perm[k];
+      --k;
+    }
+    perm[k + 1] = pi;
+  }
+  for (int p = 0; p < P; ++p) {
+    evals[p] = A[perm[p]][perm[p]].x;
+    for (int q = 0; q < P; ++q) {
+      const Cd v = V[q][perm[p]];
+      U[p * P + q] = make_float2((float)v.x, (float)-v.y);
+    }
+  }
+}
+
+// ortho_p[n] = Σ_q U[p][q] M_q[n], one pixel per thread, in place (P a compile-time constant so
+// the P modes of a pixel stay in registers)
+template <int P>
+__global__ __launch_bounds__(256) void k_ortho_apply(float2* M, long long n2, const float2* U) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n2) return;
+  float2 m[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) m[q] = M[(size_t)q * n2 + k];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    float ax = 0.f, ay = 0.f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const float2 u = U[p * P + q];
+      ax = fmaf(u.x, m[q].x, fmaf(-u.y, m[q].y, ax));
+      ay = fmaf(u.x, m[q].y, fmaf(u.y, m[q].x, ay));
+    }
+    M[(size_t)p * n2 + k] = make_float2(ax, ay);
+  }
+}
+
+}  // namespace cons
+}  // namespace ptyx

@@ -32,6 +32,7 @@
 
 #include "ptyx_common.hpp"
 #include "ptyx_fused3.hpp"
+#include "ptyx_abi.hpp"
 
 namespace ptyx {
 
@@ -658,7 +659,7 @@ static void free_plan(ptyx_plan* pl) {
   delete pl;
 }
 
-extern "C" int ptyx_version(void) { return 100; }
+extern "C" int ptyx_version(void) { return 101; }
 
 extern "C" const char* ptyx_last_error(void) { return g_err.c_str(); }
 
@@ -900,6 +901,15 @@ static int launch_status(const char* what) {
   if (e != hipSuccess) return hip_fail(e, what);
   return PTYX_OK;
 }
+
+// shared with the other translation units of libptyx.so (ptyx_abi.hpp)
+namespace ptyx {
+namespace abi {
+void clear_error() { g_err.clear(); }
+int fail(int code, const std::string& msg) { return ::fail(code, msg); }
+int launch_status(const char* what) { return ::launch_status(what); }
+}  // namespace abi
+}  // namespace ptyx
 
 // ---------------------------------------------------------------- k_fused3 path (N = 128)
 // Launch sequence of one ptyx_forward_loss_grad call on the register-resident engine.
@@ -1217,3 +1227,4 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   }
   return PTYX_OK;
 }
+

@@ -33,6 +33,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Inputs) == 8 * 8
     assert ctypes.sizeof(_lib.Grads) == 4 * 8
     assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
+    assert ctypes.sizeof(_lib.ObjConstraints) == 19 * 4
 
 
 def test_plan_create_rejects_bad_dims_without_gpu():
@@ -47,3 +48,18 @@ def test_plan_create_rejects_bad_dims_without_gpu():
     d = _lib.Dims(128, 1, 1, 1, 100, 200, 4, 4, 0)   # object smaller than the window
     assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EINVAL
     assert lib.ptyx_plan_create(None, ctypes.byref(d), 0) == _lib.PTYX_EINVAL
+
+
+def test_constraint_entry_points_validate_without_gpu():
+    lib = _lib.load()
+    assert lib.ptyx_constraints_ws_bytes() >= 8 * 8
+    assert lib.ptyx_constraints_evals_offset() < lib.ptyx_constraints_ws_bytes()
+    # argument checks happen before any HIP call
+    assert lib.ptyx_obj_rblur(None, None, None, 1, 32, 32, 4, 1.0) == _lib.PTYX_EUNSUPPORTED   # even kernel
+    assert lib.ptyx_obj_rblur(None, None, None, 1, 2, 32, 5, 1.0) == _lib.PTYX_EINVAL          # reflect pad
+    assert lib.ptyx_probe_ortho(None, None, 17, 32, None) == _lib.PTYX_EUNSUPPORTED             # > 16 modes
+    c = _lib.ObjConstraints()
+    c.zblur_a, c.zblur_ks, c.zblur_std = 1, 6, 1.0
+    assert lib.ptyx_obj_constrain(None, ctypes.c_void_p(8), ctypes.c_void_p(8), 1, 2, 4, 4, ctypes.byref(c),
+                                  None) == _lib.PTYX_EUNSUPPORTED
+    assert b"odd" in lib.ptyx_last_error()
