@@ -79,8 +79,21 @@ def run_recon(z, rank_world=None, niter=None):
     sizes = z["batch_sizes"]
     batches = np.split(z["batches"], np.cumsum(sizes)[:-1])
     ctx = DistContext()
+    cfn = None
+    if "constraint_params" in z.files and json.loads(str(z["constraint_params"])) is not None:
+        cp, pis = json.loads(str(z["constraint_params"])), float(z["probe_int_sum"])
+
+        def cfn(m, it):   # the constraints oracle on the replica's parameters (every rank alike)
+            from tests.test_oracle_golden import apply_constraint_oracle
+            prm = {"obja": m.opt_obja.detach().numpy(), "objp": m.opt_objp.detach().numpy(),
+                   "probe": m.opt_probe.detach().numpy()}
+            apply_constraint_oracle(prm, cp, pis, it)
+            with torch.no_grad():
+                m.opt_obja.copy_(torch.from_numpy(prm["obja"]))
+                m.opt_objp.copy_(torch.from_numpy(prm["objp"]))
+                m.opt_probe.copy_(torch.from_numpy(prm["probe"]))
     for it in range(1, (niter or int(z["niter"])) + 1):
-        recon_step(batches, int(z["grad_accumulation"]), model, opt, loss, None, it, verbose=False, dist_ctx=ctx)
+        recon_step(batches, int(z["grad_accumulation"]), model, opt, loss, cfn, it, verbose=False, dist_ctx=ctx)
     return {k: v.detach().numpy().copy() for k, v in (("obja", model.opt_obja), ("objp", model.opt_objp),
                                                        ("probe", model.opt_probe),
                                                        ("shifts", model.opt_probe_pos_shifts))}, model

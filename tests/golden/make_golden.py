@@ -14,7 +14,8 @@ and ``loss.backward()`` (autograd), and stores inputs + outputs as .npz:
            loss_total, g_obja, g_objp, g_probe (P,N,N,2), g_shifts (S,2)
 
 and a 3-iteration recon_step trajectory (src/ptyrad/reconstruction.py:658)
-with fixed batches, Adam, and a no-op constraint.  The data written are
+with fixed batches, Adam, and a no-op constraint (plus one with the schema-default
+CombinedConstraint, constraints.py:227-246).  The data written are
 inputs and outputs only; no reference source is copied.
 """
 import json
@@ -154,7 +155,7 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
 
-def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumulation, seed):
+def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumulation, seed, constraint_params=None):
     scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
     meas = simulate_meas(scan, probe, H, occu, gta, gtp, 5e-4)
     iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas,
@@ -171,9 +172,14 @@ def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumul
     opt = reconstruction.create_optimizer(model.optimizer_params, model.optimizable_params,
                                           verbose=False)
     hist = []
+    if constraint_params is None:
+        cfn = lambda m, i: None   # noqa: E731
+    else:
+        import ptyrad.constraints as cons
+        cfn = cons.CombinedConstraint(constraint_params, device="cpu", verbose=False)
     for it in range(1, niter + 1):
         bl = reconstruction.recon_step(batches, grad_accumulation, model, opt, loss_fn,
-                                       lambda m, i: None, it, verbose=False)
+                                       cfn, it, verbose=False)
         hist.append([float(np.mean(v)) for v in bl.values()])
     np.savez_compressed(
         os.path.join(HERE, f"{name}.npz"),
@@ -185,12 +191,27 @@ def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumul
         final_obja=model.opt_obja.detach().numpy(), final_objp=model.opt_objp.detach().numpy(),
         final_probe=torch.view_as_complex(model.opt_probe.detach()).numpy(),
         final_shifts=model.opt_probe_pos_shifts.detach().numpy(),
-        loss_hist=np.array(hist), loss_params=json.dumps(DEFAULT_LOSS))
+        loss_hist=np.array(hist), loss_params=json.dumps(DEFAULT_LOSS),
+        probe_int_sum=np.float32(model.probe_int_sum.item()),
+        constraint_params=json.dumps(constraint_params))
     print(f"{name}: loss_hist={np.array(hist).sum(1)}")
+
+
+def constrained_trajectory():
+    """3 iterations with the schema-default constraints (obj_rblur off: torchvision is absent)."""
+    import copy
+
+    from constraint_defaults import DEFAULTS
+    cp = copy.deepcopy(DEFAULTS)
+    cp["obj_rblur"]["freq"] = None
+    run_trajectory("traj_n64_p2z2_cons", 64, 2, 1, 2, 4, 4, 4, 3, 1, seed=23, constraint_params=cp)
 
 
 if __name__ == "__main__":
     torch.set_num_threads(4)
+    if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
+        constrained_trajectory()
+        sys.exit(0)
     poisson = json.loads(json.dumps(DEFAULT_LOSS))
     poisson["loss_poissn"].update(state=True, weight=0.5, dp_pow=1.0, eps=1e-6)
     poisson["loss_sparse"].update(ln_order=2, weight=0.05)
@@ -207,3 +228,4 @@ if __name__ == "__main__":
     run_case("n128_c1_b32", 128, 1, 1, 1, 8, 8, 32, seed=17, big=True)
     run_trajectory("traj_n64_b4_ga1", 64, 1, 1, 1, 4, 4, 4, 3, 1, seed=21)
     run_trajectory("traj_n32_p2_ga2", 32, 2, 1, 2, 4, 4, 4, 3, 2, seed=22)
+    constrained_trajectory()

@@ -51,8 +51,13 @@ def test_recon_step_trajectory_matches_reference(path):
     opt = create_optimizer(model.optimizer_params, model.optimizable_params)
     loss_fn = CombinedLoss(json.loads(str(z["loss_params"])), device=device)
     batches = np.split(z["batches"], np.cumsum(z["batch_sizes"])[:-1])
+    cp = json.loads(str(z["constraint_params"])) if "constraint_params" in z.files else None
+    cfn = None
+    if cp is not None:   # the reference ran its CombinedConstraint: run the on-device one
+        from ptyrad_amd.constraints import CombinedConstraint
+        cfn = CombinedConstraint(cp, device=device, verbose=False)
     for it in range(1, int(z["niter"]) + 1):
-        recon_step(batches, int(z["grad_accumulation"]), model, opt, loss_fn, None, it, verbose=False)
+        recon_step(batches, int(z["grad_accumulation"]), model, opt, loss_fn, cfn, it, verbose=False)
     for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
         got = getattr(model, k).detach().cpu().numpy().astype(np.float64)
         rms = float(np.sqrt(np.mean((got - ref) ** 2)))

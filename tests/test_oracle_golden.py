@@ -76,7 +76,8 @@ def oracle_trajectory(z, grad_fn=None):
         prm["obja"], prm["objp"], prm["probe"][..., 0] + 1j * prm["probe"][..., 1],
         prm["probe_pos_shifts"], z["crop_pos"], z["H"], z["occu"], z["meas"], [b], lp,
         shift_probes=True, grad_scale=scale)[2])
-    for _ in range(int(z["niter"])):
+    cp = json.loads(str(z["constraint_params"])) if "constraint_params" in z.files else None
+    for it in range(1, int(z["niter"]) + 1):
         acc = None
         for bi, b in enumerate(batches):
             g = grad_fn(params, b, 1.0 / ga)
@@ -88,7 +89,19 @@ def oracle_trajectory(z, grad_fn=None):
                 t += 1
                 orc.adam_step(params, {k: v.astype(np.float32) for k, v in acc.items()}, state, lrs, t)
                 acc = None
+        if cp is not None:   # CombinedConstraint after the iteration (reconstruction.py:776-780)
+            apply_constraint_oracle(params, cp, float(z["probe_int_sum"]), it)
     return params
+
+
+def apply_constraint_oracle(params, cp, probe_int_sum, niter):
+    from oracle import constraints_oracle as co
+    st = {"obja": params["obja"], "objp": params["objp"], "probe_int_sum": probe_int_sum,
+          "probe": params["probe"][..., 0] + 1j * params["probe"][..., 1]}
+    out = co.combined(cp, st, niter)
+    params["obja"] = out["obja"].astype(np.float32)
+    params["objp"] = out["objp"].astype(np.float32)
+    params["probe"] = np.stack([out["probe"].real, out["probe"].imag], -1).astype(np.float32)
 
 
 @pytest.mark.parametrize("path", TRAJ, ids=[os.path.basename(p)[:-4] for p in TRAJ])
