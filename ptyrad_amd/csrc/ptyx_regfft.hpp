@@ -128,13 +128,132 @@ __device__ __forceinline__ float2 rot_sel(float2 v, float lf) {
 __device__ __forceinline__ float2 add2(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 sub2(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 
+// PTYX_RF_PK: 1 = packed f32 butterflies (v_pk_add/mul/fma_f32: one instruction per complex
+// add, two per complex twiddle multiply, the ±i and odd-π/4 swaps folded into op_sel / neg
+// modifiers), 0 = scalar f32.  Same arithmetic per component up to FMA contraction.
+#ifndef PTYX_RF_PK
+#define PTYX_RF_PK 1
+#endif
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f pv(float2 a) { return __builtin_bit_cast(v2f, a); }
+__device__ __forceinline__ float2 pf(v2f a) { return __builtin_bit_cast(float2, a); }
+__device__ __forceinline__ float2 padd(float2 a, float2 b) { return pf(pv(a) + pv(b)); }
+__device__ __forceinline__ float2 psub(float2 a, float2 b) { return pf(pv(a) - pv(b)); }
+// e + i·o = (e.x − o.y, e.y + o.x)  and  e − i·o = (e.x + o.y, e.y − o.x), one instruction each
+__device__ __forceinline__ float2 padd_i(float2 e, float2 o) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(e)), "v"(pv(o)));
+  return pf(r);
+}
+__device__ __forceinline__ float2 psub_i(float2 e, float2 o) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(e)), "v"(pv(o)));
+  return pf(r);
+}
+// v·(DIR·i): DIR < 0 → (v.y, −v.x); DIR > 0 → (−v.y, v.x)
+template <int DIR>
+__device__ __forceinline__ float2 pmul_i(float2 v) {
+  v2f r;
+  if constexpr (DIR < 0)
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(v)));
+  else
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(v)));
+  return pf(r);
+}
+// u = (C·x − S·y, S·x + C·y) for C, S ∈ {±1}: one v_pk_add_f32 (odd multiples of π/4 before √½)
+template <int C, int S>
+__device__ __forceinline__ v2f prot45(float2 v) {
+  v2f r;
+  if constexpr (C > 0 && S > 0)
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(v)));
+  else if constexpr (C > 0 && S < 0)
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(v)));
+  else if constexpr (C < 0 && S > 0)
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[1,1] neg_hi:[1,0]" : "=v"(r) : "v"(pv(v)));
+  else
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[1,0] neg_hi:[1,1]" : "=v"(r) : "v"(pv(v)));
+  return r;
+}
+// v·(c + i s) for compile-time c, s (bit patterns CB, SB): v_pk_mul (c·x, c·y), then v_pk_fma
+// with the swapped v.  The two constants are materialised INSIDE the asm (s_mov_b64 of a
+// 32-bit literal; both halves read the low word through op_sel_hi = 0), so the compiler cannot
+// hoist ~100 distinct twiddles out of the pattern loop into SGPRs (which spills).
+template <int CB, int SB>
+__device__ __forceinline__ float2 pcmul_k(float2 v) {
+  v2f r;
+  unsigned long long k0, k1;
+  asm("s_mov_b64 %1, %4\n\t"
+      "s_mov_b64 %2, %5\n\t"
+      "v_pk_mul_f32 %0, %3, %1 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %3, %2, %0 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]"
+      : "=&v"(r), "=&s"(k0), "=&s"(k1)
+      : "v"(pv(v)), "i"(CB), "i"(SB));
+  return pf(r);
+}
+template <int M, int K, int DIR>
+__device__ __forceinline__ float2 prot(float2 v) {
+  constexpr int k = ((K % M) + M) % M;
+  if constexpr (k == 0) {
+    return v;
+  } else if constexpr (4 * k == M) {
+    return pmul_i<DIR>(v);
+  } else if constexpr (2 * k == M) {
+    return pf(-pv(v));
+  } else if constexpr (4 * k == 3 * M) {
+    return pmul_i<-DIR>(v);
+  } else if constexpr ((8 * k) % M == 0) {
+    constexpr int C = cos2pi(k, M) > 0 ? 1 : -1;
+    constexpr int S = (sin2pi(k, M) > 0 ? 1 : -1) * DIR;
+    constexpr float h = 0.70710678118654752f;
+    return pf(prot45<C, S>(v) * (v2f){h, h});
+  } else {
+    constexpr float c = (float)cos2pi(k, M);
+    constexpr float sn = (float)(DIR * sin2pi(k, M));
+    return pcmul_k<__builtin_bit_cast(int, c), __builtin_bit_cast(int, sn)>(v);
+  }
+}
+// butterfly (e + W o, e − W o) with W = exp(DIR·2πi·K/M)
+template <int M, int K, int DIR>
+__device__ __forceinline__ void pbfly(float2 e, float2 o, float2& a, float2& b) {
+  constexpr int k = ((K % M) + M) % M;
+  if constexpr (k == 0) {
+    a = padd(e, o);
+    b = psub(e, o);
+  } else if constexpr (4 * k == M) {       // W = DIR·i
+    if constexpr (DIR < 0) { a = psub_i(e, o); b = padd_i(e, o); }
+    else { a = padd_i(e, o); b = psub_i(e, o); }
+  } else if constexpr (2 * k == M) {
+    a = psub(e, o);
+    b = padd(e, o);
+  } else if constexpr (4 * k == 3 * M) {   // W = −DIR·i
+    if constexpr (DIR < 0) { a = padd_i(e, o); b = psub_i(e, o); }
+    else { a = psub_i(e, o); b = padd_i(e, o); }
+  } else if constexpr ((8 * k) % M == 0) {
+    constexpr int C = cos2pi(k, M) > 0 ? 1 : -1;
+    constexpr int S = (sin2pi(k, M) > 0 ? 1 : -1) * DIR;
+    constexpr float h = 0.70710678118654752f;
+    const v2f u = prot45<C, S>(o);
+    a = pf(__builtin_elementwise_fma(u, (v2f){h, h}, pv(e)));
+    b = pf(__builtin_elementwise_fma(u, (v2f){-h, -h}, pv(e)));
+  } else {
+    const float2 t = prot<M, K, DIR>(o);
+    a = padd(e, t);
+    b = psub(e, t);
+  }
+}
+
 // DFT of size R ∈ {2, 4, 8}, natural order in and out (radix-2 DIT recursion)
 template <int R, int DIR>
 __device__ __forceinline__ void dft(float2 (&v)[R]) {
   if constexpr (R == 2) {
     const float2 a = v[0], b = v[1];
+#if PTYX_RF_PK
+    v[0] = padd(a, b);
+    v[1] = psub(a, b);
+#else
     v[0] = add2(a, b);
     v[1] = sub2(a, b);
+#endif
   } else {
     float2 e[R / 2], o[R / 2];
 #pragma unroll
@@ -146,9 +265,13 @@ __device__ __forceinline__ void dft(float2 (&v)[R]) {
     dft<R / 2, DIR>(o);
     sfor<0, R / 2>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
+#if PTYX_RF_PK
+      pbfly<R, k, DIR>(e[k], o[k], v[k], v[k + R / 2]);
+#else
       const float2 t = rot<R, k, DIR>(o[k]);
       v[k] = add2(e[k], t);
       v[k + R / 2] = sub2(e[k], t);
+#endif
     });
   }
 }
@@ -164,7 +287,11 @@ __device__ __forceinline__ void dft64(float2 (&v)[64]) {
     dft<8, DIR>(t);
     sfor<0, 8>([&](auto K2) {
       constexpr int k2 = decltype(K2)::value;
+#if PTYX_RF_PK
+      v[n1 + 8 * k2] = prot<64, n1 * k2, DIR>(t[k2]);
+#else
       v[n1 + 8 * k2] = rot<64, n1 * k2, DIR>(t[k2]);
+#endif
     });
     PTYX_RF_SB();
   });
@@ -198,14 +325,39 @@ __device__ __forceinline__ LaneCtx lane_ctx(int lane) {
   return LaneCtx{1.0f - 2.0f * lf, lf};
 }
 
+#if PTYX_RF_PK
+// v·(lf ? W : 1) packed: u = v·(W − 1) (two instructions), v + lf·u (one)
+template <int M, int K, int DIR>
+__device__ __forceinline__ float2 prot_sel(float2 v, float lf) {
+  constexpr int k = ((K % M) + M) % M;
+  if constexpr (k == 0) {
+    return v;
+  } else {
+    constexpr float c1 = (float)(cos2pi(k, M) - 1.0);
+    constexpr float sn = (float)(DIR * sin2pi(k, M));
+    const float2 u = pcmul_k<__builtin_bit_cast(int, c1), __builtin_bit_cast(int, sn)>(v);
+    return pf(__builtin_elementwise_fma((v2f){lf, lf}, pv(u), pv(v)));
+  }
+}
+// sgn·m + (m of lane ^ 1), one v_pk_fma after the two DPP moves
+__device__ __forceinline__ float2 plane_mix(float2 m, float sgn) {
+  const v2f x = {xl1(m.x), xl1(m.y)};
+  return pf(__builtin_elementwise_fma((v2f){sgn, sgn}, pv(m), x));
+}
+#endif
+
 // DIF step: even lane a = x0 + x1, odd lane b = (x0 − x1)·W128^(DIR·j), j = register index
 template <int DIR>
 __device__ __forceinline__ void lane_pre(float2 (&v)[64], LaneCtx c) {
   sfor<0, 64>([&](auto J) {
     constexpr int j = decltype(J)::value;
     const float2 m = v[j];
+#if PTYX_RF_PK
+    v[j] = prot_sel<128, j, DIR>(plane_mix(m, c.sgn), c.lf);
+#else
     const float2 t = make_float2(fmaf(c.sgn, m.x, xl1(m.x)), fmaf(c.sgn, m.y, xl1(m.y)));
     v[j] = rot_sel<128, j, DIR>(t, c.lf);
+#endif
     if constexpr ((j & 7) == 7) PTYX_RF_SB();
   });
 }
@@ -214,8 +366,12 @@ template <int DIR>
 __device__ __forceinline__ void lane_post(float2 (&v)[64], LaneCtx c) {
   sfor<0, 64>([&](auto J) {
     constexpr int j = decltype(J)::value;
+#if PTYX_RF_PK
+    v[j] = plane_mix(prot_sel<128, j, DIR>(v[j], c.lf), c.sgn);
+#else
     const float2 m = rot_sel<128, j, DIR>(v[j], c.lf);
     v[j] = make_float2(fmaf(c.sgn, m.x, xl1(m.x)), fmaf(c.sgn, m.y, xl1(m.y)));
+#endif
     if constexpr ((j & 7) == 7) PTYX_RF_SB();
   });
 }
@@ -242,7 +398,13 @@ __device__ __forceinline__ int swz(int r) {
 // v[odd] *= s  (s = −1 on waves with w1 = 1, +1 otherwise; wave-uniform)
 __device__ __forceinline__ void flip_odd(float2 (&v)[64], float s) {
 #pragma unroll
-  for (int i = 1; i < 64; i += 2) v[i] = make_float2(v[i].x * s, v[i].y * s);
+  for (int i = 1; i < 64; i += 2) {
+#if PTYX_RF_PK
+    v[i] = pf(pv(v[i]) * (v2f){s, s});
+#else
+    v[i] = make_float2(v[i].x * s, v[i].y * s);
+#endif
+  }
 }
 
 struct XAddr {

@@ -74,7 +74,8 @@ int main(int argc, char** argv) {
   CHECK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
   int occ = 0;
   CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_loop, 256, 0));
-  const int grid = cu * 2;
+  const int wpc = argc > 2 ? std::atoi(argv[2]) : 2;   // workgroups per CU (1: one wave per SIMD)
+  const int grid = cu * wpc;
   constexpr int N = 128;
   std::vector<float2> h((size_t)grid * N * N);
   for (size_t i = 0; i < h.size(); ++i)
