@@ -163,6 +163,38 @@ int ptyx_probe_fix_int(void *stream, float *probe, int32_t P, int32_t N, const f
 int ptyx_probe_ortho(void *stream, float *probe, int32_t P, int32_t N, void *ws);
 size_t ptyx_constraints_evals_offset(void);
 
+/* ---------------------------------------------------------------------------------------------
+ * Measurement ingest: load_raw (src/ptyrad/load.py:19-49) and
+ * Initializer._process_meas (src/ptyrad/initialization.py:709-752) straight into HBM.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct ptyx_meas_proc {
+  int32_t flipud, fliplr, transpose;                 /* meas_flipT [0,0,0]            :766-792  */
+  int32_t crop_ky0, crop_ky1, crop_kx0, crop_kx1;    /* meas_crop ky / kx (after flipT), -1 = whole axis;
+                                                        the scan-axis crop is a frame selection  */
+  int32_t neg_mode, neg_force; float neg_value;      /* meas_remove_neg_values        :837-890  
+                                                        0 clip_neg, 1 subtract_min, 2 clip_value, 3 subtract_value */
+  int32_t norm_mode; float norm_value;               /* meas_normalization            :892-935
+                                                        0 max_at_one, 1 mean_at_one, 2 sum_to_one, 3 divide_const */
+} ptyx_meas_proc;
+
+/* Frames [first, first+count) of an EMPAD-style raw file (offset + file_frames × (H·W·4 + gap)
+ * bytes, size checked like load.py:27-31) into dst (count,H,W) f32 on the device, through
+ * pinned double buffers and strided DMA (gaps dropped by the copy engine).  Host-blocking. */
+int ptyx_raw_read(void *stream, const char *path, int64_t offset, int32_t H, int32_t W, int32_t gap,
+                  int64_t file_frames, int64_t first, int64_t count, float *dst);
+
+/* stats (device f64, ptyx_meas_stats_len(Ho,Wo) values = [min, n, Σraw(Ho·Wo), Σapplied(Ho·Wo)],
+ * initialised by the caller to {+inf, 0, 0, ...}) += the statistics of n frames raw (n,H,W) f32 after
+ * flipT + crop; call once per chunk; across ranks reduce stats[0] with MIN and the rest with SUM.
+ * ws: device workspace of ptyx_meas_ws_bytes(Ho,Wo) bytes. */
+size_t ptyx_meas_stats_len(int32_t Ho, int32_t Wo);
+size_t ptyx_meas_ws_bytes(int32_t Ho, int32_t Wo);
+int ptyx_meas_stats(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
+                    double *stats, void *ws);
+/* dst (n,Ho,Wo) f32 (or IEEE half with dst_f16) = _process_meas of raw, given the complete stats. */
+int ptyx_meas_finish(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
+                     const double *stats, void *ws, void *dst, int32_t dst_f16);
+
 /* Bytes of device workspace the plan holds. */
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
 /* Last error message of the calling thread ("" if none). */

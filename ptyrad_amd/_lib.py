@@ -24,7 +24,8 @@ _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
-           "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho")
+           "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
+           "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
 
 
 class PtyxError(RuntimeError):
@@ -71,6 +72,13 @@ class ObjConstraints(ctypes.Structure):
                 ("pos_on", ctypes.c_int32), ("pos_subtract_min", ctypes.c_int32), ("pos_relax", ctypes.c_float)]
 
 
+class MeasProc(ctypes.Structure):
+    _fields_ = [("flipud", ctypes.c_int32), ("fliplr", ctypes.c_int32), ("transpose", ctypes.c_int32),
+                ("crop_ky0", ctypes.c_int32), ("crop_ky1", ctypes.c_int32), ("crop_kx0", ctypes.c_int32),
+                ("crop_kx1", ctypes.c_int32), ("neg_mode", ctypes.c_int32), ("neg_force", ctypes.c_int32),
+                ("neg_value", ctypes.c_float), ("norm_mode", ctypes.c_int32), ("norm_value", ctypes.c_float)]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int32), ("total_ms", ctypes.c_float)]
 
@@ -110,9 +118,17 @@ def load(path: str | None = None):
     lib.ptyx_obj_constrain.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(ObjConstraints), vp]
     lib.ptyx_probe_fix_int.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ptyx_probe_ortho.argtypes = [vp, vp, i32, i32, vp]
+    i64 = ctypes.c_int64
+    lib.ptyx_raw_read.argtypes = [vp, ctypes.c_char_p, i64, i32, i32, i32, i64, i64, i64, vp]
+    lib.ptyx_meas_stats_len.argtypes = [i32, i32]
+    lib.ptyx_meas_stats_len.restype = ctypes.c_size_t
+    lib.ptyx_meas_ws_bytes.argtypes = [i32, i32]
+    lib.ptyx_meas_ws_bytes.restype = ctypes.c_size_t
+    lib.ptyx_meas_stats.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp]
+    lib.ptyx_meas_finish.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp, vp, i32]
     for name in ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
                  "ptyx_adjoint_dldi", "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int",
-                 "ptyx_probe_ortho"):
+                 "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -21,7 +21,8 @@ PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "lib", "libptyx.so")
 OBJ = os.path.join(ROOT, "build", "obj")
-SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_constraints.hip")]
+SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_constraints.hip"),
+           os.path.join(HERE, "ptyx_ingest.hip")]
 HEADERS = glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
 DEPS = SOURCES + HEADERS
 ARCH = os.environ.get("PTYX_ARCH", "gfx950")
@@ -47,6 +48,8 @@ def _headers_of(src: str):
     if os.path.basename(src) == "ptyx_constraints.hip":
         return [os.path.join(HERE, "ptyx_constraints.hpp"), os.path.join(HERE, "ptyx_abi.hpp"),
                 os.path.join(ROOT, "include", "ptyx.h")]
+    if os.path.basename(src) == "ptyx_ingest.hip":
+        return [os.path.join(HERE, "ptyx_abi.hpp"), os.path.join(ROOT, "include", "ptyx.h")]
     return HEADERS
 
 

@@ -1,0 +1,308 @@
+// ptyx_ingest.hip — measurement ingest straight into HBM, a translation
+// unit of libptyx.so.  Replaces load_raw (src/ptyrad/load.py:19-49) and
+// Initializer._process_meas (src/ptyrad/initialization.py:709-752: flipT, crop,
+// remove_neg_values, normalization, final clip) for EMPAD-style raw stacks.
+//
+//  ptyx_raw_read     host streaming reader: large sequential pread()s of [frames + gaps] into two
+//                    pinned buffers, each chunk handed to the DMA engine as ONE strided 2-D copy
+//                    (source pitch = frame + gap, so the gaps are dropped by the copy engine,
+//                    never touched by a kernel) while the next chunk is read.
+//  ptyx_meas_stats   per output pixel, fp64 sums over frames of the transformed (flipT + crop)
+//                    values, raw and with the negative-value rule applied, plus the minimum:
+//                    everything _meas_remove_neg_values / _meas_normalization need, accumulated
+//                    (+=) so a stack can be streamed in chunks, and summable across ranks
+//                    (min with MIN, the rest with SUM) before ptyx_meas_finish.
+//  ptyx_meas_finish  decides (on the device) whether the negative-value rule applies and the
+//                    normalisation constant, then writes the processed stack (f32, or f16 for
+//                    the fp16-storage configs) in one pass.
+// Sums run in a fixed order (frame groups g = f mod G, then g = 0..G-1): bitwise reproducible.
+#include <fcntl.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <string>
+
+#include "ptyx.h"
+#include "ptyx_abi.hpp"
+
+using namespace ptyx;
+
+namespace {
+constexpr int kGroups = 64;   // frame groups of the stats pass (partials per pixel)
+
+struct Geom {
+  int H, W, Ho, Wo, ky0, kx0, fu, fl, tr;
+};
+// output pixel (oy, ox) → source offset in the (H, W) frame: T = transpose(fliplr(flipud(S)))
+__device__ __forceinline__ int src_of(const Geom& g, int oy, int ox) {
+  const int a = g.ky0 + oy, b = g.kx0 + ox;
+  int y = g.tr ? b : a, x = g.tr ? a : b;
+  if (g.fu) y = g.H - 1 - y;
+  if (g.fl) x = g.W - 1 - x;
+  return y * g.W + x;
+}
+
+struct NegRule {
+  int mode, force;   // 0 clip_neg, 1 subtract_min, 2 clip_value, 3 subtract_value
+  float value;
+};
+// value after the rule and the clip that follows it (initialization.py:863-888)
+__device__ __forceinline__ float neg_apply(float x, const NegRule& r, float mn) {
+  switch (r.mode) {
+    case 1: x = x - mn; break;
+    case 2: x = x < r.value ? 0.f : x; break;
+    case 3: x = x - r.value; break;
+    default: break;
+  }
+  return fmaxf(x, 0.f);
+}
+
+// grid (ceil(P / 256), kGroups); part layout [g][0..P) raw, [g][P..2P) applied (rule with the
+// min unknown: subtract_min is derived from the raw sum at the end), [g][2P + block] min
+__global__ __launch_bounds__(256) void k_meas_stats(const float* __restrict__ raw, long long n, Geom g, NegRule r,
+                                                    double* __restrict__ part) {
+  __shared__ float s_min[256];
+  const int P = g.Ho * g.Wo;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = blockIdx.y;
+  double sr = 0, sa = 0;
+  float mn = __builtin_huge_valf();
+  if (p < P) {
+    const int src = src_of(g, p / g.Wo, p % g.Wo);
+    const long long fs = (long long)g.H * g.W;
+    for (long long f = grp; f < n; f += kGroups) {
+      const float x = raw[f * fs + src];
+      sr += x;
+      sa += r.mode == 1 ? 0.0 : (double)neg_apply(x, r, 0.f);
+      mn = fminf(mn, x);
+    }
+    double* pg = part + (size_t)grp * (2 * P + gridDim.x);
+    pg[p] += sr;
+    pg[P + p] += sa;
+  }
+  s_min[threadIdx.x] = mn;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) s_min[threadIdx.x] = fminf(s_min[threadIdx.x], s_min[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* pm = part + (size_t)grp * (2 * P + gridDim.x) + 2 * P + blockIdx.x;
+    *pm = fmin(*pm, (double)s_min[0]);
+  }
+}
+__global__ void k_part_init(double* part, int P, int nblk) {
+  const long long per = 2LL * P + nblk;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < per * kGroups;
+       i += (long long)gridDim.x * blockDim.x)
+    part[i] = (i % per) >= 2 * P ? __builtin_huge_val() : 0.0;
+}
+// stats = [min, n, S_raw[P], S_app[P]]; += the group partials in fixed order
+__global__ __launch_bounds__(256) void k_meas_stats_final(const double* __restrict__ part, int P, int nblk, long long n,
+                                                          double* __restrict__ stats) {
+  const long long per = 2LL * P + nblk;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    double sr = 0, sa = 0;
+    for (int grp = 0; grp < kGroups; ++grp) {
+      sr += part[grp * per + p];
+      sa += part[grp * per + P + p];
+    }
+    stats[2 + p] += sr;
+    stats[2 + P + p] += sa;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    double m = stats[0];
+    for (int grp = 0; grp < kGroups; ++grp)
+      for (int b = 0; b < nblk; ++b) m = fmin(m, part[grp * per + 2 * P + b]);
+    stats[0] = m;
+    stats[1] += (double)n;
+  }
+}
+
+// [applied flag, normalisation constant] from the (rank-reduced) stats; one workgroup
+__global__ __launch_bounds__(256) void k_meas_const(const double* __restrict__ stats, int P, NegRule r, int norm_mode,
+                                                    float norm_value, float* __restrict__ out) {
+  __shared__ double s_v[256];
+  const double mn = stats[0], n = stats[1];
+  const bool applied = mn < 0.0 || r.force;
+  double acc = norm_mode == 0 ? -__builtin_huge_val() : 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    double s = stats[2 + p];
+    if (applied) s = r.mode == 1 ? s - n * mn : stats[2 + P + p];
+    const double avg = s / n;
+    acc = norm_mode == 0 ? fmax(acc, avg) : acc + avg;
+  }
+  s_v[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = s_v[0];
+    for (int i = 1; i < (int)blockDim.x; ++i) a = norm_mode == 0 ? fmax(a, s_v[i]) : a + s_v[i];
+    double c = a;
+    if (norm_mode == 1) c = a / P;
+    if (norm_mode == 3) c = norm_value;
+    out[0] = applied ? 1.f : 0.f;
+    out[1] = (float)c;
+    out[2] = (float)mn;
+  }
+}
+
+template <bool F16>
+__global__ __launch_bounds__(256) void k_meas_finish(const float* __restrict__ raw, long long n, Geom g, NegRule r,
+                                                     const float* __restrict__ cst, void* __restrict__ dst) {
+  const int P = g.Ho * g.Wo;
+  const long long total = n * P;
+  const bool applied = cst[0] != 0.f;
+  const float c = cst[1], mn = cst[2];
+  const long long fs = (long long)g.H * g.W;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long f = i / P;
+    const int p = (int)(i - f * P);
+    float x = raw[f * fs + src_of(g, p / g.Wo, p % g.Wo)];
+    if (applied) x = neg_apply(x, r, mn);
+    x = fmaxf(x / c, 0.f);
+    if constexpr (F16) reinterpret_cast<__half*>(dst)[i] = __float2half(x);
+    else reinterpret_cast<float*>(dst)[i] = x;
+  }
+}
+
+int make_geom(const ptyx_meas_proc* pp, int H, int W, Geom& g, NegRule& r) {
+  if (!pp) return abi::fail(PTYX_EINVAL, "meas: proc is null");
+  if (H <= 0 || W <= 0) return abi::fail(PTYX_EINVAL, "meas: bad frame shape");
+  g.H = H;
+  g.W = W;
+  g.fu = pp->flipud != 0;
+  g.fl = pp->fliplr != 0;
+  g.tr = pp->transpose != 0;
+  const int Ht = g.tr ? W : H, Wt = g.tr ? H : W;
+  const int ky0 = pp->crop_ky0 < 0 ? 0 : pp->crop_ky0, ky1 = pp->crop_ky1 < 0 ? Ht : pp->crop_ky1;
+  const int kx0 = pp->crop_kx0 < 0 ? 0 : pp->crop_kx0, kx1 = pp->crop_kx1 < 0 ? Wt : pp->crop_kx1;
+  if (ky0 >= ky1 || kx0 >= kx1 || ky1 > Ht || kx1 > Wt) return abi::fail(PTYX_EINVAL, "meas: crop out of range");
+  g.ky0 = ky0;
+  g.kx0 = kx0;
+  g.Ho = ky1 - ky0;
+  g.Wo = kx1 - kx0;
+  if (pp->neg_mode < 0 || pp->neg_mode > 3) return abi::fail(PTYX_EINVAL, "meas: neg_mode must be 0..3");
+  if (pp->norm_mode < 0 || pp->norm_mode > 3) return abi::fail(PTYX_EINVAL, "meas: norm_mode must be 0..3");
+  r.mode = pp->neg_mode;
+  r.force = pp->neg_force;
+  r.value = pp->neg_value;
+  return PTYX_OK;
+}
+}  // namespace
+
+extern "C" size_t ptyx_meas_stats_len(int32_t Ho, int32_t Wo) { return 2 + 2 * (size_t)Ho * Wo; }
+extern "C" size_t ptyx_meas_ws_bytes(int32_t Ho, int32_t Wo) {
+  const size_t P = (size_t)Ho * Wo, nblk = (P + 255) / 256;
+  return (kGroups * (2 * P + nblk) + 4) * sizeof(double);
+}
+
+extern "C" int ptyx_meas_stats(void* stream, const float* raw, int64_t n, int32_t H, int32_t W,
+                               const ptyx_meas_proc* p, double* stats, void* ws) {
+  abi::clear_error();
+  Geom g;
+  NegRule r;
+  int rc = make_geom(p, H, W, g, r);
+  if (rc) return rc;
+  if (n < 0) return abi::fail(PTYX_EINVAL, "meas_stats: n < 0");
+  if (!stats || !ws || (n > 0 && !raw)) return abi::fail(PTYX_EINVAL, "meas_stats: null pointer");
+  if (n == 0) return PTYX_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int P = g.Ho * g.Wo, nblk = (P + 255) / 256;
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(k_part_init, dim3(256), dim3(256), 0, st, part, P, nblk);
+  hipLaunchKernelGGL(k_meas_stats, dim3(nblk, kGroups), dim3(256), 0, st, raw, (long long)n, g, r, part);
+  hipLaunchKernelGGL(k_meas_stats_final, dim3(nblk), dim3(256), 0, st, part, P, nblk, (long long)n, stats);
+  return abi::launch_status("meas_stats launch");
+}
+
+extern "C" int ptyx_meas_finish(void* stream, const float* raw, int64_t n, int32_t H, int32_t W,
+                                const ptyx_meas_proc* p, const double* stats, void* ws, void* dst, int32_t dst_f16) {
+  abi::clear_error();
+  Geom g;
+  NegRule r;
+  int rc = make_geom(p, H, W, g, r);
+  if (rc) return rc;
+  if (n < 0) return abi::fail(PTYX_EINVAL, "meas_finish: n < 0");
+  if (!stats || !ws || (n > 0 && (!raw || !dst))) return abi::fail(PTYX_EINVAL, "meas_finish: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int P = g.Ho * g.Wo;
+  float* cst = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_meas_const, dim3(1), dim3(256), 0, st, stats, P, r, p->norm_mode, p->norm_value, cst);
+  if (n > 0) {
+    const long long total = n * (long long)P;
+    const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+    if (dst_f16) hipLaunchKernelGGL(k_meas_finish<true>, dim3(grid), dim3(256), 0, st, raw, (long long)n, g, r, cst, dst);
+    else hipLaunchKernelGGL(k_meas_finish<false>, dim3(grid), dim3(256), 0, st, raw, (long long)n, g, r, cst, dst);
+  }
+  return abi::launch_status("meas_finish launch");
+}
+
+extern "C" int ptyx_raw_read(void* stream, const char* path, int64_t offset, int32_t H, int32_t W, int32_t gap,
+                             int64_t file_frames, int64_t first, int64_t count, float* dst) {
+  abi::clear_error();
+  if (!path || H <= 0 || W <= 0 || gap < 0 || offset < 0 || file_frames < 0)
+    return abi::fail(PTYX_EINVAL, "raw_read: bad arguments");
+  if (first < 0 || count < 0 || first + count > file_frames) return abi::fail(PTYX_EINVAL, "raw_read: frame range");
+  if (count > 0 && !dst) return abi::fail(PTYX_EINVAL, "raw_read: dst is null");
+  const size_t frame = (size_t)H * W * 4, stride = frame + (size_t)gap;
+  struct stat sb;
+  if (stat(path, &sb) != 0) return abi::fail(PTYX_EINVAL, std::string("raw_read: cannot stat ") + path);
+  const long long expected = offset + file_frames * (long long)stride;   // load.py:27-31
+  if ((long long)sb.st_size != expected)
+    return abi::fail(PTYX_EINVAL, "raw_read: file size " + std::to_string((long long)sb.st_size) + " != offset + N*(H*W*4 + gap) = " +
+                                      std::to_string(expected));
+  if (count == 0) return PTYX_OK;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return abi::fail(PTYX_EINVAL, std::string("raw_read: open failed: ") + std::strerror(errno));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const size_t chunk_frames = std::max<size_t>(1, (64u << 20) / stride);
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = PTYX_OK;
+  for (int i = 0; i < 2 && rc == PTYX_OK; ++i) {
+    if (hipHostMalloc(&buf[i], chunk_frames * stride, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+      rc = abi::fail(PTYX_ENOMEM, "raw_read: pinned buffer allocation failed");
+  }
+  bool pending[2] = {false, false};
+  for (long long f = 0, k = 0; rc == PTYX_OK && f < count; f += (long long)chunk_frames, ++k) {
+    const int b = (int)(k & 1);
+    if (pending[b] && hipEventSynchronize(ev[b]) != hipSuccess) {
+      rc = abi::fail(PTYX_EHIP, "raw_read: event sync failed");
+      break;
+    }
+    const size_t nf = (size_t)std::min<long long>((long long)chunk_frames, count - f);
+    // the last frame's trailing gap is not needed
+    const size_t bytes = nf * stride - (size_t)gap;
+    size_t got = 0;
+    const off_t base = (off_t)(offset + (first + f) * (long long)stride);
+    while (got < bytes) {
+      const ssize_t r = pread(fd, (char*)buf[b] + got, bytes - got, base + (off_t)got);
+      if (r <= 0) {
+        rc = abi::fail(PTYX_EINVAL, std::string("raw_read: short read: ") + (r < 0 ? std::strerror(errno) : "EOF"));
+        break;
+      }
+      got += (size_t)r;
+    }
+    if (rc) break;
+    if (hipMemcpy2DAsync(dst + (size_t)f * H * W, frame, buf[b], stride, frame, nf, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipEventRecord(ev[b], st) != hipSuccess) {
+      rc = abi::fail(PTYX_EHIP, "raw_read: strided DMA failed");
+      break;
+    }
+    pending[b] = true;
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (pending[i]) (void)hipEventSynchronize(ev[i]);
+    if (ev[i]) (void)hipEventDestroy(ev[i]);
+    if (buf[i]) (void)hipHostFree(buf[i]);
+  }
+  close(fd);
+  return rc;
+}
