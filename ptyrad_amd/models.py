@@ -13,7 +13,7 @@ Two ways to get gradients:
 * fused     — ``ptyrad_amd.losses.CombinedLoss.fused(model, batches)`` runs forward + loss +
               adjoint in one engine call (ptyx_forward_loss_grad), the hot path.
 
-Out of scope on the HIP path (raise NotImplementedError when enabled): tilted / optimised-dz
+Out of scope on the HIP path (raise NotImplementedError when enabled): per-position / optimised tilts, optimised-dz
 propagators (models.py:339-356), detector blur (:379-380), object pre-blur (:275-284),
 on-the-fly measurement padding / resampling (:392-409).
 """
@@ -119,8 +119,13 @@ class PtychoHIP(nn.Module):
             self.tilt_obj = bool(self.lr_params.get("obj_tilts", 0) != 0 or torch.any(self.opt_obj_tilts))
             self.shift_probes = bool(self.lr_params.get("probe_pos_shifts", 0) != 0)   # models.py:120
             self.change_thickness = bool(self.lr_params.get("slice_thickness", 0) != 0)
-            if self.tilt_obj or self.change_thickness:
-                raise NotImplementedError("tilted / optimised-thickness propagators are not on the HIP path")
+            if self.change_thickness or self.lr_params.get("obj_tilts", 0) != 0 or \
+                    (self.tilt_obj and self.opt_obj_tilts.shape[0] != 1):
+                raise NotImplementedError("optimised tilts / thickness and per-position tilts are not on the HIP "
+                                          "path (fixed global tilts are)")
+            # models.py:210-219 / :346-349 (case 2B, global): a fixed tilt only changes the one
+            # propagator every position uses, so the engine takes the tilted H as its H
+            self.register_buffer("H_eff", self._tilted_H() if self.tilt_obj else self.H)
             self.probe_int_sum = self.get_complex_probe_view().abs().pow(2).sum()
             self.loss_iters, self.iter_times, self.dz_iters, self.avg_tilt_iters = [], [], [], []
             self._current_object_patches = None
@@ -165,10 +170,23 @@ class PtychoHIP(nn.Module):
             raise IndexError("scan index out of range")
         return idx
 
+    def _tilted_H(self):
+        """H · exp(i dz (Ky tan θy + Kx tan θx)) on the half-bin-shifted, ifftshifted k grid
+        (models.py:163-171 create_grids, :215-219 init_propagator_vars)."""
+        N = self.opt_probe.shape[1]
+        dev = self.H.device
+        g = (torch.arange(-N // 2, N // 2, device=dev) + 0.5) / N
+        k = torch.fft.ifftshift(2 * torch.pi * g / self.dx)
+        Ky, Kx = torch.meshgrid(k, k, indexing="ij")
+        dz = self.opt_slice_thickness.detach()
+        ty = self.opt_obj_tilts[:, 0, None, None] / 1e3
+        tx = self.opt_obj_tilts[:, 1, None, None] / 1e3
+        return (self.H * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx))))[0].contiguous()
+
     def _engine_tensors(self):
         return {"obja": self.opt_obja.detach(), "objp": self.opt_objp.detach(),
                 "probe": self.opt_probe.detach(), "shifts": self.opt_probe_pos_shifts.detach(),
-                "H": self.H, "occu": self.omode_occu, "crop_pos": self.crop_pos,
+                "H": self.H_eff, "occu": self.omode_occu, "crop_pos": self.crop_pos,
                 "meas": self.measurements}
 
     def get_obj_patches(self, indices):
@@ -196,11 +214,11 @@ class PtychoHIP(nn.Module):
         return torch.fft.ifft2(torch.fft.fft2(probe)[None] * w[:, None])
 
     def get_propagators(self, indices):
-        return self.H[None,]
+        return self.H_eff[None,]
 
     def get_propagated_probe(self, index):
         probe = self.get_probes(index)[0].detach()
-        H = self.H[None]
+        H = self.H_eff[None]
         n_slices = self.opt_objp.shape[1]
         out = torch.zeros((n_slices, *probe.shape), dtype=probe.dtype, device=probe.device)
         psi = probe

@@ -57,12 +57,12 @@ def model_params(shift_lr=5e-4):
             "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
 
 
-def init_variables(obja, objp, probe, H, occu, crop_pos, shifts, meas, n_slow, n_fast, dz=2.0):
+def init_variables(obja, objp, probe, H, occu, crop_pos, shifts, meas, n_slow, n_fast, dz=2.0, tilts=None):
     lam = syn.electron_wavelength(syn.KV)
     n = probe.shape[-1]
     return {
         "obj": (obja * np.exp(1j * objp)).astype(np.complex64),
-        "obj_tilts": np.zeros((1, 2), np.float32),
+        "obj_tilts": np.zeros((1, 2), np.float32) if tilts is None else np.asarray(tilts, np.float32).reshape(1, 2),
         "slice_thickness": np.float32(dz),
         "probe": probe.astype(np.complex64),
         "probe_pos_shifts": shifts.astype(np.float32),
@@ -96,12 +96,12 @@ def make_inputs(n, P, O, Nz, n_slow, n_fast, seed, defocus=40.0, pstd=0.2):
     return scan, probe, H, occu, obja, objp, gta, gtp
 
 
-def simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr):
+def simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr, tilts=None):
     """Measurements = the reference forward model on a different (ground-truth) object."""
     n = probe.shape[-1]
     S = scan.crop_pos.shape[0]
     iv = init_variables(gta, gtp, probe, H, occu, scan.crop_pos, scan.shifts,
-                        np.zeros((S, n, n), np.float32), scan.n_slow, scan.n_fast)
+                        np.zeros((S, n, n), np.float32), scan.n_slow, scan.n_fast, tilts=tilts)
     m = build_model(iv, shift_lr)
     with torch.no_grad():
         dp = m(np.arange(S)).numpy()
@@ -109,10 +109,10 @@ def simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr):
 
 
 def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_params=None,
-             big=False):
+             big=False, tilts=None):
     loss_params = loss_params or DEFAULT_LOSS
     scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
-    meas = simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr)
+    meas = simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr, tilts=tilts)
     S = scan.crop_pos.shape[0]
     batch = np.random.default_rng(seed + 100).permutation(S)[:B].astype(np.int64)
     if big:  # keep the fixture small: only the batch rows of meas, stored as f16 and used as such
@@ -120,7 +120,7 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
         keep[batch] = meas[batch]
         meas = keep.astype(np.float16).astype(np.float32)
     iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas,
-                        scan.n_slow, scan.n_fast)
+                        scan.n_slow, scan.n_fast, tilts=tilts)
     model = build_model(iv, shift_lr)
     loss_fn = losses.CombinedLoss(loss_params, device="cpu")
     dp = model(batch)
@@ -135,7 +135,8 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
         obja=model.opt_obja.detach().numpy(), objp=model.opt_objp.detach().numpy(),
         probe=torch.view_as_complex(model.opt_probe.detach()).numpy(),
         shifts=model.opt_probe_pos_shifts.detach().numpy(), crop_pos=scan.crop_pos,
-        H=model.H.numpy(), occu=model.omode_occu.numpy(),
+        H=(model.H.numpy() if tilts is None else model.H_fixed_tilts_full[0].detach().numpy()),
+        occu=model.omode_occu.numpy(),
         batch=batch, loss_params=json.dumps(loss_params), shift_probes=bool(model.shift_probes),
         loss_terms=np.array([float(t) for t in terms], np.float64),
         loss_total=np.float64(float(total)),
@@ -151,6 +152,10 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
     else:
         out["meas"] = meas
         out["dp"] = dpn
+    if tilts is not None:   # fixed global tilt (models.py:346-349, case 2B): H above is the tilted one
+        out.update(H_untilted=model.H.numpy(), obj_tilts=np.asarray(tilts, np.float32).reshape(1, 2),
+                   slice_thickness=np.float32(model.opt_slice_thickness.item()), dx=np.float32(model.dx.item()),
+                   lambd=np.float32(model.lambd.item()))
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
@@ -209,6 +214,9 @@ def constrained_trajectory():
 
 if __name__ == "__main__":
     torch.set_num_threads(4)
+    if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
+        run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
         constrained_trajectory()
         sys.exit(0)
@@ -226,6 +234,7 @@ if __name__ == "__main__":
     run_case("n32_p1o2z1_q1", 32, 1, 2, 1, 3, 4, 4, seed=15, loss_params=single_q1)
     run_case("n64_p3o1z1_shift", 64, 3, 1, 1, 3, 3, 9, seed=16)
     run_case("n128_c1_b32", 128, 1, 1, 1, 8, 8, 32, seed=17, big=True)
+    run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
     run_trajectory("traj_n64_b4_ga1", 64, 1, 1, 1, 4, 4, 4, 3, 1, seed=21)
     run_trajectory("traj_n32_p2_ga2", 32, 2, 1, 2, 4, 4, 4, 3, 2, seed=22)
     constrained_trajectory()

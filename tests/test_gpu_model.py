@@ -118,3 +118,31 @@ def test_invalid_indices_raise():
         model(np.array([0, 999]))
     with pytest.raises(NotImplementedError):
         PtychoHIP(iv, {**model_params(lrs), "detector_blur_std": 1.0}, device=device, verbose=False)
+
+
+def test_fixed_global_tilt_propagator():
+    """Fixed non-zero global tilt (models.py:346-349, case 2B) on 3 slices: PtychoHIP builds the
+    tilted propagator itself from (H, obj_tilts, slice_thickness, dx) and matches the reference's
+    dp, loss terms and gradients."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    d = load_case([c for c in CASES if "tilt" in c][0])
+    lrs = {"obja": 5e-4, "objp": 5e-4, "obj_tilts": 0.0, "slice_thickness": 0.0, "probe": 1e-4,
+           "probe_pos_shifts": 5e-4}
+    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H_untilted"], d["occu"],
+                   d["meas"])
+    iv.update(obj_tilts=d["obj_tilts"], slice_thickness=float(d["slice_thickness"]), dx=float(d["dx"]))
+    model = PtychoHIP(iv, model_params(lrs), device=device, verbose=False)
+    assert rel(model.get_propagators([0])[0].cpu().numpy(), d["H"]) < 1e-6
+    loss_fn = CombinedLoss(d["loss_params"], device=device)
+    dp = model(d["batch"])
+    assert rel(dp.detach().cpu().numpy(), d["dp"]) < 1e-5
+    total, terms = loss_fn.fused(model, [d["batch"]])
+    total.backward()
+    np.testing.assert_allclose(terms.cpu().numpy()[0], d["loss_terms"], rtol=1e-5, atol=1e-7)
+    assert rel(model.opt_objp.grad.cpu().numpy(), d["g_objp"]) < 5e-5
+    assert rel(model.opt_obja.grad.cpu().numpy(), d["g_obja"]) < 5e-5
+    assert rel(model.opt_probe.grad.cpu().numpy(), d["g_probe"]) < 5e-5
+    with pytest.raises(NotImplementedError):   # optimised tilts stay out of scope
+        PtychoHIP(iv, model_params({**lrs, "obj_tilts": 1e-4}), device=device, verbose=False)
