@@ -134,11 +134,13 @@ struct LdsArray {
 };
 
 // Global scratch pair for arrays that do not fit LDS (N = 256); ping-pong between a and b.
+// lds: the workgroup's line-block tile (kG256Elems float2) when the two-stage path is used.
 template <int N>
 struct GlobalPair {
   static constexpr bool kInPlace = false;
   float2* a;
   float2* b;
+  float2* lds = nullptr;
   __device__ __forceinline__ float2 ld(int y, int x) const { return a[y * N + x]; }
   __device__ __forceinline__ void st(int y, int x, float2 v) const { a[y * N + x] = v; }
 };
@@ -151,6 +153,12 @@ struct GlobalView {
 
 // stage kinds
 enum : int { kMid = 0, kFirst = 1, kLast = 2 };
+
+// PTYX_G256_TWO_STAGE: 1 = N = 256 2-D FFTs in two LDS-tiled stages (one scratch round trip),
+// 0 = four Stockham passes through the global ping-pong pair.
+#ifndef PTYX_G256_TWO_STAGE
+#define PTYX_G256_TWO_STAGE 1
+#endif
 
 // Fused pre/post element group size between scheduling barriers (0 = let the compiler
 // schedule freely).  Without it hipcc hoists every element's global loads of a 16-point
@@ -334,6 +342,74 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
   }
 }
 
+// ---------------------------------------------------------------- N = 256, two stages
+// A 256² complex array (512 KiB) does not fit one CU, so each 2-D FFT makes ONE round trip
+// through the workgroup's global scratch instead of one per Stockham pass: stage 1 transforms
+// 64-row blocks entirely on chip (DFT16 over n2, twiddle W256^(n1·k2), LDS exchange, DFT16
+// over n1) and stores the block TRANSPOSED, so stage 2 is the same row kernel on the
+// transposed array, whose transposed store restores the natural orientation.  Both stores go
+// through an LDS tile and leave as 64 consecutive points (512 B) per line.
+constexpr int kG256RowStride = 16 * 17;                 // [row][k2][n1], one pad per 16
+constexpr int kG256Elems = 64 * kG256RowStride;         // ≥ 256 × 65 (transposed tile)
+static_assert(kG256Elems >= 256 * 65, "tile too small");
+
+template <int DIR, bool FIRST, bool LAST, bool PRELOAD, class Pre, class Post>
+__device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float2* __restrict__ dst, float2* lds,
+                                           const float2* tw, Pre& pre, Post& post) {
+  constexpr int N = 256;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lr = tid >> 4, q = tid & 15;   // block row, n1 (step 1) / k2 (step 2)
+  for (int r0 = 0; r0 < N; r0 += 64) {
+    const int row = r0 + lr;
+    float2 v[16];
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) {
+      const int x = q + 16 * n2;
+      if constexpr (FIRST) {
+        if constexpr (PRELOAD) v[n2] = call_pre(pre, row, x, src[row * N + x], n2);
+        else v[n2] = call_pre(pre, row, x, make_float2(0.f, 0.f), n2);
+        if constexpr (kFuseGroup > 0 && !kSlotPre<Pre>) {
+          if ((n2 + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        v[n2] = src[row * N + x];
+      }
+    }
+    DFT<16, DIR>::run(v);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, q * k2));
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) lds[lr * kG256RowStride + k2 * 17 + q] = v[k2];
+    __syncthreads();
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) v[n1] = lds[lr * kG256RowStride + q * 17 + n1];
+    DFT<16, DIR>::run(v);                     // X[row][q + 16·k1] = v[k1]
+    __syncthreads();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) lds[(q + 16 * k1) * 65 + lr] = v[k1];
+    __syncthreads();
+    // transposed store: dst[k][r0 + c] for k = 0..255, c = 0..63, 64 consecutive per line
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int e = tid + 1024 * i, k = e >> 6, c = e & 63;
+      float2 val = lds[k * 65 + c];
+      if constexpr (LAST) {
+        if (call_post(post, k, r0 + c, val, i)) dst[k * N + r0 + c] = val;
+      } else {
+        dst[k * N + r0 + c] = val;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int DIR, bool PRELOAD, class Pre, class Post>
+__device__ __forceinline__ void fft2d_g256(const GlobalPair<256>& arr, const float2* tw, Pre& pre, Post& post) {
+  g256_stage<DIR, true, false, PRELOAD>(arr.a, arr.b, arr.lds, tw, pre, post);
+  g256_stage<DIR, false, true, false>(arr.b, arr.a, arr.lds, tw, pre, post);
+}
+
 // Unnormalised 2-D DFT of the array (DIR = -1 forward, +1 inverse), rows then columns.
 // Result left in the array (for GlobalPair: in .a after an even number of passes).
 template <int N, int NT, int DIR, bool PRELOAD, class Arr, class Pre, class Post>
@@ -352,6 +428,12 @@ __device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pr
     }
   } else {
     static_assert(R2 != 1, "global ping-pong needs two passes per dimension");
+#if PTYX_G256_TWO_STAGE
+    if constexpr (N == 256 && NT == 1024) {
+      fft2d_g256<DIR, PRELOAD>(arr, tw, pre, post);
+      return;
+    }
+#endif
     const GlobalView<N> A{arr.a}, B{arr.b};
     stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, false>(A, B, tw, pre, post);
     stockham_pass<N, NT, R2, R1, true, DIR, kMid, false, false>(B, A, tw, pre, post);

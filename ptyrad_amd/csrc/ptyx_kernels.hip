@@ -106,7 +106,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* 
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   __shared__ float2 s_tw[N];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   __syncthreads();
   const int p = blockIdx.x;
@@ -115,6 +115,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* 
   else {
     arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
     arr.b = arr.a + N * N;
+    arr.lds = s_buf;
   }
   const float2* P0 = a.probe + (size_t)p * N * N;
   float2* out = Fp_out + (size_t)p * N * N;
@@ -137,13 +138,14 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
   constexpr float inv_n = 1.0f / (float)N;
   __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
   __shared__ float s_red[(NT / 64) * 4];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   typename ArrayFor<N, LDS>::type arr;
   if constexpr (LDS) arr.p = s_buf;
   else {
     arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
     arr.b = arr.a + N2;
+    arr.lds = s_buf;
   }
   __syncthreads();
   const bool want_sums = a.psums != nullptr;
@@ -293,13 +295,14 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   constexpr float inv_n2 = 1.0f / (float)N2;
   __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
   __shared__ float s_red[(NT / 64) * 2];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   typename ArrayFor<N, LDS>::type arr;
   if constexpr (LDS) arr.p = s_buf;
   else {
     arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
     arr.b = arr.a + N2;
+    arr.lds = s_buf;
   }
   float2* psi = scratch_psi<N>(a);
   float2* gacc = psi + (size_t)a.Nz * N2;
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_finalize(KArgs a, const fl
   constexpr int N2 = N * N;
   constexpr float inv_n2 = 1.0f / (float)N2;
   __shared__ float2 s_tw[N];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : 1];
+  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   __syncthreads();
   const int p = blockIdx.x;
@@ -485,6 +488,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_finalize(KArgs a, const fl
   else {
     arr.a = a.scratch + (long long)blockIdx.x * a.scratch_stride;
     arr.b = arr.a + N2;
+    arr.lds = s_buf;
   }
   fft2d<N, NT, +1, false>(
       arr, s_tw, [&](int y, int x, float2) { return Gp[y * N + x]; },
