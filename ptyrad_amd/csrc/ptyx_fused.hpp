@@ -342,7 +342,13 @@ struct GatherArgs {
   float* d_obja;
   float* d_objp;
 };
-constexpr int kGTX = 64, kGTY = 16, kGWaves = 4;
+#ifndef PTYX_GTY
+#define PTYX_GTY 16
+#endif
+#ifndef PTYX_GWAVES
+#define PTYX_GWAVES 16
+#endif
+constexpr int kGTX = 64, kGTY = PTYX_GTY, kGWaves = PTYX_GWAVES;
 
 // ROWPERM: slots written by k_fused3 (N = 128), row y stored at row 2(y & 63) + (y >> 6).
 template <int N, bool ROWPERM = false>
