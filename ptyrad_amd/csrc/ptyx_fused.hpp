@@ -341,6 +341,7 @@ struct GatherArgs {
   const float* objp;
   float* d_obja;
   float* d_objp;
+  int nz = 1, z = 0;     // slots hold nz planes per pattern; this launch gathers plane z
 };
 #ifndef PTYX_GTY
 #define PTYX_GTY 16
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(64 * kGWaves) void k_obj_gather(GatherArgs ga) {
       mask &= mask - 1;
       const int cy = __shfl(o.x, b, 64), cx = __shfl(o.y, b, 64);
       const float c = __shfl(cj.x, b, 64), cs = __shfl(cj.y, b, 64);
-      const float2* src = ga.ogscr + (size_t)(base + b) * N2;
+      const float2* src = ga.ogscr + ((size_t)(base + b) * ga.nz + ga.z) * N2;
       const int col = x - cx;
       const bool colok = col >= 0 && col < N;
       float2 v[kGTY];

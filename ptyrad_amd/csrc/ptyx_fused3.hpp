@@ -60,6 +60,10 @@ struct F3Args {
   float* dsu;              // per-pattern position-gradient sums, unit coefficient (2 floats)
   int tail;                // probe or position gradient wanted
   float* dp_out;
+  // multislice (k_fused3ms): Nz slices, H K-packed; slots hold Nz planes per pattern (slice n
+  // at slots + (pat·Nz + n)·N²), oc is (Nz, Ny, Nx)
+  int Nz;
+  const float2* hpk;
 };
 
 // Packed layouts (thread t = 0..255, register i = 0..63):
@@ -168,7 +172,7 @@ __global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx,
 // Σ_{window} |φ|^n into psums[kSumBase] (fp64 over rows, fixed order).  One wave per pattern.
 __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_batches, const int* crop,
                                  int n_scans, int Ny, int Nx, int* bid, int2* geo, const double* pref,
-                                 float* psums) {
+                                 float* psums, int Nz = 1) {
   const int j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -186,10 +190,11 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
   }
   if (!pref) return;
   double acc = 0;
-  for (int r = lane; r < kN; r += 64) {
-    const double* prow = pref + (size_t)(cy + r) * (Nx + 1);
-    acc += prow[cx + kN] - prow[cx];
-  }
+  for (int z = 0; z < Nz; ++z)
+    for (int r = lane; r < kN; r += 64) {
+      const double* prow = pref + ((size_t)z * Ny + cy + r) * (Nx + 1);
+      acc += prow[cx + kN] - prow[cx];
+    }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) psums[(size_t)j * kNSum + kSumBase] = (float)acc;
@@ -688,6 +693,293 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
            (int)blockIdx.x, ph_n, ph[0] / ph_n, ph[1] / ph_n, ph[2] / ph_n, ph[3] / ph_n, ph[4] / ph_n, ph[5] / ph_n,
            ph[6] / ph_n, ph[7] / ph_n, ph[8] / ph_n, ph[9] / ph_n, ph[10] / ph_n, ph[11] / ph_n);
 #endif
+}
+
+
+// ================================================================================= multislice
+// k_fused3ms: the same one-pass forward / loss / adjoint for Nz ≥ 2 slices (P = O = 1), the
+// c4 shape.  multislice_forward_model_vec_all (forward.py:50-80) and its adjoint:
+//   forward   ψ⁰ = F⁻¹(F(P)·W_b)/N²;  for n < Nz:  park ψⁿ in slot plane n;  u = ψⁿ·O_n;
+//             n < Nz−1:  ψⁿ⁺¹ = F⁻¹(H ⊙ F(u))/N²           (FFT, ×H/N² in K layout, IFFT)
+//   far field Ψ = F(u_{Nz−1})/N, loss, g_Ψ per unit mini-batch coefficient (as k_fused3)
+//   adjoint   g = F⁻¹(g_Ψ)/N;  for n = Nz−1 … 0:  slot plane n = g·conj(ψⁿ);  g ← g·conj(O_n);
+//             n > 0:  g ← F⁻¹(conj(H) ⊙ F(g))/N²            (the propagator's adjoint)
+//   then the probe / position pass on g = ∂ℓ/∂ψ⁰ exactly as k_fused3.
+// 4·Nz FFTs per pattern, the algorithmic count: no forward is recomputed.  Each slot plane
+// first parks ψⁿ and is overwritten by slice n's object gradient.
+template <bool SHIFT, bool SINGLE, int QM>
+__global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
+  using namespace rf;
+  __shared__ float2 buf[kLdsElems];
+  __shared__ float s_red[4 * 2];
+  const Coord cd = coord(threadIdx.x);
+  const LaneCtx lc = lane_ctx(cd.lane);
+  constexpr float inv_n = 1.0f / kN, inv_n2 = 1.0f / kN2;
+  const int w = blockIdx.x, G = gridDim.x;
+  const int p0 = (int)((long long)w * a.n_idx / G), p1 = (int)((long long)(w + 1) * a.n_idx / G);
+  if (p0 >= p1) return;
+  const float occ = a.occp[0], q = a.q;
+  const bool tail = a.tail != 0;
+  const int Nx = a.Nx, Nz = a.Nz;
+  const size_t plane = (size_t)a.Ny * a.Nx;
+  const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
+  const Rsrc r_hpk = rsrc(a.hpk, kN2 * 8);
+  const float gy = (float)((cd.fixed + 64) & 127) * inv_n;
+
+  float2 v[64];
+  {
+    const int tid = rf::opaque(threadIdx.x);
+    const int vpk = 8 * tid;
+    const PatInfo pi0 = pat_info<SHIFT>(a, p0);
+    Ramp rp;
+    rp.init(pi0.sy, pi0.sx, gy, tid & 1);
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+          const float2 A = rp.a(C);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
+            pin(v[4 * C + r]);
+          }
+        });
+  }
+
+  // K-layout pass: v ← v ⊙ (H or conj(H)) / N²
+  auto prop_k = [&](bool conj_h) {
+    const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_hpk, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 4 * C + r;
+            v[k] = cscale(conj_h ? cmulc(v[k], t.x[r]) : cmul(v[k], t.x[r]), inv_n2);
+            pin(v[k]);
+          }
+        });
+  };
+
+  for (int pat = p0; pat < p1; ++pat) {
+    const int tid = rf::opaque(threadIdx.x);
+    const int fx = fixed_of(tid);
+    const int l0 = tid & 1;
+    const PatInfo p = pat_info<SHIFT>(a, pat);
+    const int vslot0 = 8 * (l0 * kN + fx);
+    const int vobj0 = 8 * (64 * l0 * Nx + fx);
+    const int ostr0 = 8 * Nx;
+    if constexpr (SHIFT) {
+      fft_inv(v, buf, lc, cd.wsign);
+#pragma unroll
+      for (int j = 0; j < 64; ++j) v[j] = cscale(v[j], inv_n2);
+    }
+    // ------------------------------------------------ slices: park ψⁿ, ×O_n, propagate
+    for (int n = 0; n < Nz; ++n) {
+      const Rsrc r_slot = rsrc(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8);
+      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
+      {
+        const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+        pipeline<8>(
+            [&](auto C) {
+              Ch8 t;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
+              return t;
+            },
+            [&](auto C, const Ch8& t) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const int j = 8 * C + r;
+                st2(v[j], r_slot, vslot, 2048 * j);
+                v[j] = cmul(v[j], t.x[r]);
+                pin(v[j]);
+              }
+            });
+      }
+      if (n + 1 < Nz) {
+        fft_fwd(v, buf, lc, cd.wsign);
+        prop_k(false);
+        fft_inv(v, buf, lc, cd.wsign);
+      }
+    }
+    // ------------------------------------------------ far field; DP → LDS during the row DFTs
+    const float* dp = a.meas + (size_t)p.sidx * kN2;
+    fft_fwd(v, buf, lc, cd.wsign, [&] {
+      const int lane = cd.lane;
+      const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int gi = wv * 16 + i;
+        const int r = 2 * gi + (lane >> 5);
+        const int sl = lane & 31;
+        const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
+        __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
+                                         (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
+                                         PTYX_F3_NT ? 2 : 0);
+      }
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float S = 0.f, Ms = 0.f;
+    {
+      const int r = (fx + 64) & 127;
+      const int b = 1 - l0;
+      const float4* row4 = reinterpret_cast<const float4*>(buf) + r * 32;
+      const Rsrc r_dp = rsrc(a.dp_out ? a.dp_out + (size_t)pat * kN2 : a.psums, a.dp_out ? kN2 * 4 : 0);
+      const int vdp = 4 * (r * kN + 64 * b);
+#pragma unroll
+      for (int kq = 0; kq < 16; ++kq) {
+        const float4 M4 = row4[(kq + 16 * b) ^ ((r & 7) | (b << 3))];
+        const float Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+        float Iv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * kq + e;
+          const float2 Psi = cscale(v[k], inv_n);
+          Iv[e] = fmaf(occ, cabs2(Psi), kDpEps);
+          const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+          v[k] = cscale(Psi, 2.0f * occ * u);
+          pin(v[k]);
+        }
+        {
+          const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, i4),
+                                                 r_dp, vdp + 16 * kq, 0, 0);
+        }
+        if (kq & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    {
+      float v2[2] = {S, Ms};
+      block_sum4<2>(v2, s_red);
+      if (threadIdx.x == 0) {
+        float* ps = a.psums + (size_t)pat * kNSum;
+        const int base = SINGLE ? 0 : 2;
+        ps[base] = v2[0];
+        ps[base + 1] = v2[1];
+        ps[2 - base] = 0.f;
+        ps[3 - base] = 0.f;
+      }
+    }
+    fft_inv(v, buf, lc, cd.wsign);
+    // ------------------------------------------------ slices backwards
+    for (int n = Nz - 1; n >= 0; --n) {
+      const Rsrc r_slot = rsrc(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8);
+      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
+      const float sc = n == Nz - 1 ? inv_n : 1.0f;   // far-field ortho scale once; propagation scaled in K
+      {
+        const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+        pipeline<16>(
+            [&](auto C) {
+              Ch4x2 t;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 4 * C + r;
+                t.x[r] = ld2(r_slot, vslot, 2048 * j);
+                t.y[r] = ld2(r_obj, vobj, ostr * j);
+              }
+              return t;
+            },
+            [&](auto C, const Ch4x2& t) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 4 * C + r;
+                const float2 gv = cscale(v[j], sc);
+                st2_stream(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // slice n: g·conj(ψⁿ)
+                v[j] = cmulc(gv, t.y[r]);                                  // g·conj(O_n)
+                pin(v[j]);
+              }
+            });
+      }
+      if (n > 0) {
+        fft_fwd(v, buf, lc, cd.wsign);
+        prop_k(true);
+        fft_inv(v, buf, lc, cd.wsign);
+      }
+    }
+    // ------------------------------------------------ probe / position gradient, next pattern's v
+    const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
+    const bool first = pat == p0 || a.bid[pat - 1] != p.m;
+    const int seg = p.m + w;
+    float2* segs = a.segslab + (size_t)seg * kN2;
+    const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
+    const Rsrc r_slab_st = rsrc(segs, kN2 * 8);
+    if (first && threadIdx.x == 0) a.segbid[seg] = p.m;
+    if constexpr (SHIFT) {
+      if (tail) fft_fwd(v, buf, lc, cd.wsign);
+      const int vpk = rf::opaque(8 * tid);
+      const int l0b = rf::opaque(tid) & 1;
+      Ramp rc, rn;
+      rc.init(p.sy, p.sx, gy, l0b);
+      rn.init(pn.sy, pn.sx, gy, l0b);
+      float sim = 0.f, kim = 0.f;
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              t.x[r] = ld2(r_fpk, vpk, 2048 * k);
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * k);
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = rc.a(C), An = rn.a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              const float2 W = cmul(A, rc.B[r]);
+              const float2 FW = cmul(t.x[r], W);
+              const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);
+              sim += im;
+              kim = fmaf((float)k, im, kim);
+              st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);
+              v[k] = cmul(t.x[r], cmul(An, rn.B[r]));
+              pin(v[k]);
+            }
+          });
+      {
+        float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0b) * sim)};
+        block_sum4<2>(ds, s_red);
+        if (threadIdx.x == 0) {
+          a.dsu[2 * pat] = ds[0];
+          a.dsu[2 * pat + 1] = ds[1];
+        }
+      }
+    } else {
+      const int vpk = rf::opaque(8 * tid);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * C + r;
+              st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);
+              v[j] = t.x[r];
+              pin(v[j]);
+            }
+          });
+    }
+  }
 }
 
 }  // namespace f3

@@ -560,6 +560,8 @@ struct ptyx_plan {
   int* segbid = nullptr;      // batch of each segment id (-1 unused)
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
+  float2* hpk = nullptr;      // k_fused3ms: K-packed propagator
+  bool ms3 = false;           // k_fused3ms (multislice register engine) available
   long long seg_cap = 0;      // segment ids the segslab holds
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
@@ -753,6 +755,41 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
     }
   }
+  if (d.N == 128 && d.P * d.O == 1 && d.Nz > 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast) {
+    // multislice register engine: Nz slot planes per pattern (parked ψⁿ, then slice n's
+    // object gradient), bounded by PTYX_OBJ_SCRATCH_MB like the single-slice slots
+    const char* f3 = std::getenv("PTYX_FUSED3");
+    long long mb = 16384;
+    if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
+    const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2 * d.Nz));
+    int occ3 = 0;
+    if (!(f3 && f3[0] == '0') && cap > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3ms<true, true, 0>, 256, 0) == hipSuccess &&
+        occ3 > 0) {
+      int o2 = 0;
+      for (auto kf : {f3::k_fused3ms<true, true, 2>, f3::k_fused3ms<true, false, 2>, f3::k_fused3ms<false, true, 0>,
+                      f3::k_fused3ms<false, true, 2>, f3::k_fused3ms<false, false, 2>})
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
+      pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
+      long long div = 8;
+      if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
+      pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
+      if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * d.Nz * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->hpk, N2)) ||
+          (rc = dalloc(pl, &pl->oc, (size_t)d.Nz * d.Ny * d.Nx)) ||
+          (rc = dalloc(pl, &pl->pref, (size_t)d.Nz * d.Ny * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
+          (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
+          (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
+          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2))) {
+        free_plan(pl);
+        return rc;
+      }
+      pl->og_cap = cap;
+      pl->ms3 = true;
+    }
+  }
   // fp64 twiddles rounded once to fp32: tw[m] = exp(-2πi m/N)
   std::vector<float2> tw(d.N);
   for (int m = 0; m < d.N; ++m) {
@@ -922,6 +959,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   constexpr int N = 128, N2 = N * N;
   const ptyx_dims& d = pl->d;
   const bool sparse = cfg->sparse_on != 0;
+  const int Nz = d.Nz;                 // > 1: k_fused3ms (multislice)
   if (a.shift) {
     launch_spectrum<N>(pl, a, st);
     ProfScope ps(pl, kKPack, st);
@@ -931,16 +969,20 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256), dim3(256), 0, st,
                        reinterpret_cast<const float2*>(in->probe), pl->fpk);
   }
+  if (Nz > 1) {
+    ProfScope ps(pl, kKPack, st);
+    hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk);
+  }
   {
-    ProfScope ps(pl, kKObjPrep, st);
-    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny), dim3(256), 0, st, a.obja, a.objp, d.Ny, d.Nx, pl->oc,
+    ProfScope ps(pl, kKObjPrep, st);   // (Nz, Ny) rows: every slice's O and |φ|^n prefix sums
+    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny * Nz), dim3(256), 0, st, a.obja, a.objp, d.Ny * Nz, d.Nx, pl->oc,
                        sparse ? pl->pref : nullptr, cfg->sparse_n);
   }
   {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
                        a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo,
-                       sparse ? pl->pref : nullptr, pl->psums);
+                       sparse ? pl->pref : nullptr, pl->psums, Nz);
   }
   const bool single = cfg->single_on != 0;
   const int ci = single ? 0 : 1;
@@ -959,7 +1001,22 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   f.slots = pl->ogscr; f.segslab = pl->segslab; f.segbid = pl->segbid; f.dsu = pl->dsu;
   f.tail = (gz.d_probe != nullptr || (a.shift && gz.d_shifts != nullptr)) ? 1 : 0;
   f.dp_out = a.dp_out;
-  {
+  f.Nz = Nz;
+  f.hpk = pl->hpk;
+  if (Nz > 1) {
+    ProfScope ps(pl, kKFused, st);
+    const dim3 gr(G), bl(256);
+    const bool half = single && f.q == 0.5f;
+    if (a.shift) {
+      if (half) hipLaunchKernelGGL((f3::k_fused3ms<true, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3ms<true, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3ms<true, false, 2>), gr, bl, 0, st, f);
+    } else {
+      if (half) hipLaunchKernelGGL((f3::k_fused3ms<false, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3ms<false, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3ms<false, false, 2>), gr, bl, 0, st, f);
+    }
+  } else {
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
@@ -976,7 +1033,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   int rc = launch_status("k_fused3 launch");
   if (rc) return rc;
   FinArgs fa{};
-  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = 1; fa.O = 1;
+  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
   fa.psums = pl->psums; fa.occu = in->omode_occu;
   fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
   fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
@@ -997,7 +1054,16 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
     const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
     ProfScope ps(pl, kKGather, st);
-    hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+    const size_t plane = (size_t)d.Ny * d.Nx;
+    g.nz = Nz;
+    for (int z = 0; z < Nz; ++z) {   // one launch per slice plane of the slots
+      g.z = z;
+      g.obja = a.obja + z * plane;
+      g.objp = a.objp + z * plane;
+      g.d_obja = gz.d_obja ? gz.d_obja + z * plane : nullptr;
+      g.d_objp = gz.d_objp ? gz.d_objp + z * plane : nullptr;
+      hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+    }
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
   if (a.shift && gz.d_shifts) {
@@ -1147,7 +1213,11 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   const bool fused3 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 &&
                       n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
                       (cfg->single_on != 0) != (cfg->poissn_on != 0);
-  if (fused3) {
+  // multislice register engine (k_fused3ms): N = 128, P = O = 1, Nz ≥ 2, f32 DPs
+  const bool fused3ms = any_grad && pl->ms3 && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && !a.meas_f16 &&
+                        n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
+                        (cfg->single_on != 0) != (cfg->poissn_on != 0);
+  if (fused3 || fused3ms) {
 #ifndef PTYX_ONLY_N
     return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
 #else
