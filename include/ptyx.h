@@ -195,6 +195,12 @@ int ptyx_meas_stats(void *stream, const float *raw, int64_t n, int32_t H, int32_
 int ptyx_meas_finish(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
                      const double *stats, void *ws, void *dst, int32_t dst_f16);
 
+/* Patterns one ptyx_forward_loss_grad call may hold and still run on the register-resident
+ * engines (k_fused3 / k_fused3ms: slot capacity); larger calls take the general engine.
+ * 0 when the plan's geometry has no register engine.  Callers with host-side batch offsets
+ * split larger calls at mini-batch boundaries (gradients accumulate). */
+int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
+
 /* Bytes of device workspace the plan holds. */
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
 /* Last error message of the calling thread ("" if none). */

@@ -25,7 +25,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
            "ptyx_obj_rblur", "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
-           "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
+           "ptyx_plan_register_capacity", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
 
 
 class PtyxError(RuntimeError):
@@ -110,6 +110,8 @@ def load(path: str | None = None):
     lib.ptyx_profile_end.restype = ctypes.c_int
     lib.ptyx_plan_workspace_bytes.argtypes = [vp]
     lib.ptyx_plan_workspace_bytes.restype = ctypes.c_size_t
+    lib.ptyx_plan_register_capacity.argtypes = [vp]
+    lib.ptyx_plan_register_capacity.restype = ctypes.c_int64
     lib.ptyx_last_error.restype = ctypes.c_char_p
     lib.ptyx_version.restype = ctypes.c_int
     lib.ptyx_constraints_ws_bytes.restype = ctypes.c_size_t

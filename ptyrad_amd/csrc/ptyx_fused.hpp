@@ -342,6 +342,7 @@ struct GatherArgs {
   float* d_obja;
   float* d_objp;
   int nz = 1, z = 0;     // slots hold nz planes per pattern; this launch gathers plane z
+  const int* bbox = nullptr;   // {min cy, max cy, min cx, max cx} of the call's windows: other tiles exit
 };
 #ifndef PTYX_GTY
 #define PTYX_GTY 16
@@ -359,6 +360,8 @@ __global__ __launch_bounds__(64 * kGWaves) void k_obj_gather(GatherArgs ga) {
   __shared__ float s_cnt[kGTY * kGTX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ty = (blockIdx.x / ga.tiles_x) * kGTY, tx = (blockIdx.x % ga.tiles_x) * kGTX;
+  if (ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] || tx >= ga.bbox[3] + N))
+    return;   // no window of this call touches the tile: its gradient contribution is zero
   const int x = tx + lane;
   float2 acc[kGTY];
   float cnt[kGTY];

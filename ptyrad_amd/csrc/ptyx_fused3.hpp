@@ -126,9 +126,13 @@ __global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid
 // object point), and — for loss_sparse — per-row fp64 prefix sums of |φ|^n:
 // pref[y][x] = Σ_{x' < x} |φ(y, x')|^n, x = 0..Nx.  One workgroup per object row.
 __global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx, float2* oc, double* pref,
-                           int sparse_n) {
+                           int sparse_n, const int* bbox = nullptr, int rows_per_slice = 0) {
   __shared__ double s_part[256];
   const int y = blockIdx.x;
+  if (bbox) {   // rows no window of this call touches are never read (k_fused3*, k_pattern_table3)
+    const int r = y % rows_per_slice;
+    if (r < bbox[0] || r >= bbox[1] + kN) return;
+  }
   const float* ar = obja + (size_t)y * Nx;
   const float* pr = objp + (size_t)y * Nx;
   float2* orow = oc + (size_t)y * Nx;
@@ -166,6 +170,39 @@ __global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx,
   }
   if (x1 == Nx && x0 < x1) prow[Nx] = run;
   if (Nx == 0 && threadIdx.x == 0) prow[0] = 0;
+}
+
+// Bounding box of the call's windows: bbox = {min cy, max cy, min cx, max cx} (clamped origins);
+// initialise with k_bbox_init.  Lets k_obj_prep / k_obj_gather skip untouched object rows / tiles.
+__global__ void k_bbox_init(int* bbox) {
+  if (threadIdx.x == 0) {
+    bbox[0] = 0x7fffffff;
+    bbox[1] = -0x7fffffff;
+    bbox[2] = 0x7fffffff;
+    bbox[3] = -0x7fffffff;
+  }
+}
+__global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int Ny, int Nx, int* bbox) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  int a = 0x7fffffff, b = -0x7fffffff, c = 0x7fffffff, d = -0x7fffffff;
+  if (j < n) {
+    const int s = min(max(idx[j], 0), n_scans - 1);
+    a = b = min(max(crop[2 * s], 0), Ny - kN);
+    c = d = min(max(crop[2 * s + 1], 0), Nx - kN);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a = min(a, __shfl_xor(a, o, 64));
+    b = max(b, __shfl_xor(b, o, 64));
+    c = min(c, __shfl_xor(c, o, 64));
+    d = max(d, __shfl_xor(d, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(bbox + 0, a);
+    atomicMax(bbox + 1, b);
+    atomicMin(bbox + 2, c);
+    atomicMax(bbox + 3, d);
+  }
 }
 
 // pattern → (mini-batch, clamped window origin) and, with pref, the loss_sparse window sum

@@ -561,6 +561,7 @@ struct ptyx_plan {
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
   float2* hpk = nullptr;      // k_fused3ms: K-packed propagator
+  int* bbox = nullptr;        // k_fused3*: bounding box of a call's windows
   bool ms3 = false;           // k_fused3ms (multislice register engine) available
   long long seg_cap = 0;      // segment ids the segslab holds
   long long scratch_stride = 0;
@@ -671,6 +672,10 @@ extern "C" const char* ptyx_last_error(void) { return g_err.c_str(); }
 
 extern "C" size_t ptyx_plan_workspace_bytes(const ptyx_plan* plan) { return plan ? plan->ws_bytes : 0; }
 
+extern "C" int64_t ptyx_plan_register_capacity(const ptyx_plan* plan) {
+  return (plan && plan->nwg3 > 0) ? (int64_t)plan->og_cap : 0;
+}
+
 extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int device) {
   g_err.clear();
   if (!out || !dims) return fail(PTYX_EINVAL, "null argument");
@@ -776,7 +781,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
       if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * d.Nz * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
-          (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->hpk, N2)) ||
+          (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->hpk, N2)) || (rc = dalloc(pl, &pl->bbox, 4)) ||
           (rc = dalloc(pl, &pl->oc, (size_t)d.Nz * d.Ny * d.Nx)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Nz * d.Ny * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
@@ -973,10 +978,16 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk);
   }
+  if (pl->bbox) {   // (multislice plans) rows / tiles outside the call's windows are skipped
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
+    hipLaunchKernelGGL(f3::k_bbox, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
+                       d.Ny, d.Nx, pl->bbox);
+  }
   {
     ProfScope ps(pl, kKObjPrep, st);   // (Nz, Ny) rows: every slice's O and |φ|^n prefix sums
     hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny * Nz), dim3(256), 0, st, a.obja, a.objp, d.Ny * Nz, d.Nx, pl->oc,
-                       sparse ? pl->pref : nullptr, cfg->sparse_n);
+                       sparse ? pl->pref : nullptr, cfg->sparse_n, pl->bbox, d.Ny);
   }
   {
     ProfScope ps(pl, kKTable, st);
@@ -1056,6 +1067,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKGather, st);
     const size_t plane = (size_t)d.Ny * d.Nx;
     g.nz = Nz;
+    g.bbox = pl->bbox;
     for (int z = 0; z < Nz; ++z) {   // one launch per slice plane of the slots
       g.z = z;
       g.obja = a.obja + z * plane;

@@ -181,12 +181,19 @@ class Plan:
         max_batch: largest mini-batch size (enables the one-pass fused kernel); derived from
         host-side offsets when not given, 0 (= two-pass) for device-only offsets.
         """
+        host_off = not (isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu")
         if max_batch is None:
-            if isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu":
+            if not host_off:
                 max_batch = 0
             else:
                 off = np.asarray(batch_offsets)
                 max_batch = int(np.max(np.diff(off))) if off.size > 1 else 0
+        cap = self.register_capacity
+        if host_off and cap > 0:
+            off = np.asarray(batch_offsets.cpu() if isinstance(batch_offsets, torch.Tensor) else batch_offsets,
+                             dtype=np.int64)
+            if off[-1] - off[0] > cap and np.max(np.diff(off)) <= cap:
+                return self._chunked(t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch)
         idx_t = self._idx(idx)
         off_t = self._idx(batch_offsets)
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
@@ -199,6 +206,31 @@ class Plan:
         _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
                                                    _ptr(dp_out), ctypes.byref(g)))
+        return loss_terms
+
+    @property
+    def register_capacity(self) -> int:
+        """Patterns per call the register-resident engines take (0: none for this geometry)."""
+        return int(self.lib.ptyx_plan_register_capacity(self._h))
+
+    def _chunked(self, t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch):
+        """Split a call at mini-batch boundaries into groups of <= cap patterns (each batch keeps
+        its own normalisation; gradients accumulate across the group calls)."""
+        nb = off.size - 1
+        if loss_terms is None:
+            loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
+        idx_t = self._idx(idx)
+        b0 = 0
+        while b0 < nb:
+            b1 = b0 + 1
+            while b1 < nb and off[b1 + 1] - off[b0] <= cap:
+                b1 += 1
+            sub_off = (off[b0:b1 + 1] - off[b0]).astype(np.int32)
+            sub_idx = idx_t[int(off[b0]):int(off[b1])]
+            sub_dp = None if dp_out is None else dp_out[int(off[b0]):int(off[b1])]
+            self.forward_loss_grad(t, sub_idx, sub_off, loss_cfg, grads, grad_scale=grad_scale,
+                                   loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch)
+            b0 = b1
         return loss_terms
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):

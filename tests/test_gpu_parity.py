@@ -303,3 +303,27 @@ def test_multislice_register_engine_vs_oracle(nz, shift):
     torch.cuda.synchronize()
     stats = plan.profile_end()
     assert "k_obj_prep" in stats and "k_fused" in stats and "k_adjoint" not in stats, stats
+
+
+def test_multislice_call_split_at_batch_boundaries(monkeypatch):
+    """A call larger than the register engine's slot capacity is split by engine.Plan at
+    mini-batch boundaries: same loss terms and gradients as the oracle."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    monkeypatch.setenv("PTYX_OBJ_SCRATCH_MB", "8")      # 8 MiB / (3 x 128 KiB) = 21 patterns per call
+    pr = syn.random_problem(128, 6, 7, Nz=3, seed=31)
+    d = dict(obja=pr.obja, objp=(pr.objp / 3).astype(np.float32), probe=pr.probe * np.float32(60.0),
+             shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True,
+             loss_params=orc_default_loss())
+    perm = np.random.default_rng(6).permutation(42)
+    cuts = [0, 9, 10, 30, 42]
+    batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    assert make_plan(d, device).register_capacity == 21
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5)
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"], grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
