@@ -812,9 +812,6 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
     const PatInfo p = pat_info<SHIFT>(a, pat);
-    const int vslot0 = 8 * (l0 * kN + fx);
-    const int vobj0 = 8 * (64 * l0 * Nx + fx);
-    const int ostr0 = 8 * Nx;
     if constexpr (SHIFT) {
       fft_inv(v, buf, lc, cd.wsign);
 #pragma unroll
@@ -825,7 +822,9 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
       const Rsrc r_slot = rsrc(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8);
       const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
       {
-        const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+        const int tq = rf::opaque(threadIdx.x);
+        const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
+        const int ostr = rf::opaque(8 * Nx);
         pipeline<8>(
             [&](auto C) {
               Ch8 t;
@@ -915,7 +914,9 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
       const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
       const float sc = n == Nz - 1 ? inv_n : 1.0f;   // far-field ortho scale once; propagation scaled in K
       {
-        const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
+        const int tq = rf::opaque(threadIdx.x);
+        const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
+        const int ostr = rf::opaque(8 * Nx);
         pipeline<16>(
             [&](auto C) {
               Ch4x2 t;

@@ -750,6 +750,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
       pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
       if ((rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
+          (rc = dalloc(pl, &pl->bbox, 4)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Ny * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
           (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
@@ -978,7 +979,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk);
   }
-  if (pl->bbox) {   // (multislice plans) rows / tiles outside the call's windows are skipped
+  if (pl->bbox) {   // rows / tiles outside the call's windows are skipped (a rank's shard of a
+                    // multi-GPU scan touches only its band of the replicated object)
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
     hipLaunchKernelGGL(f3::k_bbox, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
@@ -1067,7 +1069,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKGather, st);
     const size_t plane = (size_t)d.Ny * d.Nx;
     g.nz = Nz;
-    g.bbox = pl->bbox;
+    g.bbox = pl->bbox;   // also for Nz = 1
     for (int z = 0; z < Nz; ++z) {   // one launch per slice plane of the slots
       g.z = z;
       g.obja = a.obja + z * plane;
