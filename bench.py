@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=40960, help="patterns for the CPU baseline (about 10 s on 16 cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--geom-world", type=int, default=0,
+                    help="diagnostic: build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
+                         "(no collective) to check that per-rank work stays constant as W grows")
+    ap.add_argument("--geom-rank", type=int, default=0)
     return ap.parse_args()
 
 
@@ -102,9 +106,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     N, S = a.N, a.scan
-    n_slow_g, n_fast = S * world, S
+    gw, gr = (a.geom_world, a.geom_rank) if a.geom_world else (world, rank)
+    n_slow_g, n_fast = S * gw, S
     scan = syn.raster_scan(n_slow_g, n_fast, N, seed=0)
-    sl = slice(rank * S * n_fast, (rank + 1) * S * n_fast)
+    sl = slice(gr * S * n_fast, (gr + 1) * S * n_fast)
     crop_pos, shifts = scan.crop_pos[sl], scan.shifts[sl]
     n_local = crop_pos.shape[0]
     Ny, Nx = scan.obj_shape
@@ -206,7 +211,8 @@ def main():
                                "sub-px shifts on, loss_single(q=0.5)+loss_sparse(L1), mini-batch 32",
                    "scan_per_gpu": [S, S], "N": N, "mini_batch": a.batch, "mini_batches_per_step": nb,
                    "patterns_per_gpu_per_step": n_local, "object": [Ny, Nx],
-                   "parallelism": f"dp{world} (RCCL all-reduce of object+probe grads per step)"},
+                   "parallelism": f"dp{world} (RCCL all-reduce of object+probe grads per step)",
+                   **({"geometry_only": f"rank {gr} of a {gw}-GPU scan, no collective"} if a.geom_world else {})},
         "roofline": roof,
         "fft_tflops": round(value / world * flops / 1e12, 2) if world else None,
         "kernels_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in kstats.items()},
