@@ -163,15 +163,19 @@ class Plan:
 
     # ------------------------------------------------------------------ entry points
     def forward(self, t: dict, idx, dp_out=None):
-        """ptyx_forward: dp (n, N, N) f32 = PtychoAD.forward(idx)."""
+        """ptyx_forward: dp (n, N, N) f32 = PtychoAD.forward(idx); calls larger than the plan's
+        max_patterns run in pieces (patterns are independent in the forward model)."""
         idx_t = self._idx(idx)
         n = int(idx_t.numel())
         if dp_out is None:
             dp_out = torch.empty((n, self.dims.N, self.dims.N), dtype=torch.float32, device=self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
                                   t["crop_pos"], None)
-        _lib.check(self.lib.ptyx_forward(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t), n,
-                                         _ptr(dp_out)))
+        step = max(1, int(self.dims.max_patterns))
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            _lib.check(self.lib.ptyx_forward(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t[a:b]), b - a,
+                                             _ptr(dp_out[a:b])))
         return dp_out
 
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
@@ -189,7 +193,8 @@ class Plan:
                 off = np.asarray(batch_offsets)
                 max_batch = int(np.max(np.diff(off))) if off.size > 1 else 0
         cap = self.register_capacity
-        if host_off and cap > 0:
+        cap = min(cap, int(self.dims.max_patterns)) if cap > 0 else int(self.dims.max_patterns)
+        if host_off:
             off = np.asarray(batch_offsets.cpu() if isinstance(batch_offsets, torch.Tensor) else batch_offsets,
                              dtype=np.int64)
             if off[-1] - off[0] > cap and np.max(np.diff(off)) <= cap:
@@ -241,8 +246,11 @@ class Plan:
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
                                   t["crop_pos"], None)
         g = self._grads(grads)
-        _lib.check(self.lib.ptyx_adjoint_dldi(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t), n,
-                                              _ptr(dLdI), float(grad_scale), ctypes.byref(g)))
+        step = max(1, int(self.dims.max_patterns))
+        for a in range(0, n, step):   # pieces of max_patterns: the external-loss adjoint is per pattern
+            b = min(n, a + step)
+            _lib.check(self.lib.ptyx_adjoint_dldi(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t[a:b]),
+                                                  b - a, _ptr(dLdI[a:b]), float(grad_scale), ctypes.byref(g)))
 
 
 def batch_offsets(batches) -> np.ndarray:

@@ -138,7 +138,9 @@ class PtychoHIP(nn.Module):
             O, Nz, Ny, Nx = self.opt_obja.shape
             P, N = self.opt_probe.shape[0], self.opt_probe.shape[1]
             n_scans = self.crop_pos.shape[0]
-            self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or n_scans,
+            # plan workspace scales with the largest call (per-pattern intensities of mixed-state
+            # calls are N² f32 each); larger calls are split at mini-batch boundaries by Plan
+            self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or min(n_scans, 65536),
                              shift_probes=self.shift_probes, meas_f16=(meas_dtype == torch.float16),
                              device=device)
 

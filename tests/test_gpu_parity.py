@@ -351,3 +351,33 @@ def test_register_engine_band_of_tall_object_vs_oracle():
         assert rel(g[k], og[k]) < TOL_G, k
     y0, y1 = pr.crop_pos[band, 0].min(), pr.crop_pos[band, 0].max() + 128
     assert not np.any(g["objp"][..., :y0, :]) and not np.any(g["objp"][..., y1:, :])
+
+
+def test_calls_larger_than_max_patterns_are_split():
+    """engine.Plan splits forward / adjoint calls into max_patterns pieces and fused calls at
+    mini-batch boundaries: identical to one big plan's results (mixed state, general engine)."""
+    device = dev()
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    d = load_case([c for c in CASES if "n32_p2o2z3" in c][0])
+    S = d["shifts"].shape[0]
+    idx = np.arange(S, dtype=np.int32)
+    batches = np.array_split(np.random.default_rng(1).permutation(S), 4)
+    out = []
+    for mp in (S, 5):
+        plan = make_plan(d, device, max_patterns=mp)
+        t = tensors(d, device)
+        dp = plan.forward(t, idx)
+        grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+        terms = plan.forward_loss_grad(t, np.concatenate(batches).astype(np.int32), batch_offsets(batches),
+                                       LossConfig.from_loss_params(d["loss_params"]), grads)
+        g2 = {k: torch.zeros_like(v) for k, v in grads.items()}
+        plan.adjoint_dldi(t, idx, torch.ones_like(dp), g2)
+        torch.cuda.synchronize()
+        out.append((dp.cpu().numpy(), terms.cpu().numpy(), {k: v.cpu().numpy() for k, v in grads.items()},
+                    {k: v.cpu().numpy() for k, v in g2.items()}))
+    (dp0, t0, g0, a0), (dp1, t1, g1, a1) = out
+    np.testing.assert_allclose(dp1, dp0, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(t1, t0, rtol=1e-6, atol=1e-9)
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-5, k
+        assert rel(a1[k], a0[k]) < 1e-5, k
