@@ -381,7 +381,10 @@ __device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float
     for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, q * k2));
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) lds[lr * kG256RowStride + k2 * 17 + q] = v[k2];
-    __syncthreads();
+    // the exchange stays inside the wave (its 4 rows): LDS ops retired, no workgroup barrier
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int n1 = 0; n1 < 16; ++n1) v[n1] = lds[lr * kG256RowStride + q * 17 + n1];
     DFT<16, DIR>::run(v);                     // X[row][q + 16·k1] = v[k1]
