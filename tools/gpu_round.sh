@@ -8,7 +8,7 @@ TAG=${1:-round}
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 echo "tests ok"
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench ok"
