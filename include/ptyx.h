@@ -146,6 +146,35 @@ size_t ptyx_constraints_ws_bytes(void);
 int ptyx_obj_rblur(void *stream, const float *in, float *out, int32_t n_planes, int32_t Ny, int32_t Nx,
                    int32_t kernel_size, float sigma);
 
+/* ---------------------------------------------------------------------------------------------
+ * Optional forward stages.  Composed around the engine entry points by the
+ * host mirror (ptyrad_amd/stages.py); same conventions as above.
+ *   detector_blur_std  PtychoAD.get_forward_meas  src/ptyrad/models.py:375-382
+ *                      dp = gaussian_blur(dp, 5, std): ptyx_obj_rblur on the (B,N,N) dp planes,
+ *                      backward ptyx_blur_adjoint on dL/d(blurred dp).
+ *   obj_preblur_std    PtychoAD.get_obj_patches   src/ptyrad/models.py:267-284
+ *                      patches = gaussian_blur(get_obj_ROI(idx), 5, std) per amplitude / phase
+ *                      plane: ptyx_patch_gather → ptyx_obj_rblur → engine on the patch stack;
+ *                      backward ptyx_blur_adjoint → ptyx_patch_scatter_add.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Transpose of ptyx_obj_rblur (reflect-padded separable Gaussian), i.e. the autograd backward
+ * of torchvision gaussian_blur: out = B^T in over n_planes (Ny, Nx) f32 planes, out of place,
+ * deterministic.  n_planes ≤ 65535. */
+int ptyx_blur_adjoint(void *stream, const float *in, float *out, int32_t n_planes, int32_t Ny, int32_t Nx,
+                      int32_t kernel_size, float sigma);
+
+/* get_obj_ROI (models.py:251-265) for one (O,Nz,Ny,Nx) f32 plane set: patches (O,Nz,n_idx,N,N)
+ * [o,z,b] = obj[o,z, crop_pos[idx[b]] + (0..N, 0..N)].  crop_pos (n_scans,2) int32, idx
+ * (n_idx) int32, both device; n_idx ≤ 65535, O·Nz ≤ 65535.  Windows outside the object give 0. */
+int ptyx_patch_gather(void *stream, const float *obj, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
+                      const int32_t *crop_pos, const int32_t *idx, int32_t n_idx, int32_t N, float *patches);
+
+/* Transpose of ptyx_patch_gather: gobj += scatter(gpatches) (f32 atomics; overlapping windows
+ * are summed in arrival order).  Same shapes and limits. */
+int ptyx_patch_scatter_add(void *stream, const float *gpatches, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
+                           const int32_t *crop_pos, const int32_t *idx, int32_t n_idx, int32_t N, float *gobj);
+
 /* obj_zblur → complex_ratio → mirrored_amp → obja_thresh → objp_postiv on (O,Nz,Ny,Nx) f32
  * obja / objp, in place, in CombinedConstraint.forward order (kr/kz filters, which sit between
  * zblur and complex_ratio, are the caller's: call once with only zblur, filter, call again). */

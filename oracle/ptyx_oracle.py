@@ -13,6 +13,10 @@ What it restates (NumPy, written from the equations, not from the reference code
 * loss terms          — ``src/ptyrad/losses.py:36-104, 143-155`` (single / poissn / sparse)
 * gradients           — the hand-derived adjoint of all of the above, i.e. what
                         ``loss.backward()`` (``reconstruction.py:753``) produces by autograd.
+* optional stages     — detector blur ``models.py:375-382`` and object pre-blur ``models.py:267-284``
+                        (torchvision ``gaussian_blur``: f32 1-D kernel exp(-x²/2σ²) on
+                        linspace(-(k-1)/2, (k-1)/2, k), normalised, outer product, reflect padding)
+                        and their transposes.
 
 Parity pinning: the oracle is checked against golden vectors produced by running the
 reference itself in the build container (``tests/golden/make_golden.py``,
@@ -55,6 +59,48 @@ def shift_ramp(shifts: np.ndarray, n: int, cdt=np.complex128) -> np.ndarray:
     sy = shifts[:, 0, None, None].astype(np.float64)
     sx = shifts[:, 1, None, None].astype(np.float64)
     return np.exp(-2j * np.pi * (sy * g[None, :, None] + sx * g[None, None, :])).astype(cdt)
+
+
+def gaussian_kernel1d(ks, sigma):
+    """torchvision _get_gaussian_kernel1d in f32 (the kernel gaussian_blur builds)."""
+    half = (ks - 1) * 0.5
+    x = np.linspace(-half, half, ks, dtype=np.float32)
+    pdf = np.exp(-0.5 * (x / np.float32(sigma)) ** 2).astype(np.float32)
+    return (pdf / pdf.sum(dtype=np.float32)).astype(np.float32)
+
+
+def gaussian_blur(x, sigma, ks=5):
+    """torchvision gaussian_blur over the last two axes (reflect padding), float64."""
+    k = gaussian_kernel1d(ks, sigma)
+    k2 = np.outer(k, k).astype(np.float32).astype(np.float64)
+    h = ks // 2
+    xp = np.pad(np.asarray(x, np.float64), [(0, 0)] * (x.ndim - 2) + [(h, h), (h, h)], mode="reflect")
+    Ny, Nx = x.shape[-2:]
+    out = np.zeros(x.shape, np.float64)
+    for i in range(ks):
+        for j in range(ks):
+            out += k2[i, j] * xp[..., i:i + Ny, j:j + Nx]
+    return out
+
+
+def gaussian_blur_adjoint(g, sigma, ks=5):
+    """Transpose of gaussian_blur: spread each output over its taps, then fold the reflected pad."""
+    k = gaussian_kernel1d(ks, sigma)
+    k2 = np.outer(k, k).astype(np.float32).astype(np.float64)
+    h = ks // 2
+    Ny, Nx = g.shape[-2:]
+    gp = np.zeros(g.shape[:-2] + (Ny + 2 * h, Nx + 2 * h), np.float64)
+    for i in range(ks):
+        for j in range(ks):
+            gp[..., i:i + Ny, j:j + Nx] += k2[i, j] * g
+    for r in range(h):                       # padded row r ↔ row h - r; row h+Ny+r ↔ Ny-2-r
+        gp[..., 2 * h - r, :] += gp[..., r, :]
+        gp[..., h + Ny - 2 - r, :] += gp[..., h + Ny + r, :]
+    gp = gp[..., h:h + Ny, :]
+    for c in range(h):
+        gp[..., :, 2 * h - c] += gp[..., :, c]
+        gp[..., :, h + Nx - 2 - c] += gp[..., :, h + Nx + c]
+    return gp[..., :, h:h + Nx]
 
 
 def get_patches(obja, objp, crop_pos, idx, n):
@@ -194,7 +240,8 @@ def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, 
 
 
 def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batches, loss_params,
-                      shift_probes=True, grad_scale=1.0, cdt=np.complex128):
+                      shift_probes=True, grad_scale=1.0, cdt=np.complex128, detector_blur_std=None,
+                      obj_preblur_std=None):
     """Oracle of ptyx_forward_loss_grad: per-mini-batch losses, gradients accumulated over batches.
 
     batches: list of index arrays (each its own NRMSE normalisation, losses.py:45-47);
@@ -212,11 +259,18 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     for idx in batches:
         idx = np.asarray(idx)
         amp, ph = get_patches(obja, objp, crop_pos, idx, n)
+        if obj_preblur_std:                                        # models.py:275-284
+            amp, ph = gaussian_blur(amp, obj_preblur_std), gaussian_blur(ph, obj_preblur_std)
         probes = get_probes(probe, shifts[idx], shift_probes, cdt)
         cache = forward(amp, ph, probes, H, occu, cdt=cdt)
-        terms, dLdI, dph = loss_terms(cache.dp, meas[idx], ph, occu, loss_params)
+        dp = gaussian_blur(cache.dp, detector_blur_std) if detector_blur_std else cache.dp   # :379-380
+        terms, dLdI, dph = loss_terms(dp, meas[idx], ph, occu, loss_params)
+        if detector_blur_std:
+            dLdI = gaussian_blur_adjoint(dLdI, detector_blur_std)
         dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], H, occu,
                                          shift_probes, cdt)
+        if obj_preblur_std:
+            dA, dP = gaussian_blur_adjoint(dA, obj_preblur_std), gaussian_blur_adjoint(dP, obj_preblur_std)
         for i, s in enumerate(idx):
             cy, cx = int(crop_pos[s, 0]), int(crop_pos[s, 1])
             g_obja[:, :, cy:cy + n, cx:cx + n] += grad_scale * dA[i]
@@ -224,17 +278,21 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
             g_shifts[s] += grad_scale * dshift[i]
         g_probe += grad_scale * dprobe
         all_terms.append(terms)
-        dps.append(cache.dp)
+        dps.append(dp)
     grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts)
     return np.array(all_terms), dps, grads
 
 
-def forward_dp(obja, objp, probe, shifts, crop_pos, H, occu, idx, shift_probes=True, cdt=np.complex128):
+def forward_dp(obja, objp, probe, shifts, crop_pos, H, occu, idx, shift_probes=True, cdt=np.complex128,
+               detector_blur_std=None, obj_preblur_std=None):
     """Oracle of ptyx_forward (PtychoAD.forward, models.py:422-436): (B,N,N) dp."""
     n = probe.shape[-1]
     amp, ph = get_patches(obja, objp, crop_pos, np.asarray(idx), n)
+    if obj_preblur_std:
+        amp, ph = gaussian_blur(amp, obj_preblur_std), gaussian_blur(ph, obj_preblur_std)
     probes = get_probes(probe, shifts[np.asarray(idx)], shift_probes, cdt)
-    return forward(amp, ph, probes, H, occu, cdt=cdt).dp
+    dp = forward(amp, ph, probes, H, occu, cdt=cdt).dp
+    return gaussian_blur(dp, detector_blur_std) if detector_blur_std else dp
 
 
 def adam_step(params, grads, state, lrs, t, betas=(0.9, 0.999), eps=1e-8):

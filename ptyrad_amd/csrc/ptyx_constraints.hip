@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <string>
 
 #include "ptyx.h"
 #include "ptyx_abi.hpp"
@@ -92,6 +93,62 @@ extern "C" int ptyx_obj_rblur(void* stream, const float* in, float* out, int32_t
   hipLaunchKernelGGL(cons::k_rblur, dim3((Nx + cons::kTX - 1) / cons::kTX, (Ny + cons::kTY - 1) / cons::kTY, n_planes),
                      dim3(256), 0, st, in, out, Ny, Nx, t);
   return abi::launch_status("k_rblur launch");
+}
+
+extern "C" int ptyx_blur_adjoint(void* stream, const float* in, float* out, int32_t n_planes, int32_t Ny,
+                                 int32_t Nx, int32_t kernel_size, float sigma) {
+  abi::clear_error();
+  if (n_planes < 0 || Ny <= 0 || Nx <= 0) return abi::fail(PTYX_EINVAL, "blur_adjoint: bad shape");
+  if (kernel_size < 1 || kernel_size % 2 == 0 || kernel_size / 2 > kMaxHalf)
+    return abi::fail(PTYX_EUNSUPPORTED, "blur_adjoint: kernel_size must be odd and <= 15");
+  if (!(sigma > 0.f)) return abi::fail(PTYX_EINVAL, "blur_adjoint: sigma must be > 0");
+  if (kernel_size / 2 >= Ny || kernel_size / 2 >= Nx)
+    return abi::fail(PTYX_EINVAL, "blur_adjoint: reflect padding needs kernel_size/2 < Ny, Nx");
+  if (n_planes == 0) return PTYX_OK;
+  if (!in || !out || in == out) return abi::fail(PTYX_EINVAL, "blur_adjoint: in / out null or aliased");
+  if (n_planes > 65535) return abi::fail(PTYX_EUNSUPPORTED, "blur_adjoint: at most 65535 planes per call");
+  const cons::Taps t = torchvision_taps(kernel_size, sigma);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(cons::k_rblur_adj, dim3((Nx + 63) / 64, (Ny + 3) / 4, n_planes), dim3(256), 0, st, in, out, Ny,
+                     Nx, t);
+  return abi::launch_status("k_rblur_adj launch");
+}
+
+namespace {
+int patch_args(const char* what, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx, const int32_t* crop_pos,
+               const int32_t* idx, int32_t n_idx, int32_t N, const void* a, const void* b) {
+  if (O <= 0 || Nz <= 0 || Ny <= 0 || Nx <= 0 || N <= 0 || n_idx < 0)
+    return abi::fail(PTYX_EINVAL, std::string(what) + ": bad shape");
+  if (N > Ny || N > Nx) return abi::fail(PTYX_EINVAL, std::string(what) + ": patch larger than the object");
+  if (n_idx > 65535 || (long long)O * Nz > 65535)
+    return abi::fail(PTYX_EUNSUPPORTED, std::string(what) + ": at most 65535 patches and O*Nz planes per call");
+  if (n_idx && (!crop_pos || !idx || !a || !b)) return abi::fail(PTYX_EINVAL, std::string(what) + ": null pointer");
+  return PTYX_OK;
+}
+}  // namespace
+
+extern "C" int ptyx_patch_gather(void* stream, const float* obj, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
+                                 const int32_t* crop_pos, const int32_t* idx, int32_t n_idx, int32_t N,
+                                 float* patches) {
+  abi::clear_error();
+  if (int rc = patch_args("patch_gather", O, Nz, Ny, Nx, crop_pos, idx, n_idx, N, obj, patches)) return rc;
+  if (n_idx == 0) return PTYX_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(cons::k_patch_gather, dim3((N * N + 255) / 256, n_idx, O * Nz), dim3(256), 0, st, obj, Ny, Nx,
+                     crop_pos, idx, n_idx, N, patches);
+  return abi::launch_status("k_patch_gather launch");
+}
+
+extern "C" int ptyx_patch_scatter_add(void* stream, const float* gpatches, int32_t O, int32_t Nz, int32_t Ny,
+                                      int32_t Nx, const int32_t* crop_pos, const int32_t* idx, int32_t n_idx,
+                                      int32_t N, float* gobj) {
+  abi::clear_error();
+  if (int rc = patch_args("patch_scatter_add", O, Nz, Ny, Nx, crop_pos, idx, n_idx, N, gpatches, gobj)) return rc;
+  if (n_idx == 0) return PTYX_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(cons::k_patch_scatter, dim3((N * N + 255) / 256, n_idx, O * Nz), dim3(256), 0, st, gpatches,
+                     Ny, Nx, crop_pos, idx, n_idx, N, gobj);
+  return abi::launch_status("k_patch_scatter launch");
 }
 
 extern "C" int ptyx_obj_constrain(void* stream, float* obja, float* objp, int32_t O, int32_t Nz, int32_t Ny,

@@ -77,6 +77,97 @@ __global__ __launch_bounds__(256) void k_rblur(const float* __restrict__ in, flo
   }
 }
 
+// ------------------------------------------------------------------ optional forward stages
+// (detector_blur_std models.py:379-380, obj_preblur_std :275-284)
+//
+// k_rblur_adj   exact transpose of k_rblur (reflect-padded separable Gaussian): the backward of
+//               gaussian_blur.  Output pixel u collects the input pixels s whose padded
+//               neighbourhood reads u at tap t: s = u - t + h (interior), s = -u - t + h (top /
+//               left reflection, u > 0) and s = 2(n-1) - u - t + h (bottom / right, u < n-1).
+//               Gather form, fixed order (deterministic, no atomics); one thread per output.
+// k_patch_gather   (O,Nz,Ny,Nx) plane → (O,Nz,B,N,N) patch stack at crop_pos[idx[b]]
+//               (get_obj_ROI, models.py:251-265); lanes along x, one 256-B row segment per wave.
+// k_patch_scatter  the transpose: gobj[crop + (y, x)] += gpatch, f32 atomics (overlapping
+//               patches; summation order is arrival order).
+__device__ __forceinline__ int blur_sources(int u, int t, int h, int n, int* s) {
+  int k = 0;
+  int c = u - t + h;
+  if (c >= 0 && c < n) s[k++] = c;
+  if (u > 0) {
+    c = -u - t + h;
+    if (c >= 0 && c < n) s[k++] = c;
+  }
+  if (u < n - 1) {
+    c = 2 * (n - 1) - u - t + h;
+    if (c >= 0 && c < n) s[k++] = c;
+  }
+  return k;
+}
+
+// grid (ceil(Nx/64), ceil(Ny/4), planes); block 256 = 64 x 4
+__global__ __launch_bounds__(256) void k_rblur_adj(const float* __restrict__ g, float* __restrict__ out, int Ny,
+                                                   int Nx, Taps t) {
+  const int v = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int u = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (u >= Ny || v >= Nx) return;
+  const size_t plane = (size_t)blockIdx.z * Ny * Nx;
+  const int h = t.half;
+  int xs[3 * kMaxTaps];
+  float xw[3 * kMaxTaps];
+  int nx = 0;
+  for (int j = 0; j <= 2 * h; ++j) {
+    int s[3];
+    const int k = blur_sources(v, j, h, Nx, s);
+    for (int q = 0; q < k; ++q) {
+      xs[nx] = s[q];
+      xw[nx] = t.w[j];
+      ++nx;
+    }
+  }
+  float acc = 0.f;
+  for (int i = 0; i <= 2 * h; ++i) {
+    int s[3];
+    const int k = blur_sources(u, i, h, Ny, s);
+    for (int q = 0; q < k; ++q) {
+      const float* row = g + plane + (size_t)s[q] * Nx;
+      float r = 0.f;
+      for (int e = 0; e < nx; ++e) r = fmaf(xw[e], row[xs[e]], r);
+      acc = fmaf(t.w[i], r, acc);
+    }
+  }
+  out[plane + (size_t)u * Nx + v] = acc;
+}
+
+// grid (ceil(N*N/256), B, O*Nz); block 256.  Out-of-object windows read / write nothing.
+__global__ __launch_bounds__(256) void k_patch_gather(const float* __restrict__ obj, int Ny, int Nx,
+                                                      const int* __restrict__ crop_pos, const int* __restrict__ idx,
+                                                      int B, int N, float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= N * N) return;
+  const int b = blockIdx.y, oz = blockIdx.z;
+  const int y = e / N, x = e - y * N;
+  const int s = idx[b];
+  const int cy = crop_pos[2 * s], cx = crop_pos[2 * s + 1];
+  float val = 0.f;
+  if (cy >= 0 && cx >= 0 && cy + N <= Ny && cx + N <= Nx)
+    val = obj[(size_t)oz * Ny * Nx + (size_t)(cy + y) * Nx + (cx + x)];
+  out[((size_t)oz * B + b) * N * N + e] = val;
+}
+
+__global__ __launch_bounds__(256) void k_patch_scatter(const float* __restrict__ gpatch, int Ny, int Nx,
+                                                       const int* __restrict__ crop_pos, const int* __restrict__ idx,
+                                                       int B, int N, float* __restrict__ gobj) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= N * N) return;
+  const int b = blockIdx.y, oz = blockIdx.z;
+  const int y = e / N, x = e - y * N;
+  const int s = idx[b];
+  const int cy = crop_pos[2 * s], cx = crop_pos[2 * s + 1];
+  if (cy < 0 || cx < 0 || cy + N > Ny || cx + N > Nx) return;
+  unsafeAtomicAdd(gobj + (size_t)oz * Ny * Nx + (size_t)(cy + y) * Nx + (cx + x),
+                  gpatch[((size_t)oz * B + b) * N * N + e]);
+}
+
 // ------------------------------------------------------------------ object column pass
 struct ObjCfg {
   int O, Nz, Ny, Nx;

@@ -15,19 +15,22 @@ from .engine import LOSS_TERM_NAMES, LossConfig, batch_offsets
 
 
 class _FusedLoss(torch.autograd.Function):
-    """Σ_m loss_m over mini-batches; backward = cached engine gradients × grad_output."""
+    """Σ_m loss_m over mini-batches; backward = cached engine gradients × grad_output.
+
+    ``plan`` / ``base`` name the geometry (the model's plan, or a pre-blur patch-stack plan)."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, model, idx_t, off_t, cfg):
+    def forward(ctx, obja, objp, probe_rv, shifts, plan, base, idx_t, off_t, cfg, shift_probes):
         want = {"obja": obja.requires_grad, "objp": objp.requires_grad, "probe": probe_rv.requires_grad,
-                "shifts": shifts.requires_grad and model.shift_probes}
+                "shifts": shifts.requires_grad and shift_probes}
         grads = {}
         for k, p in (("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts)):
             if want[k]:
                 grads[k] = torch.zeros_like(p)
-        terms = model.plan.forward_loss_grad(model._engine_tensors(), idx_t, off_t, cfg, grads, grad_scale=1.0)
+        t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach()}
+        t.update(base)
+        terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0)
         ctx.grads = grads
-        ctx.shift_req = shifts.requires_grad
         total = terms.sum()
         ctx.mark_non_differentiable(terms)
         return total, terms
@@ -39,7 +42,7 @@ class _FusedLoss(torch.autograd.Function):
             g = ctx.grads.get(k)
             out.append(None if g is None else g * g_total)
         ctx.grads = None
-        return out[0], out[1], out[2], out[3], None, None, None, None
+        return out[0], out[1], out[2], out[3], None, None, None, None, None, None
 
 
 class CombinedLoss(torch.nn.Module):
@@ -104,16 +107,63 @@ class CombinedLoss(torch.nn.Module):
         Returns (Σ_m total_m as a differentiable scalar, terms (n_batches, 5) tensor).
         ``(loss / grad_accumulation).backward()`` then leaves exactly the reference's accumulated
         gradients (reconstruction.py:741-760) in ``.grad``.
+
+        Optional stages (ptyrad_amd/stages.py): with ``obj_preblur_std`` the engine runs on the
+        pre-blurred patch stack (groups of ≤ PREBLUR_GROUP patterns, split at mini-batch
+        boundaries); with ``detector_blur_std`` the loss sees the blurred dp, so each mini-batch
+        runs HIP forward → HIP blur → this module's loss terms → HIP adjoints.
         """
-        cfg = LossConfig.from_loss_params(self.loss_params)
         flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
         model._check_indices(flat)
         dev = model.opt_obja.device
+        if getattr(model, "detector_blur", False):
+            return self._per_batch(model, batches)
+        cfg = LossConfig.from_loss_params(self.loss_params)
+        if getattr(model, "preblur", False):
+            return self._preblur_fused(model, batches, cfg)
         idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
         off_t = torch.as_tensor(batch_offsets(batches)).to(dev, non_blocking=True)
         total, terms = _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe,
-                                        model.opt_probe_pos_shifts, model, idx_t, off_t, cfg)
+                                        model.opt_probe_pos_shifts, model.plan, model._base(), idx_t, off_t, cfg,
+                                        model.shift_probes)
         return total, terms
+
+    PREBLUR_GROUP = 8192
+
+    def _preblur_fused(self, model, batches, cfg):
+        dev = model.opt_obja.device
+        totals, rows, group, n = [], [], [], 0
+
+        def run(group):
+            flat = np.concatenate([np.asarray(b).reshape(-1) for b in group])
+            idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev)
+            off_t = torch.as_tensor(batch_offsets(group)).to(dev, non_blocking=True)
+            A, Ph, sh, plan, base, ar, _ = model._stack_inputs(idx_t, with_meas=True)
+            t, terms = _FusedLoss.apply(A, Ph, model.opt_probe, sh, plan, base, ar, off_t, cfg, model.shift_probes)
+            totals.append(t)
+            rows.append(terms)
+
+        for b in batches:
+            nb = len(np.asarray(b).reshape(-1))
+            if group and n + nb > self.PREBLUR_GROUP:
+                run(group)
+                group, n = [], 0
+            group.append(b)
+            n += nb
+        if group:
+            run(group)
+        return sum(totals), torch.cat(rows)
+
+    def _per_batch(self, model, batches):
+        totals, rows = [], []
+        for b in batches:
+            dp = model(b)
+            total, terms = self.forward(dp, model.get_measurements(b), model._current_object_patches,
+                                        model.omode_occu)
+            totals.append(total)
+            rows.append(torch.stack([torch.as_tensor(x, device=dp.device, dtype=torch.float32).detach().reshape(())
+                                     for x in terms]))
+        return sum(totals), torch.stack(rows)
 
 
 __all__ = ["CombinedLoss", "LOSS_TERM_NAMES"]

@@ -13,9 +13,13 @@ Two ways to get gradients:
 * fused     — ``ptyrad_amd.losses.CombinedLoss.fused(model, batches)`` runs forward + loss +
               adjoint in one engine call (ptyx_forward_loss_grad), the hot path.
 
-Out of scope on the HIP path (raise NotImplementedError when enabled): per-position / optimised tilts, optimised-dz
-propagators (models.py:339-356), detector blur (:379-380), object pre-blur (:275-284),
-on-the-fly measurement padding / resampling (:392-409).
+Optional stages (ptyrad_amd/stages.py): detector blur (models.py:379-380) and
+object pre-blur (:275-284) run as HIP kernels around the engine; pre-blurred patches are handed to
+the engine as a patch-stack object (one (N, N) window per position, crop_pos (b·N, 0)).
+
+Out of scope on the HIP path (raise NotImplementedError when enabled): per-position / optimised
+tilts, optimised-dz propagators (models.py:339-356), on-the-fly measurement padding / resampling
+(:392-409).
 """
 from __future__ import annotations
 
@@ -24,39 +28,46 @@ import torch
 import torch.nn as nn
 
 from .engine import Plan
+from .stages import BlurredPatches, GaussianBlur, stack_crop_pos
 
 _PARAM_NAMES = ("obja", "objp", "obj_tilts", "slice_thickness", "probe", "probe_pos_shifts")
 
 
 class _EngineForward(torch.autograd.Function):
-    """dp = PtychoAD.forward(idx); backward = ptyx_adjoint_dldi (autograd of models.py:422-436)."""
+    """dp = PtychoAD.forward(idx); backward = ptyx_adjoint_dldi (autograd of models.py:422-436).
+
+    ``plan`` / ``base`` (H, occu, crop_pos) name the geometry: the model's own plan, or a patch-
+    stack plan when the object patches are pre-blurred (stages.BlurredPatches)."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, model, idx_t):
-        ctx.model = model
-        ctx.save_for_backward(idx_t)
+    def forward(ctx, obja, objp, probe_rv, shifts, plan, base, idx_t, shift_probes):
+        ctx.plan, ctx.base, ctx.shift_probes = plan, base, shift_probes
+        ctx.save_for_backward(obja, objp, probe_rv, shifts, idx_t)
         with torch.no_grad():
-            return model.plan.forward(model._engine_tensors(), idx_t)
+            return plan.forward(_tensors(obja, objp, probe_rv, shifts, base), idx_t)
 
     @staticmethod
     def backward(ctx, grad_dp):
-        (idx_t,) = ctx.saved_tensors
-        m = ctx.model
+        obja, objp, probe_rv, shifts, idx_t = ctx.saved_tensors
         want = ctx.needs_input_grad
         grads = {}
         outs = [None] * 4
-        for i, (k, p) in enumerate((("obja", m.opt_obja), ("objp", m.opt_objp),
-                                    ("probe", m.opt_probe), ("shifts", m.opt_probe_pos_shifts))):
+        for i, (k, p) in enumerate((("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts))):
             if want[i]:
                 outs[i] = torch.zeros_like(p)
                 grads[k] = outs[i]
-        if not m.shift_probes:
+        if not ctx.shift_probes:
             grads.pop("shifts", None)
-            if want[3]:
-                outs[3] = torch.zeros_like(m.opt_probe_pos_shifts)
         if grads:
-            m.plan.adjoint_dldi(m._engine_tensors(), idx_t, grad_dp.contiguous().float(), grads)
-        return outs[0], outs[1], outs[2], outs[3], None, None
+            ctx.plan.adjoint_dldi(_tensors(obja, objp, probe_rv, shifts, ctx.base), idx_t,
+                                  grad_dp.contiguous().float(), grads)
+        return outs[0], outs[1], outs[2], outs[3], None, None, None, None
+
+
+def _tensors(obja, objp, probe_rv, shifts, base):
+    t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach()}
+    t.update(base)
+    return t
 
 
 class PtychoHIP(nn.Module):
@@ -69,8 +80,11 @@ class PtychoHIP(nn.Module):
             self.verbose = verbose
             self.detector_blur_std = model_params.get("detector_blur_std")
             self.obj_preblur_std = model_params.get("obj_preblur_std")
-            if self.detector_blur_std not in (None, 0) or self.obj_preblur_std not in (None, 0):
-                raise NotImplementedError("detector_blur_std / obj_preblur_std are not on the HIP path")
+            for k in ("detector_blur_std", "obj_preblur_std"):
+                v = getattr(self, k)
+                if v not in (None, 0) and not float(v) > 0:
+                    raise ValueError(f"{k} must be None, 0 or > 0")
+            self._stack_plans = {}
             if init_variables.get("on_the_fly_meas_padded") is not None or \
                     init_variables.get("on_the_fly_meas_scale_factors") is not None:
                 raise NotImplementedError("on-the-fly measurement padding/resampling is not on the HIP path")
@@ -140,9 +154,9 @@ class PtychoHIP(nn.Module):
             n_scans = self.crop_pos.shape[0]
             # plan workspace scales with the largest call (per-pattern intensities of mixed-state
             # calls are N² f32 each); larger calls are split at mini-batch boundaries by Plan
+            self.meas_f16 = meas_dtype == torch.float16
             self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or min(n_scans, 65536),
-                             shift_probes=self.shift_probes, meas_f16=(meas_dtype == torch.float16),
-                             device=device)
+                             shift_probes=self.shift_probes, meas_f16=self.meas_f16, device=device)
 
     # ------------------------------------------------------------------ reference API
     def get_complex_probe_view(self):
@@ -186,14 +200,64 @@ class PtychoHIP(nn.Module):
         return (self.H * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx))))[0].contiguous()
 
     def _engine_tensors(self):
-        return {"obja": self.opt_obja.detach(), "objp": self.opt_objp.detach(),
-                "probe": self.opt_probe.detach(), "shifts": self.opt_probe_pos_shifts.detach(),
-                "H": self.H_eff, "occu": self.omode_occu, "crop_pos": self.crop_pos,
-                "meas": self.measurements}
+        return _tensors(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts, self._base())
+
+    def _base(self, crop_pos=None, meas=None, stack=False):
+        return {"H": self.H_eff, "occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
+                "meas": self.measurements if (meas is None and not stack) else meas}
+
+    # ------------------------------------------------------------------ object pre-blur (stages.py)
+    @property
+    def preblur(self):
+        return self.obj_preblur_std not in (None, 0)
+
+    @property
+    def detector_blur(self):
+        return self.detector_blur_std not in (None, 0)
+
+    def _stack_plan(self, B):
+        """Plan for a (O, Nz, B·N, N) patch-stack object (pre-blurred patches of B positions)."""
+        plan = self._stack_plans.get(B)
+        if plan is None:
+            if len(self._stack_plans) >= 4:
+                old = self._stack_plans.pop(next(iter(self._stack_plans)))
+                old.close()
+            O, Nz = self.opt_obja.shape[:2]
+            P, N = self.opt_probe.shape[:2]
+            plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes, meas_f16=self.meas_f16,
+                        device=self.opt_obja.device)
+            self._stack_plans[B] = plan
+        return plan
+
+    def _blurred_patches(self, idx_t):
+        """(O,Nz,B,N,N) pre-blurred amplitude and phase patches (models.py:267-284), differentiable."""
+        N = self.opt_probe.shape[1]
+        std = float(self.obj_preblur_std)
+        return (BlurredPatches.apply(self.opt_obja, self.crop_pos, idx_t, N, std),
+                BlurredPatches.apply(self.opt_objp, self.crop_pos, idx_t, N, std))
+
+    def _stack_inputs(self, idx_t, with_meas=False):
+        """Engine inputs on the patch stack: (obja, objp, shifts, plan, base, idx, patches)."""
+        B = int(idx_t.numel())
+        N = self.opt_probe.shape[1]
+        A, Ph = self._blurred_patches(idx_t)
+        O, Nz = A.shape[:2]
+        il = idx_t.long()
+        sh = self.opt_probe_pos_shifts[il]
+        meas = self.measurements[il].contiguous() if with_meas else None
+        base = self._base(stack_crop_pos(B, N, idx_t.device), meas, stack=True)
+        ar = torch.arange(B, dtype=torch.int32, device=idx_t.device)
+        return (A.reshape(O, Nz, B * N, N), Ph.reshape(O, Nz, B * N, N), sh, self._stack_plan(B), base, ar,
+                (A, Ph))
 
     def get_obj_patches(self, indices):
-        """models.py:251-273 (torch gather, for losses that need the patches themselves)."""
-        idx = torch.as_tensor(self._check_indices(indices), device=self.opt_obja.device, dtype=torch.long)
+        """models.py:251-284: (B,O,Nz,N,N,2) amplitude/phase patches (pre-blurred when enabled)."""
+        idx = self._check_indices(indices)
+        if self.preblur:
+            idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device)
+            A, Ph = self._blurred_patches(idx_t)
+            return torch.stack([A, Ph], dim=-1).permute(2, 0, 1, 3, 4, 5)
+        idx = torch.as_tensor(idx, device=self.opt_obja.device, dtype=torch.long)
         N = self.opt_probe.shape[1]
         r = torch.arange(N, device=self.opt_obja.device)
         cp = self.crop_pos[idx].long()
@@ -243,10 +307,17 @@ class PtychoHIP(nn.Module):
         """models.py:422-436: dp_fwd (B,N,N) f32 from the HIP engine, differentiable."""
         idx = self._check_indices(indices)
         idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device, non_blocking=True)
-        dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
-                                  self, idx_t)
-        # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
-        self._current_object_patches = self.get_obj_patches(idx)
+        if self.preblur:
+            A, Ph, sh, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
+            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, plan, base, ar, self.shift_probes)
+            self._current_object_patches = torch.stack([pa, pp], dim=-1).permute(2, 0, 1, 3, 4, 5)
+        else:
+            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
+                                      self.plan, self._base(meas=None, stack=True), idx_t, self.shift_probes)
+            # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
+            self._current_object_patches = self.get_obj_patches(idx)
+        if self.detector_blur:                      # get_forward_meas, models.py:375-382
+            dp = GaussianBlur.apply(dp, float(self.detector_blur_std))
         return dp
 
 

@@ -29,6 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
+import refimport  # noqa: E402
 from refimport import import_reference  # noqa: E402
 from ptyrad_amd import synthetic as syn  # noqa: E402
 
@@ -44,6 +45,9 @@ DEFAULT_LOSS = {
 }
 
 
+BLUR = {"detector_blur_std": None, "obj_preblur_std": None}   # set by --blur-only cases
+
+
 def model_params(shift_lr=5e-4):
     up = {
         "obja": {"start_iter": 1, "lr": 5e-4},
@@ -53,7 +57,8 @@ def model_params(shift_lr=5e-4):
         "probe": {"start_iter": 1, "lr": 1e-4},
         "probe_pos_shifts": {"start_iter": 1 if shift_lr else None, "lr": shift_lr},
     }
-    return {"detector_blur_std": None, "obj_preblur_std": None, "update_params": up,
+    return {"detector_blur_std": BLUR["detector_blur_std"], "obj_preblur_std": BLUR["obj_preblur_std"],
+            "update_params": up,
             "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
 
 
@@ -156,6 +161,9 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
         out.update(H_untilted=model.H.numpy(), obj_tilts=np.asarray(tilts, np.float32).reshape(1, 2),
                    slice_thickness=np.float32(model.opt_slice_thickness.item()), dx=np.float32(model.dx.item()),
                    lambd=np.float32(model.lambd.item()))
+    for k, v in BLUR.items():
+        if v:
+            out[k] = np.float32(v)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
@@ -216,6 +224,17 @@ if __name__ == "__main__":
     torch.set_num_threads(4)
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--blur-only":
+        # detector blur (models.py:379-380) / object pre-blur (:275-284) call torchvision's
+        # gaussian_blur, absent here: the reference runs with refimport.tv_gaussian_blur in its place
+        models.gaussian_blur = refimport.tv_gaussian_blur
+        BLUR.update(detector_blur_std=1.0, obj_preblur_std=None)
+        run_case("n32_p2o1z2_detblur", 32, 2, 1, 2, 4, 4, 6, seed=31)
+        BLUR.update(detector_blur_std=None, obj_preblur_std=0.8)
+        run_case("n32_p1o2z1_preblur", 32, 1, 2, 1, 4, 4, 5, seed=32)
+        BLUR.update(detector_blur_std=0.7, obj_preblur_std=1.2)
+        run_case("n64_p2o1z1_bothblur", 64, 2, 1, 1, 3, 3, 6, seed=33)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
         constrained_trajectory()

@@ -28,6 +28,25 @@ def _raiser(what):
     return f
 
 
+def tv_gaussian_blur(img, kernel_size, sigma):
+    """torchvision.transforms.functional.gaussian_blur restated from its published algorithm
+    (torchvision is absent here): f32 1-D kernel exp(-x²/2σ²) on linspace(-(k-1)/2, (k-1)/2, k),
+    normalised; 2-D kernel = outer product; reflect padding k//2; per-plane conv2d.  Installed
+    into ptyrad.models only for the blur fixtures (make_golden.py --blur-only)."""
+    import torch
+    import torch.nn.functional as F
+    ks = kernel_size if isinstance(kernel_size, int) else kernel_size[0]
+    s = float(sigma if not isinstance(sigma, (list, tuple)) else sigma[0])
+    half = (ks - 1) * 0.5
+    x = torch.linspace(-half, half, ks, dtype=img.dtype, device=img.device)
+    pdf = torch.exp(-0.5 * (x / s).pow(2))
+    k1 = pdf / pdf.sum()
+    k2 = torch.mm(k1[:, None], k1[None, :])
+    shape = img.shape
+    y = F.pad(img.reshape(-1, 1, shape[-2], shape[-1]), [ks // 2] * 4, mode="reflect")
+    return F.conv2d(y, k2[None, None]).reshape(shape)
+
+
 def import_reference():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     sys.dont_write_bytecode = True

@@ -63,3 +63,18 @@ def test_constraint_entry_points_validate_without_gpu():
     assert lib.ptyx_obj_constrain(None, ctypes.c_void_p(8), ctypes.c_void_p(8), 1, 2, 4, 4, ctypes.byref(c),
                                   None) == _lib.PTYX_EUNSUPPORTED
     assert b"odd" in lib.ptyx_last_error()
+
+
+def test_stage_entry_points_validate_without_gpu():
+    lib = _lib.load()
+    vp = ctypes.c_void_p(8)
+    assert lib.ptyx_blur_adjoint(None, vp, vp, 1, 32, 32, 4, 1.0) == _lib.PTYX_EUNSUPPORTED     # even kernel
+    assert lib.ptyx_blur_adjoint(None, vp, vp, 1, 2, 32, 5, 1.0) == _lib.PTYX_EINVAL            # reflect pad
+    assert lib.ptyx_blur_adjoint(None, vp, vp, 1, 32, 32, 5, 0.0) == _lib.PTYX_EINVAL           # sigma
+    assert lib.ptyx_blur_adjoint(None, vp, vp, 0, 32, 32, 5, 1.0) == _lib.PTYX_OK               # empty
+    assert lib.ptyx_patch_gather(None, vp, 1, 1, 16, 16, vp, vp, 2, 32, vp) == _lib.PTYX_EINVAL  # N > object
+    assert b"larger than the object" in lib.ptyx_last_error()
+    assert lib.ptyx_patch_gather(None, vp, 1, 1, 64, 64, vp, vp, 70000, 32, vp) == _lib.PTYX_EUNSUPPORTED
+    assert lib.ptyx_patch_scatter_add(None, vp, 1, 1, 64, 64, None, vp, 3, 32, vp) == _lib.PTYX_EINVAL
+    assert lib.ptyx_patch_scatter_add(None, vp, 1, 1, 64, 64, None, None, 0, 32, None) == _lib.PTYX_OK
+

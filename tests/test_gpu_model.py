@@ -116,8 +116,8 @@ def test_invalid_indices_raise():
     model = PtychoHIP(iv, model_params(lrs), device=device, verbose=False)
     with pytest.raises(IndexError):
         model(np.array([0, 999]))
-    with pytest.raises(NotImplementedError):
-        PtychoHIP(iv, {**model_params(lrs), "detector_blur_std": 1.0}, device=device, verbose=False)
+    with pytest.raises(ValueError):
+        PtychoHIP(iv, {**model_params(lrs), "detector_blur_std": -1.0}, device=device, verbose=False)
 
 
 def test_fixed_global_tilt_propagator():

@@ -36,12 +36,27 @@ def load_case(path):
     return d
 
 
+def blur_kw(d):
+    """Optional-stage options a fixture was made with (make_golden.py --blur-only)."""
+    return {k: float(d[k]) for k in ("detector_blur_std", "obj_preblur_std") if k in d}
+
+
+def test_blur_adjoint_is_transpose():
+    """gaussian_blur_adjoint = the transpose of gaussian_blur (explicit matrix, reflect edges)."""
+    rng = np.random.default_rng(5)
+    shape = (7, 9)
+    n = shape[0] * shape[1]
+    M = np.stack([orc.gaussian_blur(np.eye(n)[k].reshape(shape), 0.9).ravel() for k in range(n)], 1)
+    y = rng.standard_normal(n)
+    np.testing.assert_allclose(orc.gaussian_blur_adjoint(y.reshape(shape), 0.9).ravel(), M.T @ y, atol=1e-14)
+
+
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(p)[:-4] for p in CASES])
 def test_oracle_matches_reference(path):
     d = load_case(path)
     terms, dps, g = orc.forward_loss_grad(
         d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"],
-        d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]))
+        d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]), **blur_kw(d))
     dp = dps[0]
     if "dp" in d:
         assert rel(dp, d["dp"]) < 2e-6
