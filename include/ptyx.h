@@ -45,6 +45,8 @@ extern "C" {
 /* dims.flags */
 #define PTYX_SHIFT_PROBES 1u /* sub-px Fourier-shifted probes (PtychoAD.shift_probes, models.py:120) */
 #define PTYX_MEAS_F16 2u     /* measurements stored as IEEE half (fp16 storage / fp32 accumulate)   */
+#define PTYX_PROP_GRAD 4u    /* plan can return dL/dH (optimised tilts / slice thickness, §8f row 4):
+                                (Nz-1)·N² extra scratch and an N² slab per persistent workgroup */
 
 typedef struct ptyx_plan ptyx_plan;
 
@@ -56,7 +58,7 @@ typedef struct ptyx_dims {
   int32_t Ny, Nx;       /* object extent                                                   */
   int32_t n_scans;      /* number of probe positions (crop_pos.shape[0])                   */
   int32_t max_patterns; /* largest number of patterns per call (sizes the workspace)       */
-  uint32_t flags;       /* PTYX_SHIFT_PROBES | PTYX_MEAS_F16                               */
+  uint32_t flags;       /* PTYX_SHIFT_PROBES | PTYX_MEAS_F16 | PTYX_PROP_GRAD              */
 } ptyx_dims;
 
 typedef struct ptyx_inputs {
@@ -75,6 +77,10 @@ typedef struct ptyx_grads {
   float *d_objp;   /* (O,Nz,Ny,Nx)  += dL/dobjp                 or NULL */
   float *d_probe;  /* (P,N,N,2)     += dL/dRe + i dL/dIm probe  or NULL */
   float *d_shifts; /* (n_scans,2)   += dL/dshift                or NULL */
+  float *d_H;      /* (N,N,2)       += dL/dRe + i dL/dIm H      or NULL: the propagator gradient
+                      behind optimised obj_tilts / slice_thickness (get_propagators cases 1, 2A, 3,
+                      src/ptyrad/models.py:339-356).  Needs a PTYX_PROP_GRAD plan; runs the general
+                      (two-pass) engine; Nz = 1 adds nothing (H is unused). */
 } ptyx_grads;
 
 /* CombinedLoss terms on the hot path (params/loss_params.py defaults in brackets). */

@@ -133,6 +133,7 @@ class ForwardCache:
     psis: list             # psis[n] = wave entering slice n, (B,P,Om,N,N)
     Psi: np.ndarray        # (B,P,Om,N,N) far field, fftshifted
     dp: np.ndarray         # (B,N,N)
+    X: list = None         # X[n] = F(ψⁿ ⊙ Oⁿ), n < Nz-1 (ψ^{n+1} = F⁻¹(H Xⁿ))
 
 
 def forward(amp, ph, probes, H, occu, eps=1e-10, cdt=np.complex128) -> ForwardCache:
@@ -141,17 +142,18 @@ def forward(amp, ph, probes, H, occu, eps=1e-10, cdt=np.complex128) -> ForwardCa
     Nz = Ocplx.shape[2]
     psi = probes[:, :, None].astype(cdt)                               # (B,P,1,N,N)  (forward.py:57)
     psi = np.broadcast_to(psi, probes.shape[:2] + (Ocplx.shape[1],) + probes.shape[2:]).copy()
-    psis = []
+    psis, X = [], []
     Hc = H.astype(cdt)
     for n in range(Nz - 1):                                            # (forward.py:60-63)
         psis.append(psi)
-        psi = _ifft2(Hc * _fft2(psi * Ocplx[:, None, :, n])).astype(cdt)
+        X.append(_fft2(psi * Ocplx[:, None, :, n]).astype(cdt))
+        psi = _ifft2(Hc * X[-1]).astype(cdt)
     psis.append(psi)
     psi_out = psi * Ocplx[:, None, :, Nz - 1]                          # (forward.py:66-67)
     nn = psi_out.shape[-1]
     Psi = np.fft.fftshift(_fft2(psi_out) / nn, axes=(-2, -1)).astype(cdt)   # ortho + fftshift2
     dp = (np.abs(Psi) ** 2 * occu[None, None, :, None, None]).sum(axis=(1, 2)) + eps   # (forward.py:79)
-    return ForwardCache(probes, Ocplx, psis, Psi, dp)
+    return ForwardCache(probes, Ocplx, psis, Psi, dp, X)
 
 
 def loss_terms(dp, meas, ph, occu, lp):
@@ -214,9 +216,12 @@ def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, 
     gPsi = 2.0 * occu[None, None, :, None, None] * cache.Psi * dLdI[:, None, None]
     g = np.fft.ifft2(np.fft.ifftshift(gPsi, axes=(-2, -1)), axes=(-2, -1), norm="ortho").astype(cdt)
     gO = np.zeros((B, Om, Nz, n, n), cdt)
+    dH = np.zeros((n, n), np.complex128)
     for sl in range(Nz - 1, -1, -1):
         if sl < Nz - 1:                                 # adjoint of F^-1 H F is F^-1 conj(H) F
-            g = _ifft2(np.conj(Hc) * _fft2(g)).astype(cdt)
+            G = _fft2(g)
+            dH += (np.conj(cache.X[sl]) * G).sum(axis=(0, 1, 2)) / (n * n)   # dL/dH (real-view convention)
+            g = _ifft2(np.conj(Hc) * G).astype(cdt)
         gO[:, :, sl] = (np.conj(cache.psis[sl]) * g).sum(axis=1)   # Σ_p conj(ψ^n) g
         g = g * np.conj(Oc[:, None, :, sl])
     gPb = g.sum(axis=2)                                 # (B,P,N,N): Σ_o
@@ -236,6 +241,7 @@ def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, 
     else:
         dprobe = gPb.sum(axis=0)
         dshift = np.zeros((B, 2))
+    cache.dH = dH
     return dA, dP, dprobe, dshift
 
 
@@ -255,6 +261,7 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     g_objp = np.zeros(objp.shape, np.float64)
     g_probe = np.zeros(probe.shape, np.complex128)
     g_shifts = np.zeros(shifts.shape, np.float64)
+    g_H = np.zeros(probe.shape[-2:], np.complex128)
     all_terms, dps = [], []
     for idx in batches:
         idx = np.asarray(idx)
@@ -277,10 +284,37 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
             g_objp[:, :, cy:cy + n, cx:cx + n] += grad_scale * dP[i]
             g_shifts[s] += grad_scale * dshift[i]
         g_probe += grad_scale * dprobe
+        g_H += grad_scale * cache.dH
         all_terms.append(terms)
         dps.append(dp)
-    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts)
+    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts, H=g_H)
     return np.array(all_terms), dps, grads
+
+
+def propagator_param_grads(gH, H, dz, tilts, dx, lambd, case):
+    """Chain rule from dL/dH to the optimised slice thickness / global tilts (get_propagators
+    cases 1, 2A, 3, models.py:339-356): dL/dθ = Re Σ conj(gH) ∂H/∂θ, with ∂H/∂θ = i (∂φ/∂θ) H for
+    the H the forward actually used (its phase dz·Kz ≈ 300 rad is rounded in f32, and the
+    constant part dz·k of that phase cancels only against the same H).  Returns (d_dz, d_tilts)."""
+    n = gH.shape[-1]
+    g = (np.arange(-n // 2, n // 2) + 0.5) / n
+    k1 = np.fft.ifftshift(2 * np.pi * g / dx)
+    Ky, Kx = np.meshgrid(k1, k1, indexing="ij")
+    k = 2 * np.pi / lambd
+    Kz = np.sqrt(k ** 2 - Kx ** 2 - Ky ** 2)
+    ty, tx = tilts[0] / 1e3, tilts[1] / 1e3
+    T = Ky * np.tan(ty) + Kx * np.tan(tx)
+    H = np.asarray(H, np.complex128)
+    if case == 1:
+        dHdz = 1j * (Kz + T) * H
+    elif case == 2:
+        dHdz = 1j * T * H
+    else:
+        dHdz = 1j * Kz * H
+    dHty = 1j * dz * Ky / np.cos(ty) ** 2 / 1e3 * H
+    dHtx = 1j * dz * Kx / np.cos(tx) ** 2 / 1e3 * H
+    re = lambda a: float(np.real(np.sum(np.conj(gH) * a)))   # noqa: E731
+    return re(dHdz), np.array([re(dHty), re(dHtx)])
 
 
 def forward_dp(obja, objp, probe, shifts, crop_pos, H, occu, idx, shift_probes=True, cdt=np.complex128,

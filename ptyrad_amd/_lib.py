@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
 PTYX_SHIFT_PROBES = 1
 PTYX_MEAS_F16 = 2
+PTYX_PROP_GRAD = 4
 
 _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 
@@ -50,7 +51,7 @@ class Inputs(ctypes.Structure):
 
 class Grads(ctypes.Structure):
     _fields_ = [("d_obja", ctypes.c_void_p), ("d_objp", ctypes.c_void_p),
-                ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p)]
+                ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p), ("d_H", ctypes.c_void_p)]
 
 
 class LossCfg(ctypes.Structure):

@@ -60,6 +60,8 @@ struct KArgs {
   // k_fused2: pattern → mini-batch table and the per-pattern object-gradient slots
   const int* bid;
   float2* ogscr;
+  // propagator gradient (PTYX_PROP_GRAD): per-workgroup dL/dH slabs; F(ψⁿ⊙Oⁿ) parked after gacc
+  float2* hslab;
 };
 
 // ---------------------------------------------------------------- small helpers

@@ -40,11 +40,12 @@ namespace ptyx {
 // Forward chain for one (pattern, p, o): leaves ψ_out = ψ^{Nz-1} ⊙ O_{Nz-1} in the array.
 // STORE_PSI: store every ψ^n (n = 0..Nz-1, the wave ENTERING slice n) to psi[n·N²].
 // SPARSE: accumulate Σ|φ|^n of every object pixel touched (once per pattern: caller gates).
+// xs (optional): store Xⁿ = F(ψⁿ ⊙ Oⁿ), n = 0..Nz-2, for the propagator gradient.
 template <int N, int NT, bool STORE_PSI, class Arr>
 __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, const float2* tw,
                                               const float2* wy, const float2* wx,
                                               const PatternGeom& g, int p, int o, float2* psi,
-                                              bool sparse, float& sp_acc) {
+                                              bool sparse, float& sp_acc, float2* xs = nullptr) {
   constexpr int N2 = N * N;
   constexpr float inv_n2 = 1.0f / (float)N2;
   auto mul_obj = [&](int n, int y, int x, float2 w) -> float2 {
@@ -85,6 +86,7 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
     fft2d<N, NT, -1, true>(
         arr, tw, [&](int, int, float2 v) { return v; },
         [&](int y, int x, float2& v) {
+          if (STORE_PSI && xs) xs[(size_t)(n - 1) * N2 + y * N + x] = v;
           v = cmul(v, a.H[y * N + x]);
           return true;
         });
@@ -307,8 +309,13 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   float2* psi = scratch_psi<N>(a);
   float2* gacc = psi + (size_t)a.Nz * N2;
   float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
+  // propagator gradient: dL/dH += Σ_{p,o,n<Nz-1} conj(Xⁿ) ⊙ F(g^{n+1}) / N²  (ψ^{n+1} = F⁻¹(H Xⁿ))
+  float2* xs = a.hslab ? gacc + N2 : nullptr;
+  float2* hsl = a.hslab ? a.hslab + (size_t)blockIdx.x * N2 : nullptr;
   if (a.need_probe)
     for (int e = threadIdx.x; e < a.P * N2; e += NT) slab[e] = make_float2(0.f, 0.f);
+  if (hsl)
+    for (int e = threadIdx.x; e < N2; e += NT) hsl[e] = make_float2(0.f, 0.f);
   __syncthreads();
 
   for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
         const float occ = a.occu[o];
         const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
         float dummy = 0.f;
-        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy);
+        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs);
         // far field → g_Ψ = 2 occ Ψ ∂L/∂I  (left in natural FFT order)
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v) { return v; },
@@ -402,7 +409,9 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
           fft2d<N, NT, -1, true>(
               arr, s_tw, [&](int, int, float2 v) { return v; },
               [&](int y, int x, float2& v) {
-                v = cmulc(v, a.H[y * N + x]);
+                const int e = y * N + x;
+                if (hsl) hsl[e] = cadd(hsl[e], cscale(cmulc(v, xs[(size_t)n * N2 + e]), inv_n2));
+                v = cmulc(v, a.H[e]);
                 return true;
               });
           fft2d<N, NT, +1, true>(
@@ -455,6 +464,15 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
 
 #include "ptyx_single.hpp"
 #include "ptyx_fused.hpp"
+
+// d_H += Σ over workgroup propagator-gradient slabs, fixed order.
+__global__ void k_hslab_reduce(const float2* hslab, int nwg, int n2, float2* d_H) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n2) return;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int w = 0; w < nwg; ++w) acc = cadd(acc, hslab[(size_t)w * n2 + e]);
+  d_H[e] = cadd(d_H[e], acc);
+}
 
 // Σ over workgroup slabs, fixed order.
 __global__ void k_slab_reduce(const float2* slab, int nwg, long long per, float2* out) {
@@ -542,6 +560,7 @@ struct ptyx_plan {
   float* Ibuf = nullptr;
   float2* slab = nullptr;
   float2* Gsum = nullptr;
+  float2* hslab = nullptr;    // PTYX_PROP_GRAD: per-workgroup dL/dH slabs
   float2* scratch = nullptr;
   unsigned* sync = nullptr;   // k_fused1/2: dequeue head, error flag, per-batch arrivals
   // k_fused2 (single mode, N <= 128): co-resident grid, per-pattern object-gradient slots
@@ -701,7 +720,9 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->nwg =std::max(d.P, std::min(d.max_patterns, cu * blocks_per_cu(d.N)));
   const size_t N2 = (size_t)d.N * d.N;
   const bool lds = d.N <= 128;
-  pl->scratch_stride = (long long)((lds ? 0 : 2 * N2) + (size_t)d.Nz * N2 + N2);
+  const bool prop_grad = (d.flags & PTYX_PROP_GRAD) && d.Nz > 1;
+  pl->scratch_stride = (long long)((lds ? 0 : 2 * N2) + (size_t)d.Nz * N2 + N2 +
+                                   (prop_grad ? (size_t)(d.Nz - 1) * N2 : 0));
   int rc = PTYX_OK;
   const bool multi = (d.P * d.O) > 1;
   if ((rc = dalloc(pl, &pl->twg, d.N)) || (rc = dalloc(pl, &pl->Fp, d.P * N2)) ||
@@ -710,6 +731,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->Ibuf, multi ? (size_t)d.max_patterns * N2 : 0)) ||
       (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
       (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
+      (rc = dalloc(pl, &pl->hslab, prop_grad ? (size_t)pl->nwg * N2 : 0)) ||
       (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride)) ||
       (rc = dalloc(pl, &pl->sync, ((size_t)d.max_patterns + 2 + 3) / 4 * 4))) {
     free_plan(pl);
@@ -1163,6 +1185,22 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
   return launch_status("ptyx_forward launch");
 }
 
+// propagator gradient: validate the request and point the kernels at the plan's slabs
+static int setup_prop_grad(const ptyx_plan* pl, const ptyx_grads& gz, KArgs& a) {
+  if (!gz.d_H) return PTYX_OK;
+  if (!(pl->d.flags & PTYX_PROP_GRAD)) return fail(PTYX_EINVAL, "d_H needs a plan created with PTYX_PROP_GRAD");
+  a.hslab = pl->hslab;   // null when Nz == 1: H is unused, nothing to add
+  return PTYX_OK;
+}
+
+static int reduce_prop_grad(const ptyx_plan* pl, const KArgs& a, const ptyx_grads& gz, hipStream_t st) {
+  if (!gz.d_H || !a.hslab) return PTYX_OK;
+  const int n2 = pl->d.N * pl->d.N;
+  hipLaunchKernelGGL(k_hslab_reduce, dim3((n2 + 255) / 256), dim3(256), 0, st, pl->hslab, pl->nwg, n2,
+                     reinterpret_cast<float2*>(gz.d_H));
+  return launch_status("k_hslab_reduce launch");
+}
+
 extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
                                       const int32_t* boff, int32_t n_batches, int32_t n_idx,
                                       const ptyx_loss_cfg* cfg, float* loss_terms, float* dp_out,
@@ -1198,6 +1236,8 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.d_objp = gz.d_objp;
   a.d_shifts = gz.d_shifts;
   a.need_probe = gz.d_probe != nullptr;
+  if ((rc = setup_prop_grad(pl, gz, a))) return rc;
+  const bool want_H = a.hslab != nullptr;   // general two-pass engine only
 
   a.w1 = cfg->single_w;
   a.w2 = cfg->poissn_w;
@@ -1208,7 +1248,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     const char* dbg = std::getenv("PTYX_DEBUG_NOWAIT");
     a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
   }
-  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || want_H;
   const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
   // one pass per pattern (k_fused2) when every mini-batch fits the co-resident grid, the call
   // fits the object-gradient slots and exactly one data term is on (its coefficient factors out)
@@ -1228,7 +1268,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
                       n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
                       (cfg->single_on != 0) != (cfg->poissn_on != 0);
   // multislice register engine (k_fused3ms): N = 128, P = O = 1, Nz ≥ 2, f32 DPs
-  const bool fused3ms = any_grad && pl->ms3 && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && !a.meas_f16 &&
+  const bool fused3ms = any_grad && !want_H && pl->ms3 && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && !a.meas_f16 &&
                         n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
                         (cfg->single_on != 0) != (cfg->poissn_on != 0);
   if (fused3 || fused3ms) {
@@ -1278,6 +1318,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   } else if (!fused) {
     PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
     if ((rc = launch_status("k_adjoint launch"))) return rc;
+    if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
   }
   if (gz.d_probe) {
     PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, fused2 ? pl->nwg_fused : pl->nwg);
@@ -1296,7 +1337,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   if (n_idx == 0 || !grads) return PTYX_OK;
   if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
   const ptyx_grads gz = *grads;
-  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts)) return PTYX_OK;
+  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H)) return PTYX_OK;
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   KArgs a = make_args(pl, in, idx, n_idx);
@@ -1306,9 +1347,11 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   a.d_objp = gz.d_objp;
   a.d_shifts = gz.d_shifts;
   a.need_probe = gz.d_probe != nullptr;
+  if ((rc = setup_prop_grad(pl, gz, a))) return rc;
   if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
   PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, true);
   if ((rc = launch_status("k_adjoint(ext) launch"))) return rc;
+  if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
   if (gz.d_probe) {
     PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, pl->nwg);
     if ((rc = launch_status("probe finalize launch"))) return rc;

@@ -66,14 +66,15 @@ class Plan:
     """One ptyx_plan: fixed device and geometry (N, P, O, Nz, object extent, n_scans)."""
 
     def __init__(self, N, P, O, Nz, Ny, Nx, n_scans, max_patterns, shift_probes=True,
-                 meas_f16=False, device=None):
+                 meas_f16=False, device=None, prop_grad=False):
         self.lib = _lib.load()
         device = torch.device(device if device is not None else "cuda")
         if device.type != "cuda":
             raise ValueError("ptyx plans need a HIP device (torch 'cuda' device on ROCm)")
         self.device = torch.device("cuda", device.index if device.index is not None
                                    else torch.cuda.current_device())
-        flags = (_lib.PTYX_SHIFT_PROBES if shift_probes else 0) | (_lib.PTYX_MEAS_F16 if meas_f16 else 0)
+        flags = ((_lib.PTYX_SHIFT_PROBES if shift_probes else 0) | (_lib.PTYX_MEAS_F16 if meas_f16 else 0) |
+                 (_lib.PTYX_PROP_GRAD if prop_grad else 0))
         self.dims = _lib.Dims(int(N), int(P), int(O), int(Nz), int(Ny), int(Nx), int(n_scans),
                               int(max_patterns), flags)
         self.shift_probes = bool(shift_probes)
@@ -136,14 +137,14 @@ class Plan:
         grads = grads or {}
         d, dev = self.dims, self.device
         for k, shape in (("obja", (d.O, d.Nz, d.Ny, d.Nx)), ("objp", (d.O, d.Nz, d.Ny, d.Nx)),
-                         ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2))):
+                         ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2)), ("H", (d.N, d.N, 2))):
             g = grads.get(k)
             if g is not None:
                 _need(g, torch.float32, f"grad {k}", dev)
                 if tuple(g.shape) != shape:
                     raise ValueError(f"grad {k} shape {tuple(g.shape)} != {shape}")
         return _lib.Grads(_ptr(grads.get("obja")), _ptr(grads.get("objp")), _ptr(grads.get("probe")),
-                          _ptr(grads.get("shifts")))
+                          _ptr(grads.get("shifts")), _ptr(grads.get("H")))
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

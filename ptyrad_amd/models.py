@@ -17,9 +17,12 @@ Optional stages (ptyrad_amd/stages.py): detector blur (models
 object pre-blur (:275-284) run as HIP kernels around the engine; pre-blurred patches are handed to
 the engine as a patch-stack object (one (N, N) window per position, crop_pos (b·N, 0)).
 
-Out of scope on the HIP path (raise NotImplementedError when enabled): per-position / optimised
-tilts, optimised-dz propagators (models.py:339-356), on-the-fly measurement padding / resampling
-(:392-409).
+Propagators (models.py:300-360): fixed H (case 4), fixed global tilt (2B), and optimised global
+tilts / slice thickness (1, 2A, 3): H is rebuilt from the parameters on every call and the engine
+returns dL/dH (PTYX_PROP_GRAD), which torch autograd carries to dz / tilts (an (N, N) expression).
+
+Out of scope on the HIP path (raise NotImplementedError when enabled): per-position tilts
+(tilt_type 'each', models.py:330-335), on-the-fly measurement padding / resampling (:392-409).
 """
 from __future__ import annotations
 
@@ -36,36 +39,39 @@ _PARAM_NAMES = ("obja", "objp", "obj_tilts", "slice_thickness", "probe", "probe_
 class _EngineForward(torch.autograd.Function):
     """dp = PtychoAD.forward(idx); backward = ptyx_adjoint_dldi (autograd of models.py:422-436).
 
-    ``plan`` / ``base`` (H, occu, crop_pos) name the geometry: the model's own plan, or a patch-
-    stack plan when the object patches are pre-blurred (stages.BlurredPatches)."""
+    ``plan`` / ``base`` (occu, crop_pos) name the geometry: the model's own plan, or a patch-stack
+    plan when the object patches are pre-blurred (stages.BlurredPatches).  ``H_rv`` is the
+    propagator (N,N,2); its gradient (optimised tilts / thickness) comes from the engine's d_H."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, plan, base, idx_t, shift_probes):
+    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, plan, base, idx_t, shift_probes):
         ctx.plan, ctx.base, ctx.shift_probes = plan, base, shift_probes
-        ctx.save_for_backward(obja, objp, probe_rv, shifts, idx_t)
+        ctx.save_for_backward(obja, objp, probe_rv, shifts, H_rv, idx_t)
         with torch.no_grad():
-            return plan.forward(_tensors(obja, objp, probe_rv, shifts, base), idx_t)
+            return plan.forward(_tensors(obja, objp, probe_rv, shifts, H_rv, base), idx_t)
 
     @staticmethod
     def backward(ctx, grad_dp):
-        obja, objp, probe_rv, shifts, idx_t = ctx.saved_tensors
+        obja, objp, probe_rv, shifts, H_rv, idx_t = ctx.saved_tensors
         want = ctx.needs_input_grad
         grads = {}
-        outs = [None] * 4
-        for i, (k, p) in enumerate((("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts))):
+        outs = [None] * 5
+        for i, (k, p) in enumerate((("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts),
+                                    ("H", H_rv))):
             if want[i]:
                 outs[i] = torch.zeros_like(p)
                 grads[k] = outs[i]
         if not ctx.shift_probes:
             grads.pop("shifts", None)
         if grads:
-            ctx.plan.adjoint_dldi(_tensors(obja, objp, probe_rv, shifts, ctx.base), idx_t,
+            ctx.plan.adjoint_dldi(_tensors(obja, objp, probe_rv, shifts, H_rv, ctx.base), idx_t,
                                   grad_dp.contiguous().float(), grads)
-        return outs[0], outs[1], outs[2], outs[3], None, None, None, None
+        return (*outs, None, None, None, None)
 
 
-def _tensors(obja, objp, probe_rv, shifts, base):
-    t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach()}
+def _tensors(obja, objp, probe_rv, shifts, H_rv, base):
+    t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach(),
+         "H": H_rv.detach()}
     t.update(base)
     return t
 
@@ -133,13 +139,17 @@ class PtychoHIP(nn.Module):
             self.tilt_obj = bool(self.lr_params.get("obj_tilts", 0) != 0 or torch.any(self.opt_obj_tilts))
             self.shift_probes = bool(self.lr_params.get("probe_pos_shifts", 0) != 0)   # models.py:120
             self.change_thickness = bool(self.lr_params.get("slice_thickness", 0) != 0)
-            if self.change_thickness or self.lr_params.get("obj_tilts", 0) != 0 or \
-                    (self.tilt_obj and self.opt_obj_tilts.shape[0] != 1):
-                raise NotImplementedError("optimised tilts / thickness and per-position tilts are not on the HIP "
-                                          "path (fixed global tilts are)")
+            self.change_tilt = bool(self.lr_params.get("obj_tilts", 0) != 0)
+            if self.tilt_obj and self.opt_obj_tilts.shape[0] != 1:
+                raise NotImplementedError("per-position tilts (tilt_type 'each') are not on the HIP path; "
+                                          "global tilts (fixed or optimised) are")
             # models.py:210-219 / :346-349 (case 2B, global): a fixed tilt only changes the one
             # propagator every position uses, so the engine takes the tilted H as its H
             self.register_buffer("H_eff", self._tilted_H() if self.tilt_obj else self.H)
+            # cases 1 / 2A / 3 (models.py:339-356): H is rebuilt from the optimised dz / tilts on
+            # every call and the engine returns dL/dH (PTYX_PROP_GRAD), which autograd carries on
+            self.prop_opt = self.change_thickness or (self.tilt_obj and self.change_tilt)
+            self._init_propagator_grid()
             self.probe_int_sum = self.get_complex_probe_view().abs().pow(2).sum()
             self.loss_iters, self.iter_times, self.dz_iters, self.avg_tilt_iters = [], [], [], []
             self._current_object_patches = None
@@ -156,7 +166,8 @@ class PtychoHIP(nn.Module):
             # calls are N² f32 each); larger calls are split at mini-batch boundaries by Plan
             self.meas_f16 = meas_dtype == torch.float16
             self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or min(n_scans, 65536),
-                             shift_probes=self.shift_probes, meas_f16=self.meas_f16, device=device)
+                             shift_probes=self.shift_probes, meas_f16=self.meas_f16, device=device,
+                             prop_grad=self.prop_opt)
 
     # ------------------------------------------------------------------ reference API
     def get_complex_probe_view(self):
@@ -186,6 +197,38 @@ class PtychoHIP(nn.Module):
             raise IndexError("scan index out of range")
         return idx
 
+    def _init_propagator_grid(self):
+        """create_grids (models.py:163-171) + init_propagator_vars (:221-223): Ky, Kx on the
+        half-bin-shifted, ifftshifted grid; Kz = sqrt(k² - Kx² - Ky²), k = 2π/λ (f32)."""
+        N = self.opt_probe.shape[1]
+        dev = self.H.device
+        g = (torch.arange(-N // 2, N // 2, device=dev) + 0.5) / N
+        k1 = torch.fft.ifftshift(2 * torch.pi * g / self.dx)
+        Ky, Kx = torch.meshgrid(k1, k1, indexing="ij")
+        self.register_buffer("propagator_grid", torch.stack([Ky, Kx], dim=0))
+        k = 2 * torch.pi / self.lambd
+        self.register_buffer("Kz", torch.sqrt(k ** 2 - Kx ** 2 - Ky ** 2))
+
+    def _propagator(self):
+        """get_propagators (models.py:300-360) for a global tilt: the (N, N) complex64 H every
+        position uses, differentiable in opt_slice_thickness / opt_obj_tilts when they are optimised."""
+        if not self.prop_opt:
+            return self.H_eff
+        Ky, Kx = self.propagator_grid
+        dz = self.opt_slice_thickness
+        ty = self.opt_obj_tilts[:, 0, None, None] / 1e3
+        tx = self.opt_obj_tilts[:, 1, None, None] / 1e3
+        if self.tilt_obj and self.change_thickness:                       # case 1
+            H = torch.exp(1j * dz * self.Kz) * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx)))
+        elif self.tilt_obj:                                                # case 2A
+            H = self.H * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx)))
+        else:                                                              # case 3
+            H = torch.exp(1j * dz * self.Kz)[None]
+        return H[0]
+
+    def _H_rv(self):
+        return torch.view_as_real(self._propagator().contiguous())
+
     def _tilted_H(self):
         """H · exp(i dz (Ky tan θy + Kx tan θx)) on the half-bin-shifted, ifftshifted k grid
         (models.py:163-171 create_grids, :215-219 init_propagator_vars)."""
@@ -200,10 +243,11 @@ class PtychoHIP(nn.Module):
         return (self.H * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx))))[0].contiguous()
 
     def _engine_tensors(self):
-        return _tensors(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts, self._base())
+        return _tensors(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts, self._H_rv(),
+                        self._base())
 
     def _base(self, crop_pos=None, meas=None, stack=False):
-        return {"H": self.H_eff, "occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
+        return {"occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
                 "meas": self.measurements if (meas is None and not stack) else meas}
 
     # ------------------------------------------------------------------ object pre-blur (stages.py)
@@ -225,7 +269,7 @@ class PtychoHIP(nn.Module):
             O, Nz = self.opt_obja.shape[:2]
             P, N = self.opt_probe.shape[:2]
             plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes, meas_f16=self.meas_f16,
-                        device=self.opt_obja.device)
+                        device=self.opt_obja.device, prop_grad=self.prop_opt)
             self._stack_plans[B] = plan
         return plan
 
@@ -280,11 +324,11 @@ class PtychoHIP(nn.Module):
         return torch.fft.ifft2(torch.fft.fft2(probe)[None] * w[:, None])
 
     def get_propagators(self, indices):
-        return self.H_eff[None,]
+        return self._propagator()[None,]
 
     def get_propagated_probe(self, index):
         probe = self.get_probes(index)[0].detach()
-        H = self.H_eff[None]
+        H = self._propagator().detach()[None]
         n_slices = self.opt_objp.shape[1]
         out = torch.zeros((n_slices, *probe.shape), dtype=probe.dtype, device=probe.device)
         psi = probe
@@ -309,11 +353,12 @@ class PtychoHIP(nn.Module):
         idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device, non_blocking=True)
         if self.preblur:
             A, Ph, sh, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
-            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, plan, base, ar, self.shift_probes)
+            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), plan, base, ar, self.shift_probes)
             self._current_object_patches = torch.stack([pa, pp], dim=-1).permute(2, 0, 1, 3, 4, 5)
         else:
             dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
-                                      self.plan, self._base(meas=None, stack=True), idx_t, self.shift_probes)
+                                      self._H_rv(), self.plan, self._base(meas=None, stack=True), idx_t,
+                                      self.shift_probes)
             # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
             self._current_object_patches = self.get_obj_patches(idx)
         if self.detector_blur:                      # get_forward_meas, models.py:375-382

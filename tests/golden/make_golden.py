@@ -46,6 +46,7 @@ DEFAULT_LOSS = {
 
 
 BLUR = {"detector_blur_std": None, "obj_preblur_std": None}   # set by --blur-only cases
+PROP_LR = {}   # optimised obj_tilts / slice_thickness lrs, set by --prop-only cases
 
 
 def model_params(shift_lr=5e-4):
@@ -57,6 +58,8 @@ def model_params(shift_lr=5e-4):
         "probe": {"start_iter": 1, "lr": 1e-4},
         "probe_pos_shifts": {"start_iter": 1 if shift_lr else None, "lr": shift_lr},
     }
+    for k, lr in PROP_LR.items():
+        up[k] = {"start_iter": 1, "lr": lr}
     return {"detector_blur_std": BLUR["detector_blur_std"], "obj_preblur_std": BLUR["obj_preblur_std"],
             "update_params": up,
             "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
@@ -164,6 +167,15 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
     for k, v in BLUR.items():
         if v:
             out[k] = np.float32(v)
+    if PROP_LR:   # optimised propagator (models.py:339-356 cases 1 / 2A / 3): H is the untilted one
+        out.update(H=model.get_propagators(np.array([0]))[0].detach().numpy(), H_untilted=model.H.numpy(),
+                   obj_tilts=model.opt_obj_tilts.detach().numpy().copy(),
+                   slice_thickness=np.float32(model.opt_slice_thickness.item()), dx=np.float32(model.dx.item()),
+                   lambd=np.float32(model.lambd.item()), prop_lr=json.dumps(PROP_LR),
+                   g_obj_tilts=np.zeros((1, 2), np.float32) if g(model.opt_obj_tilts) is None
+                   else g(model.opt_obj_tilts),
+                   g_slice_thickness=np.float32(0.0) if g(model.opt_slice_thickness) is None
+                   else g(model.opt_slice_thickness))
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
@@ -224,6 +236,15 @@ if __name__ == "__main__":
     torch.set_num_threads(4)
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--prop-only":
+        PROP_LR.update(slice_thickness=1e-3)                         # case 3
+        run_case("n32_p2o1z3_optdz", 32, 2, 1, 3, 4, 4, 6, seed=41)
+        PROP_LR.clear()
+        PROP_LR.update(obj_tilts=1e-3)                               # case 2A
+        run_case("n32_p1o1z2_opttilt", 32, 1, 1, 2, 4, 4, 5, seed=42, tilts=[2.0, -1.0])
+        PROP_LR.update(slice_thickness=1e-3)                         # case 1
+        run_case("n64_p2o1z2_opttiltdz", 64, 2, 1, 2, 3, 3, 6, seed=43, tilts=[1.5, 2.5])
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--blur-only":
         # detector blur (models.py:379-380) / object pre-blur (:275-284) call torchvision's

@@ -31,7 +31,7 @@ def test_struct_layouts_match_header():
     # sizes of the C structs (all 4-byte fields / 8-byte pointers, no padding surprises)
     assert ctypes.sizeof(_lib.Dims) == 9 * 4
     assert ctypes.sizeof(_lib.Inputs) == 8 * 8
-    assert ctypes.sizeof(_lib.Grads) == 4 * 8
+    assert ctypes.sizeof(_lib.Grads) == 5 * 8
     assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
     assert ctypes.sizeof(_lib.ObjConstraints) == 19 * 4
 

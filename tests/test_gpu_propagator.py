@@ -1,0 +1,112 @@
+"""Optimised propagators on MI355X (get_propagators cases 1 / 2A / 3,
+src/ptyrad/models.py:339-356): the engine returns dL/dH (PTYX_PROP_GRAD) and torch autograd
+carries it through PtychoHIP's rebuilt H to opt_slice_thickness / opt_obj_tilts.
+
+Fixtures tests/golden/n*_opt*.npz come from the reference itself (make_golden.py --prop-only).
+Tolerances: H ≤ 1e-5 (its f32 phase dz·Kz ≈ 300 rad); dp ≤ 1e-5; loss terms rtol 2e-5;
+object / probe gradients ≤ 5e-5; dL/dH vs the oracle ≤ 1e-4; the dz gradient rtol 1e-2 (the
+constant part dz·k of the phase, k ≈ 150 Å⁻¹, cancels in the sum Re Σ conj(g_H) i Kz H, and
+the f32 reference's own rounding of that cancellation is ≈ 1e-3 relative); tilt gradients
+rtol 1e-3.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptyx_oracle as orc
+from tests.test_gpu_model import init_vars, model_params
+from tests.test_oracle_golden import load_case, prop_case, rel
+
+pytestmark = pytest.mark.gpu
+PROP = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz")))
+LRS = {"obja": 5e-4, "objp": 5e-4, "obj_tilts": 0.0, "slice_thickness": 0.0, "probe": 1e-4,
+       "probe_pos_shifts": 5e-4}
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _model(d, device):
+    from ptyrad_amd.models import PtychoHIP
+    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H_untilted"], d["occu"],
+                   d["meas"])
+    iv.update(obj_tilts=d["obj_tilts"], slice_thickness=float(d["slice_thickness"]), dx=float(d["dx"]),
+              lambd=float(d["lambd"]))
+    lrs = {**LRS, **json.loads(str(d["prop_lr"]))}
+    return PtychoHIP(iv, model_params(lrs), device=device, verbose=False)
+
+
+def _check(model, d, terms):
+    np.testing.assert_allclose(terms, d["loss_terms"], rtol=2e-5, atol=1e-7)
+    assert rel(model.opt_obja.grad.cpu().numpy(), d["g_obja"]) < 5e-5
+    assert rel(model.opt_objp.grad.cpu().numpy(), d["g_objp"]) < 5e-5
+    assert rel(model.opt_probe.grad.cpu().numpy(), d["g_probe"]) < 5e-5
+    case = prop_case(d)
+    if case in (1, 3):
+        np.testing.assert_allclose(model.opt_slice_thickness.grad.item(), float(d["g_slice_thickness"]), rtol=1e-2)
+    if case in (1, 2):
+        np.testing.assert_allclose(model.opt_obj_tilts.grad.cpu().numpy(), d["g_obj_tilts"], rtol=1e-3,
+                                   atol=1e-3 * np.abs(d["g_obj_tilts"]).max())
+
+
+@pytest.mark.parametrize("path", PROP, ids=[os.path.basename(p)[:-4] for p in PROP])
+def test_fused_path_optimised_propagator(path):
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = load_case(path)
+    model = _model(d, device)
+    assert rel(model.get_propagators([0])[0].detach().cpu().numpy(), d["H"]) < 1e-5
+    dp = model(d["batch"])
+    assert rel(dp.detach().cpu().numpy(), d["dp"]) < 1e-5
+    model.zero_grad(set_to_none=True)
+    total, terms = CombinedLoss(d["loss_params"], device=device).fused(model, [d["batch"]])
+    total.backward()
+    _check(model, d, terms.detach().cpu().numpy()[0])
+
+
+@pytest.mark.parametrize("path", PROP, ids=[os.path.basename(p)[:-4] for p in PROP])
+def test_generic_path_optimised_propagator(path):
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = load_case(path)
+    model = _model(d, device)
+    dp = model(d["batch"])
+    total, terms = CombinedLoss(d["loss_params"], device=device)(dp, model.get_measurements(d["batch"]),
+                                                                 model._current_object_patches, model.omode_occu)
+    total.backward()
+    _check(model, d, np.array([float(t.detach()) for t in terms]))
+
+
+def test_engine_dH_vs_oracle():
+    """ptyx_forward_loss_grad's d_H on two ragged mini-batches (3 slices, 2 probe modes) against
+    the oracle's dL/dH; a plan without PTYX_PROP_GRAD rejects d_H."""
+    device = dev()
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import LossConfig
+    d = load_case([p for p in PROP if "optdz" in p][0])
+    model = _model(d, device)
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(3).permutation(S)
+    batches = [perm[:5], perm[5:12]]
+    cfg = LossConfig.from_loss_params(d["loss_params"])
+    t = model._engine_tensors()
+    idx = np.concatenate(batches).astype(np.int32)
+    off = np.array([0, 5, 12], np.int32)
+    gH = torch.zeros((32, 32, 2), device=device)
+    model.plan.forward_loss_grad(t, idx, off, cfg, {"H": gH}, grad_scale=0.5)
+    Heff = model.get_propagators([0])[0].detach().cpu().numpy()
+    _, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], Heff, d["occu"],
+                                    d["meas"], batches, d["loss_params"], shift_probes=True, grad_scale=0.5)
+    got = gH.cpu().numpy()
+    assert rel(got[..., 0] + 1j * got[..., 1], g["H"]) < 1e-4
+    from ptyrad_amd.engine import Plan
+    plain = Plan(32, 2, 1, 3, *d["obja"].shape[-2:], S, S, device=device)
+    with pytest.raises(_lib.PtyxError, match="PTYX_PROP_GRAD"):
+        plain.forward_loss_grad(t, idx, off, cfg, {"H": gH})

@@ -129,3 +129,30 @@ def test_oracle_trajectory_matches_reference(path):
         assert rms < 1e-5, (k, rms)
     prb = p["probe"][..., 0] + 1j * p["probe"][..., 1]
     assert rel(prb, z["final_probe"]) < 1e-5
+
+
+PROP = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz")))
+
+
+def prop_case(d):
+    """get_propagators case of a --prop-only fixture: 1 (tilts + dz), 2 (2A: tilts), 3 (dz)."""
+    lr = json.loads(str(d["prop_lr"]))
+    return 1 if len(lr) == 2 else (2 if "obj_tilts" in lr else 3)
+
+
+@pytest.mark.parametrize("path", PROP, ids=[os.path.basename(p)[:-4] for p in PROP])
+def test_oracle_propagator_gradient_matches_reference(path):
+    """dL/dH from the oracle's adjoint, chained to dz / tilts, equals the reference's autograd
+    gradients of opt_slice_thickness / opt_obj_tilts (models.py:339-356)."""
+    d = load_case(path)
+    _, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                    d["occu"], d["meas"], [d["batch"]], d["loss_params"],
+                                    shift_probes=bool(d["shift_probes"]))
+    case = prop_case(d)
+    gdz, gt = orc.propagator_param_grads(g["H"], d["H"], float(d["slice_thickness"]),
+                                         d["obj_tilts"][0].astype(np.float64), float(d["dx"]), float(d["lambd"]), case)
+    if case in (1, 3):   # the f32 reference's own floor: dz·k phase cancellation (k = 2π/λ ≈ 150 Å⁻¹)
+        np.testing.assert_allclose(gdz, float(d["g_slice_thickness"]), rtol=5e-3)
+    if case in (1, 2):
+        np.testing.assert_allclose(gt, d["g_obj_tilts"][0], rtol=2e-3, atol=1e-3 * np.abs(d["g_obj_tilts"]).max())
+
