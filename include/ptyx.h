@@ -181,6 +181,15 @@ int ptyx_patch_gather(void *stream, const float *obj, int32_t O, int32_t Nz, int
 int ptyx_patch_scatter_add(void *stream, const float *gpatches, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
                            const int32_t *crop_pos, const int32_t *idx, int32_t n_idx, int32_t N, float *gobj);
 
+/* PtychoAD.get_measurements(indices) with on-the-fly padding / resampling (models.py:384-412):
+ * out (n_idx,Ho,Wo) f32 = interpolate(paste(canvas, meas[idx[b]] at (h1, w1)), scale, bilinear,
+ * align_corners=False) / (scale_y·scale_x).  meas (n_scans,Hm,Wm) f32 (f16 when meas_f16);
+ * canvas (Hp,Wp) f32 = on_the_fly_meas_padded, or NULL (no padding: Hp,Wp = Hm,Wm, h1 = w1 = 0);
+ * scale 1,1 = no resampling; Ho,Wo = floor(Hp·scale_y), floor(Wp·scale_x).  n_idx ≤ 65535. */
+int ptyx_meas_gather(void *stream, const void *meas, int32_t meas_f16, int32_t Hm, int32_t Wm, const int32_t *idx,
+                     int32_t n_idx, const float *canvas, int32_t Hp, int32_t Wp, int32_t h1, int32_t w1,
+                     double scale_y, double scale_x, int32_t Ho, int32_t Wo, float *out);
+
 /* obj_zblur → complex_ratio → mirrored_amp → obja_thresh → objp_postiv on (O,Nz,Ny,Nx) f32
  * obja / objp, in place, in CombinedConstraint.forward order (kr/kz filters, which sit between
  * zblur and complex_ratio, are the caller's: call once with only zblur, filter, call again). */

@@ -103,6 +103,42 @@ def gaussian_blur_adjoint(g, sigma, ks=5):
     return gp[..., :, h:h + Nx]
 
 
+def otf_measurements(meas, idx, canvas=None, pad_idx=None, scale=None):
+    """PtychoAD.get_measurements(indices) with on-the-fly padding / resampling (models.py:384-412):
+    paste each frame into the canvas at pad_idx = (h1, h2, w1, w2), then
+    interpolate(scale_factor, 'bilinear', align_corners=False) (aten: source index
+    s·(i+0.5)-0.5 clamped at 0 with s = f32(1/scale), i1 = min(i0+1, in-1)) and divide by
+    scale_y·scale_x.  float64 arithmetic on the f32 inputs."""
+    frames = np.asarray(meas, np.float64)[np.asarray(idx)]
+    if canvas is not None:
+        h1, h2, w1, w2 = (int(v) for v in pad_idx)
+        c = np.broadcast_to(np.asarray(canvas, np.float64), (len(frames),) + np.shape(canvas)).copy()
+        c[:, h1:h2, w1:w2] = frames
+        frames = c
+    if scale is None or all(f == 1 for f in scale):
+        return frames
+    B, Hp, Wp = frames.shape
+    sy, sx = float(scale[0]), float(scale[1])
+    Ho, Wo = int(np.floor(Hp * sy)), int(np.floor(Wp * sx))
+
+    def src(n_out, n_in, s):
+        inv = np.float32(1.0 / s)
+        real = (inv * (np.arange(n_out, dtype=np.float32) + np.float32(0.5)) - np.float32(0.5)).astype(np.float64)
+        real = np.maximum(real, 0.0)
+        i0 = np.minimum(np.floor(real).astype(np.int64), n_in - 1)
+        l1 = np.clip(real - i0, 0.0, 1.0)
+        i1 = i0 + (i0 < n_in - 1)
+        return i0, i1, l1
+
+    y0, y1, ly = src(Ho, Hp, sy)
+    x0, x1, lx = src(Wo, Wp, sx)
+    ly, lx = ly[:, None], lx[None, :]
+    f = frames
+    out = ((1 - ly) * ((1 - lx) * f[:, y0][:, :, x0] + lx * f[:, y0][:, :, x1]) +
+           ly * ((1 - lx) * f[:, y1][:, :, x0] + lx * f[:, y1][:, :, x1]))
+    return out / np.float64(np.float32(sy * sx))
+
+
 def get_patches(obja, objp, crop_pos, idx, n):
     """(B,O,Nz,N,N) amplitude and phase patches at integer crop positions (models.py:251-265)."""
     B = len(idx)

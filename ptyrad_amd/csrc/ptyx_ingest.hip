@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cerrno>
 #include <cstring>
 #include <string>
@@ -305,4 +306,87 @@ extern "C" int ptyx_raw_read(void* stream, const char* path, int64_t offset, int
   }
   close(fd);
   return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ptyx_meas_gather — PtychoAD.get_measurements(indices) with the on-the-fly options
+// (src/ptyrad/models.py:384-412): each selected frame is pasted into the padding canvas
+// (canvas[h1:h1+Hm, w1:w1+Wm] = meas[idx[b]]), then bilinearly resampled as
+// torch.nn.functional.interpolate(scale_factor, mode='bilinear', align_corners=False) does
+// (source index s·(i+0.5)-0.5 clamped at 0, s = 1/scale_factor rounded to f32) and divided by
+// scale_y·scale_x.  One thread per output pixel; the canvas composite is never materialised.
+namespace {
+struct OtfGeom {
+  int Hm, Wm, Hp, Wp, h1, w1, Ho, Wo;
+  float inv_sy, inv_sx, norm;
+  int resample, f16;
+};
+
+__device__ __forceinline__ float otf_canvas(const void* __restrict__ meas, size_t base,
+                                            const float* __restrict__ canvas, const OtfGeom& g, int r, int c) {
+  const int rr = r - g.h1, cc = c - g.w1;
+  if (rr >= 0 && rr < g.Hm && cc >= 0 && cc < g.Wm) {
+    const size_t off = base + (size_t)rr * g.Wm + cc;
+    return g.f16 ? __half2float(reinterpret_cast<const __half*>(meas)[off]) : reinterpret_cast<const float*>(meas)[off];
+  }
+  return canvas ? canvas[(size_t)r * g.Wp + c] : 0.f;
+}
+
+// aten area_pixel_compute_source_index (align_corners=False, linear) + guard_index_and_lambda
+__device__ __forceinline__ void otf_src(int i, float inv_s, int in, int& i0, int& i1, float& l1) {
+  float real = __fsub_rn(__fmul_rn(inv_s, __fadd_rn((float)i, 0.5f)), 0.5f);
+  if (real < 0.f) real = 0.f;
+  i0 = min((int)floorf(real), in - 1);
+  l1 = fminf(fmaxf(real - (float)i0, 0.f), 1.f);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_meas_gather(const void* __restrict__ meas, const int* __restrict__ idx,
+                                                     const float* __restrict__ canvas, OtfGeom g,
+                                                     float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= g.Ho * g.Wo) return;
+  const int b = blockIdx.y;
+  const int y = e / g.Wo, x = e - y * g.Wo;
+  const size_t base = (size_t)idx[b] * g.Hm * g.Wm;
+  float v;
+  if (!g.resample) {
+    v = otf_canvas(meas, base, canvas, g, y, x);
+  } else {
+    int y0, y1, x0, x1;
+    float ly, lx;
+    otf_src(y, g.inv_sy, g.Hp, y0, y1, ly);
+    otf_src(x, g.inv_sx, g.Wp, x0, x1, lx);
+    const float a00 = otf_canvas(meas, base, canvas, g, y0, x0), a01 = otf_canvas(meas, base, canvas, g, y0, x1);
+    const float a10 = otf_canvas(meas, base, canvas, g, y1, x0), a11 = otf_canvas(meas, base, canvas, g, y1, x1);
+    v = (1.f - ly) * ((1.f - lx) * a00 + lx * a01) + ly * ((1.f - lx) * a10 + lx * a11);
+    v = v / g.norm;
+  }
+  out[(size_t)b * g.Ho * g.Wo + e] = v;
+}
+}  // namespace
+
+extern "C" int ptyx_meas_gather(void* stream, const void* meas, int32_t meas_f16, int32_t Hm, int32_t Wm,
+                                const int32_t* idx, int32_t n_idx, const float* canvas, int32_t Hp, int32_t Wp,
+                                int32_t h1, int32_t w1, double scale_y, double scale_x, int32_t Ho, int32_t Wo,
+                                float* out) {
+  abi::clear_error();
+  if (Hm <= 0 || Wm <= 0 || n_idx < 0 || Ho <= 0 || Wo <= 0) return abi::fail(PTYX_EINVAL, "meas_gather: bad shape");
+  if (!canvas && (Hp != Hm || Wp != Wm || h1 != 0 || w1 != 0))
+    return abi::fail(PTYX_EINVAL, "meas_gather: without a canvas Hp, Wp must equal Hm, Wm and h1 = w1 = 0");
+  if (h1 < 0 || w1 < 0 || h1 + Hm > Hp || w1 + Wm > Wp)
+    return abi::fail(PTYX_EINVAL, "meas_gather: the frame does not fit the padding canvas");
+  if (!(scale_y > 0.0) || !(scale_x > 0.0)) return abi::fail(PTYX_EINVAL, "meas_gather: scale factors must be > 0");
+  const bool resample = scale_y != 1.0 || scale_x != 1.0;
+  if (Ho != (resample ? (int32_t)std::floor(Hp * scale_y) : Hp) ||
+      Wo != (resample ? (int32_t)std::floor(Wp * scale_x) : Wp))
+    return abi::fail(PTYX_EINVAL, "meas_gather: output size must be floor(padded size * scale_factor)");
+  if (n_idx > 65535) return abi::fail(PTYX_EUNSUPPORTED, "meas_gather: at most 65535 frames per call");
+  if (n_idx == 0) return PTYX_OK;
+  if (!meas || !idx || !out) return abi::fail(PTYX_EINVAL, "meas_gather: null pointer");
+  OtfGeom g{Hm, Wm, Hp, Wp, h1, w1, Ho, Wo, (float)(1.0 / scale_y), (float)(1.0 / scale_x),
+            (float)(scale_y * scale_x), resample ? 1 : 0, meas_f16 ? 1 : 0};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_meas_gather, dim3((Ho * Wo + 255) / 256, n_idx), dim3(256), 0, st, meas, idx, canvas, g, out);
+  return abi::launch_status("k_meas_gather launch");
 }

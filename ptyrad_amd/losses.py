@@ -122,6 +122,8 @@ class CombinedLoss(torch.nn.Module):
         cfg = LossConfig.from_loss_params(self.loss_params)
         if getattr(model, "preblur", False):
             return self._preblur_fused(model, batches, cfg)
+        if getattr(model, "otf_meas", False):
+            return self._local_fused(model, batches, cfg)
         idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
         off_t = torch.as_tensor(batch_offsets(batches)).to(dev, non_blocking=True)
         total, terms = _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe,
@@ -131,30 +133,54 @@ class CombinedLoss(torch.nn.Module):
 
     PREBLUR_GROUP = 8192
 
+    def _grouped(self, model, batches, cap, run, strict=False):
+        """Split ``batches`` at mini-batch boundaries into groups of ≤ cap patterns (a larger
+        mini-batch forms a group of its own unless ``strict``); ``run(group)`` returns
+        (total, terms) of one engine call.  Gradients accumulate across the calls."""
+        totals, rows, group, n = [], [], [], 0
+        for b in batches:
+            nb = len(np.asarray(b).reshape(-1))
+            if strict and nb > cap:
+                raise ValueError(f"a mini-batch of {nb} positions exceeds the call capacity {cap}")
+            if group and n + nb > cap:
+                t, r = run(group)
+                totals.append(t)
+                rows.append(r)
+                group, n = [], 0
+            group.append(b)
+            n += nb
+        if group:
+            t, r = run(group)
+            totals.append(t)
+            rows.append(r)
+        return sum(totals), torch.cat(rows)
+
     def _preblur_fused(self, model, batches, cfg):
         dev = model.opt_obja.device
-        totals, rows, group, n = [], [], [], 0
 
         def run(group):
             flat = np.concatenate([np.asarray(b).reshape(-1) for b in group])
             idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev)
             off_t = torch.as_tensor(batch_offsets(group)).to(dev, non_blocking=True)
             A, Ph, sh, plan, base, ar, _ = model._stack_inputs(idx_t, with_meas=True)
-            t, terms = _FusedLoss.apply(A, Ph, model.opt_probe, sh, model._H_rv(), plan, base, ar, off_t, cfg,
-                                        model.shift_probes)
-            totals.append(t)
-            rows.append(terms)
+            return _FusedLoss.apply(A, Ph, model.opt_probe, sh, model._H_rv(), plan, base, ar, off_t, cfg,
+                                    model.shift_probes)
 
-        for b in batches:
-            nb = len(np.asarray(b).reshape(-1))
-            if group and n + nb > self.PREBLUR_GROUP:
-                run(group)
-                group, n = [], 0
-            group.append(b)
-            n += nb
-        if group:
-            run(group)
-        return sum(totals), torch.cat(rows)
+        return self._grouped(model, batches, self.PREBLUR_GROUP, run)
+
+    def _local_fused(self, model, batches, cfg):
+        """On-the-fly measurements: call-local positions / shifts / gathered DPs (models.py:384-412)."""
+        dev = model.opt_obja.device
+
+        def run(group):
+            flat = np.concatenate([np.asarray(b).reshape(-1) for b in group])
+            idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev)
+            off_t = torch.as_tensor(batch_offsets(group)).to(dev, non_blocking=True)
+            sh, base, ar = model._local_inputs(idx_t, with_meas=True)
+            return _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe, sh, model._H_rv(), model.plan,
+                                    base, ar, off_t, cfg, model.shift_probes)
+
+        return self._grouped(model, batches, int(model.plan.dims.n_scans), run, strict=True)
 
     def _per_batch(self, model, batches):
         totals, rows = [], []

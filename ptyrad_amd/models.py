@@ -21,10 +21,15 @@ Propagators (models.py:300-360): fixed H (case 4), fixed global tilt (2B), and o
 tilts / slice thickness (1, 2A, 3): H is rebuilt from the parameters on every call and the engine
 returns dL/dH (PTYX_PROP_GRAD), which torch autograd carries to dz / tilts (an (N, N) expression).
 
-Out of scope on the HIP path (raise NotImplementedError when enabled): per-position tilts
-(tilt_type 'each', models.py:330-335), on-the-fly measurement padding / resampling (:392-409).
+On-the-fly measurement padding / resampling (models.py:384-412) runs as ptyx_meas_gather; engine
+calls then take call-local positions / shifts / DPs (rows 0..n-1 of plan-sized arrays).
+
+Out of scope on the HIP path (raises NotImplementedError): per-position tilts (tilt_type 'each',
+models.py:330-335).
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 import torch
@@ -91,11 +96,14 @@ class PtychoHIP(nn.Module):
                 if v not in (None, 0) and not float(v) > 0:
                     raise ValueError(f"{k} must be None, 0 or > 0")
             self._stack_plans = {}
-            if init_variables.get("on_the_fly_meas_padded") is not None or \
-                    init_variables.get("on_the_fly_meas_scale_factors") is not None:
-                raise NotImplementedError("on-the-fly measurement padding/resampling is not on the HIP path")
-            self.meas_padded = None
-            self.meas_scale_factors = None
+            # on-the-fly measurement padding / resampling (models.py:81-86, :384-412)
+            pad = init_variables.get("on_the_fly_meas_padded")
+            self.meas_padded = None if pad is None else torch.tensor(np.asarray(pad), dtype=torch.float32,
+                                                                     device=device).contiguous()
+            self.meas_padded_idx = None if pad is None else \
+                torch.tensor(np.asarray(init_variables["on_the_fly_meas_padded_idx"]), dtype=torch.int32)
+            sf = init_variables.get("on_the_fly_meas_scale_factors")
+            self.meas_scale_factors = None if sf is None else [float(f) for f in np.asarray(sf).reshape(-1)]
             start_iter, lrs = {}, {}
             for k, p in model_params["update_params"].items():
                 start_iter[k] = p["start_iter"]
@@ -165,9 +173,17 @@ class PtychoHIP(nn.Module):
             # plan workspace scales with the largest call (per-pattern intensities of mixed-state
             # calls are N² f32 each); larger calls are split at mini-batch boundaries by Plan
             self.meas_f16 = meas_dtype == torch.float16
-            self.plan = Plan(N, P, O, Nz, Ny, Nx, n_scans, max_patterns or min(n_scans, 65536),
-                             shift_probes=self.shift_probes, meas_f16=self.meas_f16, device=device,
-                             prop_grad=self.prop_opt)
+            cap = max_patterns or min(n_scans, 65536)
+            # with on-the-fly measurements every engine call is call-local: positions, shifts and
+            # the gathered DPs of the call sit in rows 0..n-1 of (cap)-row arrays
+            self.otf_meas = self.meas_padded is not None or (
+                self.meas_scale_factors is not None and any(f != 1 for f in self.meas_scale_factors))
+            if self.otf_meas:
+                cap = min(cap, 65535)
+                self._meas_buf = torch.zeros((cap, N, N), dtype=torch.float32, device=device)
+            self.plan = Plan(N, P, O, Nz, Ny, Nx, cap if self.otf_meas else n_scans, cap,
+                             shift_probes=self.shift_probes, meas_f16=self.meas_f16 and not self.otf_meas,
+                             device=device, prop_grad=self.prop_opt)
 
     # ------------------------------------------------------------------ reference API
     def get_complex_probe_view(self):
@@ -268,8 +284,9 @@ class PtychoHIP(nn.Module):
                 old.close()
             O, Nz = self.opt_obja.shape[:2]
             P, N = self.opt_probe.shape[:2]
-            plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes, meas_f16=self.meas_f16,
-                        device=self.opt_obja.device, prop_grad=self.prop_opt)
+            plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes,
+                        meas_f16=self.meas_f16 and not self.otf_meas, device=self.opt_obja.device,
+                        prop_grad=self.prop_opt)
             self._stack_plans[B] = plan
         return plan
 
@@ -288,7 +305,9 @@ class PtychoHIP(nn.Module):
         O, Nz = A.shape[:2]
         il = idx_t.long()
         sh = self.opt_probe_pos_shifts[il]
-        meas = self.measurements[il].contiguous() if with_meas else None
+        meas = None
+        if with_meas:
+            meas = self._gather_meas(idx_t) if self.otf_meas else self.measurements[il].contiguous()
         base = self._base(stack_crop_pos(B, N, idx_t.device), meas, stack=True)
         ar = torch.arange(B, dtype=torch.int32, device=idx_t.device)
         return (A.reshape(O, Nz, B * N, N), Ph.reshape(O, Nz, B * N, N), sh, self._stack_plan(B), base, ar,
@@ -337,11 +356,55 @@ class PtychoHIP(nn.Module):
             psi = torch.fft.ifft2(H[None] * torch.fft.fft2(psi))
         return out
 
+    def _gather_meas(self, idx_t, out=None):
+        """ptyx_meas_gather: the call's DPs with the on-the-fly padding / resampling applied."""
+        from . import _lib
+        n = int(idx_t.numel())
+        Hm, Wm = self.measurements.shape[-2:]
+        N = self.opt_probe.shape[1]
+        if out is None:
+            out = torch.empty((n, N, N), dtype=torch.float32, device=self.measurements.device)
+        if self.meas_padded is not None:
+            Hp, Wp = self.meas_padded.shape[-2:]
+            h1, _, w1, _ = (int(v) for v in self.meas_padded_idx)
+            canvas = ctypes.c_void_p(self.meas_padded.data_ptr())
+        else:
+            Hp, Wp, h1, w1, canvas = Hm, Wm, 0, 0, ctypes.c_void_p(0)
+        sy, sx = self.meas_scale_factors if self.meas_scale_factors is not None else (1.0, 1.0)
+        lib = _lib.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.measurements.device).cuda_stream)
+        _lib.check(lib.ptyx_meas_gather(st, ctypes.c_void_p(self.measurements.data_ptr()),
+                                        int(self.measurements.dtype == torch.float16), Hm, Wm,
+                                        ctypes.c_void_p(idx_t.data_ptr()), n, canvas, Hp, Wp, h1, w1, sy, sx, N, N,
+                                        ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def _local_inputs(self, idx_t, with_meas=False):
+        """Call-local engine inputs (on-the-fly measurements): shifts / crop_pos / DPs of the call's
+        positions in rows 0..n-1 of plan-sized arrays; the engine then runs on idx = 0..n-1."""
+        n, cap = int(idx_t.numel()), int(self.plan.dims.n_scans)
+        if n > cap:
+            raise ValueError(f"calls with on-the-fly measurements take at most {cap} positions")
+        il = idx_t.long()
+        sh, cp = self.opt_probe_pos_shifts[il], self.crop_pos[il]
+        if n < cap:
+            sh = torch.cat([sh, sh.new_zeros((cap - n, 2))])
+            cp = torch.cat([cp, cp.new_zeros((cap - n, 2))])
+        meas = None
+        if with_meas:
+            self._gather_meas(idx_t, self._meas_buf[:n])
+            meas = self._meas_buf
+        base = {"occu": self.omode_occu, "crop_pos": cp.contiguous(), "meas": meas}
+        return sh, base, torch.arange(n, dtype=torch.int32, device=idx_t.device)
+
     def get_measurements(self, indices=None):
-        """models.py:384-416 (no on-the-fly padding / resampling)."""
+        """models.py:384-416, including the on-the-fly padding / resampling (HIP gather)."""
         if indices is None:
             return self.measurements
-        idx = torch.as_tensor(self._check_indices(indices), device=self.measurements.device, dtype=torch.long)
+        idx = self._check_indices(indices)
+        if self.otf_meas:
+            return self._gather_meas(torch.as_tensor(idx, dtype=torch.int32).to(self.measurements.device))
+        idx = torch.as_tensor(idx, device=self.measurements.device, dtype=torch.long)
         return self.measurements[idx].float()
 
     def clear_cache(self):
@@ -355,6 +418,11 @@ class PtychoHIP(nn.Module):
             A, Ph, sh, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
             dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), plan, base, ar, self.shift_probes)
             self._current_object_patches = torch.stack([pa, pp], dim=-1).permute(2, 0, 1, 3, 4, 5)
+        elif self.otf_meas:
+            sh, base, ar = self._local_inputs(idx_t)
+            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, sh, self._H_rv(), self.plan,
+                                      base, ar, self.shift_probes)
+            self._current_object_patches = self.get_obj_patches(idx)
         else:
             dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
                                       self._H_rv(), self.plan, self._base(meas=None, stack=True), idx_t,

@@ -222,6 +222,43 @@ def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumul
     print(f"{name}: loss_hist={np.array(hist).sum(1)}")
 
 
+def run_otf_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, Hm, pad_to=None, scale=None):
+    """On-the-fly measurement padding / resampling (models.py:81-86, :384-412): the model holds
+    (S, Hm, Hm) frames; get_measurements pastes them into the canvas and/or resamples to n."""
+    scan, probe, H, occu, obja, objp, _, _ = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
+    rng = np.random.default_rng(seed + 7)
+    S = scan.crop_pos.shape[0]
+    meas_small = rng.uniform(0.0, 2.0 / (Hm * Hm), (S, Hm, Hm)).astype(np.float32)
+    iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas_small, scan.n_slow, scan.n_fast)
+    if pad_to is not None:
+        h1 = (pad_to - Hm) // 2
+        iv["on_the_fly_meas_padded"] = rng.uniform(0.0, 1e-4, (pad_to, pad_to)).astype(np.float32)
+        iv["on_the_fly_meas_padded_idx"] = np.array([h1, h1 + Hm, h1, h1 + Hm], np.int32)
+    if scale is not None:
+        iv["on_the_fly_meas_scale_factors"] = [float(scale), float(scale)]
+    model = build_model(iv, 5e-4)
+    loss_fn = losses.CombinedLoss(DEFAULT_LOSS, device="cpu")
+    batch = np.random.default_rng(seed + 100).permutation(S)[:B].astype(np.int64)
+    dp = model(batch)
+    mdp = model.get_measurements(batch)
+    total, terms = loss_fn(dp, mdp, model._current_object_patches, model.omode_occu)
+    total.backward()
+    out = dict(obja=model.opt_obja.detach().numpy(), objp=model.opt_objp.detach().numpy(),
+               probe=torch.view_as_complex(model.opt_probe.detach()).numpy(),
+               shifts=model.opt_probe_pos_shifts.detach().numpy(),
+               crop_pos=scan.crop_pos, H=model.H.numpy(), occu=model.omode_occu.numpy(), batch=batch,
+               loss_params=json.dumps(DEFAULT_LOSS), shift_probes=True, meas_small=meas_small,
+               meas_otf=mdp.detach().numpy(), dp=dp.detach().numpy(),
+               loss_terms=np.array([float(t) for t in terms], np.float64), loss_total=np.float64(float(total)),
+               g_obja=model.opt_obja.grad.numpy(), g_objp=model.opt_objp.grad.numpy(),
+               g_probe=model.opt_probe.grad.numpy(), g_shifts=model.opt_probe_pos_shifts.grad.numpy())
+    for k in ("on_the_fly_meas_padded", "on_the_fly_meas_padded_idx", "on_the_fly_meas_scale_factors"):
+        if k in iv:
+            out[k] = np.asarray(iv[k])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: loss={float(total):.7g} meas_otf {tuple(mdp.shape)}")
+
+
 def constrained_trajectory():
     """3 iterations with the schema-default constraints (obj_rblur off: torchvision is absent)."""
     import copy
@@ -236,6 +273,11 @@ if __name__ == "__main__":
     torch.set_num_threads(4)
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--otf-only":
+        run_otf_case("otf_n32_pad", 32, 2, 1, 1, 4, 4, 6, seed=51, Hm=24, pad_to=32)
+        run_otf_case("otf_n32_resample", 32, 1, 1, 2, 4, 4, 5, seed=52, Hm=16, scale=2.0)
+        run_otf_case("otf_n32_pad_resample", 32, 1, 2, 1, 4, 4, 6, seed=53, Hm=20, pad_to=24, scale=1.3334)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--prop-only":
         PROP_LR.update(slice_thickness=1e-3)                         # case 3

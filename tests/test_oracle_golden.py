@@ -156,3 +156,31 @@ def test_oracle_propagator_gradient_matches_reference(path):
     if case in (1, 2):
         np.testing.assert_allclose(gt, d["g_obj_tilts"][0], rtol=2e-3, atol=1e-3 * np.abs(d["g_obj_tilts"]).max())
 
+
+OTF = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "otf_*.npz")))
+
+
+def otf_args(z):
+    return (z["on_the_fly_meas_padded"] if "on_the_fly_meas_padded" in z else None,
+            z["on_the_fly_meas_padded_idx"] if "on_the_fly_meas_padded_idx" in z else None,
+            z["on_the_fly_meas_scale_factors"] if "on_the_fly_meas_scale_factors" in z else None)
+
+
+@pytest.mark.parametrize("path", OTF, ids=[os.path.basename(p)[:-4] for p in OTF])
+def test_oracle_on_the_fly_measurements_match_reference(path):
+    """get_measurements with on-the-fly padding / resampling (models.py:384-412), and the
+    loss / gradients computed on those DPs, against the reference."""
+    z = np.load(path, allow_pickle=False)
+    got = orc.otf_measurements(z["meas_small"], z["batch"], *otf_args(z))
+    assert rel(got, z["meas_otf"]) < 2e-6
+    S = z["shifts"].shape[0]
+    meas = orc.otf_measurements(z["meas_small"], np.arange(S), *otf_args(z))
+    terms, dps, g = orc.forward_loss_grad(z["obja"], z["objp"], z["probe"], z["shifts"], z["crop_pos"], z["H"],
+                                          z["occu"], meas, [z["batch"]], json.loads(str(z["loss_params"])))
+    assert rel(dps[0], z["dp"]) < 2e-6
+    np.testing.assert_allclose(terms[0], z["loss_terms"], rtol=1e-6, atol=1e-8)
+    assert rel(g["obja"], z["g_obja"]) < 5e-5
+    assert rel(g["objp"], z["g_objp"]) < 5e-5
+    gp = z["g_probe"][..., 0] + 1j * z["g_probe"][..., 1]
+    assert rel(g["probe"], gp) < 5e-5
+
