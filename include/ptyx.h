@@ -70,6 +70,11 @@ typedef struct ptyx_inputs {
   const float *omode_occu; /* (O,)         f32                                               */
   const int32_t *crop_pos; /* (n_scans,2)  i32  integer top-left (y,x) of each patch          */
   const void *meas;        /* (n_scans,N,N) f32 (or f16 with PTYX_MEAS_F16), fftshifted DPs  */
+  /* per-position object tilts (tilt_type 'each', get_propagators models.py:330-356): position s
+   * propagates with H ⊙ exp(i dz (Ky tan(θy_s/1e3) + Kx tan(θx_s/1e3))).  NULL = none. */
+  const float *obj_tilts;  /* (n_scans,2)  f32  PtychoAD.opt_obj_tilts, mrad                  */
+  const float *kvec;       /* (N)          f32  propagator_grid k values (Ky[:,0] = Kx[0,:])  */
+  float dz;                /* slice thickness used by the tilt ramps                           */
 } ptyx_inputs;
 
 typedef struct ptyx_grads {
@@ -81,6 +86,8 @@ typedef struct ptyx_grads {
                       behind optimised obj_tilts / slice_thickness (get_propagators cases 1, 2A, 3,
                       src/ptyrad/models.py:339-356).  Needs a PTYX_PROP_GRAD plan; runs the general
                       (two-pass) engine; Nz = 1 adds nothing (H is unused). */
+  float *d_tilts;  /* (n_scans,2)   += dL/dobj_tilts (per-position tilts, mrad) or NULL; needs
+                      inputs.obj_tilts and a PTYX_PROP_GRAD plan (general engine). */
 } ptyx_grads;
 
 /* CombinedLoss terms on the hot path (params/loss_params.py defaults in brackets). */

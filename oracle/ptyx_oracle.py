@@ -256,7 +256,9 @@ def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, 
     for sl in range(Nz - 1, -1, -1):
         if sl < Nz - 1:                                 # adjoint of F^-1 H F is F^-1 conj(H) F
             G = _fft2(g)
-            dH += (np.conj(cache.X[sl]) * G).sum(axis=(0, 1, 2)) / (n * n)   # dL/dH (real-view convention)
+            dHb = (np.conj(cache.X[sl]) * G).sum(axis=(1, 2)) / (n * n)      # per pattern (B,N,N)
+            cache.dHb = dHb if sl == Nz - 2 else cache.dHb + dHb
+            dH += dHb.sum(axis=0)                                              # dL/dH (real-view convention)
             g = _ifft2(np.conj(Hc) * G).astype(cdt)
         gO[:, :, sl] = (np.conj(cache.psis[sl]) * g).sum(axis=1)   # Σ_p conj(ψ^n) g
         g = g * np.conj(Oc[:, None, :, sl])
@@ -281,9 +283,19 @@ def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, 
     return dA, dP, dprobe, dshift
 
 
+def tilt_ramps(tilts_b, n, dx, dz):
+    """Per-position propagator factor exp(i dz (Ky tan θy + Kx tan θx)) (models.py:330-356),
+    (B,N,N), and the k grid (create_grids models.py:163-171)."""
+    g = (np.arange(-n // 2, n // 2) + 0.5) / n
+    k1 = np.fft.ifftshift(2 * np.pi * g / dx)
+    t = np.asarray(tilts_b, np.float64) / 1e3
+    ph = dz * (k1[None, :, None] * np.tan(t[:, 0, None, None]) + k1[None, None, :] * np.tan(t[:, 1, None, None]))
+    return np.exp(1j * ph), k1
+
+
 def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batches, loss_params,
                       shift_probes=True, grad_scale=1.0, cdt=np.complex128, detector_blur_std=None,
-                      obj_preblur_std=None):
+                      obj_preblur_std=None, tilts=None, dx=None, dz=None):
     """Oracle of ptyx_forward_loss_grad: per-mini-batch losses, gradients accumulated over batches.
 
     batches: list of index arrays (each its own NRMSE normalisation, losses.py:45-47);
@@ -298,6 +310,7 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     g_probe = np.zeros(probe.shape, np.complex128)
     g_shifts = np.zeros(shifts.shape, np.float64)
     g_H = np.zeros(probe.shape[-2:], np.complex128)
+    g_tilts = None if tilts is None else np.zeros(np.shape(tilts), np.float64)
     all_terms, dps = [], []
     for idx in batches:
         idx = np.asarray(idx)
@@ -305,13 +318,23 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
         if obj_preblur_std:                                        # models.py:275-284
             amp, ph = gaussian_blur(amp, obj_preblur_std), gaussian_blur(ph, obj_preblur_std)
         probes = get_probes(probe, shifts[idx], shift_probes, cdt)
-        cache = forward(amp, ph, probes, H, occu, cdt=cdt)
+        Hx = H
+        if tilts is not None:                                      # per-position tilts (tilt_type 'each')
+            ramp, k1 = tilt_ramps(np.asarray(tilts)[idx], n, dx, dz)
+            Hx = (np.asarray(H, np.complex128)[None] * ramp)[:, None, None]
+        cache = forward(amp, ph, probes, Hx, occu, cdt=cdt)
         dp = gaussian_blur(cache.dp, detector_blur_std) if detector_blur_std else cache.dp   # :379-380
         terms, dLdI, dph = loss_terms(dp, meas[idx], ph, occu, loss_params)
         if detector_blur_std:
             dLdI = gaussian_blur_adjoint(dLdI, detector_blur_std)
-        dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], H, occu,
+        dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], Hx, occu,
                                          shift_probes, cdt)
+        if tilts is not None and amp.shape[2] > 1:                # dL/dθ_b = Re Σ conj(g_Hb) ∂H_b/∂θ_b
+            Hb = Hx[:, 0, 0]
+            t = np.asarray(tilts, np.float64)[idx] / 1e3
+            w = np.real(np.conj(cache.dHb) * 1j * Hb)
+            g_tilts[idx, 0] += grad_scale * dz * (w * k1[None, :, None]).sum(axis=(1, 2)) / np.cos(t[:, 0]) ** 2 / 1e3
+            g_tilts[idx, 1] += grad_scale * dz * (w * k1[None, None, :]).sum(axis=(1, 2)) / np.cos(t[:, 1]) ** 2 / 1e3
         if obj_preblur_std:
             dA, dP = gaussian_blur_adjoint(dA, obj_preblur_std), gaussian_blur_adjoint(dP, obj_preblur_std)
         for i, s in enumerate(idx):
@@ -323,7 +346,7 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
         g_H += grad_scale * cache.dH
         all_terms.append(terms)
         dps.append(dp)
-    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts, H=g_H)
+    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts, H=g_H, tilts=g_tilts)
     return np.array(all_terms), dps, grads
 
 

@@ -46,12 +46,14 @@ class Dims(ctypes.Structure):
 class Inputs(ctypes.Structure):
     _fields_ = [("obja", ctypes.c_void_p), ("objp", ctypes.c_void_p), ("probe", ctypes.c_void_p),
                 ("shifts", ctypes.c_void_p), ("H", ctypes.c_void_p), ("omode_occu", ctypes.c_void_p),
-                ("crop_pos", ctypes.c_void_p), ("meas", ctypes.c_void_p)]
+                ("crop_pos", ctypes.c_void_p), ("meas", ctypes.c_void_p), ("obj_tilts", ctypes.c_void_p),
+                ("kvec", ctypes.c_void_p), ("dz", ctypes.c_float)]
 
 
 class Grads(ctypes.Structure):
     _fields_ = [("d_obja", ctypes.c_void_p), ("d_objp", ctypes.c_void_p),
-                ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p), ("d_H", ctypes.c_void_p)]
+                ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p), ("d_H", ctypes.c_void_p),
+                ("d_tilts", ctypes.c_void_p)]
 
 
 class LossCfg(ctypes.Structure):

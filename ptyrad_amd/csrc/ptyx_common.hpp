@@ -62,6 +62,11 @@ struct KArgs {
   float2* ogscr;
   // propagator gradient (PTYX_PROP_GRAD): per-workgroup dL/dH slabs; F(ψⁿ⊙Oⁿ) parked after gacc
   float2* hslab;
+  // per-position tilts: ramps exp(i dz k tan(θ/1e3)) along y and x, and their gradient
+  const float* ptilt;
+  const float* kvec;
+  float dz;
+  float* d_tilts;
 };
 
 // ---------------------------------------------------------------- small helpers

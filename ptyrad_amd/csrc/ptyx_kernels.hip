@@ -45,7 +45,8 @@ template <int N, int NT, bool STORE_PSI, class Arr>
 __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, const float2* tw,
                                               const float2* wy, const float2* wx,
                                               const PatternGeom& g, int p, int o, float2* psi,
-                                              bool sparse, float& sp_acc, float2* xs = nullptr) {
+                                              bool sparse, float& sp_acc, float2* xs = nullptr,
+                                              const float2* ty = nullptr, const float2* tx = nullptr) {
   constexpr int N2 = N * N;
   constexpr float inv_n2 = 1.0f / (float)N2;
   auto mul_obj = [&](int n, int y, int x, float2 w) -> float2 {
@@ -88,6 +89,7 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
         [&](int y, int x, float2& v) {
           if (STORE_PSI && xs) xs[(size_t)(n - 1) * N2 + y * N + x] = v;
           v = cmul(v, a.H[y * N + x]);
+          if (ty) v = cmul(v, cmul(ty[y], tx[x]));
           return true;
         });
     fft2d<N, NT, +1, true>(
@@ -99,6 +101,20 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
           return true;
         });
   }
+}
+
+// per-position tilt ramps of pattern s: ty[y] = exp(i dz Ky[y] tan(θy/1e3)), tx likewise
+// (the separable factor of exp(i dz (Ky tan θy + Kx tan θx)), models.py:330-356)
+template <int N, int NT>
+__device__ __forceinline__ void build_tilt_ramps(const KArgs& a, int s, float2* ty, float2* tx) {
+  const float tty = tanf(a.ptilt[2 * s] / 1e3f), ttx = tanf(a.ptilt[2 * s + 1] / 1e3f);
+  for (int k = opaque_tid(); k < 2 * N; k += NT) {
+    const int kk = k % N;
+    float sn, cs;
+    sincosf(a.dz * a.kvec[kk] * (k < N ? tty : ttx), &sn, &cs);
+    (k < N ? ty : tx)[kk] = make_float2(cs, sn);
+  }
+  __syncthreads();
 }
 
 // =====================================================================================
@@ -138,7 +154,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
   constexpr bool LDS = Geo<N>::kLds;
   constexpr int N2 = N * N;
   constexpr float inv_n = 1.0f / (float)N;
-  __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
+  __shared__ float2 s_tw[N], s_wy[N], s_wx[N], s_ty[N], s_tx[N];
   __shared__ float s_red[(NT / 64) * 4];
   __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
@@ -155,6 +171,8 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
   for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
     const PatternGeom g = pattern_geom(a, pat, N);
     if (a.shift) build_ramps<N, NT>(g, s_wy, s_wx);
+    const bool tilt = a.ptilt != nullptr && a.Nz > 1;
+    if (tilt) build_tilt_ramps<N, NT>(a, g.s, s_ty, s_tx);
     float sums[4] = {0.f, 0.f, 0.f, 0.f};
     auto add_sums = [&](float I, float M) {
       if (a.single_on) {
@@ -173,7 +191,8 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
-        forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp);
+        forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
+                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr);
         const float occ = a.occu[o];
         const bool first = (p == 0 && o == 0);
         // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
@@ -295,7 +314,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   constexpr int N2 = N * N;
   constexpr float inv_n = 1.0f / (float)N;
   constexpr float inv_n2 = 1.0f / (float)N2;
-  __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
+  __shared__ float2 s_tw[N], s_wy[N], s_wx[N], s_ty[N], s_tx[N];
   __shared__ float s_red[(NT / 64) * 2];
   __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
@@ -310,7 +329,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   float2* gacc = psi + (size_t)a.Nz * N2;
   float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
   // propagator gradient: dL/dH += Σ_{p,o,n<Nz-1} conj(Xⁿ) ⊙ F(g^{n+1}) / N²  (ψ^{n+1} = F⁻¹(H Xⁿ))
-  float2* xs = a.hslab ? gacc + N2 : nullptr;
+  float2* xs = (a.hslab || a.d_tilts) ? gacc + N2 : nullptr;
   float2* hsl = a.hslab ? a.hslab + (size_t)blockIdx.x * N2 : nullptr;
   if (a.need_probe)
     for (int e = threadIdx.x; e < a.P * N2; e += NT) slab[e] = make_float2(0.f, 0.f);
@@ -334,7 +353,10 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
       c2 = a.coef[(size_t)m * kNCoef + 1];
     }
     if (a.shift) build_ramps<N, NT>(g, s_wy, s_wx);
+    const bool tilt = a.ptilt != nullptr && a.Nz > 1;
+    if (tilt) build_tilt_ramps<N, NT>(a, g.s, s_ty, s_tx);
     float ds[2] = {0.f, 0.f};
+    float dt[2] = {0.f, 0.f};   // Σ_k Ky (resp. Kx) · Re(i conj(g_Hb) H_b)
     const float* Ip = (SINGLE || EXT) ? nullptr : a.Ibuf + (size_t)pat * N2;
 
     for (int p = 0; p < a.P; ++p) {
@@ -342,7 +364,8 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
         const float occ = a.occu[o];
         const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
         float dummy = 0.f;
-        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs);
+        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
+                                   tilt ? s_ty : nullptr, tilt ? s_tx : nullptr);
         // far field → g_Ψ = 2 occ Ψ ∂L/∂I  (left in natural FFT order)
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v) { return v; },
@@ -410,8 +433,23 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
               arr, s_tw, [&](int, int, float2 v) { return v; },
               [&](int y, int x, float2& v) {
                 const int e = y * N + x;
-                if (hsl) hsl[e] = cadd(hsl[e], cscale(cmulc(v, xs[(size_t)n * N2 + e]), inv_n2));
-                v = cmulc(v, a.H[e]);
+                float2 Hb = a.H[e];
+                if (tilt) {
+                  const float2 r = cmul(s_ty[y], s_tx[x]);
+                  Hb = cmul(Hb, r);
+                  if (xs) {
+                    const float2 q = cscale(cmulc(v, xs[(size_t)n * N2 + e]), inv_n2);   // g_{H_b}
+                    if (hsl) hsl[e] = cadd(hsl[e], cmulc(q, r));                        // conj(r) g_{H_b}
+                    if (a.d_tilts) {
+                      const float w = -cmulc(Hb, q).y;   // Re(i conj(q) H_b) = -Im(H_b conj(q))
+                      dt[0] = fmaf(a.kvec[y], w, dt[0]);
+                      dt[1] = fmaf(a.kvec[x], w, dt[1]);
+                    }
+                  }
+                } else if (hsl) {
+                  hsl[e] = cadd(hsl[e], cscale(cmulc(v, xs[(size_t)n * N2 + e]), inv_n2));
+                }
+                v = cmulc(v, Hb);
                 return true;
               });
           fft2d<N, NT, +1, true>(
@@ -456,6 +494,15 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
       if (threadIdx.x == 0) {
         atomicAdd(a.d_shifts + 2 * g.s, ds[0] * inv_n2);
         atomicAdd(a.d_shifts + 2 * g.s + 1, ds[1] * inv_n2);
+      }
+    }
+    if (tilt && a.d_tilts) {
+      __syncthreads();
+      block_sum<NT, 2>(dt, s_red);
+      if (threadIdx.x == 0) {   // ∂/∂θ (mrad) of tan(θ/1e3) = sec²(θ/1e3)/1e3
+        const float cy = cosf(a.ptilt[2 * g.s] / 1e3f), cx = cosf(a.ptilt[2 * g.s + 1] / 1e3f);
+        atomicAdd(a.d_tilts + 2 * g.s, dt[0] * a.dz / (cy * cy) / 1e3f);
+        atomicAdd(a.d_tilts + 2 * g.s + 1, dt[1] * a.dz / (cx * cx) / 1e3f);
       }
     }
     __syncthreads();
@@ -846,6 +893,7 @@ static int check_inputs(const ptyx_plan* pl, const ptyx_inputs* in, bool need_me
     return fail(PTYX_EINVAL, "a required input pointer is null");
   if (pl->d.Nz > 1 && !in->H) return fail(PTYX_EINVAL, "H is required for Nz > 1");
   if (need_meas && !in->meas) return fail(PTYX_EINVAL, "meas is null");
+  if (in->obj_tilts && !in->kvec) return fail(PTYX_EINVAL, "per-position tilts need kvec");
   return PTYX_OK;
 }
 
@@ -861,6 +909,7 @@ static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t
   a.shifts = in->shifts; a.crop = in->crop_pos;
   a.H = reinterpret_cast<const float2*>(in->H);
   a.occu = in->omode_occu; a.meas = in->meas;
+  a.ptilt = in->obj_tilts; a.kvec = in->kvec; a.dz = in->dz;
   a.idx = idx; a.n_idx = n_idx;
   a.Ibuf = pl->Ibuf;
   a.slab = pl->slab; a.scratch = pl->scratch; a.scratch_stride = pl->scratch_stride;
@@ -1187,9 +1236,12 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
 
 // propagator gradient: validate the request and point the kernels at the plan's slabs
 static int setup_prop_grad(const ptyx_plan* pl, const ptyx_grads& gz, KArgs& a) {
-  if (!gz.d_H) return PTYX_OK;
-  if (!(pl->d.flags & PTYX_PROP_GRAD)) return fail(PTYX_EINVAL, "d_H needs a plan created with PTYX_PROP_GRAD");
-  a.hslab = pl->hslab;   // null when Nz == 1: H is unused, nothing to add
+  if (!gz.d_H && !gz.d_tilts) return PTYX_OK;
+  if (!(pl->d.flags & PTYX_PROP_GRAD))
+    return fail(PTYX_EINVAL, "d_H / d_tilts need a plan created with PTYX_PROP_GRAD");
+  if (gz.d_tilts && !a.ptilt) return fail(PTYX_EINVAL, "d_tilts needs inputs.obj_tilts");
+  a.hslab = gz.d_H ? pl->hslab : nullptr;   // null when Nz == 1: H is unused, nothing to add
+  a.d_tilts = pl->d.Nz > 1 ? gz.d_tilts : nullptr;
   return PTYX_OK;
 }
 
@@ -1237,7 +1289,8 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.d_shifts = gz.d_shifts;
   a.need_probe = gz.d_probe != nullptr;
   if ((rc = setup_prop_grad(pl, gz, a))) return rc;
-  const bool want_H = a.hslab != nullptr;   // general two-pass engine only
+  // propagator gradients and per-position tilts: general two-pass engine only
+  const bool want_H = a.hslab != nullptr || a.d_tilts != nullptr || (a.ptilt != nullptr && pl->d.Nz > 1);
 
   a.w1 = cfg->single_w;
   a.w2 = cfg->poissn_w;
@@ -1248,7 +1301,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     const char* dbg = std::getenv("PTYX_DEBUG_NOWAIT");
     a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
   }
-  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || want_H;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts;
   const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
   // one pass per pattern (k_fused2) when every mini-batch fits the co-resident grid, the call
   // fits the object-gradient slots and exactly one data term is on (its coefficient factors out)
@@ -1337,7 +1390,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   if (n_idx == 0 || !grads) return PTYX_OK;
   if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
   const ptyx_grads gz = *grads;
-  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H)) return PTYX_OK;
+  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts)) return PTYX_OK;
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   KArgs a = make_args(pl, in, idx, n_idx);

@@ -99,7 +99,7 @@ class Plan:
             pass
 
     # ------------------------------------------------------------------ marshalling
-    def _inputs(self, obja, objp, probe_rv, shifts, H, occu, crop_pos, meas):
+    def _inputs(self, obja, objp, probe_rv, shifts, H, occu, crop_pos, meas, tilts=None, kvec=None, dz=0.0):
         d, dev = self.dims, self.device
         _need(obja, torch.float32, "obja", dev)
         _need(objp, torch.float32, "objp", dev)
@@ -123,8 +123,14 @@ class Plan:
             _need(meas, torch.float16 if self.meas_f16 else torch.float32, "meas", dev)
             if tuple(meas.shape) != (d.n_scans, d.N, d.N):
                 raise ValueError(f"meas shape {tuple(meas.shape)} != {(d.n_scans, d.N, d.N)}")
+        if tilts is not None:
+            _need(tilts, torch.float32, "obj_tilts", dev)
+            _need(kvec, torch.float32, "kvec", dev)
+            if tuple(tilts.shape) != (d.n_scans, 2) or tuple(kvec.shape) != (d.N,):
+                raise ValueError("per-position obj_tilts must be (n_scans, 2) and kvec (N,)")
         inp = _lib.Inputs(_ptr(obja), _ptr(objp), _ptr(probe_rv), _ptr(shifts), _ptr(H), _ptr(occu),
-                          _ptr(crop_pos), _ptr(meas))
+                          _ptr(crop_pos), _ptr(meas), _ptr(tilts), _ptr(kvec if tilts is not None else None),
+                          float(dz))
         return inp, H
 
     def _idx(self, idx):
@@ -137,14 +143,15 @@ class Plan:
         grads = grads or {}
         d, dev = self.dims, self.device
         for k, shape in (("obja", (d.O, d.Nz, d.Ny, d.Nx)), ("objp", (d.O, d.Nz, d.Ny, d.Nx)),
-                         ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2)), ("H", (d.N, d.N, 2))):
+                         ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2)), ("H", (d.N, d.N, 2)),
+                         ("tilts", (d.n_scans, 2))):
             g = grads.get(k)
             if g is not None:
                 _need(g, torch.float32, f"grad {k}", dev)
                 if tuple(g.shape) != shape:
                     raise ValueError(f"grad {k} shape {tuple(g.shape)} != {shape}")
         return _lib.Grads(_ptr(grads.get("obja")), _ptr(grads.get("objp")), _ptr(grads.get("probe")),
-                          _ptr(grads.get("shifts")), _ptr(grads.get("H")))
+                          _ptr(grads.get("shifts")), _ptr(grads.get("H")), _ptr(grads.get("tilts")))
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -171,7 +178,7 @@ class Plan:
         if dp_out is None:
             dp_out = torch.empty((n, self.dims.N, self.dims.N), dtype=torch.float32, device=self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
-                                  t["crop_pos"], None)
+                                  t["crop_pos"], None, t.get("tilts"), t.get("kvec"), t.get("dz", 0.0))
         step = max(1, int(self.dims.max_patterns))
         for a in range(0, n, step):
             b = min(n, a + step)
@@ -206,7 +213,7 @@ class Plan:
         if loss_terms is None:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
-                                  t["crop_pos"], t["meas"])
+                                  t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0))
         cfg = loss_cfg.to_c(grad_scale, max_batch)
         g = self._grads(grads)
         _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
@@ -245,7 +252,7 @@ class Plan:
         n = int(idx_t.numel())
         _need(dLdI, torch.float32, "dLdI", self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
-                                  t["crop_pos"], None)
+                                  t["crop_pos"], None, t.get("tilts"), t.get("kvec"), t.get("dz", 0.0))
         g = self._grads(grads)
         step = max(1, int(self.dims.max_patterns))
         for a in range(0, n, step):   # pieces of max_patterns: the external-loss adjoint is per pattern

@@ -24,8 +24,9 @@ returns dL/dH (PTYX_PROP_GRAD), which torch autograd carries to dz / tilts (an (
 On-the-fly measurement padding / resampling (models.py:384-412) runs as ptyx_meas_gather; engine
 calls then take call-local positions / shifts / DPs (rows 0..n-1 of plan-sized arrays).
 
-Out of scope on the HIP path (raises NotImplementedError): per-position tilts (tilt_type 'each',
-models.py:330-335).
+Per-position tilts (tilt_type 'each', models.py:330-356), fixed or optimised, run in the engine
+(per-pattern separable ramps, d_tilts).  Out of scope (raises NotImplementedError): per-position
+tilts together with an optimised slice thickness.
 """
 from __future__ import annotations
 
@@ -44,39 +45,39 @@ _PARAM_NAMES = ("obja", "objp", "obj_tilts", "slice_thickness", "probe", "probe_
 class _EngineForward(torch.autograd.Function):
     """dp = PtychoAD.forward(idx); backward = ptyx_adjoint_dldi (autograd of models.py:422-436).
 
-    ``plan`` / ``base`` (occu, crop_pos) name the geometry: the model's own plan, or a patch-stack
-    plan when the object patches are pre-blurred (stages.BlurredPatches).  ``H_rv`` is the
-    propagator (N,N,2); its gradient (optimised tilts / thickness) comes from the engine's d_H."""
+    ``plan`` / ``base`` (occu, crop_pos, tilt grid) name the geometry: the model's own plan, or a
+    patch-stack / call-local plan.  ``H_rv`` is the propagator (N,N,2) and ``tilts`` the
+    per-position tilts (or None); their gradients come from the engine's d_H / d_tilts."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, plan, base, idx_t, shift_probes):
+    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, tilts, plan, base, idx_t, shift_probes):
         ctx.plan, ctx.base, ctx.shift_probes = plan, base, shift_probes
-        ctx.save_for_backward(obja, objp, probe_rv, shifts, H_rv, idx_t)
+        ctx.save_for_backward(obja, objp, probe_rv, shifts, H_rv, tilts, idx_t)
         with torch.no_grad():
-            return plan.forward(_tensors(obja, objp, probe_rv, shifts, H_rv, base), idx_t)
+            return plan.forward(_tensors(obja, objp, probe_rv, shifts, H_rv, tilts, base), idx_t)
 
     @staticmethod
     def backward(ctx, grad_dp):
-        obja, objp, probe_rv, shifts, H_rv, idx_t = ctx.saved_tensors
+        obja, objp, probe_rv, shifts, H_rv, tilts, idx_t = ctx.saved_tensors
         want = ctx.needs_input_grad
         grads = {}
-        outs = [None] * 5
+        outs = [None] * 6
         for i, (k, p) in enumerate((("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts),
-                                    ("H", H_rv))):
+                                    ("H", H_rv), ("tilts", tilts))):
             if want[i]:
                 outs[i] = torch.zeros_like(p)
                 grads[k] = outs[i]
         if not ctx.shift_probes:
             grads.pop("shifts", None)
         if grads:
-            ctx.plan.adjoint_dldi(_tensors(obja, objp, probe_rv, shifts, H_rv, ctx.base), idx_t,
+            ctx.plan.adjoint_dldi(_tensors(obja, objp, probe_rv, shifts, H_rv, tilts, ctx.base), idx_t,
                                   grad_dp.contiguous().float(), grads)
         return (*outs, None, None, None, None)
 
 
-def _tensors(obja, objp, probe_rv, shifts, H_rv, base):
+def _tensors(obja, objp, probe_rv, shifts, H_rv, tilts, base):
     t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach(),
-         "H": H_rv.detach()}
+         "H": H_rv.detach(), "tilts": None if tilts is None else tilts.detach().contiguous()}
     t.update(base)
     return t
 
@@ -148,16 +149,20 @@ class PtychoHIP(nn.Module):
             self.shift_probes = bool(self.lr_params.get("probe_pos_shifts", 0) != 0)   # models.py:120
             self.change_thickness = bool(self.lr_params.get("slice_thickness", 0) != 0)
             self.change_tilt = bool(self.lr_params.get("obj_tilts", 0) != 0)
-            if self.tilt_obj and self.opt_obj_tilts.shape[0] != 1:
-                raise NotImplementedError("per-position tilts (tilt_type 'each') are not on the HIP path; "
-                                          "global tilts (fixed or optimised) are")
+            # per-position tilts (tilt_type 'each', models.py:330-356): the engine applies each
+            # position's separable ramp exp(i dz (Ky tan θy + Kx tan θx)) to H itself
+            self.pos_tilts = bool(self.tilt_obj and self.opt_obj_tilts.shape[0] != 1)
+            if self.pos_tilts and self.change_thickness:
+                raise NotImplementedError("per-position tilts together with an optimised slice thickness are not "
+                                          "on the HIP path")
             # models.py:210-219 / :346-349 (case 2B, global): a fixed tilt only changes the one
             # propagator every position uses, so the engine takes the tilted H as its H
-            self.register_buffer("H_eff", self._tilted_H() if self.tilt_obj else self.H)
+            self.register_buffer("H_eff", self._tilted_H() if (self.tilt_obj and not self.pos_tilts) else self.H)
             # cases 1 / 2A / 3 (models.py:339-356): H is rebuilt from the optimised dz / tilts on
             # every call and the engine returns dL/dH (PTYX_PROP_GRAD), which autograd carries on
             self.prop_opt = self.change_thickness or (self.tilt_obj and self.change_tilt)
             self._init_propagator_grid()
+            self._dz = float(self.opt_slice_thickness.detach().cpu())
             self.probe_int_sum = self.get_complex_probe_view().abs().pow(2).sum()
             self.loss_iters, self.iter_times, self.dz_iters, self.avg_tilt_iters = [], [], [], []
             self._current_object_patches = None
@@ -167,6 +172,8 @@ class PtychoHIP(nn.Module):
                 "probe_pos_shifts": self.opt_probe_pos_shifts}
             self.create_optimizable_params_dict(self.lr_params, verbose)
             self._validate_geometry()
+            if self.pos_tilts and self.opt_obj_tilts.shape != (self.crop_pos.shape[0], 2):
+                raise ValueError("per-position obj_tilts must be (N_scans, 2)")
             O, Nz, Ny, Nx = self.opt_obja.shape
             P, N = self.opt_probe.shape[0], self.opt_probe.shape[1]
             n_scans = self.crop_pos.shape[0]
@@ -228,7 +235,7 @@ class PtychoHIP(nn.Module):
     def _propagator(self):
         """get_propagators (models.py:300-360) for a global tilt: the (N, N) complex64 H every
         position uses, differentiable in opt_slice_thickness / opt_obj_tilts when they are optimised."""
-        if not self.prop_opt:
+        if not self.prop_opt or self.pos_tilts:
             return self.H_eff
         Ky, Kx = self.propagator_grid
         dz = self.opt_slice_thickness
@@ -260,11 +267,26 @@ class PtychoHIP(nn.Module):
 
     def _engine_tensors(self):
         return _tensors(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts, self._H_rv(),
-                        self._base())
+                        self._tilts(), self._base())
 
     def _base(self, crop_pos=None, meas=None, stack=False):
-        return {"occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
-                "meas": self.measurements if (meas is None and not stack) else meas}
+        b = {"occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
+             "meas": self.measurements if (meas is None and not stack) else meas}
+        if self.pos_tilts:
+            b.update(kvec=self.propagator_grid[0][:, 0].contiguous(), dz=self._dz)
+        return b
+
+    def _tilts(self, il=None, pad_to=None):
+        """Per-position tilts for an engine call: all positions, or rows ``il`` (call-local /
+        patch-stack calls, zero-padded to ``pad_to`` rows); None without per-position tilts."""
+        if not self.pos_tilts:
+            return None
+        if il is None:
+            return self.opt_obj_tilts
+        t = self.opt_obj_tilts[il]
+        if pad_to is not None and pad_to > t.shape[0]:
+            t = torch.cat([t, t.new_zeros((pad_to - t.shape[0], 2))])
+        return t
 
     # ------------------------------------------------------------------ object pre-blur (stages.py)
     @property
@@ -310,8 +332,8 @@ class PtychoHIP(nn.Module):
             meas = self._gather_meas(idx_t) if self.otf_meas else self.measurements[il].contiguous()
         base = self._base(stack_crop_pos(B, N, idx_t.device), meas, stack=True)
         ar = torch.arange(B, dtype=torch.int32, device=idx_t.device)
-        return (A.reshape(O, Nz, B * N, N), Ph.reshape(O, Nz, B * N, N), sh, self._stack_plan(B), base, ar,
-                (A, Ph))
+        return (A.reshape(O, Nz, B * N, N), Ph.reshape(O, Nz, B * N, N), sh, self._tilts(il), self._stack_plan(B),
+                base, ar, (A, Ph))
 
     def get_obj_patches(self, indices):
         """models.py:251-284: (B,O,Nz,N,N,2) amplitude/phase patches (pre-blurred when enabled)."""
@@ -343,11 +365,17 @@ class PtychoHIP(nn.Module):
         return torch.fft.ifft2(torch.fft.fft2(probe)[None] * w[:, None])
 
     def get_propagators(self, indices):
+        """models.py:300-360: (1,N,N), or (B,N,N) with per-position tilts."""
+        if self.pos_tilts:
+            Ky, Kx = self.propagator_grid
+            t = self.opt_obj_tilts[torch.as_tensor(self._check_indices(indices), device=Ky.device)] / 1e3
+            return self.H * torch.exp(1j * self._dz * (Ky * torch.tan(t[:, 0, None, None]) +
+                                                       Kx * torch.tan(t[:, 1, None, None])))
         return self._propagator()[None,]
 
     def get_propagated_probe(self, index):
         probe = self.get_probes(index)[0].detach()
-        H = self._propagator().detach()[None]
+        H = self.get_propagators(index)[[0]].detach()
         n_slices = self.opt_objp.shape[1]
         out = torch.zeros((n_slices, *probe.shape), dtype=probe.dtype, device=probe.device)
         psi = probe
@@ -394,8 +422,8 @@ class PtychoHIP(nn.Module):
         if with_meas:
             self._gather_meas(idx_t, self._meas_buf[:n])
             meas = self._meas_buf
-        base = {"occu": self.omode_occu, "crop_pos": cp.contiguous(), "meas": meas}
-        return sh, base, torch.arange(n, dtype=torch.int32, device=idx_t.device)
+        base = self._base(cp.contiguous(), meas, stack=True)
+        return sh, self._tilts(il, cap), base, torch.arange(n, dtype=torch.int32, device=idx_t.device)
 
     def get_measurements(self, indices=None):
         """models.py:384-416, including the on-the-fly padding / resampling (HIP gather)."""
@@ -415,18 +443,18 @@ class PtychoHIP(nn.Module):
         idx = self._check_indices(indices)
         idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device, non_blocking=True)
         if self.preblur:
-            A, Ph, sh, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
-            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), plan, base, ar, self.shift_probes)
+            A, Ph, sh, tl, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
+            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), tl, plan, base, ar, self.shift_probes)
             self._current_object_patches = torch.stack([pa, pp], dim=-1).permute(2, 0, 1, 3, 4, 5)
         elif self.otf_meas:
-            sh, base, ar = self._local_inputs(idx_t)
-            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, sh, self._H_rv(), self.plan,
+            sh, tl, base, ar = self._local_inputs(idx_t)
+            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, sh, self._H_rv(), tl, self.plan,
                                       base, ar, self.shift_probes)
             self._current_object_patches = self.get_obj_patches(idx)
         else:
             dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
-                                      self._H_rv(), self.plan, self._base(meas=None, stack=True), idx_t,
-                                      self.shift_probes)
+                                      self._H_rv(), self._tilts(), self.plan, self._base(meas=None, stack=True),
+                                      idx_t, self.shift_probes)
             # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
             self._current_object_patches = self.get_obj_patches(idx)
         if self.detector_blur:                      # get_forward_meas, models.py:375-382

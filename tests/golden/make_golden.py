@@ -70,7 +70,7 @@ def init_variables(obja, objp, probe, H, occu, crop_pos, shifts, meas, n_slow, n
     n = probe.shape[-1]
     return {
         "obj": (obja * np.exp(1j * objp)).astype(np.complex64),
-        "obj_tilts": np.zeros((1, 2), np.float32) if tilts is None else np.asarray(tilts, np.float32).reshape(1, 2),
+        "obj_tilts": np.zeros((1, 2), np.float32) if tilts is None else np.asarray(tilts, np.float32).reshape(-1, 2),
         "slice_thickness": np.float32(dz),
         "probe": probe.astype(np.complex64),
         "probe_pos_shifts": shifts.astype(np.float32),
@@ -161,7 +161,7 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
         out["meas"] = meas
         out["dp"] = dpn
     if tilts is not None:   # fixed global tilt (models.py:346-349, case 2B): H above is the tilted one
-        out.update(H_untilted=model.H.numpy(), obj_tilts=np.asarray(tilts, np.float32).reshape(1, 2),
+        out.update(H_untilted=model.H.numpy(), obj_tilts=np.asarray(tilts, np.float32).reshape(-1, 2),
                    slice_thickness=np.float32(model.opt_slice_thickness.item()), dx=np.float32(model.dx.item()),
                    lambd=np.float32(model.lambd.item()))
     for k, v in BLUR.items():
@@ -176,6 +176,8 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
                    else g(model.opt_obj_tilts),
                    g_slice_thickness=np.float32(0.0) if g(model.opt_slice_thickness) is None
                    else g(model.opt_slice_thickness))
+    if tilts is not None and np.asarray(tilts).size > 2:   # per-position tilts: H is the untilted one
+        out.update(H=model.H.numpy(), tilt_each=True)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
@@ -273,6 +275,14 @@ if __name__ == "__main__":
     torch.set_num_threads(4)
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--each-only":
+        # per-position tilts (tilt_type 'each', models.py:330-356): fixed (case 2B) and optimised (2A)
+        t16 = np.random.default_rng(61).uniform(-4.0, 4.0, (16, 2)).astype(np.float32)
+        run_case("n32_p2o1z3_tilteach", 32, 2, 1, 3, 4, 4, 6, seed=61, tilts=t16)
+        PROP_LR.update(obj_tilts=1e-3)
+        t9 = np.random.default_rng(62).uniform(-4.0, 4.0, (9, 2)).astype(np.float32)
+        run_case("n64_p1o2z2_opttilteach", 64, 1, 2, 2, 3, 3, 5, seed=62, tilts=t9)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--otf-only":
         run_otf_case("otf_n32_pad", 32, 2, 1, 1, 4, 4, 6, seed=51, Hm=24, pad_to=32)

@@ -30,8 +30,8 @@ def test_library_loads_and_exports_all_symbols():
 def test_struct_layouts_match_header():
     # sizes of the C structs (all 4-byte fields / 8-byte pointers, no padding surprises)
     assert ctypes.sizeof(_lib.Dims) == 9 * 4
-    assert ctypes.sizeof(_lib.Inputs) == 8 * 8
-    assert ctypes.sizeof(_lib.Grads) == 5 * 8
+    assert ctypes.sizeof(_lib.Inputs) == 10 * 8 + 8     # + float dz, padded to pointer alignment
+    assert ctypes.sizeof(_lib.Grads) == 6 * 8
     assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
     assert ctypes.sizeof(_lib.ObjConstraints) == 19 * 4
 

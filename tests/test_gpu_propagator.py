@@ -19,10 +19,12 @@ import torch
 
 from oracle import ptyx_oracle as orc
 from tests.test_gpu_model import init_vars, model_params
-from tests.test_oracle_golden import load_case, prop_case, rel
+from tests.test_oracle_golden import load_case, prop_case, rel, tilt_kw
 
 pytestmark = pytest.mark.gpu
-PROP = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz")))
+PROP = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz"))
+              if "each" not in p)
+EACH = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*each.npz")))
 LRS = {"obja": 5e-4, "objp": 5e-4, "obj_tilts": 0.0, "slice_thickness": 0.0, "probe": 1e-4,
        "probe_pos_shifts": 5e-4}
 
@@ -110,3 +112,58 @@ def test_engine_dH_vs_oracle():
     plain = Plan(32, 2, 1, 3, *d["obja"].shape[-2:], S, S, device=device)
     with pytest.raises(_lib.PtyxError, match="PTYX_PROP_GRAD"):
         plain.forward_loss_grad(t, idx, off, cfg, {"H": gH})
+
+
+def _each_model(d, device, max_patterns=None):
+    from ptyrad_amd.models import PtychoHIP
+    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"], d["meas"])
+    iv.update(obj_tilts=d["obj_tilts"], slice_thickness=float(d["slice_thickness"]), dx=float(d["dx"]),
+              lambd=float(d["lambd"]))
+    lrs = {**LRS, **(json.loads(str(d["prop_lr"])) if "prop_lr" in d else {})}
+    return PtychoHIP(iv, model_params(lrs), device=device, verbose=False, max_patterns=max_patterns)
+
+
+@pytest.mark.parametrize("path", EACH, ids=[os.path.basename(p)[:-4] for p in EACH])
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "generic"])
+def test_per_position_tilts_match_reference(path, fused):
+    """tilt_type 'each' (models.py:330-356): fixed (case 2B) and optimised (case 2A) per-position
+    tilts; tilt gradients rel ≤ 1e-4."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = load_case(path)
+    model = _each_model(d, device)
+    loss_fn = CombinedLoss(d["loss_params"], device=device)
+    if fused:
+        total, terms = loss_fn.fused(model, [d["batch"]])
+        terms = terms.detach().cpu().numpy()[0]
+    else:
+        dp = model(d["batch"])
+        assert rel(dp.detach().cpu().numpy(), d["dp"]) < 1e-5
+        total, terms = loss_fn(dp, model.get_measurements(d["batch"]), model._current_object_patches,
+                               model.omode_occu)
+        terms = np.array([float(t.detach()) for t in terms])
+    total.backward()
+    np.testing.assert_allclose(terms, d["loss_terms"], rtol=2e-5, atol=1e-7)
+    assert rel(model.opt_obja.grad.cpu().numpy(), d["g_obja"]) < 5e-5
+    assert rel(model.opt_objp.grad.cpu().numpy(), d["g_objp"]) < 5e-5
+    assert rel(model.opt_probe.grad.cpu().numpy(), d["g_probe"]) < 5e-5
+    if "prop_lr" in d:
+        assert rel(model.opt_obj_tilts.grad.cpu().numpy(), d["g_obj_tilts"]) < 1e-4
+
+
+def test_per_position_tilts_multi_batch_vs_oracle():
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = load_case([p for p in EACH if "opttilt" in p][0])
+    model = _each_model(d, device)
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(9).permutation(S)
+    batches = [perm[:4], perm[4:6], perm[6:9]]
+    total, terms = CombinedLoss(d["loss_params"], device=device).fused(model, batches)
+    total.backward()
+    oterms, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                         d["occu"], d["meas"], batches, d["loss_params"], **tilt_kw(d))
+    np.testing.assert_allclose(terms.detach().cpu().numpy(), oterms, rtol=2e-5, atol=1e-7)
+    assert rel(model.opt_obj_tilts.grad.cpu().numpy(), g["tilts"]) < 1e-4
+    assert rel(model.opt_objp.grad.cpu().numpy(), g["objp"]) < 5e-5
+

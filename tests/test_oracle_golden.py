@@ -36,6 +36,13 @@ def load_case(path):
     return d
 
 
+def tilt_kw(d):
+    """Per-position tilt arguments of a tilt_type 'each' fixture (make_golden.py --each-only)."""
+    if "tilt_each" not in d:
+        return {}
+    return {"tilts": d["obj_tilts"], "dx": float(d["dx"]), "dz": float(d["slice_thickness"])}
+
+
 def blur_kw(d):
     """Optional-stage options a fixture was made with (make_golden.py --blur-only)."""
     return {k: float(d[k]) for k in ("detector_blur_std", "obj_preblur_std") if k in d}
@@ -56,7 +63,8 @@ def test_oracle_matches_reference(path):
     d = load_case(path)
     terms, dps, g = orc.forward_loss_grad(
         d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"],
-        d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]), **blur_kw(d))
+        d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]), **blur_kw(d),
+        **tilt_kw(d))
     dp = dps[0]
     if "dp" in d:
         assert rel(dp, d["dp"]) < 2e-6
@@ -70,6 +78,8 @@ def test_oracle_matches_reference(path):
     assert rel(g["probe"], gp) < 5e-5
     if d["shift_probes"]:
         assert rel(g["shifts"], d["g_shifts"]) < 1e-4
+    if "tilt_each" in d and "g_obj_tilts" in d:
+        assert rel(g["tilts"], d["g_obj_tilts"]) < 1e-4
 
 
 TRAJ = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "traj_*.npz")))
@@ -131,7 +141,8 @@ def test_oracle_trajectory_matches_reference(path):
     assert rel(prb, z["final_probe"]) < 1e-5
 
 
-PROP = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz")))
+PROP = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*_opt*.npz"))
+              if "each" not in p)
 
 
 def prop_case(d):
