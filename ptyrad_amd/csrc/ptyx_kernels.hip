@@ -46,7 +46,8 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
                                               const float2* wy, const float2* wx,
                                               const PatternGeom& g, int p, int o, float2* psi,
                                               bool sparse, float& sp_acc, float2* xs = nullptr,
-                                              const float2* ty = nullptr, const float2* tx = nullptr) {
+                                              const float2* ty = nullptr, const float2* tx = nullptr,
+                                              float2* psi0 = nullptr, bool reuse0 = false) {
   constexpr int N2 = N * N;
   constexpr float inv_n2 = 1.0f / (float)N2;
   auto mul_obj = [&](int n, int y, int x, float2 w) -> float2 {
@@ -63,13 +64,24 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
   const float2* Fp = a.Fp + (size_t)p * N2;
   const float2* P0 = a.probe + (size_t)p * N2;
   // ψ^0: shifted probe F^-1(F(P) ⊙ W_b)   (image_proc.py:532) or the broadcast probe
-  if (a.shift) {
+  // psi0 (multi-object-mode calls): ψ⁰ of probe mode p depends on p only, so the o = 0 pass parks
+  // it there and the o > 0 passes reload it instead of repeating the inverse FFT
+  if (a.shift && reuse0) {
+    for (int e = opaque_tid(); e < N2; e += NT) {
+      const int y = e / N, x = e % N;
+      const float2 w = psi0[e];
+      if (STORE_PSI && psi != psi0) psi[e] = w;
+      arr.st(y, x, mul_obj(0, y, x, w));
+    }
+    __syncthreads();
+  } else if (a.shift) {
     fft2d<N, NT, +1, false>(
         arr, tw,
         [&](int y, int x, float2) { return cmul(cmul(Fp[y * N + x], wy[y]), wx[x]); },
         [&](int y, int x, float2& v) {
           const float2 w = cscale(v, inv_n2);
           if (STORE_PSI) psi[y * N + x] = w;
+          if (psi0 && !(STORE_PSI && psi == psi0)) psi0[y * N + x] = w;
           v = mul_obj(0, y, x, w);
           return true;
         });
@@ -187,12 +199,13 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
       }
     };
     float* Ip = SINGLE ? nullptr : a.Ibuf + (size_t)pat * N2;
+    float2* psi0 = scratch_psi<N>(a);   // this workgroup's ψ⁰ park (multi-object-mode calls)
     for (int p = 0; p < a.P; ++p) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
         forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
-                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr);
+                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, a.O > 1 ? psi0 : nullptr, o > 0);
         const float occ = a.occu[o];
         const bool first = (p == 0 && o == 0);
         // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
         const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
         float dummy = 0.f;
         forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
-                                   tilt ? s_ty : nullptr, tilt ? s_tx : nullptr);
+                                   tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0);
         // far field → g_Ψ = 2 occ Ψ ∂L/∂I  (left in natural FFT order)
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v) { return v; },
