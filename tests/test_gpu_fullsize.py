@@ -1,0 +1,88 @@
+"""The bench workload at its full size on MI355X (c2: 256×256 scan = 65,536 patterns, N = 128,
+object 1033², mini-batches of 32, one engine call), checked through size-independent properties:
+
+* determinism: two identical calls give bitwise-identical loss terms and gradients (fixed-order
+  reductions, no atomics on this path);
+* linearity: grad_scale 0.5 halves every gradient (rel ≤ 1e-6) and leaves the loss terms alone;
+* split invariance: the same batches in two calls give bitwise-identical per-batch loss terms and
+  the same summed gradients (rel ≤ 1e-6; only the summation order differs);
+* locality: each mini-batch's loss terms depend on its own 32 patterns only, so sampled batches
+  of the full call match the oracle run on just those patterns (rtol 1e-5).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptyx_oracle as orc
+from tests.test_oracle_golden import rel
+
+pytestmark = pytest.mark.gpu
+LP = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+      "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+      "loss_pacbed": {"state": False}, "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
+      "loss_simlar": {"state": False}}
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def test_c2_full_call_properties():
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
+    N, S = 128, 256
+    scan = syn.raster_scan(S, S, N, seed=0)
+    Ny, Nx = scan.obj_shape
+    n = S * S
+    g = torch.Generator(device=device)
+    g.manual_seed(1234)
+    obja = (1.0 + 0.05 * torch.randn((1, 1, Ny, Nx), generator=g, device=device)).float()
+    objp = (0.1 * torch.randn((1, 1, Ny, Nx), generator=g, device=device)).float()
+    probe_c = (syn.stem_probe(N) * np.float32(60.0)).astype(np.complex64)
+    gm = torch.Generator(device=device)
+    gm.manual_seed(4321)
+    meas = torch.rand((n, N, N), generator=gm, device=device)
+    H = syn.fresnel_propagator(N, syn.DX_ANG, 2.0)
+    t = {"obja": obja, "objp": objp, "probe": torch.view_as_real(torch.tensor(probe_c, device=device)[None]).contiguous(),
+         "shifts": torch.tensor(scan.shifts, device=device), "H": torch.tensor(H, device=device),
+         "occu": torch.ones(1, device=device), "crop_pos": torch.tensor(scan.crop_pos, device=device), "meas": meas}
+    plan = Plan(N, 1, 1, 1, Ny, Nx, n, n, shift_probes=True, device=device)
+    rng = np.random.default_rng(7)
+    batches = np.array_split(rng.permutation(n), n // 32)
+    cfg = LossConfig.from_loss_params(LP)
+
+    def run(bs, scale=1.0, grads=None):
+        grads = grads if grads is not None else {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+        idx_t = torch.as_tensor(np.concatenate(bs), dtype=torch.int32, device=device)
+        off_t = torch.as_tensor(batch_offsets(bs), device=device)
+        terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=scale, max_batch=32)
+        return terms.cpu().numpy(), grads
+
+    t1, g1 = run(batches)
+    t2, g2 = run(batches)
+    np.testing.assert_array_equal(t1, t2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+    del g2
+    t3, g3 = run(batches, scale=0.5)
+    np.testing.assert_array_equal(t1, t3)
+    for k in g1:
+        assert rel(g3[k].cpu().numpy(), 0.5 * g1[k].cpu().numpy()) < 1e-6, k
+    del g3
+    half = len(batches) // 2
+    ta, gs = run(batches[:half])
+    tb, gs = run(batches[half:], grads=gs)
+    np.testing.assert_array_equal(np.concatenate([ta, tb]), t1)
+    for k in g1:
+        assert rel(gs[k].cpu().numpy(), g1[k].cpu().numpy()) < 1e-6, k
+    del gs
+    oa, op = obja.cpu().numpy(), objp.cpu().numpy()
+    for k in rng.choice(len(batches), 3, replace=False):
+        b = batches[k]
+        mb = meas[torch.as_tensor(b, device=device)].cpu().numpy()
+        oterms, _, _ = orc.forward_loss_grad(oa, op, probe_c[None], scan.shifts[b], scan.crop_pos[b], H,
+                                             np.ones(1, np.float32), mb, [np.arange(len(b))], LP)
+        np.testing.assert_allclose(t1[k], oterms[0], rtol=1e-5, atol=1e-7)
