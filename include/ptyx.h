@@ -188,6 +188,18 @@ int ptyx_patch_gather(void *stream, const float *obj, int32_t O, int32_t Nz, int
 int ptyx_patch_scatter_add(void *stream, const float *gpatches, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
                            const int32_t *crop_pos, const int32_t *idx, int32_t n_idx, int32_t N, float *gobj);
 
+/* loss_pacbed (src/ptyrad/losses.py:77-89) per mini-batch, on model intensities dp (n_idx,N,N)
+ * (e.g. the dp_out of ptyx_forward_loss_grad): loss_terms[m*5 + 2] = w·sqrt(mse(mean_b dp^q…)) /
+ * mean(M^q) written for every batch m; dLdI (n_idx,N,N) = grad_scale · dL/d(dp) (NULL to skip),
+ * which ptyx_adjoint_dldi turns into gradients.  meas (n_scans,N,N) f32 / f16 addressed through
+ * idx like the engine; batch_offsets device int32.  ws: ptyx_pacbed_ws_bytes(N, n_batches) bytes
+ * of device memory, 8-byte aligned; n_batches ≤ 65535; batch_offsets[n_batches] must equal n_idx.
+ * Fixed-order fp64 sums (deterministic). */
+size_t ptyx_pacbed_ws_bytes(int32_t N, int32_t n_batches);
+int ptyx_loss_pacbed(void *stream, const float *dp, const void *meas, int32_t meas_f16, const int32_t *idx,
+                     const int32_t *batch_offsets, int32_t n_batches, int32_t n_idx, int32_t N, float weight,
+                     float dp_pow, float grad_scale, float *loss_terms, float *dLdI, void *ws);
+
 /* PtychoAD.get_measurements(indices) with on-the-fly padding / resampling (models.py:384-412):
  * out (n_idx,Ho,Wo) f32 = interpolate(paste(canvas, meas[idx[b]] at (h1, w1)), scale, bilinear,
  * align_corners=False) / (scale_y·scale_x).  meas (n_scans,Hm,Wm) f32 (f16 when meas_f16);

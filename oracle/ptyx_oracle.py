@@ -221,8 +221,18 @@ def loss_terms(dp, meas, ph, occu, lp):
         mu = Mq.mean()
         terms[1] = -p["weight"] * (Mq * np.log(Iq + e) - Iq).mean() / mu
         dLdI += -p["weight"] / (mu * K) * (Mq / (Iq + e) - 1.0) * q * I ** (q - 1)
-    if lp["loss_pacbed"]["state"] or lp["loss_simlar"]["state"]:
-        raise NotImplementedError("loss_pacbed / loss_simlar are outside the hot-path scope")
+    pb = lp["loss_pacbed"]
+    if pb["state"]:                                                    # losses.py:77-89
+        q = pb.get("dp_pow", 0.2)
+        Ib, Mb = I.mean(axis=0), M.mean(axis=0)
+        d = Ib ** q - Mb ** q
+        mu = (M ** q).mean()
+        rmse = math.sqrt((d * d).mean())
+        terms[2] = pb["weight"] * rmse / mu
+        if rmse > 0:
+            dLdI += pb["weight"] / (mu * d.size * rmse * B) * d * q * Ib ** (q - 1)
+    if lp.get("loss_simlar", {}).get("state", False):
+        raise NotImplementedError("loss_simlar (torchvision gaussian_blur of the object) is outside the hot path")
     sp = lp["loss_sparse"]
     dph = np.zeros(ph.shape, np.float64)
     if sp["state"]:                                                    # losses.py:91-104

@@ -25,7 +25,7 @@ _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
-           "ptyx_meas_gather", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
+           "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
 
@@ -121,6 +121,9 @@ def load(path: str | None = None):
     lib.ptyx_constraints_ws_bytes.restype = ctypes.c_size_t
     lib.ptyx_constraints_evals_offset.restype = ctypes.c_size_t
     lib.ptyx_obj_rblur.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32]
+    lib.ptyx_pacbed_ws_bytes.argtypes = [i32, i32]
+    lib.ptyx_pacbed_ws_bytes.restype = ctypes.c_size_t
+    lib.ptyx_loss_pacbed.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, f32, f32, vp, vp, vp]
     lib.ptyx_meas_gather.argtypes = [vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, i32, i32,
                                      ctypes.c_double, ctypes.c_double, i32, i32, vp]
     lib.ptyx_blur_adjoint.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32]
@@ -138,7 +141,7 @@ def load(path: str | None = None):
     lib.ptyx_meas_stats.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp]
     lib.ptyx_meas_finish.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp, vp, i32]
     for name in ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
-                 "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
+                 "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
                  "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish"):
         getattr(lib, name).restype = ctypes.c_int

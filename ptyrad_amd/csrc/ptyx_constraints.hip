@@ -1,7 +1,9 @@
 // ptyx_constraints.hip — C ABI of the on-device constraints (include/ptyx.h), a translation unit
 // of libptyx.so of its own (kernels in ptyx_constraints.hpp).
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 
@@ -262,4 +264,123 @@ extern "C" int ptyx_probe_ortho(void* stream, float* probe, int32_t P, int32_t N
     default: launch_ortho_apply<16>(st, M, n2, U); break;
   }
   return abi::launch_status("ortho_pmode launch");
+}
+
+// ---------------------------------------------------------------------------------------------
+// loss_pacbed (src/ptyrad/losses.py:77-89) per mini-batch m of B_m patterns:
+//   Ī = mean_b I_b,  M̄ = mean_b M_b (per pixel),  d = Ī^q − M̄^q,
+//   L_m = w · sqrt(Σ_k d_k² / N²) / mean_{b,k} M^q,
+//   dL_m/dI_{b,k} = w / (mu · N² · rmse · B_m) · d_k · q · Ī_k^(q−1).
+// k_pac_pixel: one thread per (pixel, batch): fp64 sums over the batch's patterns in order;
+// k_pac_batch: one workgroup per batch, fixed-order fp64 reduction → L_m and its coefficient;
+// k_pac_dldi: dLdI = grad_scale · coef_m · e_k.  Deterministic; ws = n_batches·(N²·(8+8+4)+16) B.
+namespace {
+__device__ __forceinline__ double pac_pow(double x, float q) {
+  if (q == 1.0f) return x;
+  if (q == 0.5f) return sqrt(x);
+  return x > 0.0 ? pow(x, (double)q) : 0.0;
+}
+
+__global__ __launch_bounds__(256) void k_pac_pixel(const float* __restrict__ dp, const void* __restrict__ meas,
+                                                   int meas_f16, const int* __restrict__ idx,
+                                                   const int* __restrict__ boff, int n2, float q, double* d2,
+                                                   double* mq, float* e) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n2) return;
+  const int m = blockIdx.y;
+  const int b0 = boff[m], b1 = boff[m + 1];
+  double sI = 0.0, sM = 0.0, sMq = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    const size_t moff = (size_t)idx[b] * n2 + k;
+    const double M = meas_f16 ? (double)__half2float(reinterpret_cast<const __half*>(meas)[moff])
+                              : (double)reinterpret_cast<const float*>(meas)[moff];
+    sI += (double)dp[(size_t)b * n2 + k];
+    sM += M;
+    sMq += pac_pow(M, q);
+  }
+  const double inv = b1 > b0 ? 1.0 / (double)(b1 - b0) : 0.0;
+  const double Ib = sI * inv, Mb = sM * inv;
+  const double d = pac_pow(Ib, q) - pac_pow(Mb, q);
+  const size_t o = (size_t)m * n2 + k;
+  d2[o] = d * d;
+  mq[o] = sMq;
+  e[o] = (float)(d * (double)q * (Ib > 0.0 ? pac_pow(Ib, q) / Ib : 0.0));
+}
+
+__global__ __launch_bounds__(256) void k_pac_batch(const double* __restrict__ d2, const double* __restrict__ mq,
+                                                   const int* __restrict__ boff, int n2, float w, double* coef,
+                                                   float* loss_terms) {
+  __shared__ double s0[256], s1[256];
+  const int m = blockIdx.x;
+  double a = 0.0, c = 0.0;
+  for (int k = threadIdx.x; k < n2; k += 256) {
+    a += d2[(size_t)m * n2 + k];
+    c += mq[(size_t)m * n2 + k];
+  }
+  s0[threadIdx.x] = a;
+  s1[threadIdx.x] = c;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      s0[threadIdx.x] += s0[threadIdx.x + h];
+      s1[threadIdx.x] += s1[threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int B = boff[m + 1] - boff[m];
+    const double rmse = sqrt(s0[0] / (double)n2);
+    const double mu = B > 0 ? s1[0] / ((double)B * n2) : 0.0;
+    loss_terms[(size_t)m * 5 + 2] = mu > 0.0 ? (float)(w * rmse / mu) : 0.f;
+    coef[m] = (rmse > 0.0 && mu > 0.0 && B > 0) ? w / (mu * (double)n2 * rmse * (double)B) : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pac_dldi(const float* __restrict__ e, const double* __restrict__ coef,
+                                                  const int* __restrict__ boff, int n_batches, int n2, float scale,
+                                                  float* __restrict__ dLdI) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n2) return;
+  const int n_idx = boff[n_batches];
+  for (int b = blockIdx.y; b < n_idx; b += gridDim.y) {
+    int lo = 0, hi = n_batches;   // batch containing b: boff[lo] <= b < boff[lo+1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (boff[mid] <= b) lo = mid;
+      else hi = mid;
+    }
+    dLdI[(size_t)b * n2 + k] = (float)((double)scale * coef[lo] * (double)e[(size_t)lo * n2 + k]);
+  }
+}
+}  // namespace
+
+extern "C" size_t ptyx_pacbed_ws_bytes(int32_t N, int32_t n_batches) {
+  const size_t n2 = (size_t)N * N;
+  return (size_t)n_batches * (n2 * (8 + 8 + 4) + 8) + 64;
+}
+
+extern "C" int ptyx_loss_pacbed(void* stream, const float* dp, const void* meas, int32_t meas_f16, const int32_t* idx,
+                                const int32_t* batch_offsets, int32_t n_batches, int32_t n_idx, int32_t N,
+                                float weight, float dp_pow, float grad_scale, float* loss_terms, float* dLdI,
+                                void* ws) {
+  abi::clear_error();
+  if (N <= 0 || n_batches < 0 || n_idx < 0) return abi::fail(PTYX_EINVAL, "loss_pacbed: bad shape");
+  if (n_batches > 65535) return abi::fail(PTYX_EUNSUPPORTED, "loss_pacbed: at most 65535 batches per call");
+  if (n_batches == 0) return PTYX_OK;
+  if (!dp || !meas || !idx || !batch_offsets || !loss_terms || !ws)
+    return abi::fail(PTYX_EINVAL, "loss_pacbed: null pointer");
+  const int n2 = N * N;
+  double* d2 = reinterpret_cast<double*>(ws);
+  double* mq = d2 + (size_t)n_batches * n2;
+  double* coef = mq + (size_t)n_batches * n2;
+  float* e = reinterpret_cast<float*>(coef + n_batches);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_pac_pixel, dim3((n2 + 255) / 256, n_batches), dim3(256), 0, st, dp, meas, meas_f16, idx,
+                     batch_offsets, n2, dp_pow, d2, mq, e);
+  hipLaunchKernelGGL(k_pac_batch, dim3(n_batches), dim3(256), 0, st, d2, mq, batch_offsets, n2, weight, coef,
+                     loss_terms);
+  if (dLdI && n_idx > 0)
+    hipLaunchKernelGGL(k_pac_dldi, dim3((n2 + 255) / 256, std::min(n_idx, 65535)), dim3(256), 0, st, e, coef,
+                       batch_offsets, n_batches, n2, grad_scale, dLdI);
+  return abi::launch_status("loss_pacbed launch");
 }

@@ -42,20 +42,29 @@ class LossConfig:
     sparse_on: bool = True
     sparse_w: float = 0.1
     sparse_n: int = 1
+    pacbed_on: bool = False     # ptyx_loss_pacbed on the fused call's dp, then ptyx_adjoint_dldi
+    pacbed_w: float = 0.5
+    pacbed_q: float = 0.2
 
     @classmethod
     def from_loss_params(cls, lp: dict) -> "LossConfig":
-        for k in ("loss_pacbed", "loss_simlar"):
-            if lp.get(k, {}).get("state", False):
-                raise NotImplementedError(f"{k} is not on the fused HIP path; use the generic "
-                                          "(autograd) path of ptyrad_amd.losses.CombinedLoss")
+        if lp.get("loss_simlar", {}).get("state", False):
+            raise NotImplementedError("loss_simlar is not on the fused HIP path; use the generic "
+                                      "(autograd) path of ptyrad_amd.losses.CombinedLoss")
         s, p, sp = lp["loss_single"], lp["loss_poissn"], lp["loss_sparse"]
+        pb = lp.get("loss_pacbed", {"state": False})
         return cls(bool(s["state"]), float(s.get("weight", 1.0)), float(s.get("dp_pow", 0.5)),
                    bool(p["state"]), float(p.get("weight", 1.0)), float(p.get("dp_pow", 1.0)),
                    float(p.get("eps", 1e-6)),
-                   bool(sp["state"]), float(sp.get("weight", 0.1)), int(sp.get("ln_order", 1)))
+                   bool(sp["state"]), float(sp.get("weight", 0.1)), int(sp.get("ln_order", 1)),
+                   bool(pb["state"]), float(pb.get("weight", 0.5)), float(pb.get("dp_pow", 0.2)))
 
     def to_c(self, grad_scale: float, max_batch: int = 0) -> _lib.LossCfg:
+        if self.pacbed_on and not (self.single_on or self.poissn_on):
+            # the engine needs one data term: a zero-weight loss_single (adds nothing)
+            return _lib.LossCfg(1, 0.0, self.single_q, 0, self.poissn_w, self.poissn_q, self.poissn_eps,
+                                int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale),
+                                int(max_batch))
         return _lib.LossCfg(int(self.single_on), self.single_w, self.single_q,
                             int(self.poissn_on), self.poissn_w, self.poissn_q, self.poissn_eps,
                             int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale),
@@ -220,6 +229,24 @@ class Plan:
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
                                                    _ptr(dp_out), ctypes.byref(g)))
         return loss_terms
+
+    def loss_pacbed(self, t: dict, idx, batch_offsets, dp, loss_cfg: LossConfig, loss_terms, grad_scale=1.0,
+                    want_dldi=True):
+        """ptyx_loss_pacbed: writes loss_terms[:, 2] and returns dL/d(dp) (or None)."""
+        idx_t = self._idx(idx)
+        off_t = self._idx(batch_offsets)
+        n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
+        _need(dp, torch.float32, "dp", self.device)
+        meas = t["meas"]
+        _need(meas, torch.float16 if self.meas_f16 else torch.float32, "meas", self.device)
+        ws = torch.empty(int(self.lib.ptyx_pacbed_ws_bytes(self.dims.N, nb)) // 8 + 1, dtype=torch.float64,
+                         device=self.device)
+        dLdI = torch.empty_like(dp) if want_dldi else None
+        _lib.check(self.lib.ptyx_loss_pacbed(self._stream(), _ptr(dp), _ptr(meas), int(self.meas_f16), _ptr(idx_t),
+                                             _ptr(off_t), nb, n, self.dims.N, float(loss_cfg.pacbed_w),
+                                             float(loss_cfg.pacbed_q), float(grad_scale), _ptr(loss_terms),
+                                             _ptr(dLdI), _ptr(ws)))
+        return dLdI
 
     @property
     def register_capacity(self) -> int:

@@ -32,7 +32,15 @@ class _FusedLoss(torch.autograd.Function):
         t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach(),
              "H": H_rv.detach(), "tilts": None if tilts is None else tilts.detach().contiguous()}
         t.update(base)
-        terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0)
+        if cfg.pacbed_on:   # loss_pacbed (losses.py:77-89): HIP loss on the call's dp, then the HIP adjoint
+            N = probe_rv.shape[1]
+            dp = torch.empty((int(idx_t.numel()), N, N), dtype=torch.float32, device=obja.device)
+            terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0, dp_out=dp)
+            dLdI = plan.loss_pacbed(t, idx_t, off_t, dp, cfg, terms, want_dldi=bool(grads))
+            if grads:
+                plan.adjoint_dldi(t, idx_t, dLdI, {k: v for k, v in grads.items() if k != "shifts" or shift_probes})
+        else:
+            terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0)
         ctx.grads = grads
         total = terms.sum()
         ctx.mark_non_differentiable(terms)

@@ -276,6 +276,15 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--pacbed-only":
+        pac = json.loads(json.dumps(DEFAULT_LOSS))
+        pac["loss_pacbed"].update(state=True, weight=0.5, dp_pow=0.2)
+        run_case("n32_p2o1z2_pacbed", 32, 2, 1, 2, 4, 4, 7, seed=71, loss_params=pac)
+        only = json.loads(json.dumps(pac))
+        only["loss_single"].update(state=False)
+        only["loss_sparse"].update(state=False)
+        run_case("n64_p1o1z1_pacbedonly", 64, 1, 1, 1, 3, 3, 6, seed=72, loss_params=only)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--each-only":
         # per-position tilts (tilt_type 'each', models.py:330-356): fixed (case 2B) and optimised (2A)
         t16 = np.random.default_rng(61).uniform(-4.0, 4.0, (16, 2)).astype(np.float32)

@@ -42,7 +42,12 @@ def test_loss_config_mapping_and_out_of_scope_terms():
     assert (c.sparse_on, c.sparse_n) == (True, 2)
     cs = c.to_c(0.25)
     assert abs(cs.grad_scale - 0.25) < 1e-9
-    lp["loss_pacbed"]["state"] = True
+    lp["loss_pacbed"] = {"state": True, "weight": 0.3, "dp_pow": 0.25}     # HIP ptyx_loss_pacbed
+    c = LossConfig.from_loss_params(lp)
+    assert (c.pacbed_on, c.pacbed_w, c.pacbed_q) == (True, 0.3, 0.25)
+    only = LossConfig(single_on=False, poissn_on=False, pacbed_on=True).to_c(1.0)
+    assert (only.single_on, only.single_w) == (1, 0.0)      # zero-weight data term for the engine
+    lp["loss_simlar"]["state"] = True
     with pytest.raises(NotImplementedError):
         LossConfig.from_loss_params(lp)
 
