@@ -231,8 +231,7 @@ def loss_terms(dp, meas, ph, occu, lp):
         terms[2] = pb["weight"] * rmse / mu
         if rmse > 0:
             dLdI += pb["weight"] / (mu * d.size * rmse * B) * d * q * Ib ** (q - 1)
-    if lp.get("loss_simlar", {}).get("state", False):
-        raise NotImplementedError("loss_simlar (torchvision gaussian_blur of the object) is outside the hot path")
+
     sp = lp["loss_sparse"]
     dph = np.zeros(ph.shape, np.float64)
     if sp["state"]:                                                    # losses.py:91-104
@@ -245,6 +244,31 @@ def loss_terms(dp, meas, ph, occu, lp):
             coef = sp["weight"] * occu[o] * (m[o] ** (1.0 / nord - 1.0) if m[o] > 0 else 0.0) / cnt
             dph[:, o] = coef * a[:, o] ** (nord - 1) * np.sign(ph[:, o])
     return terms, dLdI, dph
+
+
+def simlar_term(amp, ph, occu, lp):
+    """loss_simlar (losses.py:106-141): w Σ_{amp,phase} mean(std_o(blur(x)·occ_o)) over the
+    (B,O,Nz,N,N) patches; returns (term, dL/damp, dL/dph).  Area resampling (scale ≠ 1) is not
+    restated (the schema default is 1)."""
+    p = lp.get("loss_simlar", {"state": False})
+    if not p["state"]:
+        return 0.0, 0.0, 0.0
+    if p.get("scale_factor") is not None and any(f != 1 for f in p["scale_factor"]):
+        raise NotImplementedError("loss_simlar area resampling is not restated")
+    std, O = p.get("blur_std"), amp.shape[1]
+    term, grads = 0.0, []
+    for x, kinds in ((amp, ("amplitude", "both")), (ph, ("phase", "both"))):
+        if p.get("obj_type", "both") not in kinds:
+            grads.append(0.0)
+            continue
+        xb = gaussian_blur(x, std) if std else np.asarray(x, np.float64)
+        y = xb * occu[None, :, None, None, None]
+        s = y.std(axis=1, ddof=1)
+        term += p["weight"] * s.mean()
+        gy = p["weight"] / s.size * (y - y.mean(axis=1, keepdims=True)) / ((O - 1) * np.where(s > 0, s, np.inf))[:, None]
+        gx = gy * occu[None, :, None, None, None]
+        grads.append(gaussian_blur_adjoint(gx, std) if std else gx)
+    return term, grads[0], grads[1]
 
 
 def adjoint(cache: ForwardCache, dLdI, dph_sparse, amp, ph, probe, shifts_b, H, occu, shift_probes,
@@ -337,8 +361,11 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
         terms, dLdI, dph = loss_terms(dp, meas[idx], ph, occu, loss_params)
         if detector_blur_std:
             dLdI = gaussian_blur_adjoint(dLdI, detector_blur_std)
+        st, sdA, sdP = simlar_term(amp, ph, occu, loss_params)
+        terms[4] = st
         dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], Hx, occu,
                                          shift_probes, cdt)
+        dA, dP = dA + sdA, dP + sdP
         if tilts is not None and amp.shape[2] > 1:                # dL/dθ_b = Re Σ conj(g_Hb) ∂H_b/∂θ_b
             Hb = Hx[:, 0, 0]
             t = np.asarray(tilts, np.float64)[idx] / 1e3

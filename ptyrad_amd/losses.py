@@ -98,10 +98,24 @@ class CombinedLoss(torch.nn.Module):
         return p["weight"] * (m.pow(1.0 / n) * omode_occu).sum()
 
     def get_loss_simlar(self, object_patches, omode_occu):      # losses.py:106-141
+        """Std over object modes of the (blurred / resampled) patches; the blur is the HIP
+        gaussian_blur of ptyrad_amd.stages (torchvision's kernel, reflect padding)."""
         p = self.loss_params.get("loss_simlar", {"state": False})
         if not p["state"]:
             return torch.tensor(0.0, device=object_patches.device)
-        raise NotImplementedError("loss_simlar (needs torchvision gaussian_blur) is outside the hot path")
+        from .stages import GaussianBlur
+        std, sf = p.get("blur_std"), p.get("scale_factor")
+        total = torch.tensor(0.0, device=object_patches.device)
+        for c, kinds in ((0, ("amplitude", "both")), (1, ("phase", "both"))):
+            if p.get("obj_type", "both") not in kinds:
+                continue
+            x = object_patches[..., c]
+            if std is not None and std != 0:
+                x = GaussianBlur.apply(x.contiguous(), float(std))
+            if sf is not None and any(f != 1 for f in sf):
+                x = torch.nn.functional.interpolate(x, scale_factor=sf, mode="area")
+            total = total + (x * omode_occu[:, None, None, None]).std(1).mean()
+        return p["weight"] * total
 
     def forward(self, model_DP, measured_DP, object_patches, omode_occu):
         losses = [self.get_loss_single(model_DP, measured_DP),
@@ -127,7 +141,9 @@ class CombinedLoss(torch.nn.Module):
         flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
         model._check_indices(flat)
         dev = model.opt_obja.device
-        if getattr(model, "detector_blur", False):
+        if getattr(model, "detector_blur", False) or self.loss_params.get("loss_simlar", {}).get("state", False):
+            # the loss sees blurred intensities / blurred patches: HIP forward → HIP blur → loss
+            # terms of this module → HIP adjoints, per mini-batch
             return self._per_batch(model, batches)
         cfg = LossConfig.from_loss_params(self.loss_params)
         if getattr(model, "preblur", False):

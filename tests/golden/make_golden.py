@@ -276,6 +276,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--tilt-only":
         run_case("n64_p2o1z3_tilt", 64, 2, 1, 3, 3, 3, 6, seed=18, tilts=[3.0, -2.0])
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--simlar-only":
+        # loss_simlar (losses.py:106-141) blurs the patches with torchvision's gaussian_blur
+        models.gaussian_blur = refimport.tv_gaussian_blur
+        losses.gaussian_blur = refimport.tv_gaussian_blur
+        sim = json.loads(json.dumps(DEFAULT_LOSS))
+        sim["loss_simlar"].update(state=True, weight=0.2, obj_type="both", blur_std=1.0)
+        run_case("n32_p1o2z2_simlar", 32, 1, 2, 2, 4, 4, 6, seed=81, loss_params=sim)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--pacbed-only":
         pac = json.loads(json.dumps(DEFAULT_LOSS))
         pac["loss_pacbed"].update(state=True, weight=0.5, dp_pow=0.2)

@@ -17,7 +17,7 @@ from tests.test_oracle_golden import CASES as ALL_CASES, load_case, rel
 
 # raw C-ABI cases: the optional-stage (blur) and optimised-propagator fixtures run through
 # PtychoHIP in test_gpu_stages.py / test_gpu_propagator.py
-CASES = [c for c in ALL_CASES if not any(k in c for k in ("blur", "_opt", "each", "pacbed"))]
+CASES = [c for c in ALL_CASES if not any(k in c for k in ("blur", "_opt", "each", "pacbed", "simlar"))]
 
 pytestmark = pytest.mark.gpu
 

@@ -156,7 +156,8 @@ def test_recon_step_with_stages_runs_on_device():
     assert np.all(np.isfinite(hist)) and hist[-1] < hist[0]
 
 
-PACBED = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*pacbed*.npz")))
+PACBED = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*pacbed*.npz")) +
+                glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*simlar*.npz")))
 
 
 @pytest.mark.parametrize("path", PACBED, ids=[os.path.basename(p)[:-4] for p in PACBED])
@@ -164,7 +165,9 @@ PACBED = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "n*p
 def test_loss_pacbed_matches_reference(path, fused):
     """loss_pacbed (losses.py:77-89): fused path = engine call with dp_out → ptyx_loss_pacbed →
     ptyx_adjoint_dldi; generic path = torch loss on the engine's dp.  Reference fixtures from
-    make_golden.py --pacbed-only (one with loss_single + loss_sparse, one with pacbed alone)."""
+    make_golden.py --pacbed-only (one with loss_single + loss_sparse, one with pacbed alone).
+    Also loss_simlar (losses.py:106-141; patches blurred by the HIP gaussian_blur), whose
+    fused call runs per mini-batch (make_golden.py --simlar-only)."""
     device = dev()
     from ptyrad_amd.losses import CombinedLoss
     d = load_case(path)
