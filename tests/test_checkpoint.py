@@ -1,0 +1,93 @@
+"""Checkpoint / resume on CPU: the reference's save-dict key layout
+(save.py:85-137), a .pt round trip readable with torch.load(weights_only=True), and a resumed
+reconstruction that continues bit-for-bit like an uninterrupted one (Adam state restored)."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ptyrad_amd.checkpoint import MODEL_ATTRIBUTES, load_ptyrad, make_save_dict, resume, save_ptyrad
+from ptyrad_amd.reconstruction import DistContext, recon_step
+from tests.dist_helpers import OracleLoss, OracleModel
+
+TRAJ = os.path.join(os.path.dirname(__file__), "golden", "traj_n64_b4_ga1.npz")
+REF_KEYS = {"ptyrad_version", "output_path", "optimizable_tensors", "optim_state_dict", "params",
+            "model_attributes", "loss_iters", "iter_times", "dz_iters", "avg_iter_t", "niter", "indices",
+            "batch_losses", "avg_losses"}
+
+
+def _setup(z):
+    model = OracleModel(z)
+    for k in MODEL_ATTRIBUTES:          # the PtychoAD attributes make_save_dict records
+        if not hasattr(model, k):
+            setattr(model, k, None)
+    opt = torch.optim.Adam(model.optimizable_params)
+    batches = np.split(z["batches"], np.cumsum(z["batch_sizes"])[:-1])
+    return model, opt, OracleLoss(json.loads(str(z["loss_params"]))), batches
+
+
+def _step(model, opt, loss, batches, z, it):
+    return recon_step(batches, int(z["grad_accumulation"]), model, opt, loss, None, it, verbose=False,
+                      dist_ctx=DistContext())
+
+
+def test_save_dict_layout_and_pt_round_trip(tmp_path):
+    z = np.load(TRAJ, allow_pickle=False)
+    model, opt, loss, batches = _setup(z)
+    bl = _step(model, opt, loss, batches, z, 1)
+    params = {"recon_params": {"save_result": ["model", "optim_state"]}}
+    d = make_save_dict(str(tmp_path), model, params, opt, 1, np.arange(16), bl)
+    assert set(d) == REF_KEYS
+    assert set(d["model_attributes"]) == set(MODEL_ATTRIBUTES)
+    assert set(d["optimizable_tensors"]) == {"obja", "objp", "obj_tilts", "slice_thickness", "probe",
+                                             "probe_pos_shifts"}
+    assert d["optimizable_tensors"]["probe"].is_complex()
+    p = save_ptyrad(str(tmp_path / "model_iter0001.pt"), d)
+    back = load_ptyrad(p)
+    assert set(back) == REF_KEYS
+    assert torch.equal(back["optimizable_tensors"]["obja"], model.opt_obja.detach())
+    assert torch.equal(torch.view_as_real(back["optimizable_tensors"]["probe"]), model.opt_probe.detach())
+    assert torch.equal(back["indices"], torch.arange(16))
+    with pytest.raises(NotImplementedError):
+        save_ptyrad(str(tmp_path / "x.hdf5"), d)
+
+
+def test_resume_continues_bitwise(tmp_path):
+    z = np.load(TRAJ, allow_pickle=False)
+    ref, opt_r, loss, batches = _setup(z)
+    for it in (1, 2, 3):
+        _step(ref, opt_r, loss, batches, z, it)
+    model, opt, loss, batches = _setup(z)
+    bl = _step(model, opt, loss, batches, z, 1)
+    params = {"recon_params": {"save_result": ["model", "optim_state"]}}
+    p = save_ptyrad(str(tmp_path / "ckpt.pt"), make_save_dict(str(tmp_path), model, params, opt, 1, None, bl))
+    model2, opt2, loss2, _ = _setup(z)
+    start = resume(model2, opt2, load_ptyrad(p))
+    assert start == 1
+    for it in (2, 3):
+        _step(model2, opt2, loss2, batches, z, it)
+    for a, b in ((ref.opt_obja, model2.opt_obja), (ref.opt_objp, model2.opt_objp), (ref.opt_probe, model2.opt_probe),
+                 (ref.opt_probe_pos_shifts, model2.opt_probe_pos_shifts)):
+        assert torch.equal(a.detach(), b.detach())
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference not present (build container only)")
+def test_reference_load_ptyrad_reads_our_checkpoint(tmp_path):
+    """The reference's own loader (load.py:495 → load_pt :479) opens the .pt we write."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from refimport import import_reference
+    import_reference()
+    from ptyrad.load import load_ptyrad as ref_load
+    z = np.load(TRAJ, allow_pickle=False)
+    model, opt, loss, batches = _setup(z)
+    bl = _step(model, opt, loss, batches, z, 1)
+    p = save_ptyrad(str(tmp_path / "model_iter0001.pt"),
+                    make_save_dict(str(tmp_path), model, {"recon_params": {"save_result": ["model"]}}, opt, 1, None, bl))
+    d = ref_load(p)
+    obja = d["optimizable_tensors"]["obja"]
+    np.testing.assert_array_equal(np.asarray(obja), model.opt_obja.detach().numpy())
+    assert d["niter"] == 1
