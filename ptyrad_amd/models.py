@@ -302,8 +302,8 @@ class PtychoHIP(nn.Module):
         plan = self._stack_plans.get(B)
         if plan is None:
             if len(self._stack_plans) >= 4:
-                old = self._stack_plans.pop(next(iter(self._stack_plans)))
-                old.close()
+                # drop the oldest; an autograd graph that still holds it keeps it alive (Plan.__del__)
+                self._stack_plans.pop(next(iter(self._stack_plans)))
             O, Nz = self.opt_obja.shape[:2]
             P, N = self.opt_probe.shape[:2]
             plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes,
