@@ -67,6 +67,10 @@ struct KArgs {
   const float* kvec;
   float dz;
   float* d_tilts;
+  // far-field cache (general engine, Nz = 1, P·O > 1): k_forward leaves every mode's F(ψ_out)
+  // and every probe mode's ψ⁰ per pattern, so k_adjoint skips the recomputed forward
+  float2* ffc;
+  long long ffc_per;   // float2 per pattern: (P·O + P)·N²
 };
 
 // ---------------------------------------------------------------- small helpers

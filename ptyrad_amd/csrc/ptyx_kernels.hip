@@ -200,18 +200,22 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
     };
     float* Ip = SINGLE ? nullptr : a.Ibuf + (size_t)pat * N2;
     float2* psi0 = scratch_psi<N>(a);   // this workgroup's ψ⁰ park (multi-object-mode calls)
+    float2* cache = (!SINGLE && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
     for (int p = 0; p < a.P; ++p) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
+        float2* park0 = cache ? cache + (size_t)(a.P * a.O + p) * N2 : (a.O > 1 ? psi0 : nullptr);
         forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
-                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, a.O > 1 ? psi0 : nullptr, o > 0);
+                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, park0, o > 0);
+        float2* ffp = cache ? cache + (size_t)(p * a.O + o) * N2 : nullptr;
         const float occ = a.occu[o];
         const bool first = (p == 0 && o == 0);
         // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v) { return v; },
             [&](int y, int x, float2& v) {
+              if (ffp) ffp[y * N + x] = v;
               const float2 Psi = cscale(v, inv_n);
               const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
               const float c = occ * cabs2(Psi);
@@ -339,6 +343,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
     arr.lds = s_buf;
   }
   float2* psi = scratch_psi<N>(a);
+  const float2* psi_rd = psi;   // ψⁿ the slice adjoints read: scratch, or the far-field cache's ψ⁰
   float2* gacc = psi + (size_t)a.Nz * N2;
   float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
   // propagator gradient: dL/dH += Σ_{p,o,n<Nz-1} conj(Xⁿ) ⊙ F(g^{n+1}) / N²  (ψ^{n+1} = F⁻¹(H Xⁿ))
@@ -377,12 +382,8 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
         const float occ = a.occu[o];
         const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
         float dummy = 0.f;
-        forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
-                                   tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0);
         // far field → g_Ψ = 2 occ Ψ ∂L/∂I  (left in natural FFT order)
-        fft2d<N, NT, -1, true>(
-            arr, s_tw, [&](int, int, float2 v) { return v; },
-            [&](int y, int x, float2& v) {
+        auto ff_post = [&](int y, int x, float2& v) {
               const float2 Psi = cscale(v, inv_n);
               const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
               float dLdI;
@@ -404,7 +405,24 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
               }
               v = cscale(Psi, 2.0f * occ * dLdI);
               return true;
-            });
+            };
+        const float2* cache = (!EXT && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
+        if (cache) {   // k_forward left F(ψ_out) of this (p, o) and ψ⁰ of p: no recomputed forward
+          psi_rd = cache + (size_t)(a.P * a.O + p) * N2;
+          const float2* ffp = cache + (size_t)(p * a.O + o) * N2;
+          for (int e = opaque_tid(); e < N2; e += NT) {
+            const int y = e / N, x = e % N;
+            float2 v = ffp[e];
+            ff_post(y, x, v);
+            arr.st(y, x, v);
+          }
+          __syncthreads();
+        } else {
+          psi_rd = psi;
+          forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
+                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0);
+          fft2d<N, NT, -1, true>(arr, s_tw, [&](int, int, float2 v) { return v; }, ff_post);
+        }
         // adjoint of slice n: g_O += conj(ψ^n) g → dA, dφ; g ← g ⊙ conj(O_n)
         auto slice_adj = [&](int n, int y, int x, float2 gv) -> float2 {
           const size_t off = obj_off(a, o, n, g.cy + y, g.cx + x);
@@ -412,7 +430,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
           float sn, cs;
           phase_sincos(ph, &sn, &cs);
           const float2 Ov = make_float2(A * cs, A * sn);
-          const float2 gO = cmulc(gv, psi[(size_t)n * N2 + y * N + x]);
+          const float2 gO = cmulc(gv, psi_rd[(size_t)n * N2 + y * N + x]);
           if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));   // Re(g_O e^{-iφ})
           if (a.d_objp) {
             float dph = fmaf(gO.y, Ov.x, -gO.x * Ov.y);                          // Im(conj(O) g_O)
@@ -621,6 +639,8 @@ struct ptyx_plan {
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* hslab = nullptr;    // PTYX_PROP_GRAD: per-workgroup dL/dH slabs
+  float2* ffc = nullptr;      // far-field cache (general engine, Nz = 1, P·O > 1)
+  long long ffc_per = 0, ffc_cap = 0;
   float2* scratch = nullptr;
   unsigned* sync = nullptr;   // k_fused1/2: dequeue head, error flag, per-batch arrivals
   // k_fused2 (single mode, N <= 128): co-resident grid, per-pattern object-gradient slots
@@ -752,7 +772,8 @@ extern "C" const char* ptyx_last_error(void) { return g_err.c_str(); }
 extern "C" size_t ptyx_plan_workspace_bytes(const ptyx_plan* plan) { return plan ? plan->ws_bytes : 0; }
 
 extern "C" int64_t ptyx_plan_register_capacity(const ptyx_plan* plan) {
-  return (plan && plan->nwg3 > 0) ? (int64_t)plan->og_cap : 0;
+  if (plan && plan->nwg3 > 0) return (int64_t)plan->og_cap;
+  return (plan && plan->ffc_cap > 0) ? (int64_t)plan->ffc_cap : 0;   // far-field cache capacity
 }
 
 extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int device) {
@@ -796,6 +817,24 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->sync, ((size_t)d.max_patterns + 2 + 3) / 4 * 4))) {
     free_plan(pl);
     return rc;
+  }
+  if (d.Nz == 1 && d.P * d.O > 1 && pl->fast && !std::getenv("PTYX_NO_FFC")) {
+    // far-field cache: (P·O + P)·N² float2 per pattern of a call, within PTYX_FFC_MB (default the
+    // smaller of 64 GiB and a third of the free HBM); calls beyond its capacity are split by the host
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    long long mb = std::min<long long>(65536, (long long)(free_b / 3 / (1 << 20)));
+    if (const char* e = std::getenv("PTYX_FFC_MB")) mb = std::atoll(e);
+    const long long per = (long long)(d.P * d.O + d.P) * (long long)N2;
+    const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (per * (long long)sizeof(float2)));
+    if (cap >= std::min<long long>(d.max_patterns, pl->nwg)) {
+      if ((rc = dalloc(pl, &pl->ffc, (size_t)cap * per))) {
+        free_plan(pl);
+        return rc;
+      }
+      pl->ffc_per = per;
+      pl->ffc_cap = cap;
+    }
   }
   if (lds && d.P * d.O * d.Nz == 1 && pl->fast) {
     // one-pass path: g_O slot per pattern of a call (N² float2), bounded by PTYX_OBJ_SCRATCH_MB
@@ -1357,6 +1396,10 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     }
     if ((rc = launch_status("k_fused launch"))) return rc;
   } else {
+    if (any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
+      a.ffc = pl->ffc;
+      a.ffc_per = pl->ffc_per;
+    }
     PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
     if ((rc = launch_status("k_forward launch"))) return rc;
   }
