@@ -167,3 +167,31 @@ def test_per_position_tilts_multi_batch_vs_oracle():
     assert rel(model.opt_obj_tilts.grad.cpu().numpy(), g["tilts"]) < 1e-4
     assert rel(model.opt_objp.grad.cpu().numpy(), g["objp"]) < 5e-5
 
+
+
+@pytest.mark.parametrize("stages", [{"obj_preblur_std": 0.6}, {"detector_blur_std": 0.8, "obj_preblur_std": 0.6}],
+                         ids=["preblur", "preblur+detblur"])
+def test_per_position_tilts_compose_with_blur_stages(stages):
+    """Per-position tilts on the patch-stack (pre-blur) and per-batch (detector blur) paths, two
+    ragged mini-batches, against the oracle with every option on."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    d = load_case([p for p in EACH if "n32_p2o1z3_tilteach" in p][0])
+    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"], d["meas"])
+    iv.update(obj_tilts=d["obj_tilts"], slice_thickness=float(d["slice_thickness"]), dx=float(d["dx"]),
+              lambd=float(d["lambd"]))
+    model = PtychoHIP(iv, {**model_params(LRS), **stages}, device=device, verbose=False)
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(12).permutation(S)
+    batches = [perm[:5], perm[5:11]]
+    total, terms = CombinedLoss(d["loss_params"], device=device).fused(model, batches)
+    total.backward()
+    oterms, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                         d["occu"], d["meas"], batches, d["loss_params"], **tilt_kw(d), **stages)
+    np.testing.assert_allclose(terms.detach().cpu().numpy(), oterms, rtol=2e-5, atol=1e-7)
+    assert rel(model.opt_obja.grad.cpu().numpy(), g["obja"]) < 5e-5
+    assert rel(model.opt_objp.grad.cpu().numpy(), g["objp"]) < 5e-5
+    gp = model.opt_probe.grad.cpu().numpy()
+    assert rel(gp[..., 0] + 1j * gp[..., 1], g["probe"]) < 5e-5
+    assert rel(model.opt_probe_pos_shifts.grad.cpu().numpy(), g["shifts"]) < 2e-4
