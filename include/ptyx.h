@@ -88,6 +88,9 @@ typedef struct ptyx_grads {
                       (two-pass) engine; Nz = 1 adds nothing (H is unused). */
   float *d_tilts;  /* (n_scans,2)   += dL/dobj_tilts (per-position tilts, mrad) or NULL; needs
                       inputs.obj_tilts and a PTYX_PROP_GRAD plan (general engine). */
+  float *d_dz;     /* (1)           += the per-position tilt ramps' part of dL/d(slice_thickness)
+                      (∂/∂dz of exp(i dz (Ky tan θy + Kx tan θx))) or NULL; the part through H
+                      comes from d_H.  Same requirements as d_tilts. */
 } ptyx_grads;
 
 /* CombinedLoss terms on the hot path (params/loss_params.py defaults in brackets). */

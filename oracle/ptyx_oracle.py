@@ -345,6 +345,7 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     g_shifts = np.zeros(shifts.shape, np.float64)
     g_H = np.zeros(probe.shape[-2:], np.complex128)
     g_tilts = None if tilts is None else np.zeros(np.shape(tilts), np.float64)
+    g_dz_ramp, g_H_base = 0.0, np.zeros(probe.shape[-2:], np.complex128)
     all_terms, dps = [], []
     for idx in batches:
         idx = np.asarray(idx)
@@ -372,6 +373,9 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
             w = np.real(np.conj(cache.dHb) * 1j * Hb)
             g_tilts[idx, 0] += grad_scale * dz * (w * k1[None, :, None]).sum(axis=(1, 2)) / np.cos(t[:, 0]) ** 2 / 1e3
             g_tilts[idx, 1] += grad_scale * dz * (w * k1[None, None, :]).sum(axis=(1, 2)) / np.cos(t[:, 1]) ** 2 / 1e3
+            T = k1[None, :, None] * np.tan(t[:, 0, None, None]) + k1[None, None, :] * np.tan(t[:, 1, None, None])
+            g_dz_ramp += grad_scale * float((w * T).sum())                       # ∂/∂dz of the ramps
+            g_H_base += grad_scale * (np.conj(ramp) * cache.dHb).sum(axis=0)     # Σ_b conj(r_b) g_Hb
         if obj_preblur_std:
             dA, dP = gaussian_blur_adjoint(dA, obj_preblur_std), gaussian_blur_adjoint(dP, obj_preblur_std)
         for i, s in enumerate(idx):
@@ -383,7 +387,8 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
         g_H += grad_scale * cache.dH
         all_terms.append(terms)
         dps.append(dp)
-    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts, H=g_H, tilts=g_tilts)
+    grads = dict(obja=g_obja, objp=g_objp, probe=g_probe, shifts=g_shifts, H=g_H, tilts=g_tilts,
+                 dz_ramp=g_dz_ramp, H_base=g_H_base)
     return np.array(all_terms), dps, grads
 
 

@@ -53,7 +53,7 @@ class Inputs(ctypes.Structure):
 class Grads(ctypes.Structure):
     _fields_ = [("d_obja", ctypes.c_void_p), ("d_objp", ctypes.c_void_p),
                 ("d_probe", ctypes.c_void_p), ("d_shifts", ctypes.c_void_p), ("d_H", ctypes.c_void_p),
-                ("d_tilts", ctypes.c_void_p)]
+                ("d_tilts", ctypes.c_void_p), ("d_dz", ctypes.c_void_p)]
 
 
 class LossCfg(ctypes.Structure):

@@ -67,6 +67,7 @@ struct KArgs {
   const float* kvec;
   float dz;
   float* d_tilts;
+  float* d_dz;      // ramp part of dL/d(dz) with per-position tilts
   // far-field cache (general engine, Nz = 1, P·O > 1): k_forward leaves every mode's F(ψ_out)
   // and every probe mode's ψ⁰ per pattern, so k_adjoint skips the recomputed forward
   float2* ffc;

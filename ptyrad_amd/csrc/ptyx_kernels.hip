@@ -347,7 +347,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
   float2* gacc = psi + (size_t)a.Nz * N2;
   float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
   // propagator gradient: dL/dH += Σ_{p,o,n<Nz-1} conj(Xⁿ) ⊙ F(g^{n+1}) / N²  (ψ^{n+1} = F⁻¹(H Xⁿ))
-  float2* xs = (a.hslab || a.d_tilts) ? gacc + N2 : nullptr;
+  float2* xs = (a.hslab || a.d_tilts || a.d_dz) ? gacc + N2 : nullptr;
   float2* hsl = a.hslab ? a.hslab + (size_t)blockIdx.x * N2 : nullptr;
   if (a.need_probe)
     for (int e = threadIdx.x; e < a.P * N2; e += NT) slab[e] = make_float2(0.f, 0.f);
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
                   if (xs) {
                     const float2 q = cscale(cmulc(v, xs[(size_t)n * N2 + e]), inv_n2);   // g_{H_b}
                     if (hsl) hsl[e] = cadd(hsl[e], cmulc(q, r));                        // conj(r) g_{H_b}
-                    if (a.d_tilts) {
+                    if (a.d_tilts || a.d_dz) {
                       const float w = -cmulc(Hb, q).y;   // Re(i conj(q) H_b) = -Im(H_b conj(q))
                       dt[0] = fmaf(a.kvec[y], w, dt[0]);
                       dt[1] = fmaf(a.kvec[x], w, dt[1]);
@@ -527,13 +527,17 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
         atomicAdd(a.d_shifts + 2 * g.s + 1, ds[1] * inv_n2);
       }
     }
-    if (tilt && a.d_tilts) {
+    if (tilt && (a.d_tilts || a.d_dz)) {
       __syncthreads();
       block_sum<NT, 2>(dt, s_red);
       if (threadIdx.x == 0) {   // ∂/∂θ (mrad) of tan(θ/1e3) = sec²(θ/1e3)/1e3
-        const float cy = cosf(a.ptilt[2 * g.s] / 1e3f), cx = cosf(a.ptilt[2 * g.s + 1] / 1e3f);
-        atomicAdd(a.d_tilts + 2 * g.s, dt[0] * a.dz / (cy * cy) / 1e3f);
-        atomicAdd(a.d_tilts + 2 * g.s + 1, dt[1] * a.dz / (cx * cx) / 1e3f);
+        const float ay = a.ptilt[2 * g.s] / 1e3f, ax = a.ptilt[2 * g.s + 1] / 1e3f;
+        const float cy = cosf(ay), cx = cosf(ax);
+        if (a.d_tilts) {
+          atomicAdd(a.d_tilts + 2 * g.s, dt[0] * a.dz / (cy * cy) / 1e3f);
+          atomicAdd(a.d_tilts + 2 * g.s + 1, dt[1] * a.dz / (cx * cx) / 1e3f);
+        }
+        if (a.d_dz) atomicAdd(a.d_dz, fmaf(dt[0], tanf(ay), dt[1] * tanf(ax)));   // ∂/∂dz of the ramps
       }
     }
     __syncthreads();
@@ -1288,12 +1292,13 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
 
 // propagator gradient: validate the request and point the kernels at the plan's slabs
 static int setup_prop_grad(const ptyx_plan* pl, const ptyx_grads& gz, KArgs& a) {
-  if (!gz.d_H && !gz.d_tilts) return PTYX_OK;
+  if (!gz.d_H && !gz.d_tilts && !gz.d_dz) return PTYX_OK;
   if (!(pl->d.flags & PTYX_PROP_GRAD))
     return fail(PTYX_EINVAL, "d_H / d_tilts need a plan created with PTYX_PROP_GRAD");
-  if (gz.d_tilts && !a.ptilt) return fail(PTYX_EINVAL, "d_tilts needs inputs.obj_tilts");
+  if ((gz.d_tilts || gz.d_dz) && !a.ptilt) return fail(PTYX_EINVAL, "d_tilts / d_dz need inputs.obj_tilts");
   a.hslab = gz.d_H ? pl->hslab : nullptr;   // null when Nz == 1: H is unused, nothing to add
   a.d_tilts = pl->d.Nz > 1 ? gz.d_tilts : nullptr;
+  a.d_dz = pl->d.Nz > 1 ? gz.d_dz : nullptr;
   return PTYX_OK;
 }
 
@@ -1342,7 +1347,8 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.need_probe = gz.d_probe != nullptr;
   if ((rc = setup_prop_grad(pl, gz, a))) return rc;
   // propagator gradients and per-position tilts: general two-pass engine only
-  const bool want_H = a.hslab != nullptr || a.d_tilts != nullptr || (a.ptilt != nullptr && pl->d.Nz > 1);
+  const bool want_H = a.hslab != nullptr || a.d_tilts != nullptr || a.d_dz != nullptr ||
+                      (a.ptilt != nullptr && pl->d.Nz > 1);
 
   a.w1 = cfg->single_w;
   a.w2 = cfg->poissn_w;
@@ -1353,7 +1359,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     const char* dbg = std::getenv("PTYX_DEBUG_NOWAIT");
     a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
   }
-  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;
   const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
   // one pass per pattern (k_fused2) when every mini-batch fits the co-resident grid, the call
   // fits the object-gradient slots and exactly one data term is on (its coefficient factors out)
@@ -1446,7 +1452,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   if (n_idx == 0 || !grads) return PTYX_OK;
   if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
   const ptyx_grads gz = *grads;
-  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts)) return PTYX_OK;
+  if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz)) return PTYX_OK;
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   KArgs a = make_args(pl, in, idx, n_idx);

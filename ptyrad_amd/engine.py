@@ -153,14 +153,15 @@ class Plan:
         d, dev = self.dims, self.device
         for k, shape in (("obja", (d.O, d.Nz, d.Ny, d.Nx)), ("objp", (d.O, d.Nz, d.Ny, d.Nx)),
                          ("probe", (d.P, d.N, d.N, 2)), ("shifts", (d.n_scans, 2)), ("H", (d.N, d.N, 2)),
-                         ("tilts", (d.n_scans, 2))):
+                         ("tilts", (d.n_scans, 2)), ("dz", ())):
             g = grads.get(k)
             if g is not None:
                 _need(g, torch.float32, f"grad {k}", dev)
                 if tuple(g.shape) != shape:
                     raise ValueError(f"grad {k} shape {tuple(g.shape)} != {shape}")
         return _lib.Grads(_ptr(grads.get("obja")), _ptr(grads.get("objp")), _ptr(grads.get("probe")),
-                          _ptr(grads.get("shifts")), _ptr(grads.get("H")), _ptr(grads.get("tilts")))
+                          _ptr(grads.get("shifts")), _ptr(grads.get("H")), _ptr(grads.get("tilts")),
+                          _ptr(grads.get("dz")))
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

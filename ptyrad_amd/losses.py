@@ -20,13 +20,13 @@ class _FusedLoss(torch.autograd.Function):
     ``plan`` / ``base`` name the geometry (the model's plan, or a pre-blur patch-stack plan)."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, tilts, plan, base, idx_t, off_t, cfg, shift_probes):
+    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, tilts, dz_t, plan, base, idx_t, off_t, cfg, shift_probes):
         want = {"obja": obja.requires_grad, "objp": objp.requires_grad, "probe": probe_rv.requires_grad,
                 "shifts": shifts.requires_grad and shift_probes, "H": H_rv.requires_grad,
-                "tilts": tilts is not None and tilts.requires_grad}
+                "tilts": tilts is not None and tilts.requires_grad, "dz": dz_t is not None and dz_t.requires_grad}
         grads = {}
         for k, p in (("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts), ("H", H_rv),
-                     ("tilts", tilts)):
+                     ("tilts", tilts), ("dz", dz_t)):
             if want[k]:
                 grads[k] = torch.zeros_like(p)
         t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach(),
@@ -49,7 +49,7 @@ class _FusedLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_total, g_terms):
         out = []
-        for k in ("obja", "objp", "probe", "shifts", "H", "tilts"):
+        for k in ("obja", "objp", "probe", "shifts", "H", "tilts", "dz"):
             g = ctx.grads.get(k)
             out.append(None if g is None else g * g_total)
         ctx.grads = None
@@ -153,8 +153,8 @@ class CombinedLoss(torch.nn.Module):
         idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
         off_t = torch.as_tensor(batch_offsets(batches)).to(dev, non_blocking=True)
         total, terms = _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe,
-                                        model.opt_probe_pos_shifts, model._H_rv(), model._tilts(), model.plan,
-                                        model._base(), idx_t, off_t, cfg, model.shift_probes)
+                                        model.opt_probe_pos_shifts, model._H_rv(), model._tilts(), model._dz_t(),
+                                        model.plan, model._base(), idx_t, off_t, cfg, model.shift_probes)
         return total, terms
 
     PREBLUR_GROUP = 8192
@@ -189,8 +189,8 @@ class CombinedLoss(torch.nn.Module):
             idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev)
             off_t = torch.as_tensor(batch_offsets(group)).to(dev, non_blocking=True)
             A, Ph, sh, tl, plan, base, ar, _ = model._stack_inputs(idx_t, with_meas=True)
-            return _FusedLoss.apply(A, Ph, model.opt_probe, sh, model._H_rv(), tl, plan, base, ar, off_t, cfg,
-                                    model.shift_probes)
+            return _FusedLoss.apply(A, Ph, model.opt_probe, sh, model._H_rv(), tl, model._dz_t(), plan, base, ar,
+                                    off_t, cfg, model.shift_probes)
 
         return self._grouped(model, batches, self.PREBLUR_GROUP, run)
 
@@ -204,7 +204,7 @@ class CombinedLoss(torch.nn.Module):
             off_t = torch.as_tensor(batch_offsets(group)).to(dev, non_blocking=True)
             sh, tl, base, ar = model._local_inputs(idx_t, with_meas=True)
             return _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe, sh, model._H_rv(), tl,
-                                    model.plan, base, ar, off_t, cfg, model.shift_probes)
+                                    model._dz_t(), model.plan, base, ar, off_t, cfg, model.shift_probes)
 
         return self._grouped(model, batches, int(model.plan.dims.n_scans), run, strict=True)
 

@@ -24,9 +24,8 @@ returns dL/dH (PTYX_PROP_GRAD), which torch autograd carries to dz / tilts (an (
 On-the-fly measurement padding / resampling (models.py:384-412) runs as ptyx_meas_gather; engine
 calls then take call-local positions / shifts / DPs (rows 0..n-1 of plan-sized arrays).
 
-Per-position tilts (tilt_type 'each', models.py:330-356), fixed or optimised, run in the engine
-(per-pattern separable ramps, d_tilts).  Out of scope (raises NotImplementedError): per-position
-tilts together with an optimised slice thickness.
+Per-position tilts (tilt_type 'each', models.py:330-356), fixed or optimised, also with an optimised slice thickness,
+run in the engine (per-pattern separable ramps, d_tilts, d_dz).
 """
 from __future__ import annotations
 
@@ -50,20 +49,20 @@ class _EngineForward(torch.autograd.Function):
     per-position tilts (or None); their gradients come from the engine's d_H / d_tilts."""
 
     @staticmethod
-    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, tilts, plan, base, idx_t, shift_probes):
+    def forward(ctx, obja, objp, probe_rv, shifts, H_rv, tilts, dz_t, plan, base, idx_t, shift_probes):
         ctx.plan, ctx.base, ctx.shift_probes = plan, base, shift_probes
-        ctx.save_for_backward(obja, objp, probe_rv, shifts, H_rv, tilts, idx_t)
+        ctx.save_for_backward(obja, objp, probe_rv, shifts, H_rv, tilts, dz_t, idx_t)
         with torch.no_grad():
             return plan.forward(_tensors(obja, objp, probe_rv, shifts, H_rv, tilts, base), idx_t)
 
     @staticmethod
     def backward(ctx, grad_dp):
-        obja, objp, probe_rv, shifts, H_rv, tilts, idx_t = ctx.saved_tensors
+        obja, objp, probe_rv, shifts, H_rv, tilts, dz_t, idx_t = ctx.saved_tensors
         want = ctx.needs_input_grad
         grads = {}
-        outs = [None] * 6
+        outs = [None] * 7
         for i, (k, p) in enumerate((("obja", obja), ("objp", objp), ("probe", probe_rv), ("shifts", shifts),
-                                    ("H", H_rv), ("tilts", tilts))):
+                                    ("H", H_rv), ("tilts", tilts), ("dz", dz_t))):
             if want[i]:
                 outs[i] = torch.zeros_like(p)
                 grads[k] = outs[i]
@@ -152,9 +151,6 @@ class PtychoHIP(nn.Module):
             # per-position tilts (tilt_type 'each', models.py:330-356): the engine applies each
             # position's separable ramp exp(i dz (Ky tan θy + Kx tan θx)) to H itself
             self.pos_tilts = bool(self.tilt_obj and self.opt_obj_tilts.shape[0] != 1)
-            if self.pos_tilts and self.change_thickness:
-                raise NotImplementedError("per-position tilts together with an optimised slice thickness are not "
-                                          "on the HIP path")
             # models.py:210-219 / :346-349 (case 2B, global): a fixed tilt only changes the one
             # propagator every position uses, so the engine takes the tilted H as its H
             self.register_buffer("H_eff", self._tilted_H() if (self.tilt_obj and not self.pos_tilts) else self.H)
@@ -235,7 +231,9 @@ class PtychoHIP(nn.Module):
     def _propagator(self):
         """get_propagators (models.py:300-360) for a global tilt: the (N, N) complex64 H every
         position uses, differentiable in opt_slice_thickness / opt_obj_tilts when they are optimised."""
-        if not self.prop_opt or self.pos_tilts:
+        if self.pos_tilts:   # the engine applies the per-position ramps; H is exp(i dz Kz) or the fixed H
+            return torch.exp(1j * self.opt_slice_thickness * self.Kz) if self.change_thickness else self.H_eff
+        if not self.prop_opt:
             return self.H_eff
         Ky, Kx = self.propagator_grid
         dz = self.opt_slice_thickness
@@ -272,9 +270,14 @@ class PtychoHIP(nn.Module):
     def _base(self, crop_pos=None, meas=None, stack=False):
         b = {"occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
              "meas": self.measurements if (meas is None and not stack) else meas}
-        if self.pos_tilts:
-            b.update(kvec=self.propagator_grid[0][:, 0].contiguous(), dz=self._dz)
+        if self.pos_tilts:   # the ramps use the current dz (a host value: one sync per call if optimised)
+            dz = float(self.opt_slice_thickness.detach()) if self.change_thickness else self._dz
+            b.update(kvec=self.propagator_grid[0][:, 0].contiguous(), dz=dz)
         return b
+
+    def _dz_t(self):
+        """opt_slice_thickness as an engine input when its gradient runs through the tilt ramps."""
+        return self.opt_slice_thickness if (self.pos_tilts and self.change_thickness) else None
 
     def _tilts(self, il=None, pad_to=None):
         """Per-position tilts for an engine call: all positions, or rows ``il`` (call-local /
@@ -444,17 +447,18 @@ class PtychoHIP(nn.Module):
         idx_t = torch.as_tensor(idx, dtype=torch.int32).to(self.opt_obja.device, non_blocking=True)
         if self.preblur:
             A, Ph, sh, tl, plan, base, ar, (pa, pp) = self._stack_inputs(idx_t)
-            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), tl, plan, base, ar, self.shift_probes)
+            dp = _EngineForward.apply(A, Ph, self.opt_probe, sh, self._H_rv(), tl, self._dz_t(), plan, base, ar,
+                                      self.shift_probes)
             self._current_object_patches = torch.stack([pa, pp], dim=-1).permute(2, 0, 1, 3, 4, 5)
         elif self.otf_meas:
             sh, tl, base, ar = self._local_inputs(idx_t)
-            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, sh, self._H_rv(), tl, self.plan,
-                                      base, ar, self.shift_probes)
+            dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, sh, self._H_rv(), tl,
+                                      self._dz_t(), self.plan, base, ar, self.shift_probes)
             self._current_object_patches = self.get_obj_patches(idx)
         else:
             dp = _EngineForward.apply(self.opt_obja, self.opt_objp, self.opt_probe, self.opt_probe_pos_shifts,
-                                      self._H_rv(), self._tilts(), self.plan, self._base(meas=None, stack=True),
-                                      idx_t, self.shift_probes)
+                                      self._H_rv(), self._tilts(), self._dz_t(), self.plan,
+                                      self._base(meas=None, stack=True), idx_t, self.shift_probes)
             # object patches for losses that use them (loss_sparse / loss_simlar, losses.py:152-153)
             self._current_object_patches = self.get_obj_patches(idx)
         if self.detector_blur:                      # get_forward_meas, models.py:375-382

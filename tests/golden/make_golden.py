@@ -176,8 +176,10 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
                    else g(model.opt_obj_tilts),
                    g_slice_thickness=np.float32(0.0) if g(model.opt_slice_thickness) is None
                    else g(model.opt_slice_thickness))
-    if tilts is not None and np.asarray(tilts).size > 2:   # per-position tilts: H is the untilted one
-        out.update(H=model.H.numpy(), tilt_each=True)
+    if tilts is not None and np.asarray(tilts).size > 2:   # per-position tilts: H is the base one
+        base = model.H if "slice_thickness" not in PROP_LR else \
+            torch.exp(1j * model.opt_slice_thickness * model.Kz)   # case 1: exp(i dz Kz)
+        out.update(H=base.detach().numpy(), tilt_each=True)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
@@ -300,6 +302,10 @@ if __name__ == "__main__":
         PROP_LR.update(obj_tilts=1e-3)
         t9 = np.random.default_rng(62).uniform(-4.0, 4.0, (9, 2)).astype(np.float32)
         run_case("n64_p1o2z2_opttilteach", 64, 1, 2, 2, 3, 3, 5, seed=62, tilts=t9)
+        if len(sys.argv) > 2 and sys.argv[2] == "--with-dz":   # case 1 with per-position tilts
+            PROP_LR.update(slice_thickness=1e-3)
+            t16b = np.random.default_rng(63).uniform(-4.0, 4.0, (16, 2)).astype(np.float32)
+            run_case("n32_p2o1z3_opttiltdzeach", 32, 2, 1, 3, 4, 4, 6, seed=63, tilts=t16b)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--otf-only":
         run_otf_case("otf_n32_pad", 32, 2, 1, 1, 4, 4, 6, seed=51, Hm=24, pad_to=32)

@@ -31,7 +31,7 @@ def test_struct_layouts_match_header():
     # sizes of the C structs (all 4-byte fields / 8-byte pointers, no padding surprises)
     assert ctypes.sizeof(_lib.Dims) == 9 * 4
     assert ctypes.sizeof(_lib.Inputs) == 10 * 8 + 8     # + float dz, padded to pointer alignment
-    assert ctypes.sizeof(_lib.Grads) == 6 * 8
+    assert ctypes.sizeof(_lib.Grads) == 7 * 8
     assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
     assert ctypes.sizeof(_lib.ObjConstraints) == 19 * 4
 

@@ -145,6 +145,6 @@ def test_fixed_global_tilt_propagator():
     assert rel(model.opt_obja.grad.cpu().numpy(), d["g_obja"]) < 5e-5
     assert rel(model.opt_probe.grad.cpu().numpy(), d["g_probe"]) < 5e-5
     S = d["shifts"].shape[0]
-    with pytest.raises(NotImplementedError):   # per-position tilts with an optimised dz stay out of scope
-        PtychoHIP({**iv, "obj_tilts": np.tile(d["obj_tilts"], (S, 1))},
+    with pytest.raises(ValueError):   # per-position tilts must have one row per scan position
+        PtychoHIP({**iv, "obj_tilts": np.tile(d["obj_tilts"], (S + 1, 1))},
                   model_params({**lrs, "slice_thickness": 1e-3}), device=device, verbose=False)

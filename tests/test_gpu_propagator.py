@@ -116,7 +116,8 @@ def test_engine_dH_vs_oracle():
 
 def _each_model(d, device, max_patterns=None):
     from ptyrad_amd.models import PtychoHIP
-    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"], d["meas"])
+    H = d["H_untilted"] if "H_untilted" in d else d["H"]
+    iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], H, d["occu"], d["meas"])
     iv.update(obj_tilts=d["obj_tilts"], slice_thickness=float(d["slice_thickness"]), dx=float(d["dx"]),
               lambd=float(d["lambd"]))
     lrs = {**LRS, **(json.loads(str(d["prop_lr"])) if "prop_lr" in d else {})}
@@ -149,6 +150,9 @@ def test_per_position_tilts_match_reference(path, fused):
     assert rel(model.opt_probe.grad.cpu().numpy(), d["g_probe"]) < 5e-5
     if "prop_lr" in d:
         assert rel(model.opt_obj_tilts.grad.cpu().numpy(), d["g_obj_tilts"]) < 1e-4
+        if "slice_thickness" in json.loads(str(d["prop_lr"])):   # case 1 with per-position tilts
+            np.testing.assert_allclose(model.opt_slice_thickness.grad.item(), float(d["g_slice_thickness"]),
+                                       rtol=1e-2)
 
 
 def test_per_position_tilts_multi_batch_vs_oracle():

@@ -195,3 +195,15 @@ def test_oracle_on_the_fly_measurements_match_reference(path):
     gp = z["g_probe"][..., 0] + 1j * z["g_probe"][..., 1]
     assert rel(g["probe"], gp) < 5e-5
 
+
+def test_oracle_dz_gradient_with_per_position_tilts():
+    """Case 1 with tilt_type 'each' (models.py:339-344): dL/d(dz) = Re Σ conj(g_H) i Kz H (base H =
+    exp(i dz Kz)) + the tilt ramps' part, against the reference's autograd (rtol 1e-2: the dz·k
+    phase cancellation floor of the f32 reference, see test_oracle_propagator_gradient_*)."""
+    d = load_case(os.path.join(os.path.dirname(__file__), "golden", "n32_p2o1z3_opttiltdzeach.npz"))
+    _, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"],
+                                    d["meas"], [d["batch"]], d["loss_params"], **tilt_kw(d))
+    gdz_base, _ = orc.propagator_param_grads(g["H_base"], d["H"], float(d["slice_thickness"]), np.zeros(2),
+                                             float(d["dx"]), float(d["lambd"]), 3)
+    np.testing.assert_allclose(gdz_base + g["dz_ramp"], float(d["g_slice_thickness"]), rtol=1e-2)
+
