@@ -96,3 +96,29 @@ def test_fused_call_local_groups_vs_oracle():
     np.testing.assert_allclose(terms.detach().cpu().numpy(), oterms, rtol=2e-5, atol=1e-7)
     assert rel(model.opt_objp.grad.cpu().numpy(), g["objp"]) < 5e-5
     assert rel(model.opt_probe_pos_shifts.grad.cpu().numpy(), g["shifts"]) < 2e-4
+
+
+def test_on_the_fly_measurements_with_optimised_thickness_vs_oracle():
+    """Call-local (on-the-fly) engine calls compose with the propagator gradient: optimised slice
+    thickness (case 3) on 2 slices with resampled measurements, two mini-batches, vs the oracle."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    z = np.load([p for p in OTF if p.endswith("otf_n32_resample.npz")][0], allow_pickle=False)
+    lp = json.loads(str(z["loss_params"]))
+    iv = init_vars(z["obja"], z["objp"], z["probe"], z["shifts"], z["crop_pos"], z["H"], z["occu"], z["meas_small"])
+    iv["on_the_fly_meas_scale_factors"] = z["on_the_fly_meas_scale_factors"]
+    model = PtychoHIP(iv, model_params({**LRS, "slice_thickness": 1e-3}), device=device, verbose=False)
+    S = z["shifts"].shape[0]
+    perm = np.random.default_rng(5).permutation(S)
+    batches = [perm[:6], perm[6:11]]
+    total, terms = CombinedLoss(lp, device=device).fused(model, batches)
+    total.backward()
+    Heff = model.get_propagators([0])[0].detach().cpu().numpy()
+    meas = orc.otf_measurements(z["meas_small"], np.arange(S), *otf_args(z))
+    oterms, _, g = orc.forward_loss_grad(z["obja"], z["objp"], z["probe"], z["shifts"], z["crop_pos"], Heff,
+                                         z["occu"], meas, batches, lp)
+    np.testing.assert_allclose(terms.detach().cpu().numpy(), oterms, rtol=2e-5, atol=1e-7)
+    assert rel(model.opt_objp.grad.cpu().numpy(), g["objp"]) < 5e-5
+    gdz, _ = orc.propagator_param_grads(g["H"], Heff, 2.0, np.zeros(2), 0.1494, float(model.lambd), 3)
+    np.testing.assert_allclose(model.opt_slice_thickness.grad.item(), gdz, rtol=1e-2)
