@@ -1,7 +1,6 @@
 """Checkpoint / resume on CPU: the reference's save-dict key layout
 (save.py:85-137), a .pt round trip readable with torch.load(weights_only=True), and a resumed
 reconstruction that continues bit-for-bit like an uninterrupted one (Adam state restored)."""
-import glob
 import json
 import os
 
