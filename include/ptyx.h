@@ -36,6 +36,10 @@
 extern "C" {
 #endif
 
+/* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
+ * against another revision of this header); ptyx_version() returns it too. */
+#define PTYX_ABI_VERSION 200
+
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
 #define PTYX_ENOMEM 2
@@ -51,7 +55,7 @@ extern "C" {
 typedef struct ptyx_plan ptyx_plan;
 
 typedef struct ptyx_dims {
-  int32_t N;            /* probe / DP side, power of two, 16..256                         */
+  int32_t N;            /* probe / DP side: 32, 64, 128 or 256                             */
   int32_t P;            /* probe modes  (opt_probe.shape[0])                               */
   int32_t O;            /* object modes (opt_obja.shape[0])                                */
   int32_t Nz;           /* object slices (opt_obja.shape[1])                               */
@@ -59,6 +63,7 @@ typedef struct ptyx_dims {
   int32_t n_scans;      /* number of probe positions (crop_pos.shape[0])                   */
   int32_t max_patterns; /* largest number of patterns per call (sizes the workspace)       */
   uint32_t flags;       /* PTYX_SHIFT_PROBES | PTYX_MEAS_F16 | PTYX_PROP_GRAD              */
+  int32_t abi_version;  /* = PTYX_ABI_VERSION                                              */
 } ptyx_dims;
 
 typedef struct ptyx_inputs {
@@ -69,12 +74,17 @@ typedef struct ptyx_inputs {
   const float *H;          /* (N,N,2)      f32  PtychoAD.H, zero frequency at the corner      */
   const float *omode_occu; /* (O,)         f32                                               */
   const int32_t *crop_pos; /* (n_scans,2)  i32  integer top-left (y,x) of each patch          */
-  const void *meas;        /* (n_scans,N,N) f32 (or f16 with PTYX_MEAS_F16), fftshifted DPs  */
+  const void *meas;        /* (rows,N,N) f32 (or f16 with PTYX_MEAS_F16), fftshifted DPs:
+                              rows = n_scans, or a rank-local block addressed via meas_rows  */
   /* per-position object tilts (tilt_type 'each', get_propagators models.py:330-356): position s
    * propagates with H ⊙ exp(i dz (Ky tan(θy_s/1e3) + Kx tan(θx_s/1e3))).  NULL = none. */
   const float *obj_tilts;  /* (n_scans,2)  f32  PtychoAD.opt_obj_tilts, mrad                  */
   const float *kvec;       /* (N)          f32  propagator_grid k values (Ky[:,0] = Kx[0,:])  */
   float dz;                /* slice thickness used by the tilt ramps                           */
+  /* rank-local measurement storage (the data-parallel driver keeps only the DPs of its own
+   * mini-batches): meas_rows[s] = row of `meas` holding scan position s, for every s
+   * a call touches.  NULL = row s (the whole stack).                                          */
+  const int32_t *meas_rows; /* (n_scans) i32 device, or NULL                                     */
 } ptyx_inputs;
 
 typedef struct ptyx_grads {
@@ -99,9 +109,8 @@ typedef struct ptyx_loss_cfg {
   int32_t poissn_on;  float poissn_w, poissn_q, poissn_eps;  /* loss_poissn [0, 1.0, 1.0, 1e-6] */
   int32_t sparse_on;  float sparse_w; int32_t sparse_n;      /* loss_sparse [1, 0.1, 1]         */
   float grad_scale;   /* multiplies every gradient: 1/grad_accumulation, reconstruction.py:750 */
-  int32_t max_batch;  /* largest mini-batch of the call, 0 = unknown.  When it fits the resident
-                         grid, single-mode calls run forward, loss and adjoint in ONE pass per
-                         pattern (per-mini-batch arrival counter instead of a second forward). */
+  int32_t max_batch;  /* largest mini-batch of the call, 0 = unknown (informational: engine
+                         choice depends only on the geometry and the call's capacity)      */
 } ptyx_loss_cfg;
 
 /* Create a plan: validates dims, allocates the device workspace and twiddle tables.
@@ -271,8 +280,15 @@ int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);
 /* Last error message of the calling thread ("" if none). */
 const char *ptyx_last_error(void);
-/* ABI version (major*100 + minor). */
+/* sha1 (40 hex digits) of the sources and flags the library was built from: the loader refuses a
+ * library whose id does not match the sources shipped next to it (no silently stale builds). */
+const char *ptyx_build_id(void);
+/* ABI version (major*100 + minor) = PTYX_ABI_VERSION. */
 int ptyx_version(void);
+/* sizeof of every struct of this header, in declaration order: ptyx_dims, ptyx_inputs,
+ * ptyx_grads, ptyx_loss_cfg, ptyx_kernel_stat, ptyx_obj_constraints, ptyx_meas_proc.  Writes
+ * min(cap, 7) values and returns 7; a binding checks its own struct sizes against them. */
+int ptyx_abi_struct_sizes(size_t *out, int32_t cap);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
+PTYX_ABI_VERSION = 200     # include/ptyx.h
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
 PTYX_SHIFT_PROBES = 1
 PTYX_MEAS_F16 = 2
@@ -27,7 +28,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
            "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
-           "ptyx_plan_register_capacity", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
+           "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish")
 
 
 class PtyxError(RuntimeError):
@@ -40,14 +41,19 @@ class Dims(ctypes.Structure):
     _fields_ = [("N", ctypes.c_int32), ("P", ctypes.c_int32), ("O", ctypes.c_int32),
                 ("Nz", ctypes.c_int32), ("Ny", ctypes.c_int32), ("Nx", ctypes.c_int32),
                 ("n_scans", ctypes.c_int32), ("max_patterns", ctypes.c_int32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("abi_version", ctypes.c_int32)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if len(args) < 10 and "abi_version" not in kw:
+            self.abi_version = PTYX_ABI_VERSION
 
 
 class Inputs(ctypes.Structure):
     _fields_ = [("obja", ctypes.c_void_p), ("objp", ctypes.c_void_p), ("probe", ctypes.c_void_p),
                 ("shifts", ctypes.c_void_p), ("H", ctypes.c_void_p), ("omode_occu", ctypes.c_void_p),
                 ("crop_pos", ctypes.c_void_p), ("meas", ctypes.c_void_p), ("obj_tilts", ctypes.c_void_p),
-                ("kvec", ctypes.c_void_p), ("dz", ctypes.c_float)]
+                ("kvec", ctypes.c_void_p), ("dz", ctypes.c_float), ("meas_rows", ctypes.c_void_p)]
 
 
 class Grads(ctypes.Structure):
@@ -118,6 +124,9 @@ def load(path: str | None = None):
     lib.ptyx_plan_register_capacity.restype = ctypes.c_int64
     lib.ptyx_last_error.restype = ctypes.c_char_p
     lib.ptyx_version.restype = ctypes.c_int
+    lib.ptyx_abi_struct_sizes.argtypes = [ctypes.POINTER(ctypes.c_size_t), i32]
+    lib.ptyx_abi_struct_sizes.restype = ctypes.c_int
+    lib.ptyx_build_id.restype = ctypes.c_char_p
     lib.ptyx_constraints_ws_bytes.restype = ctypes.c_size_t
     lib.ptyx_constraints_evals_offset.restype = ctypes.c_size_t
     lib.ptyx_obj_rblur.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32]
@@ -145,8 +154,30 @@ def load(path: str | None = None):
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
                  "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish"):
         getattr(lib, name).restype = ctypes.c_int
+    _check_abi(lib)
     _lib = lib
     return lib
+
+
+STRUCTS = ("Dims", "Inputs", "Grads", "LossCfg", "KernelStat", "ObjConstraints", "MeasProc")   # header order
+
+
+def _check_abi(lib):
+    """The library's ABI version and C struct sizes must match these ctypes mirrors, and its build
+    id the sources next to it (PTYX_LIB pointing elsewhere, e.g. a variant build, skips that)."""
+    if "PTYX_LIB" not in os.environ:
+        from .csrc import build as _build
+        want, got = _build.source_hash(), lib.ptyx_build_id().decode()
+        if got != want:
+            raise ImportError(f"libptyx.so was built from other sources (build id {got[:12]} != {want[:12]}): "
+                              "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+    if lib.ptyx_version() != PTYX_ABI_VERSION:
+        raise ImportError(f"libptyx.so ABI {lib.ptyx_version()} != {PTYX_ABI_VERSION}: rebuild the library")
+    sizes = (ctypes.c_size_t * len(STRUCTS))()
+    lib.ptyx_abi_struct_sizes(sizes, len(STRUCTS))
+    for name, sz in zip(STRUCTS, sizes):
+        if ctypes.sizeof(globals()[name]) != sz:
+            raise ImportError(f"ctypes {name} is {ctypes.sizeof(globals()[name])} B, libptyx.so says {sz} B")
 
 
 def check(rc: int):

@@ -4,6 +4,11 @@
 
 Each translation unit compiles to its own object under build/obj/ (in parallel, and only when
 it or a header is newer than its object), then one hipcc -shared link.
+
+Freshness is keyed on CONTENT, not mtimes: the sha1 of every source and header (plus the flags)
+is compiled into the library (ptyx_build_id(), a generated one-line translation unit), so
+``up_to_date`` rebuilds whenever the library was built from other sources, and ``_lib.load()``
+refuses a library whose build id does not match the sources next to it.
 """
 from __future__ import annotations
 
@@ -36,11 +41,28 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm is required to build libptyx.so)")
 
 
+def source_hash(defs=()) -> str:
+    """sha1 over the contents of every source / header and the compile flags."""
+    h = hashlib.sha1()
+    for d in sorted(DEPS, key=os.path.basename):
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join([ARCH, *FLAGS, *defs]).encode())
+    return h.hexdigest()
+
+
+def library_build_id(path: str = OUT) -> str | None:
+    """The build id compiled into a built library (without loading HIP): the marker string."""
+    if not os.path.exists(path):
+        return None
+    data = open(path, "rb").read()
+    i = data.find(b"PTYX_BUILD_ID=")
+    return data[i + 14:i + 54].decode() if i >= 0 else None
+
+
 def up_to_date(out: str = OUT) -> bool:
-    if not os.path.exists(out):
-        return False
-    t = os.path.getmtime(out)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    return library_build_id(out) == source_hash()
 
 
 def _headers_of(src: str):
@@ -83,7 +105,15 @@ def build(force: bool = False, only_n: int | None = None, out: str = OUT, extra=
 
     with ThreadPoolExecutor(len(SOURCES)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    # build id: the content hash of the sources this library is made of
+    bid = source_hash(defs)
+    bsrc = os.path.join(odir, "ptyx_build_id.cpp")
+    with open(bsrc, "w") as f:
+        f.write('static const char kId[] = "PTYX_BUILD_ID=%s";\n'
+                'extern "C" const char* ptyx_build_id(void) { return kId + 14; }\n' % bid)
+    bobj = bsrc + ".o"
+    subprocess.run([cc, "-fPIC", "-O2", "-c", bsrc, "-o", bobj], check=True)
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, bobj, "-o", out + ".tmp"]
     if verbose:
         print("[ptyx build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

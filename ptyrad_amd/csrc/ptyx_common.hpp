@@ -52,14 +52,9 @@ struct KArgs {
   float2* scratch;
   long long scratch_stride;
   const float2* twg;
-  // one-pass fused kernel: loss weights and the per-call sync words
-  // sync[0] = dequeue head, sync[1] = error flag (spin timeout), sync[2 + m] = arrivals of batch m
   float w1, w2, ws, grad_scale;
-  unsigned* sync;
-  int debug_nowait;   // PTYX_DEBUG_NOWAIT=1: skip the batch wait (timing experiments only; wrong gradients)
-  // k_fused2: pattern → mini-batch table and the per-pattern object-gradient slots
-  const int* bid;
-  float2* ogscr;
+  // rank-local measurement block: row of meas holding scan position s (NULL: row s)
+  const int* mrow;
   // propagator gradient (PTYX_PROP_GRAD): per-workgroup dL/dH slabs; F(ψⁿ⊙Oⁿ) parked after gacc
   float2* hslab;
   // per-position tilts: ramps exp(i dz k tan(θ/1e3)) along y and x, and their gradient
@@ -139,7 +134,7 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
 }
 
 struct PatternGeom {
-  int s, cy, cx;
+  int s, m, cy, cx;   // scan index, its measurement row, clamped window origin
   float sy, sx;
 };
 
@@ -148,6 +143,7 @@ __device__ __forceinline__ PatternGeom pattern_geom(const KArgs& a, int pat, int
   int s = a.idx[pat];
   s = min(max(s, 0), a.n_scans - 1);  // defensive clamp; the host validates indices
   g.s = s;
+  g.m = a.mrow ? a.mrow[s] : s;
   g.cy = min(max(a.crop[2 * s], 0), a.Ny - N);
   g.cx = min(max(a.crop[2 * s + 1], 0), a.Nx - N);
   g.sy = a.shifts[2 * s];
@@ -191,7 +187,5 @@ template <int N>
 __device__ __forceinline__ float2* scratch_psi(const KArgs& a) {
   return a.scratch + (long long)blockIdx.x * a.scratch_stride + (Geo<N>::kLds ? 0 : 2 * N * N);
 }
-
-constexpr unsigned kMaxSpins = 1u << 24;   // ≈1 s of s_sleep polling (bounded batch waits)
 
 }  // namespace ptyx

@@ -445,143 +445,5 @@ __device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pr
   }
 }
 
-// =====================================================================================
-// Wave-owned 2-D FFT (N ≤ 128, LDS-resident): N = R1·R2, R2 threads per line, each thread
-// holding R1 points of its line.
-//   row phase   : wave w owns rows [w·64/R2, (w+1)·64/R2): in-register DFT_R1 over n2
-//                 (x = t + R2·n2), twiddle W_N^{t·k2}, WAVE-LOCAL LDS exchange (its own rows,
-//                 no workgroup barrier), DFT_R2 over n1, natural-order store;
-//   barrier;
-//   column phase: wave w owns columns [w·64/R2, ...): the same on columns, then post().
-//   barrier.
-// Two workgroup barriers per 2-D FFT (the Stockham version has eight), so waves drift out of
-// phase and LDS traffic of one wave overlaps the DFT arithmetic of another.
-template <int N> struct WPlan;
-template <> struct WPlan<32>  { static constexpr int R1 = 8,  R2 = 4; };
-template <> struct WPlan<64>  { static constexpr int R1 = 8,  R2 = 8; };
-template <> struct WPlan<128> { static constexpr int R1 = 16, R2 = 8; };
-
-template <int N>
-struct WGeom {
-  static constexpr int R1 = WPlan<N>::R1, R2 = WPlan<N>::R2;
-  static constexpr int NT = N * R2;      // threads per workgroup
-  static constexpr int LPW = 64 / R2;    // lines owned per wave
-  static constexpr int K2 = R1 / R2;     // second-stage butterflies per thread
-  static_assert(R1 % R2 == 0 && NT % 64 == 0 && N % LPW == 0, "bad wave FFT plan");
-};
-
-// LDS layout: one pad point per 16 columns and 8 pad points per 16 rows keep the row reads,
-// the column reads and both exchanges free of (or at worst 2-way) bank conflicts.
-template <int N>
-struct LdsArrayW {
-  static constexpr bool kInPlace = true;
-  static constexpr int kRowStride = N + N / 16;
-  static constexpr int kElems = N * kRowStride + 8 * (N / 16);
-  float2* p;
-  __device__ __forceinline__ int off(int y, int x) const {
-    return y * kRowStride + x + (x >> 4) + 8 * (y >> 4);
-  }
-  __device__ __forceinline__ float2 ld(int y, int x) const { return p[off(y, x)]; }
-  __device__ __forceinline__ void st(int y, int x, float2 v) const { p[off(y, x)] = v; }
-};
-
-// Order LDS accesses of the lanes of one wave around a wave-local exchange: no compiler
-// reordering across it, and the wave's own LDS operations retired (lgkmcnt(0)).
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  asm volatile("" ::: "memory");
-}
-
-// Points a thread owns in the row phase (pre hook, slot = n2) and the column phase (post
-// hook, slot = j·R2 + k1) — for register prefetch outside the FFT.
-template <int N>
-struct PassMapW {
-  using G = WGeom<N>;
-  static constexpr int kFirstSlots = G::R1, kLastSlots = G::R1;
-  __device__ __forceinline__ static void first(int tid, int s, int& y, int& x) {
-    const int lane = tid & 63, wave = tid >> 6;
-    y = wave * G::LPW + lane / G::R2;
-    x = lane % G::R2 + G::R2 * s;
-  }
-  __device__ __forceinline__ static void last(int tid, int s, int& y, int& x) {
-    const int lane = tid & 63, wave = tid >> 6;
-    const int t = lane / G::LPW, j = s / G::R2, k1 = s % G::R2;
-    y = (t * G::K2 + j) + G::R1 * k1;
-    x = wave * G::LPW + lane % G::LPW;
-  }
-  __device__ __forceinline__ static bool last_active(int, int) { return true; }
-};
-
-template <int N, int DIR, bool PRELOAD, class Pre, class Post>
-__device__ __forceinline__ void fft2d_w(const LdsArrayW<N>& arr, const float2* tw, Pre&& pre, Post&& post) {
-  using G = WGeom<N>;
-  constexpr int R1 = G::R1, R2 = G::R2, K2 = G::K2, LPW = G::LPW;
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wave = tid >> 6;
-  // ---------------------------------------------------------------- rows
-  {
-    const int t = lane % R2, y = wave * LPW + lane / R2;
-    float2 v[R1];
-#pragma unroll
-    for (int n2 = 0; n2 < R1; ++n2) {
-      const int x = t + R2 * n2;
-      if constexpr (PRELOAD) v[n2] = call_pre(pre, y, x, arr.ld(y, x), n2);
-      else v[n2] = call_pre(pre, y, x, make_float2(0.f, 0.f), n2);
-    }
-    DFT<R1, DIR>::run(v);
-#pragma unroll
-    for (int k2 = 1; k2 < R1; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, t * k2));
-    wave_lds_sync();
-#pragma unroll
-    for (int k2 = 0; k2 < R1; ++k2) arr.st(y, k2 * R2 + t, v[k2]);
-    wave_lds_sync();
-    float2 u[K2][R2];
-#pragma unroll
-    for (int j = 0; j < K2; ++j)
-#pragma unroll
-      for (int n1 = 0; n1 < R2; ++n1) u[j][n1] = arr.ld(y, (t * K2 + j) * R2 + n1);
-#pragma unroll
-    for (int j = 0; j < K2; ++j) DFT<R2, DIR>::run(u[j]);
-    wave_lds_sync();
-#pragma unroll
-    for (int j = 0; j < K2; ++j)
-#pragma unroll
-      for (int k1 = 0; k1 < R2; ++k1) arr.st(y, (t * K2 + j) + R1 * k1, u[j][k1]);
-  }
-  __syncthreads();
-  // ---------------------------------------------------------------- columns
-  {
-    const int t = lane / LPW, x = wave * LPW + lane % LPW;
-    float2 v[R1];
-#pragma unroll
-    for (int n2 = 0; n2 < R1; ++n2) v[n2] = arr.ld(t + R2 * n2, x);
-    DFT<R1, DIR>::run(v);
-#pragma unroll
-    for (int k2 = 1; k2 < R1; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, t * k2));
-    wave_lds_sync();
-#pragma unroll
-    for (int k2 = 0; k2 < R1; ++k2) arr.st(k2 * R2 + t, x, v[k2]);
-    wave_lds_sync();
-    float2 u[K2][R2];
-#pragma unroll
-    for (int j = 0; j < K2; ++j)
-#pragma unroll
-      for (int n1 = 0; n1 < R2; ++n1) u[j][n1] = arr.ld((t * K2 + j) * R2 + n1, x);
-#pragma unroll
-    for (int j = 0; j < K2; ++j) DFT<R2, DIR>::run(u[j]);
-    wave_lds_sync();
-#pragma unroll
-    for (int j = 0; j < K2; ++j)
-#pragma unroll
-      for (int k1 = 0; k1 < R2; ++k1) {
-        const int y = (t * K2 + j) + R1 * k1;
-        float2 val = u[j][k1];
-        if (call_post(post, y, x, val, j * R2 + k1)) arr.st(y, x, val);
-      }
-  }
-  __syncthreads();
-}
 
 }  // namespace ptyx

@@ -14,9 +14,9 @@
 //   IFFT  →   g  = F⁻¹(g_Ψ)/N                  R layout
 //             slot = g·conj(ψ⁰)   (object gradient per unit c_m; k_obj_gather reduces the slots)
 //             h    = g·conj(O)
-//   wait for mini-batch m (arrival counter), c_m from its partial sums (k_finalize arithmetic)
 //   FFT   →   G  = F(h)                        K layout
-//             slab += c_m G conj(W_b);  d_shift += c_m 2π/N² Σ g·Im(F(P) W_b conj(G))
+//             slab += G conj(W_b);  d_shift sums += Σ g·Im(F(P) W_b conj(G))   (unit c_m; scaled
+//             by c_m after k_finalize: k_segslab_reduce, k_shift_apply)
 //
 // Every global operand is laid out so that one register's access is contiguous across lanes:
 // F(P) and the slab are K-packed ([k][thread]); slots are stored row-permuted
@@ -50,7 +50,8 @@ struct F3Args {
   const float* shifts;     // (n_scans, 2)
   const float2* fpk;       // SHIFT: F(probe) K-packed; else the probe R-packed
   const float2* oc;        // A e^{iφ}, (Ny, Nx)
-  const float* meas;       // (n_scans, 128, 128) f32, fftshifted
+  const float* meas;       // (rows, 128, 128) f32, fftshifted
+  const int* mrow;         // measurement row of scan position s (NULL: row s; rank-local blocks)
   const float* occp;       // omode_occu (device), occ = occp[0]
   float q, eps2;
   float* psums;            // per-pattern loss partial sums (k_finalize)
@@ -386,7 +387,7 @@ struct Ch4x2 {
 
 // Per-pattern scalars.
 struct PatInfo {
-  int m, cy, cx, sidx;
+  int m, cy, cx, sidx, mi;   // mini-batch, window origin, scan index, measurement row
   float sy, sx;
 };
 template <bool SHIFT>
@@ -398,6 +399,7 @@ __device__ __forceinline__ PatInfo pat_info(const F3Args& a, int pat) {
   p.cy = g.x;
   p.cx = g.y;
   p.sidx = min(max(a.idx[pp], 0), a.n_scans - 1);
+  p.mi = a.mrow ? a.mrow[p.sidx] : p.sidx;
   p.sy = SHIFT ? a.shifts[2 * p.sidx] : 0.f;
   p.sx = SHIFT ? a.shifts[2 * p.sidx + 1] : 0.f;
   return p;
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
     }
     F3PH(2);
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
-    const float* dp = a.meas + (size_t)p.sidx * kN2;
+    const float* dp = a.meas + (size_t)p.mi * kN2;
     fft_fwd(v, buf, lc, cd.wsign, [&] {
       const int lane = cd.lane;
       const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
       }
     }
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
-    const float* dp = a.meas + (size_t)p.sidx * kN2;
+    const float* dp = a.meas + (size_t)p.mi * kN2;
     fft_fwd(v, buf, lc, cd.wsign, [&] {
       const int lane = cd.lane;
       const int wv = __builtin_amdgcn_readfirstlane(cd.wave);

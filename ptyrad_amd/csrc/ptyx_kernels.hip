@@ -222,7 +222,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
               if constexpr (SINGLE) {
                 const float I = c + kDpEps;
                 if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
-                if (want_sums) add_sums(I, meas_at(a, g.s, e, N2));
+                if (want_sums) add_sums(I, meas_at(a, g.m, e, N2));
               } else {
                 Ip[e] = first ? c : Ip[e] + c;
               }
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
         const float I = Ip[e] + kDpEps;
         Ip[e] = I;
         if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
-        if (want_sums) add_sums(I, meas_at(a, g.s, e, N2));
+        if (want_sums) add_sums(I, meas_at(a, g.m, e, N2));
       }
     }
     if (want_sums) {
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
                 dLdI = a.ext_scale * a.dLdI_ext[(size_t)pat * N2 + e];
               } else {
                 const float I = SINGLE ? fmaf(occ, cabs2(Psi), kDpEps) : Ip[e];
-                const float M = meas_at(a, g.s, e, N2);
+                const float M = meas_at(a, g.m, e, N2);
                 const float rI = 1.0f / I;
                 dLdI = 0.f;
                 if (a.single_on) {
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
 }
 
 #include "ptyx_single.hpp"
-#include "ptyx_fused.hpp"
+#include "ptyx_gather.hpp"
 
 // d_H += Σ over workgroup propagator-gradient slabs, fixed order.
 __global__ void k_hslab_reduce(const float2* hslab, int nwg, int n2, float2* d_H) {
@@ -646,9 +646,7 @@ struct ptyx_plan {
   float2* ffc = nullptr;      // far-field cache (general engine, Nz = 1, P·O > 1)
   long long ffc_per = 0, ffc_cap = 0;
   float2* scratch = nullptr;
-  unsigned* sync = nullptr;   // k_fused1/2: dequeue head, error flag, per-batch arrivals
-  // k_fused2 (single mode, N <= 128): co-resident grid, per-pattern object-gradient slots
-  int nwg_fused = 0;
+  // register engines (k_fused3 / k_fused3ms): per-pattern object-gradient slots
   long long og_cap = 0;       // patterns per call the slots can hold (0: path unavailable)
   float2* ogscr = nullptr;
   int* bid = nullptr;
@@ -747,29 +745,20 @@ static int dalloc(ptyx_plan* pl, T** p, size_t count) {
   return PTYX_OK;
 }
 
-// Workgroups of k_fused2<N> that are co-resident on the whole device (its batch wait relies
-// on every workgroup running at once); 0 when N has no fused kernel.
-template <int N>
-static int fused_resident(int cu) {
-  if constexpr (N <= 128) {
-    constexpr int NT = FusedKit<N>::NT;
-    int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_fused2<N, true>, NT, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_fused2<N, false>, NT, 0) != hipSuccess)
-      return 0;
-    return cu * std::min(a, b);
-  } else {
-    (void)cu;
-    return 0;
-  }
-}
-
 static void free_plan(ptyx_plan* pl) {
   for (void* q : pl->allocs) (void)hipFree(q);
   delete pl;
 }
 
-extern "C" int ptyx_version(void) { return 101; }
+extern "C" int ptyx_version(void) { return PTYX_ABI_VERSION; }
+
+extern "C" int ptyx_abi_struct_sizes(size_t* out, int32_t cap) {
+  const size_t sz[7] = {sizeof(ptyx_dims),        sizeof(ptyx_inputs),          sizeof(ptyx_grads),
+                        sizeof(ptyx_loss_cfg),    sizeof(ptyx_kernel_stat),     sizeof(ptyx_obj_constraints),
+                        sizeof(ptyx_meas_proc)};
+  for (int i = 0; out && i < cap && i < 7; ++i) out[i] = sz[i];
+  return 7;
+}
 
 extern "C" const char* ptyx_last_error(void) { return g_err.c_str(); }
 
@@ -785,6 +774,10 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   if (!out || !dims) return fail(PTYX_EINVAL, "null argument");
   *out = nullptr;
   const ptyx_dims& d = *dims;
+  if (d.abi_version != PTYX_ABI_VERSION)
+    return fail(PTYX_EINVAL, "ptyx_dims.abi_version " + std::to_string(d.abi_version) + " != " +
+                                 std::to_string(PTYX_ABI_VERSION) +
+                                 ": the binding's structs follow another revision of include/ptyx.h");
   if (!is_supported_n(d.N)) return fail(PTYX_EUNSUPPORTED, "N must be one of 32, 64, 128, 256");
   if (d.P < 1 || d.O < 1 || d.Nz < 1 || d.n_scans < 1 || d.max_patterns < 1)
     return fail(PTYX_EINVAL, "P, O, Nz, n_scans, max_patterns must be >= 1");
@@ -817,8 +810,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
       (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
       (rc = dalloc(pl, &pl->hslab, prop_grad ? (size_t)pl->nwg * N2 : 0)) ||
-      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride)) ||
-      (rc = dalloc(pl, &pl->sync, ((size_t)d.max_patterns + 2 + 3) / 4 * 4))) {
+      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride))) {
     free_plan(pl);
     return rc;
   }
@@ -840,28 +832,15 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->ffc_cap = cap;
     }
   }
-  if (lds && d.P * d.O * d.Nz == 1 && pl->fast) {
-    // one-pass path: g_O slot per pattern of a call (N² float2), bounded by PTYX_OBJ_SCRATCH_MB
+  if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast) {
+    // single-slice register engine: one g_O slot per pattern of a call (N² float2), bounded by
+    // PTYX_OBJ_SCRATCH_MB; larger calls are split by the host at mini-batch boundaries
     long long mb = 16384;
     if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2));
-    int res = 0;
-    PTYX_DISPATCH_N(d.N, res = fused_resident, cu);
-    pl->nwg_fused = std::min(res, pl->nwg);
-    if (cap > 0 && pl->nwg_fused > 0) {
-      if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
-          (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) ||
-          (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns))) {
-        free_plan(pl);
-        return rc;
-      }
-      pl->og_cap = cap;
-    }
-  }
-  if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast && pl->og_cap > 0) {
     const char* f3 = std::getenv("PTYX_FUSED3");
     int occ3 = 0;
-    if (!(f3 && f3[0] == '0') &&
+    if (!(f3 && f3[0] == '0') && cap > 0 &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, 0) == hipSuccess &&
         occ3 > 0) {
       int o2 = 0;
@@ -870,11 +849,13 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
       // segment ids = mini-batches + workgroups of a call; sized for a mean mini-batch of ≥ 8
-      // patterns (PTYX_SEG_DIV); calls with more segments take the k_fused2 path
+      // patterns (PTYX_SEG_DIV); calls with more segments take the two-pass engine
       long long div = 8;
       if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
       pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
-      if ((rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
+      if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
           (rc = dalloc(pl, &pl->bbox, 4)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Ny * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
@@ -884,6 +865,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
         free_plan(pl);
         return rc;
       }
+      pl->og_cap = cap;
     }
   }
   if (d.N == 128 && d.P * d.O == 1 && d.Nz > 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast) {
@@ -966,6 +948,7 @@ static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t
   a.H = reinterpret_cast<const float2*>(in->H);
   a.occu = in->omode_occu; a.meas = in->meas;
   a.ptilt = in->obj_tilts; a.kvec = in->kvec; a.dz = in->dz;
+  a.mrow = in->meas_rows;
   a.idx = idx; a.n_idx = n_idx;
   a.Ibuf = pl->Ibuf;
   a.slab = pl->slab; a.scratch = pl->scratch; a.scratch_stride = pl->scratch_stride;
@@ -1018,42 +1001,6 @@ static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, 
     hipLaunchKernelGGL((k_adjoint<N, true, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
   else
     hipLaunchKernelGGL((k_adjoint<N, false, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
-}
-template <int N>
-static void launch_fused(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
-  if constexpr (Geo<N>::kLds) {
-    ProfScope ps(pl, kKFused, st);
-    const dim3 gr(pl->nwg), bl(Geo<N>::NT);   // persistent: every workgroup resident (1 per CU at N = 128)
-    if (a.shift) hipLaunchKernelGGL((k_fused1<N, true>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_fused1<N, false>), gr, bl, 0, st, a);
-  }
-}
-template <int N>
-static void launch_fused2(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
-  if constexpr (N <= 128) {
-    constexpr int NT = FusedKit<N>::NT;
-    {
-      ProfScope ps(pl, kKTable, st);
-      hipLaunchKernelGGL(k_pattern_table, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
-                         a.n_batches, a.crop, a.n_scans, a.Ny, a.Nx, N, pl->bid, pl->geo);
-    }
-    ProfScope ps(pl, kKFused, st);
-    const dim3 gr(pl->nwg_fused), bl(NT);   // every workgroup co-resident (fused_resident)
-    if (a.shift) hipLaunchKernelGGL((k_fused2<N, true>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_fused2<N, false>), gr, bl, 0, st, a);
-  }
-}
-template <int N>
-static void launch_gather(const ptyx_plan* pl, const KArgs& a, hipStream_t st, int sparse_n) {
-  if constexpr (N <= 128) {
-    GatherArgs g{};
-    g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
-    g.Ny = a.Ny; g.Nx = a.Nx; g.tiles_x = (a.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse_n;
-    g.obja = a.obja; g.objp = a.objp; g.d_obja = a.d_obja; g.d_objp = a.d_objp;
-    const int tiles = g.tiles_x * ((a.Ny + kGTY - 1) / kGTY);
-    ProfScope ps(pl, kKGather, st);
-    hipLaunchKernelGGL(k_obj_gather<N>, dim3(tiles), dim3(64 * kGWaves), 0, st, g);
-  }
 }
 template <int N>
 static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe,
@@ -1133,7 +1080,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   f3::F3Args f{};
   f.n_idx = a.n_idx; f.n_scans = a.n_scans; f.Ny = d.Ny; f.Nx = d.Nx;
   f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.shifts = a.shifts;
-  f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas);
+  f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas); f.mrow = a.mrow;
   f.occp = in->omode_occu;
   f.q = single ? cfg->single_q : cfg->poissn_q;
   f.eps2 = cfg->poissn_eps;
@@ -1354,25 +1301,8 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.w2 = cfg->poissn_w;
   a.ws = cfg->sparse_w;
   a.grad_scale = cfg->grad_scale;
-  a.sync = pl->sync;
-  {
-    const char* dbg = std::getenv("PTYX_DEBUG_NOWAIT");
-    a.debug_nowait = (dbg && dbg[0] == '1') ? 1 : 0;
-  }
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;
   const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
-  // one pass per pattern (k_fused2) when every mini-batch fits the co-resident grid, the call
-  // fits the object-gradient slots and exactly one data term is on (its coefficient factors out)
-  const bool fused2 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && !std::getenv("PTYX_FUSED_V1") &&
-                      cfg->max_batch > 0 && cfg->max_batch <= pl->nwg_fused && n_idx <= pl->og_cap &&
-                      (cfg->single_on != 0) != (cfg->poissn_on != 0);
-  // earlier one-pass variant (atomics, dynamic dequeue): both data terms on, or PTYX_FUSED_V1=1
-  const bool fused = !fused2 && any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && cfg->max_batch > 0 &&
-                     cfg->max_batch <= pl->nwg;
-  if (fused2) {
-    a.bid = pl->bid;
-    a.ogscr = pl->ogscr;
-  }
   // register-resident engine (k_fused3): N = 128, f32 DPs, one data term, slots and segment
   // slabs large enough for the call (no co-residency or max_batch condition: it never waits)
   const bool fused3 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 &&
@@ -1390,53 +1320,31 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
 #endif
   }
 
+  // two-pass engine: k_forward (dp, loss partial sums) → k_finalize → k_adjoint
   if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
-  if (fused || fused2) {
-    const size_t sync_bytes = ((size_t)(2 + n_batches) * sizeof(unsigned) + 15) / 16 * 16;
-    hipError_t e = hipMemsetAsync(pl->sync, 0, sync_bytes, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(sync)");
-    if (fused2) {
-      PTYX_DISPATCH_N(pl->d.N, launch_fused2, pl, a, st);
-    } else {
-      PTYX_DISPATCH_N(pl->d.N, launch_fused, pl, a, st);
-    }
-    if ((rc = launch_status("k_fused launch"))) return rc;
-  } else {
-    if (any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
-      a.ffc = pl->ffc;
-      a.ffc_per = pl->ffc_per;
-    }
-    PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
-    if ((rc = launch_status("k_forward launch"))) return rc;
+  if (any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
+    a.ffc = pl->ffc;
+    a.ffc_per = pl->ffc_per;
   }
+  PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+  if ((rc = launch_status("k_forward launch"))) return rc;
   FinArgs f{};
   f.boff = boff; f.n_batches = n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
   f.psums = pl->psums; f.occu = in->omode_occu;
   f.single_on = cfg->single_on; f.pois_on = cfg->poissn_on; f.sparse_on = cfg->sparse_on;
   f.sparse_n = cfg->sparse_n; f.w1 = cfg->single_w; f.w2 = cfg->poissn_w; f.ws = cfg->sparse_w;
   f.grad_scale = cfg->grad_scale; f.coef = pl->coef; f.loss_terms = loss_terms;
-  if (fused2 && (gz.d_obja || gz.d_objp)) {
-    f.pcoef = pl->pcoef;
-    f.ci = cfg->single_on ? 0 : 1;
-  }
   {
     ProfScope ps(pl, kKFinalize, st);
     hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
   }
   if ((rc = launch_status("k_finalize launch"))) return rc;
   if (!any_grad) return PTYX_OK;
-  if (fused2) {
-    if (gz.d_obja || gz.d_objp) {
-      PTYX_DISPATCH_N(pl->d.N, launch_gather, pl, a, st, cfg->sparse_on ? cfg->sparse_n : 1);
-      if ((rc = launch_status("k_obj_gather launch"))) return rc;
-    }
-  } else if (!fused) {
-    PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
-    if ((rc = launch_status("k_adjoint launch"))) return rc;
-    if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
-  }
+  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
+  if ((rc = launch_status("k_adjoint launch"))) return rc;
+  if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
   if (gz.d_probe) {
-    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, fused2 ? pl->nwg_fused : pl->nwg);
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, pl->nwg);
     if ((rc = launch_status("probe finalize launch"))) return rc;
   }
   return PTYX_OK;

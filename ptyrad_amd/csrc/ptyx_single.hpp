@@ -170,7 +170,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward1(KArgs a) {
       for (int s = 0; s < SL; ++s) {
         int y, x;
         PM::last(tid, s, y, x);
-        mv[s] = load_meas_nt(a, g.s, fftshift_index<N>(y, x), N2);
+        mv[s] = load_meas_nt(a, g.m, fftshift_index<N>(y, x), N2);
       }
     }
     float sums[4] = {0.f, 0.f, 0.f, 0.f};
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
       PM::last(tid, s, y, x);
       const int e = fftshift_index<N>(y, x);
       if constexpr (EXT) mv[s] = __builtin_nontemporal_load(a.dLdI_ext + (size_t)pat * N2 + e);
-      else mv[s] = load_meas_nt(a, g.s, e, N2);
+      else mv[s] = load_meas_nt(a, g.m, e, N2);
     }
     // far field → g_Ψ = 2 occ Ψ ∂L/∂I
     fft2d<N, NT, -1, true>(
@@ -372,275 +372,4 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
       }
     }
   }
-}
-
-// =====================================================================================
-// One pass per pattern: forward, loss and adjoint fused (4 FFTs instead of 6).
-//
-// The NRMSE of a mini-batch needs Σ over the whole batch before any of its patterns can be
-// back-propagated (losses.py:45-47).  Workgroups dequeue patterns in batch order (one atomic
-// head), run the forward pass, keep Ψ in registers, publish the pattern's partial sums and
-// arrive on the batch's counter; then they wait for the batch's last arrival, reduce its sums
-// (same fixed order in every workgroup, so every workgroup derives identical coefficients) and
-// continue with the adjoint.  Deadlock-free when the resident grid is at least the largest
-// mini-batch (launcher checks): the batch at the dequeue front always has free workgroups.
-// Spins are bounded; a timeout sets sync[1] instead of hanging.
-// Hand-off per MI355X_MICROARCH.md "Valid forms": plain stores → fence(release, agent) →
-// vmcnt(0) → relaxed agent atomic add; consumer: relaxed poll → fence(acquire, agent) →
-// vmcnt(0) → barrier → plain loads.
-
-template <int N, bool SHIFT>
-__global__ __launch_bounds__(Geo<N>::NT) void k_fused1(KArgs a) {
-  constexpr int NT = Geo<N>::NT;
-  constexpr int N2 = N * N;
-  using PM = PassMap<N, NT>;
-  constexpr int SF = PM::kFirstSlots, SL = PM::kLastSlots;
-  constexpr float inv_n = 1.0f / (float)N, inv_n2 = 1.0f / (float)N2;
-  __shared__ float2 s_tw[N], s_wy[N], s_wx[N];
-  __shared__ float s_red[(NT / 64) * 5];
-  __shared__ float s_coef[4];
-  __shared__ int s_pat;
-  __shared__ float2 s_buf[LdsArray<N>::kElems];
-  for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
-  const LdsArray<N> arr{s_buf};
-  float2* slab = a.slab + (size_t)blockIdx.x * N2;
-  if (a.need_probe)
-    for (int e = opaque_tid(); e < N2; e += NT) slab[e] = make_float2(0.f, 0.f);
-  unsigned* head = a.sync;
-  unsigned* err = a.sync + 1;
-  unsigned* arrive = a.sync + 2;
-  const float occ = a.occu[0];
-  if (threadIdx.x == 0) s_pat = (int)atomicAdd(head, 1u);
-  __syncthreads();
-#if PTYX_EXP_PHASE_TIMES
-  unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long ph_prev = wall_clock64();
-  int ph_n = 0;
-#endif
-
-  for (;;) {
-    const int pat = s_pat;
-    if (pat >= a.n_idx) break;
-#if PTYX_EXP_PHASE_TIMES
-    ++ph_n;
-#endif
-    int m;
-    {
-      int lo = 0, hi = a.n_batches;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.boff[mid] <= pat) lo = mid;
-        else hi = mid;
-      }
-      m = lo;
-    }
-    const int b0 = a.boff[m], b1 = a.boff[m + 1];
-    const PatternGeom g = pattern_geom(a, pat, N);
-    const int tid = opaque_tid();
-    float2 fp[SF];
-    float oa[SL], op[SL];
-    prefetch_spectrum<N, NT, SHIFT>(a, tid, fp);
-    prefetch_object<N, NT>(a, g, tid, oa, op);
-    if constexpr (SHIFT) build_ramps<N, NT>(g, s_wy, s_wx);
-    float sp = 0.f;
-    if (a.sparse_on) {
-#pragma unroll
-      for (int s = 0; s < SL; ++s) {
-        const float ap = fabsf(op[s]);
-        sp += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
-      }
-    }
-    PTYX_PHASE(0);
-    float2 pb[SL];   // ψ⁰
-    exit_wave<N, NT, SHIFT>(a, arr, s_tw, s_wy, s_wx, tid, fp, oa, op, [&](float2 w, int s) { pb[s] = w; });
-    PTYX_PHASE(1);
-    float mv[SL];
-#pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      int y, x;
-      PM::last(tid, s, y, x);
-      mv[s] = load_meas_nt(a, g.s, fftshift_index<N>(y, x), N2);
-    }
-    // far field: Ψ stays in LDS across the batch wait; partial sums of the loss
-    float sums[4] = {0.f, 0.f, 0.f, 0.f};
-    fft2d<N, NT, -1, true>(
-        arr, s_tw, [&](int, int, float2 v, int) { return v; },
-        [&](int y, int x, float2& v, int s) {
-          const float2 Psi = cscale(v, inv_n);
-          v = Psi;
-          const float I = fmaf(occ, cabs2(Psi), kDpEps), M = mv[s];
-          if (a.dp_out) a.dp_out[(size_t)pat * N2 + fftshift_index<N>(y, x)] = I;
-          if (a.single_on) {
-            const float Iq = powq(I, a.q1), Mq = powq(M, a.q1), d = Iq - Mq;
-            sums[0] = fmaf(d, d, sums[0]);
-            sums[1] += Mq;
-          }
-          if (a.pois_on) {
-            const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
-            sums[2] += Mq * fast_ln(Iq + a.eps2) - Iq;
-            sums[3] += Mq;
-          }
-          return true;
-        });
-    PTYX_PHASE(2);
-    {
-      float v5[5] = {sums[0], sums[1], sums[2], sums[3], sp};
-      block_sum<NT, 5>(v5, s_red);
-      if (threadIdx.x == 0) {
-        // write-through (sc1) stores of the partial sums, drained, then the arrival: no release
-        // fence (it would write back the whole, slab-dirtied XCD L2 on every pattern)
-        float* ps_out = a.psums + (size_t)pat * kNSum;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) __hip_atomic_store(ps_out + i, v5[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ps_out + kSumBase, v5[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(arrive + m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // wait for the whole mini-batch
-        const unsigned want = (unsigned)(b1 - b0);
-        unsigned spins = 0;
-        while (!a.debug_nowait &&
-               __hip_atomic_load(arrive + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > kMaxSpins) {
-            atomicOr(err, 1u);
-            break;
-          }
-        }
-        // next pattern: dequeued only now (after the wait), so a workgroup never holds an
-        // unstarted pattern of a batch it is waiting on
-        s_pat = (int)atomicAdd(head, 1u);
-      }
-      __syncthreads();
-    }
-    PTYX_PHASE(3);
-    // batch coefficients (wave 0, after the barrier its polling lane joined; sc1 loads, as the
-    // sums were stored sc1; identical fixed-order reduction in every workgroup)
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      double t[5] = {0, 0, 0, 0, 0};
-      for (int q = b0 + lane; q < b1; q += 64) {
-        float* pq = a.psums + (size_t)q * kNSum;
-        t[0] += __hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t[1] += __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t[2] += __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t[3] += __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t[4] += __hip_atomic_load(pq + kSumBase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int msk = 32; msk >= 1; msk >>= 1) t[i] += __shfl_xor(t[i], msk, 64);
-      if (lane == 0) {
-        const double B = (double)(b1 - b0), K = B * N2;
-        double c1 = 0, c2 = 0, cs = 0;
-        if (a.single_on) {
-          const double mu = t[1] / K, rmse = (double)sqrtf((float)(t[0] / K));
-          c1 = rmse > 0 ? a.w1 / (mu * K * rmse) : 0.0;
-        }
-        if (a.pois_on) c2 = -a.w2 / ((t[3] / K) * K);
-        if (a.sparse_on) {
-          const double cnt = B * a.Nz * N2, mo = t[4] / cnt;
-          // mo^(1/n - 1) on the exp2/log2 units (a libm pow here would inflate the register
-          // allocation of the whole persistent loop)
-          const double dm = a.sparse_n == 1 ? 1.0
-                            : (mo > 0 ? (double)powq((float)mo, 1.0f / (float)a.sparse_n - 1.0f) : 0.0);
-          cs = a.ws * occ * dm / cnt;
-        }
-        s_coef[0] = (float)(c1 * a.grad_scale);
-        s_coef[1] = (float)(c2 * a.grad_scale);
-        s_coef[2] = (float)(cs * a.grad_scale);
-      }
-    }
-    __syncthreads();
-    PTYX_PHASE(4);
-    const float c1 = s_coef[0], c2 = s_coef[1], csp = s_coef[2];
-    // g_Ψ = 2 occ Ψ ∂L/∂I into LDS (the far-field pass's own point order)
-#pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      int y, x;
-      PM::last(tid, s, y, x);
-      const float2 Psi = arr.ld(y, x);
-      const float I = fmaf(occ, cabs2(Psi), kDpEps), M = mv[s], rI = 1.0f / I;
-      float dLdI = 0.f;
-      if (a.single_on) {
-        const float Iq = powq(I, a.q1), Mq = powq(M, a.q1);
-        dLdI = c1 * (Iq - Mq) * a.q1 * Iq * rI;
-      }
-      if (a.pois_on) {
-        const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
-        dLdI += c2 * (Mq / (Iq + a.eps2) - 1.0f) * a.q2 * Iq * rI;
-      }
-      if (PM::last_active(tid, s)) arr.st(y, x, cscale(Psi, 2.0f * occ * dLdI));
-    }
-    __syncthreads();
-    PTYX_PHASE(5);
-    // back to real space; object gradient (scatter-add); g ⊙ conj(O) into LDS
-    fft2d<N, NT, +1, true>(
-        arr, s_tw, [&](int, int, float2 v, int) { return v; },
-        [&](int y, int x, float2& v, int s) {
-          const float2 gv = cscale(v, inv_n);
-          const size_t off = obj_off(a, 0, 0, g.cy + y, g.cx + x);
-          const float A = a.obja[off], ph = a.objp[off];
-          float sn, cs;
-          phase_sincos(ph, &sn, &cs);
-          const float2 gO = cmulc(gv, pb[s]);
-#if !PTYX_EXP_NO_OBJ_ATOMIC
-          if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));
-          if (a.d_objp) {
-            float dph = A * fmaf(gO.y, cs, -gO.x * sn);
-            if (csp != 0.f) {
-              const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
-              dph += a.sparse_n == 1 ? csp * sg : csp * powq(fabsf(ph), (float)(a.sparse_n - 1)) * sg;
-            }
-            atomicAdd(a.d_objp + off, dph);
-          }
-#else
-          if (gO.x == 1234.5f) a.d_obja[off] = gO.y;   // keep gO live
-#endif
-          v = cmulc(gv, make_float2(A * cs, A * sn));
-          return true;
-        });
-    PTYX_PHASE(6);
-    if constexpr (SHIFT) {
-      if (a.need_probe || a.d_shifts) {
-        float ds[2] = {0.f, 0.f};
-        fft2d<N, NT, -1, true>(
-            arr, s_tw, [&](int, int, float2 v, int) { return v; },
-            [&](int y, int x, float2& G, int) {
-              const float2 W = cmul(s_wy[y], s_wx[x]);
-              const float im = cmulc(cmul(a.Fp[y * N + x], W), G).y;
-              ds[0] = fmaf(6.283185307179586f * shift_g<N>(y), im, ds[0]);
-              ds[1] = fmaf(6.283185307179586f * shift_g<N>(x), im, ds[1]);
-#if !PTYX_EXP_NO_SLAB
-              if (a.need_probe) slab[y * N + x] = cadd(slab[y * N + x], cmulc(G, W));
-#endif
-              return false;
-            });
-        if (a.d_shifts) {
-          block_sum<NT, 2>(ds, s_red);
-          if (threadIdx.x == 0) {
-            atomicAdd(a.d_shifts + 2 * g.s, ds[0] * inv_n2);
-            atomicAdd(a.d_shifts + 2 * g.s + 1, ds[1] * inv_n2);
-          }
-        }
-      }
-    } else {
-      if (a.need_probe) {
-#pragma unroll
-        for (int s = 0; s < SL; ++s) {
-          int y, x;
-          PM::last(tid, s, y, x);
-          if (PM::last_active(tid, s)) slab[y * N + x] = cadd(slab[y * N + x], arr.ld(y, x));
-        }
-      }
-    }
-    __syncthreads();
-    PTYX_PHASE(7);
-  }
-#if PTYX_EXP_PHASE_TIMES
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 128))
-    printf("PHASES wg %d n %d us: pre %.1f ifft1 %.1f fft2 %.1f wait %.1f coef %.1f gpsi %.1f ifft3 %.1f fft4 %.1f\n",
-           (int)blockIdx.x, ph_n, ph_acc[0] * 0.01, ph_acc[1] * 0.01, ph_acc[2] * 0.01, ph_acc[3] * 0.01,
-           ph_acc[4] * 0.01, ph_acc[5] * 0.01, ph_acc[6] * 0.01, ph_acc[7] * 0.01);
-#endif
 }

@@ -108,7 +108,8 @@ class Plan:
             pass
 
     # ------------------------------------------------------------------ marshalling
-    def _inputs(self, obja, objp, probe_rv, shifts, H, occu, crop_pos, meas, tilts=None, kvec=None, dz=0.0):
+    def _inputs(self, obja, objp, probe_rv, shifts, H, occu, crop_pos, meas, tilts=None, kvec=None, dz=0.0,
+                meas_rows=None):
         d, dev = self.dims, self.device
         _need(obja, torch.float32, "obja", dev)
         _need(objp, torch.float32, "objp", dev)
@@ -130,8 +131,13 @@ class Plan:
                 raise ValueError("H must be (N, N) complex64")
         if meas is not None:
             _need(meas, torch.float16 if self.meas_f16 else torch.float32, "meas", dev)
-            if tuple(meas.shape) != (d.n_scans, d.N, d.N):
-                raise ValueError(f"meas shape {tuple(meas.shape)} != {(d.n_scans, d.N, d.N)}")
+            rows = d.n_scans if meas_rows is None else meas.shape[0]
+            if tuple(meas.shape) != (rows, d.N, d.N):
+                raise ValueError(f"meas shape {tuple(meas.shape)} != {(rows, d.N, d.N)}")
+        if meas_rows is not None:   # rank-local measurement block (scan index -> row)
+            _need(meas_rows, torch.int32, "meas_rows", dev)
+            if tuple(meas_rows.shape) != (d.n_scans,):
+                raise ValueError("meas_rows must be (n_scans,) int32")
         if tilts is not None:
             _need(tilts, torch.float32, "obj_tilts", dev)
             _need(kvec, torch.float32, "kvec", dev)
@@ -139,7 +145,7 @@ class Plan:
                 raise ValueError("per-position obj_tilts must be (n_scans, 2) and kvec (N,)")
         inp = _lib.Inputs(_ptr(obja), _ptr(objp), _ptr(probe_rv), _ptr(shifts), _ptr(H), _ptr(occu),
                           _ptr(crop_pos), _ptr(meas), _ptr(tilts), _ptr(kvec if tilts is not None else None),
-                          float(dz))
+                          float(dz), _ptr(meas_rows))
         return inp, H
 
     def _idx(self, idx):
@@ -200,8 +206,9 @@ class Plan:
                           grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None):
         """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5).
 
-        max_batch: largest mini-batch size (enables the one-pass fused kernel); derived from
-        host-side offsets when not given, 0 (= two-pass) for device-only offsets.
+        batch_offsets on the host (numpy / list / CPU tensor) let calls larger than the plan's
+        capacity (max_patterns, or the register engines' slot capacity) be split at mini-batch
+        boundaries; device offsets must fit in one call.
         """
         host_off = not (isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu")
         if max_batch is None:
@@ -223,7 +230,8 @@ class Plan:
         if loss_terms is None:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
-                                  t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0))
+                                  t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0),
+                                  t.get("meas_rows"))
         cfg = loss_cfg.to_c(grad_scale, max_batch)
         g = self._grads(grads)
         _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
@@ -239,6 +247,8 @@ class Plan:
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
         _need(dp, torch.float32, "dp", self.device)
         meas = t["meas"]
+        if t.get("meas_rows") is not None:   # pacbed addresses meas through idx only: map it to rows
+            idx_t = t["meas_rows"][idx_t.long()].contiguous()
         _need(meas, torch.float16 if self.meas_f16 else torch.float32, "meas", self.device)
         ws = torch.empty(int(self.lib.ptyx_pacbed_ws_bytes(self.dims.N, nb)) // 8 + 1, dtype=torch.float64,
                          device=self.device)

@@ -14,6 +14,21 @@ import torch
 from .engine import LOSS_TERM_NAMES, LossConfig, batch_offsets
 
 
+def _engine_terms(plan, t, idx_t, off, cfg, grads, grad_scale, shift_probes):
+    """One ptyx_forward_loss_grad call (plus the pacbed loss and its adjoint when on); gradients
+    are accumulated (+=) into ``grads``, scaled by ``grad_scale``.  ``off``: host batch offsets
+    (the Plan splits calls beyond its capacity at mini-batch boundaries)."""
+    if cfg.pacbed_on:   # loss_pacbed (losses.py:77-89): HIP loss on the call's dp, then the HIP adjoint
+        N = t["probe"].shape[1]
+        dp = torch.empty((int(idx_t.numel()), N, N), dtype=torch.float32, device=t["obja"].device)
+        terms = plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale, dp_out=dp)
+        dLdI = plan.loss_pacbed(t, idx_t, off, dp, cfg, terms, grad_scale=grad_scale, want_dldi=bool(grads))
+        if grads:
+            plan.adjoint_dldi(t, idx_t, dLdI, {k: v for k, v in grads.items() if k != "shifts" or shift_probes})
+        return terms
+    return plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale)
+
+
 class _FusedLoss(torch.autograd.Function):
     """Σ_m loss_m over mini-batches; backward = cached engine gradients × grad_output.
 
@@ -32,15 +47,7 @@ class _FusedLoss(torch.autograd.Function):
         t = {"obja": obja.detach(), "objp": objp.detach(), "probe": probe_rv.detach(), "shifts": shifts.detach(),
              "H": H_rv.detach(), "tilts": None if tilts is None else tilts.detach().contiguous()}
         t.update(base)
-        if cfg.pacbed_on:   # loss_pacbed (losses.py:77-89): HIP loss on the call's dp, then the HIP adjoint
-            N = probe_rv.shape[1]
-            dp = torch.empty((int(idx_t.numel()), N, N), dtype=torch.float32, device=obja.device)
-            terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0, dp_out=dp)
-            dLdI = plan.loss_pacbed(t, idx_t, off_t, dp, cfg, terms, want_dldi=bool(grads))
-            if grads:
-                plan.adjoint_dldi(t, idx_t, dLdI, {k: v for k, v in grads.items() if k != "shifts" or shift_probes})
-        else:
-            terms = plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0)
+        terms = _engine_terms(plan, t, idx_t, off_t, cfg, grads, 1.0, shift_probes)
         ctx.grads = grads
         total = terms.sum()
         ctx.mark_non_differentiable(terms)
@@ -150,12 +157,66 @@ class CombinedLoss(torch.nn.Module):
             return self._preblur_fused(model, batches, cfg)
         if getattr(model, "otf_meas", False):
             return self._local_fused(model, batches, cfg)
+        self._check_held(model, flat)
         idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
-        off_t = torch.as_tensor(batch_offsets(batches)).to(dev, non_blocking=True)
+        off = batch_offsets(batches)   # host offsets: the Plan splits at mini-batch boundaries
         total, terms = _FusedLoss.apply(model.opt_obja, model.opt_objp, model.opt_probe,
                                         model.opt_probe_pos_shifts, model._H_rv(), model._tilts(), model._dz_t(),
-                                        model.plan, model._base(), idx_t, off_t, cfg, model.shift_probes)
+                                        model.plan, model._base(), idx_t, off, cfg, model.shift_probes)
         return total, terms
+
+    @staticmethod
+    def _check_held(model, flat):
+        held = getattr(model, "holds_measurements", None)
+        if held is not None and not held(flat):
+            raise IndexError("mini-batch positions outside this rank's measurement block (measurements_index)")
+
+    def fused_into(self, model, batches, grad_scale=1.0):
+        """The hot path without autograd: gradients of (Σ_m loss_m)·grad_scale are ACCUMULATED
+        straight into the ``.grad`` tensors of the optimisable parameters the loss reaches
+        (created, zeroed, when missing) — the engine writes them in place, no temporaries.
+        Equivalent to ``(fused(model, batches)[0] * grad_scale).backward()``.  Returns the
+        (n_batches, 5) loss terms.  Stages that need torch autograd (detector blur, pre-blur,
+        on-the-fly measurements, loss_simlar) run exactly that way, into the same ``.grad``."""
+        names = model.engine_grad_names()
+        for k in names:
+            p = model.optimizable_tensors[k]
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+        special = (getattr(model, "detector_blur", False) or getattr(model, "preblur", False) or
+                   getattr(model, "otf_meas", False) or self.loss_params.get("loss_simlar", {}).get("state", False))
+        if special:
+            total, terms = self.fused(model, batches)
+            if total.requires_grad:
+                torch.autograd.backward(total * grad_scale)
+            return terms
+        flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
+        model._check_indices(flat)
+        self._check_held(model, flat)
+        cfg = LossConfig.from_loss_params(self.loss_params)
+        dev = model.opt_obja.device
+        idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
+        H_rv = model._H_rv()
+        tilts, dz_t = model._tilts(), model._dz_t()
+        t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
+             "shifts": model.opt_probe_pos_shifts.detach(), "H": H_rv.detach(),
+             "tilts": None if tilts is None else tilts.detach().contiguous()}
+        t.update(model._base())
+        live = lambda p: p is not None and p.requires_grad and p.grad is not None  # noqa: E731
+        grads = {}
+        for k, p in (("obja", model.opt_obja), ("objp", model.opt_objp), ("probe", model.opt_probe),
+                     ("tilts", tilts), ("dz", dz_t)):
+            if live(p):
+                grads[k] = p.grad
+        if model.shift_probes and live(model.opt_probe_pos_shifts):
+            grads["shifts"] = model.opt_probe_pos_shifts.grad
+        if H_rv.requires_grad:          # optimised dz / tilts: dL/dH, then autograd through H(dz, tilts)
+            grads["H"] = torch.zeros_like(H_rv)
+        terms = _engine_terms(model.plan, t, idx_t, batch_offsets(batches), cfg, grads, float(grad_scale),
+                              model.shift_probes)
+        if "H" in grads:
+            torch.autograd.backward(H_rv, grads["H"])
+        return terms
 
     PREBLUR_GROUP = 8192
 

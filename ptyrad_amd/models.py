@@ -26,6 +26,12 @@ calls then take call-local positions / shifts / DPs (rows 0..n-1 of plan-sized a
 
 Per-position tilts (tilt_type 'each', models.py:330-356), fixed or optimised, also with an optimised slice thickness,
 run in the engine (per-pattern separable ramps, d_tilts, d_dz).
+
+Rank-local measurements (the data-parallel driver): ``init_variables["measurements"]``
+may hold only the DPs of the scan positions listed in ``init_variables["measurements_index"]``
+(e.g. ``DistContext.local_indices(batches, grad_accumulation)``); the engine reads them through a
+scan-index → row map (ptyx_inputs.meas_rows), and any call on a position outside the block raises.
+The reference registers the full stack on every rank (models.py:109).
 """
 from __future__ import annotations
 
@@ -133,13 +139,35 @@ class PtychoHIP(nn.Module):
                                                             dtype=torch.float32, device=device))
             self.register_buffer("H", torch.tensor(np.asarray(init_variables["H"]).astype(np.complex64), device=device))
             meas = init_variables.get("measurements")
-            meas_dtype = torch.float16 if (meas is not None and np.asarray(meas).dtype == np.float16) else torch.float32
-            self.register_buffer("measurements", None if meas is None else
-                                 torch.as_tensor(np.asarray(meas)).to(device=device, dtype=meas_dtype))
+            if isinstance(meas, torch.Tensor):   # e.g. ptyrad_amd.ingest output, already on the device
+                meas_dtype = torch.float16 if meas.dtype == torch.float16 else torch.float32
+                meas_t = meas.to(device=device, dtype=meas_dtype).contiguous()
+            else:
+                meas_dtype = torch.float16 if (meas is not None and np.asarray(meas).dtype == np.float16) \
+                    else torch.float32
+                meas_t = None if meas is None else torch.as_tensor(np.asarray(meas)).to(device=device,
+                                                                                        dtype=meas_dtype)
+            self.register_buffer("measurements", meas_t)
             for k, dt in (("N_scan_slow", torch.int32), ("N_scan_fast", torch.int32)):
                 self.register_buffer(k, torch.tensor(init_variables.get(k, 0), dtype=dt, device=device))
             self.register_buffer("crop_pos", torch.tensor(np.asarray(init_variables["crop_pos"]), dtype=torch.int32,
                                                           device=device))
+            # rank-local measurement block: row r of `measurements` is scan position meas_index[r]
+            mi = init_variables.get("measurements_index")
+            self.meas_index = None if mi is None else np.asarray(mi, dtype=np.int64).reshape(-1)
+            self.meas_rows = None
+            self._meas_rows_np = None
+            if self.meas_index is not None:
+                n_sc = int(self.crop_pos.shape[0])
+                if meas_t is None or meas_t.shape[0] != self.meas_index.size:
+                    raise ValueError("measurements_index must list one scan index per measurement row")
+                if self.meas_index.size and (self.meas_index.min() < 0 or self.meas_index.max() >= n_sc or
+                                             np.unique(self.meas_index).size != self.meas_index.size):
+                    raise ValueError("measurements_index must hold distinct scan indices in [0, N_scans)")
+                rows = np.full(n_sc, -1, np.int32)
+                rows[self.meas_index] = np.arange(self.meas_index.size, dtype=np.int32)
+                self._meas_rows_np = rows
+                self.meas_rows = torch.tensor(rows, device=device)
             for k in ("slice_thickness", "dx", "dk", "lambd"):
                 self.register_buffer(k, torch.tensor(float(init_variables.get(k, 0.0)), dtype=torch.float32,
                                                      device=device))
@@ -184,9 +212,18 @@ class PtychoHIP(nn.Module):
             if self.otf_meas:
                 cap = min(cap, 65535)
                 self._meas_buf = torch.zeros((cap, N, N), dtype=torch.float32, device=device)
-            self.plan = Plan(N, P, O, Nz, Ny, Nx, cap if self.otf_meas else n_scans, cap,
-                             shift_probes=self.shift_probes, meas_f16=self.meas_f16 and not self.otf_meas,
-                             device=device, prop_grad=self.prop_opt)
+            # the main plan (its workspace sized for `cap` patterns per call) is created on first use:
+            # pre-blur models run on patch-stack plans only
+            self._plan = None
+            self._plan_args = (N, P, O, Nz, Ny, Nx, cap if self.otf_meas else n_scans, cap)
+
+    @property
+    def plan(self):
+        if self._plan is None:
+            self._plan = Plan(*self._plan_args, shift_probes=self.shift_probes,
+                              meas_f16=self.meas_f16 and not self.otf_meas, device=self.opt_obja.device,
+                              prop_grad=self.prop_opt)
+        return self._plan
 
     # ------------------------------------------------------------------ reference API
     def get_complex_probe_view(self):
@@ -215,6 +252,32 @@ class PtychoHIP(nn.Module):
         if idx.size and (idx.min() < 0 or idx.max() >= self.crop_pos.shape[0]):
             raise IndexError("scan index out of range")
         return idx
+
+    def holds_measurements(self, indices) -> bool:
+        """True when this model's measurement block has the DPs of every scan index given."""
+        idx = self._check_indices(indices)
+        return self._meas_rows_np is None or bool(np.all(self._meas_rows_np[idx] >= 0))
+
+    def _meas_row_index(self, idx_t):
+        """Rows of `measurements` for scan indices idx_t (device int32); raises outside the block."""
+        if self.meas_rows is None:
+            return idx_t
+        if not self.holds_measurements(idx_t):
+            raise IndexError("a scan index outside this rank's measurement block (measurements_index)")
+        return self.meas_rows[idx_t.long()].contiguous()
+
+    def engine_grad_names(self):
+        """Optimisable tensors the loss reaches (the reference's autograd leaves .grad None for the
+        rest, e.g. slice_thickness with one slice: H is then unused, forward.py:60-63)."""
+        Nz = int(self.opt_obja.shape[1])
+        names = ["obja", "objp", "probe"]
+        if self.shift_probes:
+            names.append("probe_pos_shifts")
+        if self.change_thickness and Nz > 1:
+            names.append("slice_thickness")
+        if self.tilt_obj and self.change_tilt and Nz > 1:
+            names.append("obj_tilts")
+        return names
 
     def _init_propagator_grid(self):
         """create_grids (models.py:163-171) + init_propagator_vars (:221-223): Ky, Kx on the
@@ -270,6 +333,8 @@ class PtychoHIP(nn.Module):
     def _base(self, crop_pos=None, meas=None, stack=False):
         b = {"occu": self.omode_occu, "crop_pos": self.crop_pos if crop_pos is None else crop_pos,
              "meas": self.measurements if (meas is None and not stack) else meas}
+        if self.meas_rows is not None and meas is None and not stack:
+            b["meas_rows"] = self.meas_rows
         if self.pos_tilts:   # the ramps use the current dz (a host value: one sync per call if optimised)
             dz = float(self.opt_slice_thickness.detach()) if self.change_thickness else self._dz
             b.update(kvec=self.propagator_grid[0][:, 0].contiguous(), dz=dz)
@@ -300,19 +365,25 @@ class PtychoHIP(nn.Module):
     def detector_blur(self):
         return self.detector_blur_std not in (None, 0)
 
-    def _stack_plan(self, B):
-        """Plan for a (O, Nz, B·N, N) patch-stack object (pre-blurred patches of B positions)."""
-        plan = self._stack_plans.get(B)
+    @staticmethod
+    def _stack_capacity(B):
+        """Patch-stack plans come in power-of-two capacities (≥ 32), so the k / k+1 mini-batch
+        sizes of array_split, grad_accumulation groups and the last group share one plan."""
+        return max(32, 1 << (int(B) - 1).bit_length())
+
+    def _stack_plan(self, C):
+        """Plan for a (O, Nz, C·N, N) patch-stack object (pre-blurred patches, capacity C)."""
+        plan = self._stack_plans.get(C)
         if plan is None:
             if len(self._stack_plans) >= 4:
                 # drop the oldest; an autograd graph that still holds it keeps it alive (Plan.__del__)
                 self._stack_plans.pop(next(iter(self._stack_plans)))
             O, Nz = self.opt_obja.shape[:2]
             P, N = self.opt_probe.shape[:2]
-            plan = Plan(N, P, O, Nz, B * N, N, B, B, shift_probes=self.shift_probes,
+            plan = Plan(N, P, O, Nz, C * N, N, C, C, shift_probes=self.shift_probes,
                         meas_f16=self.meas_f16 and not self.otf_meas, device=self.opt_obja.device,
                         prop_grad=self.prop_opt)
-            self._stack_plans[B] = plan
+            self._stack_plans[C] = plan
         return plan
 
     def _blurred_patches(self, idx_t):
@@ -323,20 +394,33 @@ class PtychoHIP(nn.Module):
                 BlurredPatches.apply(self.opt_objp, self.crop_pos, idx_t, N, std))
 
     def _stack_inputs(self, idx_t, with_meas=False):
-        """Engine inputs on the patch stack: (obja, objp, shifts, plan, base, idx, patches)."""
+        """Engine inputs on the patch stack: (obja, objp, shifts, plan, base, idx, patches).
+
+        The stack is zero-padded to the plan capacity C; the engine runs on patterns 0..B-1 only."""
         B = int(idx_t.numel())
+        C = self._stack_capacity(B)
         N = self.opt_probe.shape[1]
         A, Ph = self._blurred_patches(idx_t)
         O, Nz = A.shape[:2]
         il = idx_t.long()
+        pad = C - B
         sh = self.opt_probe_pos_shifts[il]
+        if pad:
+            sh = torch.cat([sh, sh.new_zeros((pad, 2))])
+            Ap = torch.nn.functional.pad(A, (0, 0, 0, 0, 0, pad))
+            Php = torch.nn.functional.pad(Ph, (0, 0, 0, 0, 0, pad))
+        else:
+            Ap, Php = A, Ph
         meas = None
         if with_meas:
-            meas = self._gather_meas(idx_t) if self.otf_meas else self.measurements[il].contiguous()
-        base = self._base(stack_crop_pos(B, N, idx_t.device), meas, stack=True)
+            meas = self._gather_meas(idx_t) if self.otf_meas else \
+                self.measurements[self._meas_row_index(idx_t).long()].contiguous()
+            if pad:
+                meas = torch.cat([meas, meas.new_zeros((pad, N, N))])
+        base = self._base(stack_crop_pos(C, N, idx_t.device), meas, stack=True)
         ar = torch.arange(B, dtype=torch.int32, device=idx_t.device)
-        return (A.reshape(O, Nz, B * N, N), Ph.reshape(O, Nz, B * N, N), sh, self._tilts(il), self._stack_plan(B),
-                base, ar, (A, Ph))
+        return (Ap.reshape(O, Nz, C * N, N), Php.reshape(O, Nz, C * N, N), sh, self._tilts(il, C),
+                self._stack_plan(C), base, ar, (A, Ph))
 
     def get_obj_patches(self, indices):
         """models.py:251-284: (B,O,Nz,N,N,2) amplitude/phase patches (pre-blurred when enabled)."""
@@ -372,8 +456,11 @@ class PtychoHIP(nn.Module):
         if self.pos_tilts:
             Ky, Kx = self.propagator_grid
             t = self.opt_obj_tilts[torch.as_tensor(self._check_indices(indices), device=Ky.device)] / 1e3
-            return self.H * torch.exp(1j * self._dz * (Ky * torch.tan(t[:, 0, None, None]) +
-                                                       Kx * torch.tan(t[:, 1, None, None])))
+            ramp_arg = Ky * torch.tan(t[:, 0, None, None]) + Kx * torch.tan(t[:, 1, None, None])
+            if self.change_thickness:            # case 1 (models.py:339-342): the current dz
+                dz = self.opt_slice_thickness
+                return torch.exp(1j * dz * self.Kz) * torch.exp(1j * dz * ramp_arg)
+            return self.H * torch.exp(1j * self._dz * ramp_arg)
         return self._propagator()[None,]
 
     def get_propagated_probe(self, index):
@@ -403,6 +490,7 @@ class PtychoHIP(nn.Module):
             Hp, Wp, h1, w1, canvas = Hm, Wm, 0, 0, ctypes.c_void_p(0)
         sy, sx = self.meas_scale_factors if self.meas_scale_factors is not None else (1.0, 1.0)
         lib = _lib.load()
+        idx_t = self._meas_row_index(idx_t)
         st = ctypes.c_void_p(torch.cuda.current_stream(self.measurements.device).cuda_stream)
         _lib.check(lib.ptyx_meas_gather(st, ctypes.c_void_p(self.measurements.data_ptr()),
                                         int(self.measurements.dtype == torch.float16), Hm, Wm,
@@ -435,8 +523,8 @@ class PtychoHIP(nn.Module):
         idx = self._check_indices(indices)
         if self.otf_meas:
             return self._gather_meas(torch.as_tensor(idx, dtype=torch.int32).to(self.measurements.device))
-        idx = torch.as_tensor(idx, device=self.measurements.device, dtype=torch.long)
-        return self.measurements[idx].float()
+        idx = torch.as_tensor(idx, device=self.measurements.device, dtype=torch.int32)
+        return self.measurements[self._meas_row_index(idx).long()].float()
 
     def clear_cache(self):
         self._current_object_patches = None

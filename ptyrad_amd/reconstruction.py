@@ -1,18 +1,26 @@
 """Reconstruction loop on the HIP engine: PtyRAD's recon_step contract + RCCL data parallelism.
 
 Mirrors ``src/ptyrad/reconstruction.py``:
-  select_scan_indices :441-477, make_batches :479-587 ('random' and 'compact'),
+  select_scan_indices :441-477, make_batches :479-587 ('random', 'compact' and 'sparse'),
   recon_step :658-781 (Adam / SGD branch), toggle_grad_requires :783-790, loss_logger :808-832.
 
-Hot loop: every optimizer step's group of ``grad_accumulation`` mini-batches is ONE
-``CombinedLoss.fused`` engine call (each batch keeps its own NRMSE normalisation; the summed
-gradient / grad_accumulation equals the reference's accumulated ``.grad``).
+Hot loop: every optimizer step's group of ``grad_accumulation`` mini-batches is ONE engine call
+(``CombinedLoss.fused_into``: each batch keeps its own NRMSE normalisation, and the engine
+accumulates Σ_m ∂loss_m/∂θ / grad_accumulation straight into ``.grad`` — the reference's
+accumulated gradient, reconstruction.py:741-760, without autograd temporaries).
 
-Multi-GPU (replaces the accelerate/DDP wrapper, utils/common.py:58-90): ``DistContext``.  The
-mini-batches of a group are dealt round-robin to ranks, each rank runs its share, then ONE
-all-reduce(sum) over a flat buffer of every gradient gives all ranks the exact single-device
-accumulated gradient (up to fp32 summation order); every rank then takes the same optimizer
-step, so replicas stay identical.  No per-forward buffer broadcast, no loss averaging.
+Multi-GPU (replaces the accelerate/DDP wrapper, utils/common.py:58-90): ``DistContext``.
+* The mini-batches of a group are dealt round-robin to ranks.  Batches are fixed for the run
+  (recon_loop never regroups, reconstruction.py:634-636), so ``DistContext.local_indices`` tells
+  each rank, before loading anything, which scan positions' DPs it needs: the rank keeps only
+  those (PtychoHIP ``measurements_index``), unlike DDP which holds and broadcasts the whole stack.
+* The ``.grad`` of every parameter the loss reaches and that is trainable this iteration
+  (``toggle_grad_requires``) is a view into ONE flat buffer; the engine accumulates into the
+  views, ONE all-reduce(sum) of the buffer gives every rank the exact single-device accumulated
+  gradient (up to fp32 summation order), with no pack / unpack copies.  Frozen or unreached
+  parameters keep ``.grad = None`` (Adam skips them, as on one device).
+* Every rank then takes the same optimizer step, so replicas stay identical.  No per-forward
+  buffer broadcast, no loss averaging.
 """
 from __future__ import annotations
 
@@ -45,19 +53,60 @@ def select_scan_indices(N_scan_slow, N_scan_fast, subscan_slow=None, subscan_fas
     raise ValueError(f"Indices selection mode {mode} not implemented, use 'full', 'center' or 'sub'")
 
 
-def make_batches(indices, pos, batch_size, mode="random", verbose=True, rng=None):
-    """Mini-batches of ~batch_size indices (reference :479-587).  'random' = shuffled array_split."""
+def make_batches(indices, pos, batch_size, mode="random", verbose=True, rng=None, random_state=None):
+    """Mini-batches of ~batch_size indices (reference :479-587).
+
+    'random'  = shuffled array_split;
+    'compact' = MiniBatchKMeans clusters of the positions;
+    'sparse'  = one seed per compact cluster (the position closest to its centroid), then every
+                other index, in index order, joins the group whose nearest member is FARTHEST
+                from it (reference :548-587).  Same greedy rule; the per-group minimum distances
+                are kept as a running (groups × positions) array instead of the reference's full
+                pairwise-distance matrix, so memory is O(groups · positions), not O(positions²).
+    """
     indices = np.asarray(indices)
+    if pos is not None and len(indices) and indices.max() >= len(pos):
+        raise ValueError(f"Maximum index '{indices.max()}' is larger than total number of probe positions ({len(pos)})")
     num_batch = max(1, len(indices) // batch_size)
     if mode == "random":
         rng = rng if rng is not None else np.random.default_rng()
         return np.array_split(rng.permutation(indices), num_batch)
+    if mode not in ("compact", "sparse"):
+        raise ValueError(f"GROUP_MODE '{mode}' must be 'random', 'compact' or 'sparse'")
+    from sklearn.cluster import MiniBatchKMeans
+    pos = np.asarray(pos)
+    pos_s = pos[indices]
+    km = MiniBatchKMeans(init="k-means++", n_init=10, n_clusters=num_batch, max_iter=10, batch_size=3072,
+                         random_state=random_state)
+    km.fit(pos_s)
+    compact = [indices[np.where(km.labels_ == b)[0]] for b in range(num_batch)]
     if mode == "compact":
-        from sklearn.cluster import MiniBatchKMeans
-        km = MiniBatchKMeans(init="k-means++", n_init=10, n_clusters=num_batch, max_iter=10, batch_size=3072)
-        km.fit(np.asarray(pos)[indices])
-        return [indices[km.labels_ == b] for b in range(num_batch) if np.any(km.labels_ == b)]
-    raise NotImplementedError(f"GROUP_MODE '{mode}' is not implemented on this path (use 'random' or 'compact')")
+        return compact
+    return sparse_groups(indices, pos, compact)
+
+
+def sparse_groups(indices, pos, compact):
+    """The 'sparse' grouping of make_batches (reference :548-587) from its compact clusters."""
+    from scipy.spatial.distance import cdist
+    indices = np.asarray(indices)
+    pos = np.asarray(pos)
+    pos_s = pos[indices]
+    groups, used = [], []
+    for cb in compact:
+        centroid = np.mean(pos[cb], axis=0)
+        j = int(np.argmin(np.linalg.norm(pos_s - centroid, axis=1)))
+        groups.append([int(indices[j])])
+        used.append(j)
+    # dmin[g, s] = min over members m of group g of |pos[m] - pos[s]| (cdist, as the reference)
+    dmin = np.stack([cdist(pos[[g[0]]], pos)[0] for g in groups])
+    for idx in np.delete(indices.copy(), used):
+        g = int(np.argmax(dmin[:, idx]))
+        groups[g].append(int(idx))
+        np.minimum(dmin[g], cdist(pos[[idx]], pos)[0], out=dmin[g])
+    flat = np.sort(np.concatenate(groups))
+    if not np.array_equal(flat, np.sort(indices)):
+        raise AssertionError("sparse grouping lost or duplicated an index")
+    return [np.array(g) for g in groups]
 
 
 def toggle_grad_requires(model, niter, verbose=False):
@@ -93,15 +142,53 @@ class DistContext:
         """Round-robin deal of a group's mini-batches to ranks (positions of batch b on rank b % world)."""
         return [i for i in range(len(group_batches)) if i % self.world == self.rank]
 
+    def local_batches(self, batches, grad_accumulation=1):
+        """The mini-batches this rank processes over one iteration of recon_step (fixed batches)."""
+        ga = max(1, int(grad_accumulation))
+        out = []
+        for g0 in range(0, len(batches), ga):
+            group = batches[g0:g0 + ga]
+            out += [group[i] for i in self.my_batches(group)]
+        return out
+
+    def local_indices(self, batches, grad_accumulation=1):
+        """Sorted scan indices whose DPs this rank needs: its ``measurements_index`` block."""
+        mine = self.local_batches(batches, grad_accumulation)
+        if not mine:
+            return np.zeros(0, np.int64)
+        return np.unique(np.concatenate([np.asarray(b).reshape(-1) for b in mine]))
+
+    def grad_views(self, params):
+        """Give each param a zeroed ``.grad`` that is a view into ONE flat f32 buffer; returns it.
+        ``params`` must be the same list, in the same order, on every rank."""
+        n = sum(p.numel() for p in params)
+        dev = params[0].device if params else torch.device("cpu")
+        flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:
+            p.grad = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        return flat
+
+    def allreduce(self, flat):
+        """ONE all-reduce(sum) of the gradient buffer (in place)."""
+        if self.world > 1 and flat is not None and flat.numel():
+            dist.all_reduce(flat, group=self.group)
+
     def allreduce_grads(self, params):
-        """ONE all-reduce(sum) over a flat buffer of all gradients (zeros where a rank had none)."""
+        """All-reduce(sum) of the ``.grad`` of the trainable params (requires_grad True, a set
+        toggle_grad_requires makes identical on every rank); frozen ones keep ``.grad = None``
+        (reference zero_grad / toggle_grad_requires, reconstruction.py:739, 783-790)."""
         if self.world == 1:
             return
+        live = [p for p in params if p.requires_grad]
         grads = []
-        for p in params:
+        for p in live:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
             grads.append(p.grad)
+        if not grads:
+            return
         flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat, group=self.group)
         off = 0
@@ -137,20 +224,23 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     t0 = time_sync()
     toggle_grad_requires(model, niter, verbose)
     params = [p for g in optimizer.param_groups for p in g["params"]]
-    optimizer.zero_grad()
+    optimizer.zero_grad(set_to_none=True)
     ga = max(1, int(grad_accumulation))
     dev = model.opt_obja.device
+    # parameters whose .grad this iteration's steps fill: trainable now and reached by the loss
+    reached = {id(model.optimizable_tensors[k]) for k in model.engine_grad_names()}
+    live = [p for p in params if p.requires_grad and id(p) in reached]
     for g0 in range(0, len(batches), ga):
         group = batches[g0:g0 + ga]
         mine = ctx.my_batches(group)
+        flat = ctx.grad_views(live)
         if mine:
-            total, terms = loss_fn.fused(model, [group[i] for i in mine])
-            (total / ga).backward()
+            terms = loss_fn.fused_into(model, [group[i] for i in mine], grad_scale=1.0 / ga)
         else:
             terms = torch.zeros((0, 5), device=dev)
-        ctx.allreduce_grads(params)
+        ctx.allreduce(flat)
         optimizer.step()
-        optimizer.zero_grad()
+        optimizer.zero_grad(set_to_none=True)
         all_terms = ctx.gather_terms(terms, mine, len(group), dev).cpu().numpy()   # one sync per step
         for row in all_terms:
             for name, v in zip(LOSS_TERM_NAMES, row):

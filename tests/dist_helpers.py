@@ -15,6 +15,19 @@ from oracle import ptyx_oracle as orc
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+def _oracle_grads(model, batches, lp):
+    probe = (model.opt_probe[..., 0] + 1j * model.opt_probe[..., 1]).detach().numpy()
+    flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
+    rows = getattr(model, "meas_rows", None)
+    if rows is not None and np.any(rows[flat] < 0):
+        raise IndexError("a mini-batch position outside this rank's measurement block")
+    terms, _, g = orc.forward_loss_grad(
+        model.opt_obja.detach().numpy(), model.opt_objp.detach().numpy(), probe,
+        model.opt_probe_pos_shifts.detach().numpy(), model.crop_pos_np, model.H_np, model.occu_np,
+        model.meas_np, batches, lp, shift_probes=True)
+    return terms, g
+
+
 class _OracleFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, obja, objp, probe_rv, shifts, model, batches, lp):
@@ -37,7 +50,7 @@ class _OracleFused(torch.autograd.Function):
 class OracleModel(torch.nn.Module):
     """Parameter holder with the PtychoAD attribute contract recon_step uses."""
 
-    def __init__(self, z):
+    def __init__(self, z, start_iter=None, meas_index=None):
         super().__init__()
         self.opt_obja = torch.nn.Parameter(torch.tensor(z["init_obja"]))
         self.opt_objp = torch.nn.Parameter(torch.tensor(z["init_objp"]))
@@ -50,6 +63,15 @@ class OracleModel(torch.nn.Module):
         lrs = json.loads(str(z["lrs"]))
         self.lr_params = lrs
         self.start_iter = {k: (1 if v else None) for k, v in lrs.items()}
+        self.start_iter.update(start_iter or {})
+        self.meas_rows = None
+        if meas_index is not None:   # rank-local measurement block: other rows poisoned with NaN
+            rows = np.full(self.meas_np.shape[0], -1)
+            rows[meas_index] = np.arange(len(meas_index))
+            self.meas_rows = rows
+            m = np.full_like(self.meas_np, np.nan)
+            m[meas_index] = self.meas_np[meas_index]
+            self.meas_np = m
         self.optimizable_tensors = {"obja": self.opt_obja, "objp": self.opt_objp, "obj_tilts": self.opt_obj_tilts,
                                     "slice_thickness": self.opt_slice_thickness, "probe": self.opt_probe,
                                     "probe_pos_shifts": self.opt_probe_pos_shifts}
@@ -59,26 +81,46 @@ class OracleModel(torch.nn.Module):
     def clear_cache(self):
         pass
 
+    def engine_grad_names(self):
+        return ["obja", "objp", "probe", "probe_pos_shifts"]
+
 
 class OracleLoss:
     def __init__(self, lp):
         self.loss_params = lp
+
+    def fused_into(self, model, batches, grad_scale=1.0):
+        """recon_step's direct path: accumulate the oracle's gradients into the existing .grad."""
+        terms, g = _oracle_grads(model, batches, self.loss_params)
+        vals = {"obja": g["obja"], "objp": g["objp"], "probe": np.stack([g["probe"].real, g["probe"].imag], -1),
+                "probe_pos_shifts": g["shifts"]}
+        for k in model.engine_grad_names():
+            p = model.optimizable_tensors[k]
+            if p.requires_grad:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                p.grad += torch.tensor(vals[k], dtype=torch.float32) * grad_scale
+        return torch.tensor(terms, dtype=torch.float32)
 
     def fused(self, model, batches):
         return _OracleFused.apply(model.opt_obja, model.opt_objp, model.opt_probe, model.opt_probe_pos_shifts,
                                   model, batches, self.loss_params)
 
 
-def run_recon(z, rank_world=None, niter=None):
-    """Run the trajectory fixture through ptyrad_amd.reconstruction.recon_step; returns final params."""
+def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False):
+    """Run the trajectory fixture through ptyrad_amd.reconstruction.recon_step; returns final params.
+
+    start_iter: per-tensor overrides (staggered toggle_grad_requires); shard: each rank keeps only
+    its DistContext.local_indices rows of the measurements (others NaN-poisoned)."""
     from ptyrad_amd.reconstruction import DistContext, recon_step
-    model = OracleModel(z)
-    lp = json.loads(str(z["loss_params"]))
-    loss = OracleLoss(lp)
-    opt = torch.optim.Adam(model.optimizable_params)
     sizes = z["batch_sizes"]
     batches = np.split(z["batches"], np.cumsum(sizes)[:-1])
     ctx = DistContext()
+    mi = ctx.local_indices(batches, int(z["grad_accumulation"])) if shard else None
+    model = OracleModel(z, start_iter=start_iter, meas_index=mi)
+    lp = json.loads(str(z["loss_params"]))
+    loss = OracleLoss(lp)
+    opt = torch.optim.Adam(model.optimizable_params)
     cfn = None
     if "constraint_params" in z.files and json.loads(str(z["constraint_params"])) is not None:
         cp, pis = json.loads(str(z["constraint_params"])), float(z["probe_int_sum"])
@@ -99,16 +141,65 @@ def run_recon(z, rank_world=None, niter=None):
                                                        ("shifts", model.opt_probe_pos_shifts))}, model
 
 
-def dist_worker(rank, world, port, path, out_path):
+def dist_worker(rank, world, port, path, out_path, kw=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         z = np.load(path, allow_pickle=False)
-        params, model = run_recon(z)
+        params, model = run_recon(z, **(kw or {}))
         if rank == 0:
             np.savez(out_path, losses=np.array([v for _, v in model.loss_iters]), **params)
         else:
             np.savez(out_path.replace(".npz", f"_r{rank}.npz"), **params)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def gpu_recon(z, dist_ctx=None, shard=False, niter=None, ret_all=False):
+    """The trajectory fixture through PtychoHIP + CombinedLoss + recon_step on cuda:0 (the HIP
+    engine); with ``shard`` the model holds only DistContext.local_indices rows of the DPs."""
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    from ptyrad_amd.reconstruction import DistContext, create_optimizer, recon_step
+    device = torch.device("cuda", 0)
+    ctx = dist_ctx or DistContext()
+    lrs = json.loads(str(z["lrs"]))
+    batches = np.split(z["batches"], np.cumsum(z["batch_sizes"])[:-1])
+    iv = {"obja": z["init_obja"], "objp": z["init_objp"], "obj": z["init_obja"] * np.exp(1j * z["init_objp"]),
+          "probe": z["init_probe"], "probe_pos_shifts": z["init_shifts"], "omode_occu": z["occu"], "H": z["H"],
+          "measurements": z["meas"], "crop_pos": z["crop_pos"], "N_scan_slow": 4, "N_scan_fast": 4,
+          "slice_thickness": 2.0, "dx": 0.1494, "dk": 0.05, "lambd": 0.04, "obj_tilts": np.zeros((1, 2), np.float32)}
+    if shard:
+        mi = ctx.local_indices(batches, int(z["grad_accumulation"]))
+        iv["measurements"] = np.ascontiguousarray(z["meas"][mi])
+        iv["measurements_index"] = mi
+    up = {k: {"start_iter": (1 if v else None), "lr": v} for k, v in lrs.items()}
+    mp_ = {"detector_blur_std": None, "obj_preblur_std": None, "update_params": up,
+           "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
+    model = PtychoHIP(iv, mp_, device=device, verbose=False)
+    opt = create_optimizer(model.optimizer_params, model.optimizable_params)
+    loss_fn = CombinedLoss(json.loads(str(z["loss_params"])), device=device)
+    last = None
+    for it in range(1, (int(z["niter"]) if niter is None else niter) + 1):
+        last = recon_step(batches, int(z["grad_accumulation"]), model, opt, loss_fn, None, it, verbose=False,
+                          dist_ctx=ctx)
+    if ret_all:
+        return model, opt, loss_fn, batches, last
+    return model
+
+
+def gpu_dist_worker(rank, world, port, path, out_path):
+    """One rank of a gloo job whose engine runs on cuda:0 (both ranks share the one GPU)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ptyrad_amd.reconstruction import DistContext
+        z = np.load(path, allow_pickle=False)
+        model = gpu_recon(z, DistContext(), shard=True)
+        np.savez(out_path.replace(".npz", f"_r{rank}.npz"), obja=model.opt_obja.detach().cpu().numpy(),
+                 objp=model.opt_objp.detach().cpu().numpy(), probe=model.opt_probe.detach().cpu().numpy(),
+                 held=np.array(model.measurements.shape[0]))
     finally:
         torch.distributed.destroy_process_group()

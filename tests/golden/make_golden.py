@@ -184,12 +184,13 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
     print(f"{name}: loss={float(total):.7g} terms={[round(float(t), 7) for t in terms]}")
 
 
-def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumulation, seed, constraint_params=None):
+def run_trajectory(name, n, P, O, Nz, n_slow, n_fast, bsize, niter, grad_accumulation, seed, constraint_params=None,
+                   shift_lr=5e-4):
     scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
-    meas = simulate_meas(scan, probe, H, occu, gta, gtp, 5e-4)
+    meas = simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr)
     iv = init_variables(obja, objp, probe, H, occu, scan.crop_pos, scan.shifts, meas,
                         scan.n_slow, scan.n_fast)
-    model = build_model(iv, 5e-4)
+    model = build_model(iv, shift_lr)
     init_state = dict(obja=model.opt_obja.detach().numpy().copy(),
                       objp=model.opt_objp.detach().numpy().copy(),
                       probe=torch.view_as_complex(model.opt_probe.detach()).numpy().copy(),
@@ -331,6 +332,11 @@ if __name__ == "__main__":
         run_case("n32_p1o2z1_preblur", 32, 1, 2, 1, 4, 4, 5, seed=32)
         BLUR.update(detector_blur_std=0.7, obj_preblur_std=1.2)
         run_case("n64_p2o1z1_bothblur", 64, 2, 1, 1, 3, 3, 6, seed=33)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--c1-traj":
+        # BASELINE configs[0] shape: tBL_WSe2 params (demo/params/tBL_WSe2_reconstruct.yml:118-123:
+        # obja / objp lr 5e-4, probe 1e-4, probe_pos_shifts 1e-4), N = 128, 8×8 scan, batch 32
+        run_trajectory("traj_c1_n128", 128, 1, 1, 1, 8, 8, 32, 2, 1, seed=24, shift_lr=1e-4)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
         constrained_trajectory()

@@ -2,6 +2,7 @@
 import ctypes
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -27,13 +28,88 @@ def test_library_loads_and_exports_all_symbols():
     assert lib.ptyx_last_error() == b""
 
 
-def test_struct_layouts_match_header():
-    # sizes of the C structs (all 4-byte fields / 8-byte pointers, no padding surprises)
-    assert ctypes.sizeof(_lib.Dims) == 9 * 4
-    assert ctypes.sizeof(_lib.Inputs) == 10 * 8 + 8     # + float dz, padded to pointer alignment
-    assert ctypes.sizeof(_lib.Grads) == 7 * 8
-    assert ctypes.sizeof(_lib.LossCfg) == 12 * 4
-    assert ctypes.sizeof(_lib.ObjConstraints) == 19 * 4
+STRUCT_C = {"Dims": "ptyx_dims", "Inputs": "ptyx_inputs", "Grads": "ptyx_grads", "LossCfg": "ptyx_loss_cfg",
+            "KernelStat": "ptyx_kernel_stat", "ObjConstraints": "ptyx_obj_constraints", "MeasProc": "ptyx_meas_proc"}
+
+
+def c_layout(tmp_path, classes):
+    """{struct: (sizeof, {field: offsetof})} from the C compiler on include/ptyx.h."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ptyx.h"', "int main(void) {"]
+    for py, cs in classes.items():
+        lines.append(f'  printf("S {py} %zu\\n", sizeof({cs}));')
+        for f, _ in getattr(_lib, py)._fields_:
+            lines.append(f'  printf("F {py} {f} %zu\\n", offsetof({cs}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n"):
+        parts = ln.split()
+        if parts and parts[0] == "S":
+            out.setdefault(parts[1], [0, {}])[0] = int(parts[2])
+        elif parts and parts[0] == "F":
+            out.setdefault(parts[1], [0, {}])[1][parts[2]] = int(parts[3])
+    return out
+
+
+def py_layout(cls):
+    return ctypes.sizeof(cls), {f: getattr(cls, f).offset for f, _ in cls._fields_}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror in ptyrad_amd/_lib.py has the C header's size and field offsets, and
+    names every C field (gcc on include/ptyx.h), and the library agrees on the sizes."""
+    c = c_layout(tmp_path, STRUCT_C)
+    hdr = open(os.path.join(ROOT, "include", "ptyx.h")).read()
+    for py, cs in STRUCT_C.items():
+        size, offs = py_layout(getattr(_lib, py))
+        assert c[py][0] == size, (py, c[py][0], size)
+        assert c[py][1] == offs, py
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cs, cs), hdr, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        cnames = re.findall(r"\*?\s*(\w+)\s*(?:\[\d+\])?\s*[,;]", body)
+        assert sorted(cnames) == sorted(offs), (py, cnames)
+    lib = _lib.load()          # load() itself checks ptyx_abi_struct_sizes against the mirrors
+    sizes = (ctypes.c_size_t * 7)()
+    assert lib.ptyx_abi_struct_sizes(sizes, 7) == 7
+    assert list(sizes) == [c[py][0] for py in STRUCT_C]
+
+
+def integration_stub():
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    return re.search(r"## 1\. Minimal ctypes stub.*?```python\n(.*?)```", text, re.S).group(1)
+
+
+def test_integration_stub_matches_header_and_library(tmp_path, monkeypatch):
+    """The binding INTEGRATION.md shows PtyRAD maintainers, executed as written: its structs have
+    the header's layout field for field, check_abi() passes against libptyx.so, and a plan request
+    travels through its Dims (abi_version included) to the library's validation."""
+    monkeypatch.setenv("PTYX_LIB", _lib.LIB_PATH)
+    _lib.load()
+    ns = {}
+    exec(compile(integration_stub(), "INTEGRATION.md", "exec"), ns)
+    c = c_layout(tmp_path, {k: STRUCT_C[k] for k in ("Dims", "Inputs", "Grads", "LossCfg")})
+    for py in ("Dims", "Inputs", "Grads", "LossCfg"):
+        assert py_layout(ns[py]) == (c[py][0], c[py][1]), py
+    ns["check_abi"]()
+
+    class M:   # N = 100 is rejected by ptyx_plan_create before any HIP call
+        opt_obja = __import__("torch").zeros((1, 1, 200, 200))
+        opt_probe = __import__("torch").zeros((1, 100, 100, 2))
+        crop_pos = __import__("torch").zeros((4, 2), dtype=__import__("torch").int32)
+        shift_probes = True
+    with pytest.raises(RuntimeError, match="N must be"):
+        ns["make_plan"](M, 4)
+
+
+def test_plan_create_rejects_stale_abi_version():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    d = _lib.Dims(128, 1, 1, 1, 200, 200, 4, 4, 0, 101)
+    assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EINVAL
+    assert b"abi_version" in lib.ptyx_last_error()
 
 
 def test_plan_create_rejects_bad_dims_without_gpu():

@@ -1,0 +1,169 @@
+"""BASELINE configs c3 / c5 at their shapes through the HIP path vs the oracle, rank-local
+measurement storage, GPU checkpoint resume, and the c1-shape trajectory.
+
+c3: N = 256, P = 8 probe modes × O = 2 object modes, Nz = 1 (BASELINE configs[2]);
+c5: N = 256, P = 4, fp16 DP storage / fp32 accumulate (configs[4]).  A 3×3 scan in the
+config's geometry, two mini-batches per call, random DPs (SURVEY §8d allows them for c3-c5);
+the oracle runs on the same fp16-rounded DPs.  Tolerances as tests/test_gpu_parity.py.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptyx_oracle as orc
+from tests.test_gpu_parity import TOL_DP, TOL_G, TOL_SH, TOL_TERMS, orc_default_loss, run_fused
+from tests.test_oracle_golden import rel
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def config_problem(P, O, meas_f16, seed):
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(256, 3, 3, P=P, O=O, Nz=1, seed=seed)
+    meas = pr.meas.astype(np.float16).astype(np.float32) if meas_f16 else pr.meas
+    return dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts,
+                crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=meas, shift_probes=True,
+                loss_params=json.loads(json.dumps(orc_default_loss())))
+
+
+def check_against_oracle(d, batches, meas_f16):
+    terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=meas_f16)
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"])
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_c3_shape_p8_o2_vs_oracle():
+    d = config_problem(8, 2, False, seed=11)
+    check_against_oracle(d, [np.array([0, 4, 8]), np.array([5, 1])], meas_f16=False)
+
+
+def test_c5_shape_p4_fp16_dps_vs_oracle():
+    d = config_problem(4, 1, True, seed=12)
+    check_against_oracle(d, [np.array([2, 6, 7, 3]), np.array([8, 0])], meas_f16=True)
+
+
+# ------------------------------------------------------------------ rank-local measurements
+def test_rank_local_measurement_block_equals_full_stack():
+    """PtychoHIP holding only the DPs of the positions it uses (rows in a shuffled order, via
+    measurements_index) gives bit-identical loss terms and gradients to the full stack, on the
+    register engine (c1 shape, k_fused3) and on the general engine (mixed state)."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    from tests.test_gpu_model import init_vars, model_params
+    from tests.test_oracle_golden import CASES, load_case
+    for name in ("n128_c1_b32", "n32_p2o2z3"):
+        d = load_case([c for c in CASES if name in c][0])
+        b = d["batch"]
+        lrs = {"obja": 5e-4, "objp": 5e-4, "obj_tilts": 0.0, "slice_thickness": 0.0, "probe": 1e-4,
+               "probe_pos_shifts": 5e-4}
+        out = []
+        for shard in (False, True):
+            iv = init_vars(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"], d["occu"], d["meas"])
+            if shard:
+                mi = np.random.default_rng(0).permutation(np.unique(b))
+                iv["measurements"] = np.ascontiguousarray(d["meas"][mi])
+                iv["measurements_index"] = mi
+            model = PtychoHIP(iv, model_params(lrs), device=device, verbose=False)
+            loss = CombinedLoss(d["loss_params"], device=device)
+            terms = loss.fused_into(model, [b])
+            out.append((terms.cpu().numpy(), [p.grad.cpu().numpy() for p in
+                                              (model.opt_obja, model.opt_objp, model.opt_probe,
+                                               model.opt_probe_pos_shifts)]))
+            if shard:
+                assert model.measurements.shape[0] == np.unique(b).size
+                outside = np.setdiff1d(np.arange(d["shifts"].shape[0]), b)
+                if outside.size:
+                    with pytest.raises(IndexError):
+                        loss.fused_into(model, [outside[:1]])
+        np.testing.assert_array_equal(out[0][0], out[1][0])
+        for a, c in zip(out[0][1], out[1][1]):
+            assert rel(c, a) < 1e-6, name          # same arithmetic; atomics may reorder sums
+        np.testing.assert_allclose(out[0][0][0], d["loss_terms"], rtol=TOL_TERMS, atol=1e-7)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_each_holding_half_the_dps_match_reference_trajectory(tmp_path):
+    """Two gloo ranks (both on cuda:0), each PtychoHIP holding only its own mini-batches' DPs
+    (DistContext.local_indices), one all-reduce per optimizer step: bitwise-identical replicas
+    whose final object matches the reference's recon_step trajectory (RMS < 1e-5)."""
+    dev()
+    import torch.multiprocessing as mp
+    from tests.dist_helpers import gpu_dist_worker
+    path = os.path.join(GOLDEN, "traj_n32_p2_ga2.npz")
+    z = np.load(path, allow_pickle=False)
+    out = str(tmp_path / "r.npz")
+    mp.start_processes(gpu_dist_worker, args=(2, _free_port(), path, out), nprocs=2, start_method="spawn")
+    r0, r1 = np.load(out.replace(".npz", "_r0.npz")), np.load(out.replace(".npz", "_r1.npz"))
+    assert int(r0["held"]) + int(r1["held"]) == z["batches"].size      # each rank: only its DPs
+    assert int(r0["held"]) < z["batches"].size and int(r1["held"]) < z["batches"].size
+    for k in ("obja", "objp", "probe"):
+        assert np.array_equal(r0[k], r1[k]), k
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((r0[k].astype(np.float64) - ref) ** 2))) < 1e-5, k
+
+
+# ------------------------------------------------------------------ checkpoint resume on the GPU
+def test_ptychohip_checkpoint_resume_matches_reference_trajectory(tmp_path):
+    """save after iteration 1 (save.py:85-140 layout, Adam state included), resume into a fresh
+    PtychoHIP + Adam (reconstruction.py:356-366), run iterations 2-3: the reference trajectory's
+    final object is reproduced (RMS < 1e-5) and equals the uninterrupted run."""
+    dev()
+    from ptyrad_amd.checkpoint import load_ptyrad, make_save_dict, resume, save_ptyrad
+    from ptyrad_amd.reconstruction import recon_step
+    from tests.dist_helpers import gpu_recon
+    z = np.load(os.path.join(GOLDEN, "traj_n64_b4_ga1.npz"), allow_pickle=False)
+    full = gpu_recon(z)
+    model, opt, loss_fn, batches, bl = gpu_recon(z, niter=1, ret_all=True)
+    params = {"recon_params": {"save_result": ["model", "optim_state"]}}
+    p = save_ptyrad(str(tmp_path / "model_iter0001.pt"),
+                    make_save_dict(str(tmp_path), model, params, opt, 1, None, bl))
+    model2, opt2, _, _, _ = gpu_recon(z, niter=0, ret_all=True)
+    assert resume(model2, opt2, load_ptyrad(p)) == 1
+    for it in (2, 3):
+        recon_step(batches, int(z["grad_accumulation"]), model2, opt2, loss_fn, None, it, verbose=False)
+    for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
+        got = getattr(model2, k).detach().cpu().numpy().astype(np.float64)
+        assert float(np.sqrt(np.mean((got - ref) ** 2))) < 1e-5, k
+        assert rel(got, getattr(full, k).detach().cpu().numpy()) < 1e-6, k
+    assert len(model2.loss_iters) == 3
+
+
+# ------------------------------------------------------------------ c1 shape trajectory
+def test_c1_shape_trajectory_matches_reference():
+    """c1 (tBL_WSe2 params: N = 128, 8×8 scan, probe / position lr 1e-4, 2 iterations of Adam)
+    through PtychoHIP + recon_step: final object RMS < 1e-5 vs the reference run."""
+    path = os.path.join(GOLDEN, "traj_c1_n128.npz")
+    if not os.path.exists(path):
+        pytest.skip("traj_c1_n128.npz not generated")
+    from tests.dist_helpers import gpu_recon
+    z = np.load(path, allow_pickle=False)
+    model = gpu_recon(z)
+    for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
+        got = getattr(model, k).detach().cpu().numpy().astype(np.float64)
+        assert float(np.sqrt(np.mean((got - ref) ** 2))) < 1e-5, k
+    prb = torch.view_as_complex(model.opt_probe.detach()).cpu().numpy()
+    assert rel(prb, z["final_probe"]) < 1e-5

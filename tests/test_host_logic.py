@@ -64,3 +64,33 @@ def test_toggle_grad_requires_follows_start_iter():
     assert [m.optimizable_tensors[k].requires_grad for k in ("obja", "probe", "obj_tilts")] == [True, False, False]
     toggle_grad_requires(m, 3)
     assert m.optimizable_tensors["probe"].requires_grad
+
+
+def test_make_batches_sparse_matches_reference_greedy_rule():
+    """'sparse' grouping (reconstruction.py:548-587): seeds nearest the compact centroids, then
+    each remaining index joins the group whose nearest member is farthest.  Checked against a
+    direct restatement with the reference's full pairwise-distance matrix on the same clusters."""
+    from scipy.spatial.distance import cdist
+    from ptyrad_amd.reconstruction import sparse_groups
+    rng = np.random.default_rng(3)
+    yy, xx = np.meshgrid(np.arange(9), np.arange(9), indexing="ij")
+    pos = np.stack([yy.ravel(), xx.ravel()], 1) * 2.87 + rng.normal(0, 0.15, (81, 2))
+    idx = np.arange(81)
+    compact = make_batches(idx, pos, 10, mode="compact", random_state=0)
+    got = sparse_groups(idx, pos, compact)
+    # reference rule, literally
+    pw = cdist(pos, pos)
+    pos_s = pos[idx]
+    groups, used = [], []
+    for cb in compact:
+        c = np.mean(pos[cb], axis=0)
+        j = int(np.argmin(np.linalg.norm(pos_s - c, axis=1)))
+        groups.append([idx[j]])
+        used.append(j)
+    for i in np.delete(idx.copy(), used):
+        g = int(np.argmax([np.min(pw[grp, i]) for grp in groups]))
+        groups[g].append(i)
+    assert [list(g) for g in got] == [list(map(int, g)) for g in groups]
+    assert np.array_equal(np.sort(np.concatenate(got)), idx)
+    bs = make_batches(idx, pos, 10, mode="sparse", random_state=0)
+    assert np.array_equal(np.sort(np.concatenate(bs)), idx)
