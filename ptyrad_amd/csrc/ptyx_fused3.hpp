@@ -127,12 +127,12 @@ __global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid
 // object point), and — for loss_sparse — per-row fp64 prefix sums of |φ|^n:
 // pref[y][x] = Σ_{x' < x} |φ(y, x')|^n, x = 0..Nx.  One workgroup per object row.
 __global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx, float2* oc, double* pref,
-                           int sparse_n, const int* bbox = nullptr, int rows_per_slice = 0) {
+                           int sparse_n, const int* bbox = nullptr, int rows_per_slice = 0, int win = kN) {
   __shared__ double s_part[256];
   const int y = blockIdx.x;
   if (bbox) {   // rows no window of this call touches are never read (k_fused3*, k_pattern_table3)
     const int r = y % rows_per_slice;
-    if (r < bbox[0] || r >= bbox[1] + kN) return;
+    if (r < bbox[0] || r >= bbox[1] + win) return;
   }
   const float* ar = obja + (size_t)y * Nx;
   const float* pr = objp + (size_t)y * Nx;
@@ -183,13 +183,13 @@ __global__ void k_bbox_init(int* bbox) {
     bbox[3] = -0x7fffffff;
   }
 }
-__global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int Ny, int Nx, int* bbox) {
+__global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int Ny, int Nx, int* bbox, int win = kN) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   int a = 0x7fffffff, b = -0x7fffffff, c = 0x7fffffff, d = -0x7fffffff;
   if (j < n) {
     const int s = min(max(idx[j], 0), n_scans - 1);
-    a = b = min(max(crop[2 * s], 0), Ny - kN);
-    c = d = min(max(crop[2 * s + 1], 0), Nx - kN);
+    a = b = min(max(crop[2 * s], 0), Ny - win);
+    c = d = min(max(crop[2 * s + 1], 0), Nx - win);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {

@@ -32,6 +32,7 @@
 
 #include "ptyx_common.hpp"
 #include "ptyx_fused3.hpp"
+#include "ptyx_stripe.hpp"
 #include "ptyx_abi.hpp"
 
 namespace ptyx {
@@ -664,6 +665,15 @@ struct ptyx_plan {
   float2* hpk = nullptr;      // k_fused3ms: K-packed propagator
   int* bbox = nullptr;        // k_fused3*: bounding box of a call's windows
   bool ms3 = false;           // k_fused3ms (multislice register engine) available
+  // N = 256 stripe engine (ptyx_stripe.hpp): per-call intermediates for stripe_cap patterns
+  long long stripe_cap = 0;
+  int stripe_groups = 0;
+  float2* st14 = nullptr;
+  float2* spsi0 = nullptr;
+  float2* st23 = nullptr;
+  float* spsum = nullptr;
+  float* sdsp = nullptr;
+  float2* sslab = nullptr;
   long long seg_cap = 0;      // segment ids the segslab holds
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
@@ -681,12 +691,14 @@ struct ptyx_plan {
 
 enum KernelKind {
   kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather,
-  kKObjPrep, kKPack, kKCount
+  kKObjPrep, kKPack, kKS1, kKS2, kKS3, kKS4, kKS5, kKCount
 };
 static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize",
                                                   "k_adjoint",        "k_slab_reduce",    "k_probe_finalize",
                                                   "k_fused",          "k_pattern_table",  "k_obj_gather",
-                                                  "k_obj_prep",       "k_pack"};
+                                                  "k_obj_prep",       "k_pack",           "k_s1",
+                                                  "k_s2",             "k_s3",             "k_s4",
+                                                  "k_s5"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -766,6 +778,7 @@ extern "C" size_t ptyx_plan_workspace_bytes(const ptyx_plan* plan) { return plan
 
 extern "C" int64_t ptyx_plan_register_capacity(const ptyx_plan* plan) {
   if (plan && plan->nwg3 > 0) return (int64_t)plan->og_cap;
+  if (plan && plan->stripe_cap > 0) return (int64_t)plan->stripe_cap;
   return (plan && plan->ffc_cap > 0) ? (int64_t)plan->ffc_cap : 0;   // far-field cache capacity
 }
 
@@ -814,7 +827,35 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     free_plan(pl);
     return rc;
   }
-  if (d.Nz == 1 && d.P * d.O > 1 && pl->fast && !std::getenv("PTYX_NO_FFC")) {
+  const bool stripe = d.N == 256 && d.Nz == 1 && d.O <= sp::kMaxO && (d.flags & PTYX_SHIFT_PROBES) && pl->fast &&
+                      !std::getenv("PTYX_NO_STRIPE");
+  if (stripe) {
+    // per-call intermediates (T1/T4, ψ⁰: P fields; T2/T3: P·O fields per pattern) within
+    // PTYX_STRIPE_MB (default the smaller of 16 GiB and a quarter of the free HBM); calls beyond
+    // the capacity are split by the host at mini-batch boundaries
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    long long mb = std::min<long long>(16384, (long long)(free_b / 4 / (1 << 20)));
+    if (const char* e = std::getenv("PTYX_STRIPE_MB")) mb = std::atoll(e);
+    const long long per = (long long)(2 * d.P + d.P * d.O) * (long long)N2 * (long long)sizeof(float2);
+    const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / per);
+    if (cap >= 1) {
+      const int groups = std::max(1, std::min<int>((int)cap, (2048 + 16 * d.P - 1) / (16 * d.P)));
+      if ((rc = dalloc(pl, &pl->st14, (size_t)cap * d.P * N2)) || (rc = dalloc(pl, &pl->spsi0, (size_t)cap * d.P * N2)) ||
+          (rc = dalloc(pl, &pl->st23, (size_t)cap * d.P * d.O * N2)) ||
+          (rc = dalloc(pl, &pl->spsum, (size_t)cap * sp::kStripes * kNSum)) ||
+          (rc = dalloc(pl, &pl->sdsp, (size_t)cap * sp::kStripes * d.P * 2)) ||
+          (rc = dalloc(pl, &pl->sslab, (size_t)groups * d.P * N2)) ||
+          (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->oc, (size_t)d.O * d.Ny * d.Nx)) || (rc = dalloc(pl, &pl->bbox, 4))) {
+        free_plan(pl);
+        return rc;
+      }
+      pl->stripe_cap = cap;
+      pl->stripe_groups = groups;
+    }
+  }
+  if (!stripe && d.Nz == 1 && d.P * d.O > 1 && pl->fast && !std::getenv("PTYX_NO_FFC")) {
     // far-field cache: (P·O + P)·N² float2 per pattern of a call, within PTYX_FFC_MB (default the
     // smaller of 64 GiB and a third of the free HBM); calls beyond its capacity are split by the host
     size_t free_b = 0, total_b = 0;
@@ -1177,6 +1218,122 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   return PTYX_OK;
 }
 
+// ---------------------------------------------------------------- stripe engine (N = 256)
+// Launch sequence of one ptyx_forward_loss_grad call on the stripe engine (ptyx_stripe.hpp).
+static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                      const ptyx_grads& gz, hipStream_t st, float* loss_terms) {
+  using namespace sp;
+  const ptyx_dims& d = pl->d;
+  const int n = a.n_idx, P = d.P, O = d.O;
+  const bool single = cfg->single_on != 0;
+  const bool tail = gz.d_probe != nullptr || gz.d_shifts != nullptr;
+  const bool any_grad = gz.d_obja || gz.d_objp || tail;
+  launch_spectrum<256>(pl, a, st);                       // F(P_p), natural order
+  {
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
+                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo);
+    hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
+    hipLaunchKernelGGL(f3::k_bbox, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
+                       pl->bbox, kN);
+  }
+  {
+    ProfScope ps(pl, kKObjPrep, st);   // O = A e^{iφ} on the rows the call's windows touch
+    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.O * d.Ny), dim3(256), 0, st, a.obja, a.objp, d.O * d.Ny, d.Nx, pl->oc,
+                       nullptr, 1, pl->bbox, d.Ny, kN);
+  }
+  SArgs s{};
+  s.n = n; s.P = P; s.O = O; s.Ny = d.Ny; s.Nx = d.Nx; s.n_scans = d.n_scans; s.meas_f16 = a.meas_f16;
+  s.idx = a.idx; s.bid = pl->bid; s.geo = pl->geo; s.shifts = a.shifts; s.mrow = a.mrow;
+  s.Fp = pl->Fp; s.oc = pl->oc; s.obja = a.obja; s.objp = a.objp; s.meas = a.meas; s.occu = a.occu;
+  s.q = single ? cfg->single_q : cfg->poissn_q;
+  s.eps2 = cfg->poissn_eps;
+  s.sparse_on = cfg->sparse_on; s.sparse_n = cfg->sparse_n;
+  s.t14 = pl->st14; s.psi0 = pl->spsi0; s.t23 = pl->st23; s.psum_s = pl->spsum; s.dp_out = a.dp_out;
+  s.coef = pl->coef; s.ci = single ? 0 : 1;
+  s.d_obja = gz.d_obja; s.d_objp = gz.d_objp;
+  s.groups = std::max(1, std::min(pl->stripe_groups, n));
+  s.slabpart = pl->sslab; s.dsp = pl->sdsp;
+  s.twg = pl->twg;
+  const dim3 bl(256);
+  {
+    ProfScope ps(pl, kKS1, st);
+    hipLaunchKernelGGL(k_s1, dim3(n, kStripes, P), bl, 0, st, s);
+  }
+  {
+    ProfScope ps(pl, kKS2, st);
+    if (O == 1) hipLaunchKernelGGL(k_s2<1>, dim3(n, kStripes), bl, 0, st, s);
+    else hipLaunchKernelGGL(k_s2<2>, dim3(n, kStripes), bl, 0, st, s);
+  }
+  {
+    ProfScope ps(pl, kKS3, st);
+    const dim3 gr(n, kStripes);
+    const int PO = P * O;
+    const bool half = single && s.q == 0.5f;
+#define PTYX_S3(SG, QM)                                                                                  \
+  switch (PO) {                                                                                        \
+    case 1: hipLaunchKernelGGL((k_s3<SG, QM, 1>), gr, bl, 0, st, s); break;                             \
+    case 2: hipLaunchKernelGGL((k_s3<SG, QM, 2>), gr, bl, 0, st, s); break;                             \
+    case 3: hipLaunchKernelGGL((k_s3<SG, QM, 3>), gr, bl, 0, st, s); break;                             \
+    case 4: hipLaunchKernelGGL((k_s3<SG, QM, 4>), gr, bl, 0, st, s); break;                             \
+    default: hipLaunchKernelGGL((k_s3<SG, QM, 0>), gr, bl, 0, st, s); break;                            \
+  }
+    if (half) { PTYX_S3(true, 0) }
+    else if (single) { PTYX_S3(true, 2) }
+    else { PTYX_S3(false, 2) }
+#undef PTYX_S3
+  }
+  int rc = launch_status("stripe forward launch");
+  if (rc) return rc;
+  {
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(k_s_psum, dim3((n * kNSum + 255) / 256), dim3(256), 0, st, pl->spsum, n, pl->psums);
+  }
+  FinArgs fa{};
+  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = kN; fa.Nz = 1; fa.O = O;
+  fa.psums = pl->psums; fa.occu = in->omode_occu;
+  fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
+  fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
+  fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  {
+    ProfScope ps(pl, kKFinalize, st);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
+  }
+  if ((rc = launch_status("k_finalize launch"))) return rc;
+  if (!any_grad) return PTYX_OK;
+  {
+    ProfScope ps(pl, kKS4, st);
+    SArgs s4 = s;
+    if (!tail) s4.t14 = nullptr;   // no probe / position gradient: skip the gP transform
+    if (O == 1) hipLaunchKernelGGL(k_s4<1>, dim3(n, kStripes), bl, 0, st, s4);
+    else hipLaunchKernelGGL(k_s4<2>, dim3(n, kStripes), bl, 0, st, s4);
+  }
+  if ((rc = launch_status("k_s4 launch"))) return rc;
+  if (!tail) return PTYX_OK;
+  {
+    ProfScope ps(pl, kKS5, st);
+    hipLaunchKernelGGL(k_s5, dim3(kStripes, P, s.groups), bl, 0, st, s);
+  }
+  if ((rc = launch_status("k_s5 launch"))) return rc;
+  if (gz.d_shifts) {
+    ProfScope ps(pl, kKSlabReduce, st);
+    hipLaunchKernelGGL(k_s_shift, dim3((n + 255) / 256), dim3(256), 0, st, pl->sdsp, n, kStripes * P, a.idx,
+                       a.n_scans, gz.d_shifts);
+  }
+  if (gz.d_probe) {
+    const long long per = (long long)P * kN2;
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, st, pl->sslab, s.groups,
+                         per, pl->Gsum);
+    }
+    ProfScope ps(pl, kKProbeFinalize, st);
+    hipLaunchKernelGGL(k_probe_finalize<256>, dim3(P), dim3(Geo<256>::NT), 0, st, a, pl->Gsum,
+                       reinterpret_cast<float2*>(gz.d_probe));
+  }
+  return launch_status("stripe adjoint launch");
+}
+
 extern "C" int ptyx_profile_begin(ptyx_plan* pl) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
@@ -1317,6 +1474,14 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
     return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
 #else
     if (PTYX_ONLY_N == 128) return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
+#endif
+  }
+  // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): one data term, call within capacity
+  const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift &&
+                      (cfg->single_on != 0) != (cfg->poissn_on != 0) && !std::getenv("PTYX_TWO_PASS");
+  if (stripe) {
+#if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 256
+    return run_stripe(pl, in, a, cfg, gz, st, loss_terms);
 #endif
   }
 

@@ -1,0 +1,504 @@
+// ptyx_stripe.hpp — the N = 256 engine (BASELINE c3: P = 8 probe × O = 2 object modes; c5: P = 4,
+// fp16 DPs): forward, loss and adjoint of multislice_forward_model_vec_all (forward.py:20-80,
+// Nz = 1) + CombinedLoss (losses.py:36-104) + the autograd adjoint as five
+// mode-batched STRIPE passes.  Included by ptyx_kernels.hip.
+//
+// Why not a register-resident 2-D FFT as at N = 128 (ptyx_regfft.hpp): one 256² complex field is
+// 512 KiB, exactly the whole vector register file of a CU (4 SIMDs × 512 VGPRs × 64 lanes × 4 B),
+// and LDS is 160 KiB, so no CU can hold a field plus working registers.  Every 2-D transform must
+// cross HBM (or the 256 MiB Infinity Cache) once.  The engine therefore spends exactly ONE round
+// trip per 2-D FFT, by alternating the transform axis between passes (the second half of one 2-D
+// FFT and the first half of the next run on the same in-register lines), and batches the probe /
+// object modes inside each pass so that the mode sums (Σ occ|Ψ|², Σ_p g·conj(ψ⁰), Σ_o g·conj(O))
+// never leave the chip:
+//
+//   P1  columns  v = F(P_p)·wy  → column IFFT                                     → T1[p]
+//   P2  rows     ×wx → row IFFT → ψ⁰_p/N² (kept: PSI0[p]); per o: ψ⁰_p·O_o → row FFT → T23[p,o]
+//                (loss_sparse window sums of |φ|ⁿ from the same object rows)
+//   P3  columns  per (p,o): column FFT → Ψ = ·/N;  I = Σ occ|Ψ|² + 1e-10 (registers);  DP read,
+//                loss partial sums, u = ∂ℓ/∂I per UNIT mini-batch coefficient;  per (p,o):
+//                g_Ψ = 2 occ Ψ u → column IFFT                                     → T23[p,o]
+//                (Ψ of every mode is held in registers when P·O ≤ 4, else its column FFT is redone)
+//   --- k_finalize: the mini-batch NRMSE coefficients c_m (losses.py:45-47) ---
+//   P4  rows     per p: per o: row IFFT → g/N;  slot_o += g·conj(ψ⁰_p);  gP += g·conj(O_o);
+//                row FFT(gP) → T4[p] (= T1's storage);  then dA, dφ (+ the sparse sign term)
+//                scaled by c_m, f32 atomics into the object gradient
+//   P5  columns  per pattern: column FFT(T4[p]) → G;  slab += c_m conj(W_b) G (registers, the
+//                block's stripe of the probe-gradient spectrum across its patterns);  position
+//                gradient Σ 2π g·Im(F(P) W conj(G)) per pattern (Parseval, no extra FFT)
+//
+// A stripe is 16 lines (rows or columns) × 256 points, one 256-thread workgroup: 16 threads per
+// line, 16 points per thread.  A 256-point line transform is DFT16 in registers (n = n1 + 16 n2),
+// the W256^(n1·k2) twiddles, one 16×16 exchange through LDS, DFT16 again: natural order in and
+// out, thread slot t holding points t + 16 r.  Row passes read / write whole 2 KiB rows; column
+// passes read / write 128 B row segments (one cache line).  All intermediates are in natural
+// (N, N) layout, chunked per call (the host splits calls at mini-batch boundaries:
+// ptyx_plan_register_capacity).
+#pragma once
+#include "ptyx_common.hpp"
+#include "ptyx_fused3.hpp"
+#include "ptyx_regfft.hpp"
+
+namespace ptyx {
+namespace sp {
+
+constexpr int kN = 256, kN2 = kN * kN;
+constexpr int kL = 16;                 // lines per stripe
+constexpr int kStripes = kN / kL;      // 16
+constexpr int kXElems = kL * 272;      // LDS exchange buffer (float2), row stride padded 256 → 272
+constexpr int kMaxO = 2;
+
+struct SArgs {
+  int n, P, O, Ny, Nx, n_scans, meas_f16;
+  const int* idx;        // scan index per pattern
+  const int* bid;        // mini-batch per pattern
+  const int2* geo;       // clamped window origin per pattern
+  const float* shifts;   // (n_scans, 2)
+  const int* mrow;       // measurement row of a scan index (NULL: the index itself)
+  const float2* Fp;      // (P, N, N) F(probe), natural order
+  const float2* oc;      // (O, Ny, Nx) A e^{iφ}
+  const float* obja;
+  const float* objp;
+  const void* meas;
+  const float* occu;
+  float q, eps2;
+  int sparse_on, sparse_n;
+  float2* t14;           // (n, P, N²)   T1, later T4
+  float2* psi0;          // (n, P, N²)
+  float2* t23;           // (n, P·O, N²) T2, later T3
+  float* psum_s;         // (n, kStripes, kNSum) per-stripe loss partial sums
+  float* dp_out;         // (n, N, N) or NULL
+  const float* coef;     // (batches, kNCoef) from k_finalize
+  int ci;                // data-term coefficient index (0 single, 1 poissn)
+  float* d_obja;
+  float* d_objp;
+  float2* slabpart;      // (groups, P, N²) probe-gradient spectrum partials
+  int groups;
+  float* dsp;            // (n, kStripes·P, 2) position-gradient partials
+  const float2* twg;     // W256^m, m = 0..255 (fp64-rounded)
+};
+
+struct Map {
+  int line, slot;
+};
+// COL: thread t owns column line = t & 15 of the stripe and points y = slot + 16 r (slot = t >> 4):
+// one register's load is 16 consecutive columns × 4 rows per wave (128 B segments).
+// ROW: line = t >> 4 (the wave holds 4 rows), points x = slot + 16 r: 128 B per 16 lanes.
+template <bool COL>
+__device__ __forceinline__ Map map_of(int t) {
+  return COL ? Map{t & 15, t >> 4} : Map{t >> 4, t & 15};
+}
+// exchange slot of (line, n1, k2); both forms are bank-conflict free for the ds_write_b64 /
+// ds_read_b64 lane groups of their mapping (row stride 272: the two lines of a 32-lane read group
+// fall in different bank halves; the XOR spreads a 16-lane write group over 16 banks pairs)
+template <bool COL>
+__device__ __forceinline__ int xidx(int line, int n1, int k2) {
+  return COL ? ((n1 << 4) + k2) * 16 + line : line * 272 + (n1 << 4) + (k2 ^ n1);
+}
+
+__device__ __forceinline__ int opq(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// 256-point DFT of every line of the stripe (DIR -1 forward, +1 unnormalised inverse).
+template <int DIR, bool COL>
+__device__ __forceinline__ void fft_line(float2 (&v)[16], Map m, float2* xb, const float2* tw) {
+  rf::dft<16, DIR>(v);   // over n2: v[k2]
+#pragma unroll
+  for (int k2 = 1; k2 < 16; ++k2) {
+    float2 w = tw[(m.slot * k2) & 255];
+    if (DIR > 0) w.y = -w.y;
+    v[k2] = cmul(v[k2], w);
+  }
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) xb[xidx<COL>(m.line, m.slot, k2)] = v[k2];
+  __syncthreads();
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) v[n1] = xb[xidx<COL>(m.line, n1, m.slot)];
+  __syncthreads();
+  rf::dft<16, DIR>(v);   // over n1: v[k1] = X[slot + 16 k1]
+}
+
+__device__ __forceinline__ float shift_g(int k) { return (float)((k + kN / 2) & (kN - 1)) * (1.0f / kN); }
+
+__device__ __forceinline__ void load_tw(float2* tw, const float2* twg) {
+  for (int i = threadIdx.x; i < kN; i += blockDim.x) tw[i] = twg[i];
+}
+
+__device__ __forceinline__ int scan_of(const SArgs& a, int j) { return min(max(a.idx[j], 0), a.n_scans - 1); }
+
+// workgroup (4 waves) sum of NV floats, fixed order, result valid in every thread
+template <int NV>
+__device__ __forceinline__ void bsum(float (&v)[NV], float* red) {
+  f3::block_sum4<NV>(v, red);
+}
+
+// ---------------------------------------------------------------------------------- P1
+// grid (n, kStripes, P): columns kx of F(P_p)·wy → column IFFT → T1[j][p]
+__global__ __launch_bounds__(256, 2) void k_s1(SArgs a) {
+  __shared__ float2 xb[kXElems];
+  __shared__ float2 tw[kN];
+  load_tw(tw, a.twg);
+  __syncthreads();
+  const int j = blockIdx.x, s = blockIdx.y, p = blockIdx.z;
+  const Map m = map_of<true>(opq(threadIdx.x));
+  const int kx = s * kL + m.line;
+  const float sy = a.shifts[2 * scan_of(a, j)];
+  const float2* F = a.Fp + (size_t)p * kN2 + kx;
+  float2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ky = m.slot + 16 * r;
+    v[r] = cmul(F[ky * kN], f3::cis_rev(-sy * shift_g(ky)));
+  }
+  fft_line<+1, true>(v, m, xb, tw);
+  float2* out = a.t14 + ((size_t)j * a.P + p) * kN2 + kx;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[(m.slot + 16 * k) * kN] = v[k];
+}
+
+// ---------------------------------------------------------------------------------- P2
+// grid (n, kStripes): rows y of every probe mode: ×wx → row IFFT → ψ⁰ (PSI0); ×O_o → row FFT → T2
+template <int O_>
+__global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
+  __shared__ float2 xb[kXElems];
+  __shared__ float2 tw[kN];
+  __shared__ float red[4 * kMaxO];
+  load_tw(tw, a.twg);
+  __syncthreads();
+  const int j = blockIdx.x, s = blockIdx.y;
+  const Map m = map_of<false>(opq(threadIdx.x));
+  const int y = s * kL + m.line;
+  const int sidx = scan_of(a, j);
+  const float sx = a.shifts[2 * sidx + 1];
+  const int2 g0 = a.geo[j];
+  const int P = a.P;
+  constexpr float inv_n2 = 1.0f / kN2;
+  float2 wx[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) wx[r] = f3::cis_rev(-sx * shift_g(m.slot + 16 * r));
+  for (int p = 0; p < P; ++p) {
+    const float2* in = a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = cmul(in[16 * r], wx[r]);
+    fft_line<+1, false>(v, m, xb, tw);
+    float2* ps = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k] = cscale(v[k], inv_n2);
+      ps[16 * k] = v[k];
+    }
+    rf::sfor<0, O_>([&](auto OO) {
+      constexpr int o = decltype(OO)::value;
+      const float2* orow = a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+      float2 u[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) u[k] = cmul(v[k], orow[16 * k]);
+      fft_line<-1, false>(u, m, xb, tw);
+      float2* out = a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[16 * r] = u[r];
+    });
+  }
+  // loss_sparse (losses.py:101): Σ |φ|ⁿ over this stripe of the window, per object mode
+  float sp[O_];
+#pragma unroll
+  for (int o = 0; o < O_; ++o) {
+    sp[o] = 0.f;
+    if (a.sparse_on) {
+      const float* prow = a.objp + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float ap = fabsf(prow[16 * k]);
+        sp[o] += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
+      }
+    }
+  }
+  bsum<O_>(sp, red);
+  if (threadIdx.x == 0) {
+    float* ps = a.psum_s + ((size_t)j * kStripes + s) * kNSum + kSumBase;
+#pragma unroll
+    for (int o = 0; o < O_; ++o) ps[o] = sp[o];
+  }
+}
+
+// ---------------------------------------------------------------------------------- P3
+// grid (n, kStripes): columns kx of every mode: column FFT → Ψ, intensity, loss, g_Ψ → column IFFT.
+// HOLD > 0 (= P·O): every mode's Ψ stays in registers between the two sweeps; 0: recomputed.
+template <bool SINGLE, int QM, int HOLD>
+__global__ __launch_bounds__(256, 2) void k_s3(SArgs a) {
+  __shared__ float2 xb[kXElems];
+  __shared__ float2 tw[kN];
+  __shared__ float red[8];
+  load_tw(tw, a.twg);
+  __syncthreads();
+  const int j = blockIdx.x, s = blockIdx.y;
+  const Map m = map_of<true>(opq(threadIdx.x));
+  const int kx = s * kL + m.line;
+  const int PO = HOLD > 0 ? HOLD : a.P * a.O;
+  const int O = a.O;
+  constexpr float inv_n = 1.0f / kN;
+  float2* base = a.t23 + (size_t)j * PO * kN2 + kx;
+  auto far_field = [&](int q, float2 (&v)[16]) {
+    const float2* in = base + (size_t)q * kN2 + m.slot * kN;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = in[16 * r * kN];
+    fft_line<-1, true>(v, m, xb, tw);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n);
+  };
+  float I[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) I[k] = 0.f;
+  float2 hold[HOLD > 0 ? HOLD : 1][16];
+  if constexpr (HOLD > 0) {
+    rf::sfor<0, HOLD>([&](auto QQ) {
+      constexpr int q = decltype(QQ)::value;
+      far_field(q, hold[q]);
+      const float occ = a.occu[q % O];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(hold[q][k]), I[k]);
+    });
+  } else {
+    for (int q = 0; q < PO; ++q) {
+      float2 v[16];
+      far_field(q, v);
+      const float occ = a.occu[q % O];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(v[k]), I[k]);
+    }
+  }
+  // loss at every point of the stripe (fftshifted DP index), unit-coefficient ∂ℓ/∂I
+  const int sidx = scan_of(a, j);
+  const size_t mi = (size_t)(a.mrow ? a.mrow[sidx] : sidx);
+  const int col = (kx + kN / 2) & (kN - 1);
+  float S = 0.f, Ms = 0.f, u[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int ky = m.slot + 16 * k;
+    const int e = ((ky + kN / 2) & (kN - 1)) * kN + col;
+    const float Iv = I[k] + kDpEps;
+    const float M = a.meas_f16 ? __half2float(reinterpret_cast<const __half*>(a.meas)[mi * kN2 + e])
+                               : reinterpret_cast<const float*>(a.meas)[mi * kN2 + e];
+    if (a.dp_out) a.dp_out[(size_t)j * kN2 + e] = Iv;
+    u[k] = f3::loss_point<QM, SINGLE>(Iv, M, a.q, a.eps2, S, Ms);
+  }
+  {
+    float v2[2] = {S, Ms};
+    bsum<2>(v2, red);
+    if (threadIdx.x == 0) {
+      float* ps = a.psum_s + ((size_t)j * kStripes + s) * kNSum;
+      const int b0 = SINGLE ? 0 : 2;
+      ps[b0] = v2[0];
+      ps[b0 + 1] = v2[1];
+      ps[2 - b0] = 0.f;
+      ps[3 - b0] = 0.f;
+    }
+  }
+  // g_Ψ = 2 occ Ψ u → column IFFT, in place over T2
+  auto back = [&](int q, float2 (&v)[16]) {
+    const float c = 2.0f * a.occu[q % O];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], c * u[k]);
+    fft_line<+1, true>(v, m, xb, tw);
+    float2* out = base + (size_t)q * kN2 + m.slot * kN;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) out[16 * k * kN] = v[k];
+  };
+  if constexpr (HOLD > 0) {
+    rf::sfor<0, HOLD>([&](auto QQ) {
+      constexpr int q = decltype(QQ)::value;
+      back(q, hold[q]);
+    });
+  } else {
+    for (int q = 0; q < PO; ++q) {
+      float2 v[16];
+      far_field(q, v);
+      back(q, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- P4
+// grid (n, kStripes): rows y: per p: per o: row IFFT → g;  slot_o += g conj(ψ⁰_p);
+// gP += g conj(O_o);  row FFT(gP) → T4.  Then the object gradient (× c_m) by f32 atomics.
+template <int O_>
+__global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
+  __shared__ float2 xb[kXElems];
+  __shared__ float2 tw[kN];
+  load_tw(tw, a.twg);
+  __syncthreads();
+  const int j = blockIdx.x, s = blockIdx.y;
+  const Map m = map_of<false>(opq(threadIdx.x));
+  const int y = s * kL + m.line;
+  const int2 g0 = a.geo[j];
+  const int P = a.P;
+  const int mb = a.bid[j];
+  constexpr float inv_n = 1.0f / kN;
+  const bool want_t4 = a.t14 != nullptr;
+  float2 so[O_][16];
+#pragma unroll
+  for (int o = 0; o < O_; ++o)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) so[o][k] = make_float2(0.f, 0.f);
+  for (int p = 0; p < P; ++p) {
+    float2 psi[16], gp[16];
+    const float2* pin = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      psi[k] = pin[16 * k];
+      gp[k] = make_float2(0.f, 0.f);
+    }
+    rf::sfor<0, O_>([&](auto OO) {
+      constexpr int o = decltype(OO)::value;
+      const float2* in = a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot;
+      float2 v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = in[16 * r];
+      fft_line<+1, false>(v, m, xb, tw);
+      const float2* orow = a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float2 g = cscale(v[k], inv_n);
+        so[o][k] = cadd(so[o][k], cmulc(g, psi[k]));
+        gp[k] = cadd(gp[k], cmulc(g, orow[16 * k]));
+      }
+    });
+    if (want_t4) {
+      fft_line<-1, false>(gp, m, xb, tw);
+      float2* out = a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[16 * r] = gp[r];
+    }
+  }
+  if (!a.d_obja && !a.d_objp) return;
+  const float c = a.coef[(size_t)mb * kNCoef + a.ci];
+#pragma unroll
+  for (int o = 0; o < O_; ++o) {
+    const float csp = a.sparse_on ? a.coef[(size_t)mb * kNCoef + 2 + o] : 0.f;
+    const size_t row = ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const size_t off = row + 16 * k;
+      const float A = a.obja[off], ph = a.objp[off];
+      float sn, cs;
+      phase_sincos(ph, &sn, &cs);
+      const float2 gO = cscale(so[o][k], c);
+      if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));   // Re(g_O e^{-iφ})
+      if (a.d_objp) {
+        float dph = A * fmaf(gO.y, cs, -gO.x * sn);                          // Im(conj(O) g_O)
+        if (csp != 0.f) {
+          const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
+          dph += a.sparse_n == 1 ? csp * sg : csp * powq(fabsf(ph), (float)(a.sparse_n - 1)) * sg;
+        }
+        atomicAdd(a.d_objp + off, dph);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- P5
+// grid (kStripes, P, groups): block (s, p, g) sweeps patterns g, g + groups, ...: column FFT of
+// T4[p] → G;  slab += c_m conj(W_b) G (kept in registers across the sweep);  position-gradient
+// partials per pattern.  The slab stripe is written once at the end (k_slab_reduce sums groups).
+__global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
+  __shared__ float2 xb[kXElems];
+  __shared__ float2 tw[kN];
+  __shared__ float red[8];
+  load_tw(tw, a.twg);
+  __syncthreads();
+  const int s = blockIdx.x, p = blockIdx.y, gi = blockIdx.z;
+  const Map m = map_of<true>(opq(threadIdx.x));
+  const int kx = s * kL + m.line;
+  const int P = a.P;
+  constexpr float two_pi_n2 = 6.283185307179586f / (float)kN2;
+  float2 fp[16], acc[16];
+  const float2* F = a.Fp + (size_t)p * kN2 + kx;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    fp[k] = F[(m.slot + 16 * k) * kN];
+    acc[k] = make_float2(0.f, 0.f);
+  }
+  const float gx = shift_g(kx);
+  for (int j = gi; j < a.n; j += a.groups) {
+    const int sidx = scan_of(a, j);
+    const float sy = a.shifts[2 * sidx], sx = a.shifts[2 * sidx + 1];
+    const float c = a.coef[(size_t)a.bid[j] * kNCoef + a.ci];
+    const float2* in = a.t14 + ((size_t)j * P + p) * kN2 + m.slot * kN + kx;
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = in[16 * r * kN];
+    fft_line<-1, true>(v, m, xb, tw);
+    const float2 wx = f3::cis_rev(-sx * gx);
+    float sy_acc = 0.f, sim = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int ky = m.slot + 16 * k;
+      const float gyk = shift_g(ky);
+      const float2 W = cmul(f3::cis_rev(-sy * gyk), wx);
+      const float2 FW = cmul(fp[k], W);
+      const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);   // Im(F(P) W conj(G))
+      sy_acc = fmaf(gyk, im, sy_acc);
+      sim += im;
+      const float2 t = cmulc(v[k], W);                        // G conj(W)
+      acc[k].x = fmaf(c, t.x, acc[k].x);
+      acc[k].y = fmaf(c, t.y, acc[k].y);
+    }
+    float ds[2] = {sy_acc, gx * sim};
+    bsum<2>(ds, red);
+    if (threadIdx.x == 0) {
+      float* o = a.dsp + (((size_t)j * kStripes + s) * P + p) * 2;
+      o[0] = ds[0] * c * two_pi_n2;
+      o[1] = ds[1] * c * two_pi_n2;
+    }
+  }
+  float2* out = a.slabpart + ((size_t)gi * P + p) * kN2 + kx;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[(m.slot + 16 * k) * kN] = acc[k];
+}
+
+// ---------------------------------------------------------------------------------- small kernels
+// pattern → (mini-batch, clamped window origin)
+__global__ void k_s_table(const int* idx, int n, const int* boff, int n_batches, const int* crop, int n_scans, int Ny,
+                          int Nx, int* bid, int2* geo) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  int lo = 0, hi = n_batches;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (boff[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  bid[j] = lo;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  geo[j] = make_int2(min(max(crop[2 * s], 0), Ny - kN), min(max(crop[2 * s + 1], 0), Nx - kN));
+}
+
+// psums[j][i] = Σ_stripes psum_s[j][s][i]   (fixed order)
+__global__ void k_s_psum(const float* psum_s, int n, float* psums) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * kNSum) return;
+  const int j = t / kNSum, i = t % kNSum;
+  float acc = 0.f;
+  for (int s = 0; s < kStripes; ++s) acc += psum_s[((size_t)j * kStripes + s) * kNSum + i];
+  psums[(size_t)j * kNSum + i] = acc;
+}
+
+// d_shifts[idx[j]] += Σ over the pattern's stripe / mode partials (fixed order)
+__global__ void k_s_shift(const float* dsp, int n, int per, const int* idx, int n_scans, float* d_shifts) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  float y = 0.f, x = 0.f;
+  for (int i = 0; i < per; ++i) {
+    y += dsp[((size_t)j * per + i) * 2];
+    x += dsp[((size_t)j * per + i) * 2 + 1];
+  }
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  atomicAdd(d_shifts + 2 * s, y);
+  atomicAdd(d_shifts + 2 * s + 1, x);
+}
+
+}  // namespace sp
+}  // namespace ptyx

@@ -38,7 +38,9 @@ def config_problem(P, O, meas_f16, seed):
 
 
 def check_against_oracle(d, batches, meas_f16):
-    terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=meas_f16)
+    ks = {}
+    terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=meas_f16, kernels=ks)
+    assert {"k_s1", "k_s2", "k_s3", "k_s4", "k_s5"} <= set(ks), ks      # the N = 256 stripe engine ran
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"])
     assert rel(dp, np.concatenate(odps)) < TOL_DP

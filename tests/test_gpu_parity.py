@@ -52,9 +52,13 @@ def make_plan(d, device, max_patterns=None, meas_f16=False):
                 shift_probes=bool(d["shift_probes"]), meas_f16=meas_f16, device=device)
 
 
-def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", "objp", "probe", "shifts")):
+def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", "objp", "probe", "shifts"),
+              kernels=None):
+    """kernels: a dict that receives the plan's per-kernel launch statistics (engine check)."""
     from ptyrad_amd.engine import LossConfig, batch_offsets
     plan = make_plan(d, device, meas_f16=meas_f16)
+    if kernels is not None:
+        plan.profile_begin()
     t = tensors(d, device, torch.float16 if meas_f16 else torch.float32)
     grads = {k: torch.zeros_like(t[k if k != "shifts" else "shifts"]) for k in want}
     if not d["shift_probes"]:
@@ -65,6 +69,8 @@ def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", 
     terms = plan.forward_loss_grad(t, flat, batch_offsets(batches), LossConfig.from_loss_params(d["loss_params"]),
                                    grads, grad_scale=grad_scale, dp_out=dp)
     torch.cuda.synchronize()
+    if kernels is not None:
+        kernels.update(plan.profile_end())
     g = {k: v.cpu().numpy() for k, v in grads.items()}
     if "probe" in g:
         g["probe"] = g["probe"][..., 0] + 1j * g["probe"][..., 1]
