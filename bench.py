@@ -1,16 +1,26 @@
 """Benchmark: diffraction-patterns/sec/iter (fwd+loss+adjoint) on the MI355X engine.
 
-Workload = BASELINE.json configs[1] ("c2"): synthetic 4D-STEM, 256x256 scan per GPU, 128x128 DPs,
-1 probe mode, 1 object mode, single slice, sub-px probe shifts on (schema default), loss_single
-(dp_pow 0.5) + loss_sparse (L1, w 0.1), reference mini-batch B = 32 with its own NRMSE
-normalisation.  One step = one iteration over the GPU's whole shard (65,536 patterns = 2,048
-mini-batches) through ptyx_forward_loss_grad, gradients of every mini-batch accumulated (the
-reference's grad_accumulation over the iteration), followed - with N > 1 GPUs - by one RCCL
-all-reduce(sum) of the object + probe gradients.  Weak scaling: the global scan is
-(256·N) x 256 positions, GPU r owns rows [256 r, 256 r + 256) and its DPs; object and probe are
-replicated.  Inputs are resident in HBM before the timed region.
+Default workload = BASELINE.json configs[1] ("c2"): synthetic 4D-STEM, 256x256 scan per GPU,
+128x128 DPs simulated by the engine's own forward model from a ground-truth atom-lattice object
+(SURVEY §8d), 1 probe mode, 1 object mode, single slice, sub-px probe shifts on (schema
+default), loss_single (dp_pow 0.5) + loss_sparse (L1, w 0.1), reference mini-batch B = 32 with
+its own NRMSE normalisation.  One step = one iteration over the GPU's whole shard (65,536
+patterns = 2,048 mini-batches) through ptyx_forward_loss_grad, the gradients of every
+mini-batch accumulated into ONE flat buffer (the reference's grad_accumulation over the
+iteration), then - with N > 1 GPUs - one RCCL all-reduce(sum) of that buffer
+(ptyrad_amd.reconstruction.DistContext, the replacement of the DDP wrapper).  Weak scaling: the
+global scan is (256·N) x 256 positions, GPU r owns rows [256 r, 256 r + 256) and holds only its
+DPs; object and probe are replicated.  Inputs are resident in HBM before the timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Other workloads (--config; all one process per GPU, same step structure):
+  c2-strong  a fixed 256x256 scan split over the ranks (strong scaling of the c2 step)
+  c3         N=256, P=8 probe x O=2 object modes, a --patterns block of the 512² raster per rank
+  c4         N=128, Nz=16, position correction: the 1024² scan sharded over the ranks
+             (one optimizer step per iteration, all-reduce of the 2x16x3679² object gradient)
+  c5         N=256, P=4, fp16 DP storage: a resident sub-stripe (--patterns positions) of each
+             rank's shard of the 4096² scan (the full shard is 275 GB of DPs per GPU)
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
        torchrun --nproc-per-node N bench.py --gpus N ...   (driver, one rank per GPU, RCCL)
 """
 from __future__ import annotations
@@ -28,7 +38,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-FP32_PEAK_TFLOPS = 157.3
+FP32_PEAK_TFLOPS = 157.3     # FP32 vector = FP32 MFMA rate on gfx950
+
+CONFIGS = {
+    "c2": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="weak"),
+    "c2-strong": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="strong"),
+    "c3": dict(N=256, P=8, O=2, Nz=1, f16=False, scan=512, mode="block"),
+    "c4": dict(N=128, P=1, O=1, Nz=16, f16=False, scan=1024, mode="strong"),
+    "c5": dict(N=256, P=4, O=1, Nz=1, f16=True, scan=4096, mode="block"),
+}
 
 
 def parse():
@@ -36,20 +54,38 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=32, help="reference mini-batch size (BATCH_SIZE.size)")
-    ap.add_argument("--scan", type=int, default=256, help="scan positions per side per GPU shard")
-    ap.add_argument("--N", type=int, default=128)
-    ap.add_argument("--cpu-sample", type=int, default=40960, help="patterns for the CPU baseline (about 10 s on 16 cores)")
+    ap.add_argument("--scan", type=int, default=None, help="c2: scan positions per side per GPU shard")
+    ap.add_argument("--patterns", type=int, default=16384, help="c3 / c5: positions per rank (a block of the raster)")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="patterns for the CPU baseline (0: about 20 s of the host's cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--geom-world", type=int, default=0,
-                    help="diagnostic: build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
+                    help="diagnostic (c2): build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
                          "(no collective) to check that per-rank work stays constant as W grows")
     ap.add_argument("--geom-rank", type=int, default=0)
     return ap.parse_args()
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle port)
+def host_cores() -> int:
+    """CPU cores this process may use: the cgroup CPU quota when there is one (the GPU box gives a
+    job a share of a large host; os.cpu_count() shows the whole machine), else the affinity mask.
+    PTYX_CPU_CORES overrides."""
+    if os.environ.get("PTYX_CPU_CORES"):
+        return max(1, int(os.environ["PTYX_CPU_CORES"]))
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def _cpu_worker(args):
     n, seed, nbatch, bsize = args
     from oracle import ptyx_oracle as orc
@@ -67,9 +103,12 @@ def _cpu_worker(args):
 
 
 def cpu_baseline(n, bsize, sample):
-    """Oracle (NumPy port of the reference path) on the host cores, before any GPU call."""
+    """Oracle (NumPy port of the reference path) on the host cores, one process per core, before
+    any GPU call.  sample 0: about 20 s of work (≈ 110 patterns/s per core measured)."""
     import multiprocessing as mp
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = host_cores()
+    if not sample:
+        sample = 110 * 20 * cores
     nb_total = max(cores, sample // bsize)
     per = [nb_total // cores + (1 if i < nb_total % cores else 0) for i in range(cores)]
     jobs = [(n, 100 + i, per[i], bsize) for i in range(cores) if per[i] > 0]
@@ -78,14 +117,46 @@ def cpu_baseline(n, bsize, sample):
         res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
     pats = sum(r[0] for r in res)
-    return {"value": pats / wall, "unit": "patterns/s", "cores": len(jobs), "kind": "port",
-            "sample": f"{pats} patterns ({len(jobs)} processes x mini-batches of {bsize}), N={n}, P=O=Nz=1, "
-                      f"shifts on, oracle/ptyx_oracle.py complex64 NumPy, wall {wall:.1f}s incl. pool start"}
+    out = {"value": round(pats / wall, 1), "unit": "patterns/s", "cores": len(jobs), "kind": "port",
+           "sample": f"{pats} patterns of the c2 shape ({len(jobs)} processes x mini-batches of {bsize}), N={n}, "
+                     f"P=O=Nz=1, shifts on, oracle/ptyx_oracle.py complex64 NumPy, wall {wall:.1f}s incl. pool start"}
+    ratio = os.path.join(ROOT, "tests", "golden", "cpu_ratio.json")
+    if os.path.exists(ratio):   # reference CPU path vs this port, same cores, measured in the build container
+        r = json.load(open(ratio))
+        out["ratio_to_reference"] = r["ratio_reference_over_port"]
+        out["reference_equivalent"] = round(out["value"] * r["ratio_reference_over_port"], 1)
+        out["ratio_measured"] = f"{r['host']}: reference {r['reference_patterns_per_s']} / port " \
+                                f"{r['port_patterns_per_s']} patterns/s (tests/golden/measure_cpu_ratio.py)"
+    return out
 
 
 # ------------------------------------------------------------------ GPU workload
+def gt_object(shape, dev, seed=1):
+    """Ground-truth object on the device: unit amplitude, Gaussian atoms (σ 1.5 px,
+    peak 0.3 rad) on a 3.3 Å hexagonal lattice — ptyrad_amd.synthetic.atom_phase_object in torch."""
+    import torch
+    from ptyrad_amd import synthetic as syn
+    O, Nz, ny, nx = shape
+    rng = np.random.default_rng(seed)
+    sp = 3.3 / syn.DX_ANG
+    basis = torch.tensor([[0.0, sp], [sp * math.sqrt(3) / 2, sp / 2]], dtype=torch.float64, device=dev)
+    inv = torch.linalg.inv(basis.T)
+    phase = torch.empty(shape, dtype=torch.float32, device=dev)
+    yy = torch.arange(ny, dtype=torch.float64, device=dev)[:, None]
+    xx = torch.arange(nx, dtype=torch.float64, device=dev)[None, :]
+    for z in range(Nz):
+        off = rng.uniform(0, sp, size=2)
+        fy, fx = torch.broadcast_tensors(yy - off[0], xx - off[1])
+        c = torch.einsum("ij,jyx->iyx", inv, torch.stack([fy, fx]))
+        c = c - torch.round(c)
+        d = torch.einsum("ij,jyx->iyx", basis.T, c)
+        phase[:, z] = ((0.3 / Nz) * torch.exp(-(d[0] ** 2 + d[1] ** 2) / (2 * 1.5 ** 2))).float()
+    return torch.ones_like(phase), phase
+
+
 def main():
     a = parse()
+    cfg = CONFIGS[a.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -94,58 +165,119 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.N, a.batch, a.cpu_sample)          # before the GPU is touched
+        cpu = cpu_baseline(128, a.batch, a.cpu_sample)          # before the GPU is touched
 
     import torch
     import torch.distributed as dist
     from ptyrad_amd import synthetic as syn
     from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
+    from ptyrad_amd.reconstruction import DistContext
 
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    N, S = a.N, a.scan
+    ctx = DistContext()
+    N, P, O, Nz, f16 = cfg["N"], cfg["P"], cfg["O"], cfg["Nz"], cfg["f16"]
+    step_px = syn.STEP_ANG / syn.DX_ANG
     gw, gr = (a.geom_world, a.geom_rank) if a.geom_world else (world, rank)
-    n_slow_g, n_fast = S * gw, S
-    scan = syn.raster_scan(n_slow_g, n_fast, N, seed=0)
-    sl = slice(gr * S * n_fast, (gr + 1) * S * n_fast)
-    crop_pos, shifts = scan.crop_pos[sl], scan.shifts[sl]
+
+    # -------------------------------------------------- geometry: this rank's positions
+    if a.config == "c2":
+        S = a.scan or cfg["scan"]
+        scan = syn.raster_scan(S * gw, S, N, seed=0)
+        sl = slice(gr * S * S, (gr + 1) * S * S)
+        crop_pos, shifts, (Ny, Nx) = scan.crop_pos[sl], scan.shifts[sl], scan.obj_shape
+        desc = f"c2: synthetic 4D-STEM, {S}x{S} scan per GPU (weak scaling), 128x128 DP, P=O=Nz=1"
+    elif cfg["mode"] == "strong":     # c2-strong, c4: a fixed global scan, rows split over ranks
+        S = cfg["scan"] if a.config == "c4" else (a.scan or cfg["scan"])
+        scan = syn.raster_scan(S, S, N, seed=0)
+        r0, r1 = S * gr // gw, S * (gr + 1) // gw
+        sl = slice(r0 * S, r1 * S)
+        crop_pos, shifts, (Ny, Nx) = scan.crop_pos[sl], scan.shifts[sl], scan.obj_shape
+        desc = (f"{a.config}: {S}x{S} scan split over {gw} GPU(s) (rows {r0}-{r1} here), {N}x{N} DP, "
+                f"P={P}, O={O}, Nz={Nz}")
+    else:                             # c3 / c5: a block of --patterns positions of the rank's shard
+        S = cfg["scan"]
+        side = syn.object_side(S, N, step_px)
+        n_fast = min(S, a.patterns)
+        n_slow = max(1, a.patterns // n_fast)
+        rows_per_rank = S // max(1, gw)
+        # the block starts at this rank's first scan row of the full S x S raster
+        blk = syn.raster_scan(n_slow, n_fast, N, obj_shape=(side, side), seed=gr)
+        full_y0 = (side - ((S - 1) * step_px + N)) / 2.0
+        blk_y0 = (side - ((n_slow - 1) * step_px + N)) / 2.0
+        dy = int(round(full_y0 + gr * rows_per_rank * step_px - blk_y0))
+        crop_pos = blk.crop_pos.copy()
+        crop_pos[:, 0] = np.clip(crop_pos[:, 0] + dy, 0, side - N)
+        shifts, (Ny, Nx) = blk.shifts, (side, side)
+        desc = (f"{a.config}: {n_slow}x{n_fast} block of the {S}x{S} scan per GPU (rank shard rows from "
+                f"{gr * rows_per_rank}), object {side}x{side}, {N}x{N} DP, P={P}, O={O}, Nz={Nz}"
+                f"{', fp16 DP storage' if f16 else ''}")
     n_local = crop_pos.shape[0]
-    Ny, Nx = scan.obj_shape
+
+    # -------------------------------------------------- parameters (replicated) and this rank's DPs
     g = torch.Generator(device=dev)
-    g.manual_seed(1234)          # identical object / probe on every rank (replicas)
-    obja = (1.0 + 0.05 * torch.randn((1, 1, Ny, Nx), generator=g, device=dev)).float()
-    objp = (0.1 * torch.randn((1, 1, Ny, Nx), generator=g, device=dev)).float()
-    probe = torch.view_as_real(torch.tensor(syn.stem_probe(N) * np.float32(60.0), device=dev)[None]).contiguous()
-    gm = torch.Generator(device=dev)
-    gm.manual_seed(4321 + rank)
-    meas = torch.rand((n_local, N, N), generator=gm, device=dev)      # this GPU's DPs, HBM-resident
-    t = {"obja": obja, "objp": objp, "probe": probe,
-         "shifts": torch.tensor(shifts, device=dev), "H": torch.tensor(syn.fresnel_propagator(N, syn.DX_ANG, 2.0),
-                                                                        device=dev),
-         "occu": torch.ones(1, device=dev), "crop_pos": torch.tensor(crop_pos, device=dev), "meas": meas}
-    plan = Plan(N, 1, 1, 1, Ny, Nx, n_local, n_local, shift_probes=True, device=dev)
+    g.manual_seed(1234)               # identical reconstruction init / probe on every rank
+    base = syn.stem_probe(N) * np.float32(60.0 if N == 128 else 30.0)
+    probe_c = syn.mixed_probe(base, P) if P > 1 else base[None]
+    probe = torch.view_as_real(torch.tensor(probe_c.astype(np.complex64), device=dev)).contiguous()
+    t = {"probe": probe, "shifts": torch.tensor(shifts, device=dev),
+         "H": torch.tensor(syn.fresnel_propagator(N, syn.DX_ANG, 2.0), device=dev),
+         "occu": torch.tensor(syn.omode_occupancy(O), device=dev), "crop_pos": torch.tensor(crop_pos, device=dev)}
+    plan = Plan(N, P, O, Nz, Ny, Nx, n_local, n_local, shift_probes=True, meas_f16=f16, device=dev)
+    if a.config in ("c2", "c2-strong"):
+        # DPs = the forward model on the ground-truth object (+1e-10), then the reconstruction
+        # starts from exp(1e-8 i U)
+        gta, gtp = gt_object((O, Nz, Ny, Nx), dev)
+        meas = torch.empty((n_local, N, N), dtype=torch.float32, device=dev)
+        plan.forward({**t, "obja": gta, "objp": gtp}, np.arange(n_local, dtype=np.int32), dp_out=meas)
+        del gta, gtp
+        t["obja"] = torch.ones((O, Nz, Ny, Nx), device=dev)
+        t["objp"] = (1e-8 * torch.rand((O, Nz, Ny, Nx), generator=g, device=dev)).float()
+        data = "synthetic: DPs = engine forward model of a ground-truth atom-lattice object; recon init exp(1e-8 iU)"
+    else:
+        t["obja"] = (1.0 + 0.05 * torch.randn((O, Nz, Ny, Nx), generator=g, device=dev)).float()
+        t["objp"] = (0.1 / Nz * torch.randn((O, Nz, Ny, Nx), generator=g, device=dev)).float()
+        gm = torch.Generator(device=dev)
+        gm.manual_seed(4321 + rank)
+        meas = torch.rand((n_local, N, N), generator=gm, device=dev)
+        data = "synthetic: seeded uniform DPs (SURVEY §8d allows random DPs for c3-c5), random object"
+    t["meas"] = meas.half() if f16 else meas
+    del meas
     rng = np.random.default_rng(7 + rank)
-    batches = np.array_split(rng.permutation(n_local), n_local // a.batch)     # make_batches 'random'
+    batches = np.array_split(rng.permutation(n_local), max(1, n_local // a.batch))   # make_batches 'random'
     idx_t = torch.as_tensor(np.concatenate(batches), dtype=torch.int32, device=dev)
-    off_t = torch.as_tensor(batch_offsets(batches), device=dev)
+    off = batch_offsets(batches)       # host offsets: the Plan splits a call at mini-batch boundaries
     nb = len(batches)
     max_batch = max(len(b) for b in batches)
-    cfg = LossConfig()
-    n_obj = obja.numel()
-    flat = torch.zeros(2 * n_obj + probe.numel(), device=dev)     # one all-reduce buffer
-    grads = {"obja": flat[:n_obj].view_as(obja), "objp": flat[n_obj:2 * n_obj].view_as(objp),
-             "probe": flat[2 * n_obj:].view_as(probe), "shifts": torch.zeros_like(t["shifts"])}
+    lcfg = LossConfig()
+    # every gradient of the step in ONE flat buffer (position gradients are rank-local)
+    names = ("obja", "objp", "probe")
+    flat = torch.zeros(sum(t[k].numel() for k in names), device=dev)
+    grads, o_ = {}, 0
+    for k in names:
+        grads[k] = flat[o_:o_ + t[k].numel()].view_as(t[k])
+        o_ += t[k].numel()
+    grads["shifts"] = torch.zeros_like(t["shifts"])
     terms = torch.empty((nb, 5), device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ar_ev = []
 
-    def step():
+    def step(timed=False):
         flat.zero_()
         grads["shifts"].zero_()
-        plan.forward_loss_grad(t, idx_t, off_t, cfg, grads, grad_scale=1.0 / nb, loss_terms=terms,
+        plan.forward_loss_grad(t, idx_t, off, lcfg, grads, grad_scale=1.0 / nb, loss_terms=terms,
                                max_batch=max_batch)
         if world > 1:
-            dist.all_reduce(flat)          # object + probe gradients; positions are rank-local
+            e0 = torch.cuda.Event(enable_timing=True) if timed else None
+            e1 = torch.cuda.Event(enable_timing=True) if timed else None
+            if timed:
+                e0.record(stream)
+            ctx.allreduce(flat)        # object + probe gradients: ONE RCCL all-reduce per step
+            if timed:
+                e1.record(stream)
+                ar_ev.append((e0, e1))
 
     for _ in range(a.warmup):
         step()
@@ -156,65 +288,85 @@ def main():
     plan.profile_begin()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kstats = plan.profile_end()
+    assert bool(torch.isfinite(terms).all()), "non-finite loss terms"
+    ar_ms = sum(e0.elapsed_time(e1) for e0, e1 in ar_ev) / max(1, len(ar_ev)) if ar_ev else 0.0
+    engine_ms = sum(v[1] for v in kstats.values()) / a.steps
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        e = torch.tensor([elapsed, engine_ms, ar_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    total_patterns = world * n_local * a.steps
+        elapsed, engine_max, ar_max = (float(x) for x in e.tolist())
+    else:
+        engine_max, ar_max = engine_ms, ar_ms
+    total_patterns = world * n_local * a.steps if cfg["mode"] != "strong" else scan.crop_pos.shape[0] * a.steps
+    if a.geom_world:
+        total_patterns = n_local * a.steps
     value = total_patterns / elapsed
     ms_per_step = 1e3 * elapsed / a.steps
 
-    # roofline of the dominant kernel (k_fused: forward + loss + adjoint in one pass; k_adjoint on
-    # the two-pass path).  SURVEY §8d per pattern: B_alg = N^2 (s_m + 16 O Nz) bytes,
-    # F_alg = n_fft 5 N^2 log2 N^2 flops (n_fft = 2 P O (2 Nz - 1) + 2P with shifts).
-    b_alg = N * N * (4 + 16 * 1 * 1)
-    n_fft = 2 * 1 * 1 * (2 * 1 - 1) + 2
-    flops = n_fft * 5 * N * N * math.log2(N * N)
-    dom = "k_fused" if "k_fused" in kstats else "k_adjoint"
-    launches, dom_ms = kstats.get(dom, (0, 0.0))
+    # roofline.  SURVEY §8d per pattern: B_alg = N^2 (s_m + 16 O Nz) bytes (DP read once, object patch
+    # read and patch-gradient write), F_alg = n_fft 5 N^2 log2 N^2 flops, n_fft = 2 P O (2 Nz - 1) + 2P.
+    s_m = 2 if f16 else 4
+    b_alg = N * N * (s_m + 16 * O * Nz)
+    n_fft = 2 * P * O * (2 * Nz - 1) + 2 * P
+    f_alg = n_fft * 5 * N * N * math.log2(N * N)
     roof = None
-    if launches:
+    stripe = [k for k in kstats if k.startswith("k_s")]
+    if "k_fused" in kstats:
+        # the register engines (k_fused3 / k_fused3ms): forward + loss + adjoint in one launch per call
+        launches, dom_ms = kstats["k_fused"]
         avg_s = dom_ms / launches / 1e3
-        achieved = b_alg * n_local / avg_s / 1e9
+        per_launch = n_local / max(1, launches // a.steps)       # patterns per launch
+        achieved = b_alg * per_launch / avg_s / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_c2.json")
-        if os.path.exists(pmc):
-            # PMC summary of the same workload (profiles/collect_pmc.sh → summarize_pmc.py); its
-            # kernel names are the HIP symbols: k_fused3 (register engine) or k_fused2
-            engine = "k_fused3" if "k_obj_prep" in kstats else "k_fused2"
+        if a.config == "c2" and os.path.exists(pmc):
+            # PMC summary of the same workload (profiles/collect_pmc.sh → summarize_pmc.py)
             with open(pmc) as f:
-                tb = json.load(f).get("hbm_bytes_per_launch", {})
-            traffic = tb.get(engine) if dom == "k_fused" else tb.get(dom)
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": b_alg * n_local, "avg_launch_ms": round(avg_s * 1e3, 4),
-                "fft_fp32_frac": round(flops * n_local / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4)}
+                traffic = json.load(f).get("hbm_bytes_per_launch", {}).get("k_fused3")
+        roof = {"kernel": "k_fused3" if Nz == 1 else "k_fused3ms", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": int(b_alg * per_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
+                "fft_fp32_frac": round(f_alg * per_launch / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4)}
         g_launches, g_ms = kstats.get("k_obj_gather", (0, 0.0))
         if g_launches:
-            # gather reads one N^2 complex g_O slot per pattern (+ the object tile, negligible)
             g_s = g_ms / g_launches / 1e3
             roof["gather"] = {"avg_launch_ms": round(g_s * 1e3, 4),
-                              "achieved_GBps": round(8 * N * N * n_local / g_s / 1e9, 1)}
+                              "achieved_GBps": round(8 * N * N * Nz * per_launch / g_s / 1e9, 1)}
+    elif stripe:
+        # the N = 256 stripe engine (k_s1..k_s5): FP32-FFT bound (c3 AI 107, c5 AI 71 flop/B)
+        s_ms = sum(kstats[k][1] for k in stripe) / a.steps
+        achieved = f_alg * n_local / (s_ms / 1e3) / 1e12
+        roof = {"kernel": "stripe engine k_s1..k_s5", "bound": "mfma", "achieved": round(achieved, 2),
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "traffic": None, "alg_flops_per_step": f_alg * n_local, "engine_ms_per_step": round(s_ms, 3),
+                "note": "FP32 vector peak = FP32 MFMA rate on gfx950; the FFTs run on the vector ALUs",
+                "hbm_alg_frac": round(b_alg * n_local / (s_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    par = f"dp{world} (RCCL all-reduce of object+probe grads per step)" if world > 1 else "dp1"
     out = {
-        "metric": "diffraction-patterns/sec/iter (fwd+bwd), 256x256 probe positions, 128x128 DP",
+        "metric": "diffraction-patterns/sec/iter (fwd+bwd), 256x256 probe positions, 128x128 DP"
+        if a.config.startswith("c2") else f"diffraction-patterns/sec/iter (fwd+bwd), BASELINE {a.config}",
         "value": round(value, 1), "unit": "patterns/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32", "data": "synthetic (seeded torch.rand DPs, random object, aperture STEM probe)",
-        "config": {"workload": "c2: synthetic 4D-STEM, 256x256 scan per GPU, 128x128 DP, P=O=Nz=1, "
-                               "sub-px shifts on, loss_single(q=0.5)+loss_sparse(L1), mini-batch 32",
-                   "scan_per_gpu": [S, S], "N": N, "mini_batch": a.batch, "mini_batches_per_step": nb,
-                   "patterns_per_gpu_per_step": n_local, "object": [Ny, Nx],
-                   "parallelism": f"dp{world} (RCCL all-reduce of object+probe grads per step)",
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "strong" if cfg["mode"] == "strong" else "weak", "vs_baseline": None,
+        "dtype": "f32", "data": data,
+        "config": {"workload": desc + ", sub-px shifts on, loss_single(q=0.5)+loss_sparse(L1), mini-batch "
+                   f"{a.batch}, one optimizer step (all-reduce) per iteration",
+                   "N": N, "P": P, "O": O, "Nz": Nz, "dp_storage": "f16" if f16 else "f32",
+                   "mini_batch": a.batch, "mini_batches_per_step": nb, "patterns_per_gpu_per_step": n_local,
+                   "object": [Ny, Nx], "parallelism": par,
                    **({"geometry_only": f"rank {gr} of a {gw}-GPU scan, no collective"} if a.geom_world else {})},
         "roofline": roof,
-        "fft_tflops": round(value / world * flops / 1e12, 2) if world else None,
+        "per_rank_ms": {"engine": round(engine_max, 3), "allreduce": round(ar_max, 3),
+                        "allreduce_bytes": int(flat.numel() * 4)},
+        "fft_tflops": round(value / world * f_alg / 1e12, 2) if cfg["mode"] != "strong" else
+        round(value * f_alg / 1e12 / world, 2),
         "kernels_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in kstats.items()},
         "cpu_baseline": cpu,
     }

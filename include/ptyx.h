@@ -38,13 +38,21 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 200
+#define PTYX_ABI_VERSION 201
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
 #define PTYX_ENOMEM 2
 #define PTYX_EHIP 3
 #define PTYX_EUNSUPPORTED 4
+
+/* loss_cfg.prep: per-call preparation of the object (A e^{iφ}, loss_sparse prefix sums) and of
+ * the probe spectrum.  A caller that splits one optimizer step's group of mini-batches into
+ * several calls (obja / objp / probe / H unchanged between them) passes PTYX_PREP_FULL on the
+ * first call and PTYX_PREP_REUSE on the others. */
+#define PTYX_PREP_CALL 0   /* prepare what this call's windows touch                           */
+#define PTYX_PREP_FULL 1   /* prepare the whole object, for later PTYX_PREP_REUSE calls          */
+#define PTYX_PREP_REUSE 2  /* reuse the previous call's preparation on this plan                */
 
 /* dims.flags */
 #define PTYX_SHIFT_PROBES 1u /* sub-px Fourier-shifted probes (PtychoAD.shift_probes, models.py:120) */
@@ -111,6 +119,7 @@ typedef struct ptyx_loss_cfg {
   float grad_scale;   /* multiplies every gradient: 1/grad_accumulation, reconstruction.py:750 */
   int32_t max_batch;  /* largest mini-batch of the call, 0 = unknown (informational: engine
                          choice depends only on the geometry and the call's capacity)      */
+  int32_t prep;       /* PTYX_PREP_CALL | PTYX_PREP_FULL | PTYX_PREP_REUSE                   */
 } ptyx_loss_cfg;
 
 /* Create a plan: validates dims, allocates the device workspace and twiddle tables.

@@ -1,13 +1,18 @@
 #!/bin/bash
-# PMC counter passes for the c2 bench workload (one counter group per rocprofv3 run; FETCH_SIZE and
-# WRITE_SIZE in separate passes, MI355X_MICROARCH.md "rocprofv3 PMC slots").  Run on the GPU box:
-#   bash profiles/collect_pmc.sh <outdir> [extra bench args]
+# PMC counter passes (one counter group per rocprofv3 run; FETCH_SIZE and WRITE_SIZE in separate
+# passes, MI355X_MICROARCH.md "rocprofv3 PMC slots").  Run on the GPU box:
+#   bash profiles/collect_pmc.sh <outdir> [extra bench args]              (bench.py, the c2 workload)
+#   PMC_SCRIPT=tools/bench_configs.py bash profiles/collect_pmc.sh <outdir> --config c5 --patterns 4096
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=${1:-$R/gpurun_out/pmc}
 shift || true
 mkdir -p "$OUT"
+OUT=$(cd "$OUT" && pwd)
 export TMPDIR=/tmp
+SCRIPT=${PMC_SCRIPT:-bench.py}
+EXTRA=""
+[ "$SCRIPT" = "bench.py" ] && EXTRA="--no-cpu-baseline"
 cd /tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 i=0
@@ -18,6 +23,6 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i + 1))
   timeout -k 10 300 rocprofv3 --pmc $pass --output-format csv -d "$OUT/pass$i" -o pmc -- \
-    python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pass$i.json" 2> "$OUT/pass$i.err"
+    python3 "$R/$SCRIPT" --steps 1 --warmup 1 $EXTRA "$@" > "$OUT/pass$i.json" 2> "$OUT/pass$i.err"
 done
 echo "pmc passes done: $i"

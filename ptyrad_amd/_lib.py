@@ -14,7 +14,8 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 200     # include/ptyx.h
+PTYX_ABI_VERSION = 201     # include/ptyx.h
+PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
 PTYX_SHIFT_PROBES = 1
 PTYX_MEAS_F16 = 2
@@ -67,7 +68,7 @@ class LossCfg(ctypes.Structure):
                 ("poissn_on", ctypes.c_int32), ("poissn_w", ctypes.c_float), ("poissn_q", ctypes.c_float),
                 ("poissn_eps", ctypes.c_float),
                 ("sparse_on", ctypes.c_int32), ("sparse_w", ctypes.c_float), ("sparse_n", ctypes.c_int32),
-                ("grad_scale", ctypes.c_float), ("max_batch", ctypes.c_int32)]
+                ("grad_scale", ctypes.c_float), ("max_batch", ctypes.c_int32), ("prep", ctypes.c_int32)]
 
 
 class ObjConstraints(ctypes.Structure):

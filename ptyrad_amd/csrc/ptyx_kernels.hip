@@ -830,18 +830,22 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   const bool stripe = d.N == 256 && d.Nz == 1 && d.O <= sp::kMaxO && (d.flags & PTYX_SHIFT_PROBES) && pl->fast &&
                       !std::getenv("PTYX_NO_STRIPE");
   if (stripe) {
-    // per-call intermediates (T1/T4, ψ⁰: P fields; T2/T3: P·O fields per pattern) within
-    // PTYX_STRIPE_MB (default the smaller of 16 GiB and a quarter of the free HBM); calls beyond
-    // the capacity are split by the host at mini-batch boundaries
+    // per-call intermediates (T1/T4, ψ⁰: P fields; T2/T3: P·O fields per pattern; PTYX_S_PSI0=0
+    // drops ψ⁰ and P4 recomputes it) within PTYX_STRIPE_MB (default the smaller of 16 GiB
+    // and a quarter of the free HBM); calls beyond the capacity are split by the host at
+    // mini-batch boundaries
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     long long mb = std::min<long long>(16384, (long long)(free_b / 4 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_STRIPE_MB")) mb = std::atoll(e);
-    const long long per = (long long)(2 * d.P + d.P * d.O) * (long long)N2 * (long long)sizeof(float2);
+    const char* ppsi = std::getenv("PTYX_S_PSI0");
+    const bool park = !(ppsi && ppsi[0] == '0');   // measured: parking ψ⁰ beats recomputing it in P4
+    const long long per = (long long)((park ? 2 : 1) * d.P + d.P * d.O) * (long long)N2 * (long long)sizeof(float2);
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / per);
     if (cap >= 1) {
       const int groups = std::max(1, std::min<int>((int)cap, (2048 + 16 * d.P - 1) / (16 * d.P)));
-      if ((rc = dalloc(pl, &pl->st14, (size_t)cap * d.P * N2)) || (rc = dalloc(pl, &pl->spsi0, (size_t)cap * d.P * N2)) ||
+      if ((rc = dalloc(pl, &pl->st14, (size_t)cap * d.P * N2)) ||
+          (rc = dalloc(pl, &pl->spsi0, park ? (size_t)cap * d.P * N2 : 0)) ||
           (rc = dalloc(pl, &pl->st23, (size_t)cap * d.P * d.O * N2)) ||
           (rc = dalloc(pl, &pl->spsum, (size_t)cap * sp::kStripes * kNSum)) ||
           (rc = dalloc(pl, &pl->sdsp, (size_t)cap * sp::kStripes * d.P * 2)) ||
@@ -893,7 +897,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       // patterns (PTYX_SEG_DIV); calls with more segments take the two-pass engine
       long long div = 8;
       if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
-      pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
+      pl->seg_cap = pl->nwg3 + (cap + div - 1) / div;   // a call holds at most `cap` patterns
       if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
@@ -927,7 +931,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
       long long div = 8;
       if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
-      pl->seg_cap = pl->nwg3 + (d.max_patterns + div - 1) / div;
+      pl->seg_cap = pl->nwg3 + (cap + div - 1) / div;   // a call holds at most `cap` patterns
       if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * d.Nz * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->hpk, N2)) || (rc = dalloc(pl, &pl->bbox, 4)) ||
@@ -1081,7 +1085,9 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const ptyx_dims& d = pl->d;
   const bool sparse = cfg->sparse_on != 0;
   const int Nz = d.Nz;                 // > 1: k_fused3ms (multislice)
-  if (a.shift) {
+  const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
+  if (reuse) {
+  } else if (a.shift) {
     launch_spectrum<N>(pl, a, st);
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, pl->Fp, pl->fpk);
@@ -1090,7 +1096,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256), dim3(256), 0, st,
                        reinterpret_cast<const float2*>(in->probe), pl->fpk);
   }
-  if (Nz > 1) {
+  if (Nz > 1 && !reuse) {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk);
   }
@@ -1101,10 +1107,11 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(f3::k_bbox, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
                        d.Ny, d.Nx, pl->bbox);
   }
-  {
+  if (!reuse) {
     ProfScope ps(pl, kKObjPrep, st);   // (Nz, Ny) rows: every slice's O and |φ|^n prefix sums
     hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny * Nz), dim3(256), 0, st, a.obja, a.objp, d.Ny * Nz, d.Nx, pl->oc,
-                       sparse ? pl->pref : nullptr, cfg->sparse_n, pl->bbox, d.Ny);
+                       sparse ? pl->pref : nullptr, cfg->sparse_n,
+                       cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, 128);
   }
   {
     ProfScope ps(pl, kKTable, st);
@@ -1228,7 +1235,8 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const bool single = cfg->single_on != 0;
   const bool tail = gz.d_probe != nullptr || gz.d_shifts != nullptr;
   const bool any_grad = gz.d_obja || gz.d_objp || tail;
-  launch_spectrum<256>(pl, a, st);                       // F(P_p), natural order
+  const bool reuse = cfg->prep == PTYX_PREP_REUSE;     // object / probe prepared by the previous call
+  if (!reuse) launch_spectrum<256>(pl, a, st);         // F(P_p), natural order
   {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
@@ -1237,10 +1245,10 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(f3::k_bbox, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
                        pl->bbox, kN);
   }
-  {
-    ProfScope ps(pl, kKObjPrep, st);   // O = A e^{iφ} on the rows the call's windows touch
+  if (!reuse) {
+    ProfScope ps(pl, kKObjPrep, st);   // O = A e^{iφ} on the rows the call's windows touch (or all)
     hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.O * d.Ny), dim3(256), 0, st, a.obja, a.objp, d.O * d.Ny, d.Nx, pl->oc,
-                       nullptr, 1, pl->bbox, d.Ny, kN);
+                       nullptr, 1, cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, kN);
   }
   SArgs s{};
   s.n = n; s.P = P; s.O = O; s.Ny = d.Ny; s.Nx = d.Nx; s.n_scans = d.n_scans; s.meas_f16 = a.meas_f16;
@@ -1268,7 +1276,11 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   {
     ProfScope ps(pl, kKS3, st);
     const dim3 gr(n, kStripes);
-    const int PO = P * O;
+    // Ψ held in registers for P·O ≤ 2; above that the column FFTs are redone (measured faster than
+    // holding 3-4 modes at one workgroup per CU; PTYX_S3_HOLD=1 holds up to 4)
+    const char* hl = std::getenv("PTYX_S3_HOLD");
+    const int hold_max = (hl && hl[0] == '1') ? 4 : 2;
+    const int PO = P * O <= hold_max ? P * O : 99;
     const bool half = single && s.q == 0.5f;
 #define PTYX_S3(SG, QM)                                                                                  \
   switch (PO) {                                                                                        \
@@ -1304,7 +1316,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   {
     ProfScope ps(pl, kKS4, st);
     SArgs s4 = s;
-    if (!tail) s4.t14 = nullptr;   // no probe / position gradient: skip the gP transform
+    s4.t4 = tail ? pl->st14 : nullptr;   // no probe / position gradient: skip the gP transform
     if (O == 1) hipLaunchKernelGGL(k_s4<1>, dim3(n, kStripes), bl, 0, st, s4);
     else hipLaunchKernelGGL(k_s4<2>, dim3(n, kStripes), bl, 0, st, s4);
   }
@@ -1486,7 +1498,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   }
 
   // two-pass engine: k_forward (dp, loss partial sums) → k_finalize → k_adjoint
-  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  if (a.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
   if (any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
     a.ffc = pl->ffc;
     a.ffc_per = pl->ffc_per;

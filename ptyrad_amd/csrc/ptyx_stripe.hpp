@@ -64,7 +64,8 @@ struct SArgs {
   float q, eps2;
   int sparse_on, sparse_n;
   float2* t14;           // (n, P, N²)   T1, later T4
-  float2* psi0;          // (n, P, N²)
+  float2* t4;            // = t14 when P4 writes T4 (probe / position gradients wanted), else NULL
+  float2* psi0;          // (n, P, N²) parked ψ⁰, or NULL: P4 recomputes ψ⁰ from T1 (one row IFFT)
   float2* t23;           // (n, P·O, N²) T2, later T3
   float* psum_s;         // (n, kStripes, kNSum) per-stripe loss partial sums
   float* dp_out;         // (n, N, N) or NULL
@@ -101,15 +102,31 @@ __device__ __forceinline__ int opq(int v) {
   return v;
 }
 
+// Scheduling fence: everything above is issued before anything below.  Used after a batch of
+// loads so that the 16 loads of a register array are all in flight before the first use (left
+// alone, the scheduler interleaves load / wait / use one register at a time).
+__device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0); }
+
+// v[r] = p[r·stride] for the 16 points of a thread, all issued before any is used
+__device__ __forceinline__ void ld16(float2 (&v)[16], const float2* p, int stride) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = p[r * stride];
+  fence_sched();
+}
+
 // 256-point DFT of every line of the stripe (DIR -1 forward, +1 unnormalised inverse).
 template <int DIR, bool COL>
 __device__ __forceinline__ void fft_line(float2 (&v)[16], Map m, float2* xb, const float2* tw) {
+  float2 w[15];
+#pragma unroll
+  for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = tw[(m.slot * k2) & 255];
+  fence_sched();
   rf::dft<16, DIR>(v);   // over n2: v[k2]
 #pragma unroll
   for (int k2 = 1; k2 < 16; ++k2) {
-    float2 w = tw[(m.slot * k2) & 255];
-    if (DIR > 0) w.y = -w.y;
-    v[k2] = cmul(v[k2], w);
+    float2 t = w[k2 - 1];
+    if (DIR > 0) t.y = -t.y;
+    v[k2] = cmul(v[k2], t);
   }
 #pragma unroll
   for (int k2 = 0; k2 < 16; ++k2) xb[xidx<COL>(m.line, m.slot, k2)] = v[k2];
@@ -147,11 +164,9 @@ __global__ __launch_bounds__(256, 2) void k_s1(SArgs a) {
   const float sy = a.shifts[2 * scan_of(a, j)];
   const float2* F = a.Fp + (size_t)p * kN2 + kx;
   float2 v[16];
+  ld16(v, F + m.slot * kN, 16 * kN);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int ky = m.slot + 16 * r;
-    v[r] = cmul(F[ky * kN], f3::cis_rev(-sy * shift_g(ky)));
-  }
+  for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sy * shift_g(m.slot + 16 * r)));
   fft_line<+1, true>(v, m, xb, tw);
   float2* out = a.t14 + ((size_t)j * a.P + p) * kN2 + kx;
 #pragma unroll
@@ -175,27 +190,39 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
   const int2 g0 = a.geo[j];
   const int P = a.P;
   constexpr float inv_n2 = 1.0f / kN2;
-  float2 wx[16];
+  // this stripe of the object window (O_o does not depend on the probe mode: loaded once)
+  float2 ob[O_][16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) wx[r] = f3::cis_rev(-sx * shift_g(m.slot + 16 * r));
+  for (int o = 0; o < O_; ++o) ld16(ob[o], a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);
+  // the next probe mode's T1 rows are prefetched during this mode's transforms (O = 1: the
+  // registers of a second object mode would not fit beside them)
+  constexpr bool PREF = O_ == 1;
+  float2 nxt[16];
+  if constexpr (PREF) ld16(nxt, a.t14 + (size_t)j * P * kN2 + y * kN + m.slot, 16);
   for (int p = 0; p < P; ++p) {
-    const float2* in = a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
     float2 v[16];
+    if constexpr (PREF) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = cmul(in[16 * r], wx[r]);
+      for (int r = 0; r < 16; ++r) v[r] = nxt[r];
+      if (p + 1 < P) ld16(nxt, a.t14 + ((size_t)j * P + p + 1) * kN2 + y * kN + m.slot, 16);
+    } else {
+      ld16(v, a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
     fft_line<+1, false>(v, m, xb, tw);
-    float2* ps = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      v[k] = cscale(v[k], inv_n2);
-      ps[16 * k] = v[k];
+    for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n2);
+    if (a.psi0) {
+      float2* ps = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) ps[16 * k] = v[k];
     }
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
-      const float2* orow = a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
       float2 u[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) u[k] = cmul(v[k], orow[16 * k]);
+      for (int k = 0; k < 16; ++k) u[k] = cmul(v[k], ob[o][k]);
       fft_line<-1, false>(u, m, xb, tw);
       float2* out = a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot;
 #pragma unroll
@@ -209,9 +236,13 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
     sp[o] = 0.f;
     if (a.sparse_on) {
       const float* prow = a.objp + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+      float ph[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) ph[k] = prow[16 * k];
+      fence_sched();
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const float ap = fabsf(prow[16 * k]);
+        const float ap = fabsf(ph[k]);
         sp[o] += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
       }
     }
@@ -228,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
 // grid (n, kStripes): columns kx of every mode: column FFT → Ψ, intensity, loss, g_Ψ → column IFFT.
 // HOLD > 0 (= P·O): every mode's Ψ stays in registers between the two sweeps; 0: recomputed.
 template <bool SINGLE, int QM, int HOLD>
-__global__ __launch_bounds__(256, 2) void k_s3(SArgs a) {
+__global__ __launch_bounds__(256, HOLD >= 4 ? 1 : 2) void k_s3(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
@@ -242,9 +273,7 @@ __global__ __launch_bounds__(256, 2) void k_s3(SArgs a) {
   constexpr float inv_n = 1.0f / kN;
   float2* base = a.t23 + (size_t)j * PO * kN2 + kx;
   auto far_field = [&](int q, float2 (&v)[16]) {
-    const float2* in = base + (size_t)q * kN2 + m.slot * kN;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = in[16 * r * kN];
+    ld16(v, base + (size_t)q * kN2 + m.slot * kN, 16 * kN);
     fft_line<-1, true>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n);
@@ -274,14 +303,21 @@ __global__ __launch_bounds__(256, 2) void k_s3(SArgs a) {
   const int sidx = scan_of(a, j);
   const size_t mi = (size_t)(a.mrow ? a.mrow[sidx] : sidx);
   const int col = (kx + kN / 2) & (kN - 1);
+  float Mv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = ((m.slot + 16 * k + kN / 2) & (kN - 1)) * kN + col;
+    Mv[k] = a.meas_f16 ? __half2float(reinterpret_cast<const __half*>(a.meas)[mi * kN2 + e])
+                       : reinterpret_cast<const float*>(a.meas)[mi * kN2 + e];
+  }
+  fence_sched();
   float S = 0.f, Ms = 0.f, u[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int ky = m.slot + 16 * k;
     const int e = ((ky + kN / 2) & (kN - 1)) * kN + col;
     const float Iv = I[k] + kDpEps;
-    const float M = a.meas_f16 ? __half2float(reinterpret_cast<const __half*>(a.meas)[mi * kN2 + e])
-                               : reinterpret_cast<const float*>(a.meas)[mi * kN2 + e];
+    const float M = Mv[k];
     if (a.dp_out) a.dp_out[(size_t)j * kN2 + e] = Iv;
     u[k] = f3::loss_point<QM, SINGLE>(Iv, M, a.q, a.eps2, S, Ms);
   }
@@ -328,6 +364,10 @@ template <int O_>
 __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
+  // O_ = 2: the per-probe-mode accumulator gP lives in LDS ([k][thread], conflict free), so the
+  // two object-mode slot accumulators fit the registers of two workgroups per CU
+  constexpr bool GP_LDS = O_ > 1;
+  __shared__ float2 gpl[GP_LDS ? 16 * 256 : 1];
   load_tw(tw, a.twg);
   __syncthreads();
   const int j = blockIdx.x, s = blockIdx.y;
@@ -337,55 +377,91 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
   const int P = a.P;
   const int mb = a.bid[j];
   constexpr float inv_n = 1.0f / kN;
-  const bool want_t4 = a.t14 != nullptr;
+  const bool want_t4 = a.t4 != nullptr;
+  const float sx = a.shifts[2 * scan_of(a, j) + 1];
+  constexpr float inv_n2 = 1.0f / kN2;
   float2 so[O_][16];
 #pragma unroll
   for (int o = 0; o < O_; ++o)
 #pragma unroll
     for (int k = 0; k < 16; ++k) so[o][k] = make_float2(0.f, 0.f);
   for (int p = 0; p < P; ++p) {
-    float2 psi[16], gp[16];
-    const float2* pin = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+    float2 psi[16];
+    if (a.psi0) {
+      ld16(psi, a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
+    } else {   // ψ⁰_p = F⁻¹_x(wx · T1_p)/N² again: one row transform instead of a parked field
+      ld16(psi, a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      psi[k] = pin[16 * k];
-      gp[k] = make_float2(0.f, 0.f);
+      for (int r = 0; r < 16; ++r) psi[r] = cmul(psi[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
+      fft_line<+1, false>(psi, m, xb, tw);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) psi[k] = cscale(psi[k], inv_n2);
+    }
+    float2 gp[GP_LDS ? 1 : 16];
+    if constexpr (!GP_LDS) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) gp[k] = make_float2(0.f, 0.f);
     }
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
-      const float2* in = a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot;
-      float2 v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = in[16 * r];
+      float2 v[16], ob[16];
+      ld16(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot, 16);
       fft_line<+1, false>(v, m, xb, tw);
-      const float2* orow = a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
+      ld16(ob, a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const float2 g = cscale(v[k], inv_n);
         so[o][k] = cadd(so[o][k], cmulc(g, psi[k]));
-        gp[k] = cadd(gp[k], cmulc(g, orow[16 * k]));
+        const float2 h = cmulc(g, ob[k]);
+        if constexpr (GP_LDS) {
+          float2& e = gpl[k * 256 + threadIdx.x];
+          e = o == 0 ? h : cadd(e, h);
+        } else {
+          gp[k] = cadd(gp[k], h);
+        }
       }
     });
     if (want_t4) {
-      fft_line<-1, false>(gp, m, xb, tw);
-      float2* out = a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
+      float2 gq[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) out[16 * r] = gp[r];
+      for (int k = 0; k < 16; ++k) gq[k] = GP_LDS ? gpl[k * 256 + threadIdx.x] : gp[GP_LDS ? 0 : k];
+      fft_line<-1, false>(gq, m, xb, tw);
+      float2* out = a.t4 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;   // over T1_p's rows (read above)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[16 * r] = gq[r];
     }
   }
   if (!a.d_obja && !a.d_objp) return;
+  // object gradient.  The slot accumulators are re-mapped through the (now free) exchange buffer
+  // so that each wave owns 4 whole rows: every atomic / object load is 256 contiguous bytes per
+  // wave instruction (the full-rate shape of global float atomics) instead of 4 × 64 B.
   const float c = a.coef[(size_t)mb * kNCoef + a.ci];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int o = 0; o < O_; ++o) {
     const float csp = a.sparse_on ? a.coef[(size_t)mb * kNCoef + 2 + o] : 0.f;
-    const size_t row = ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const size_t off = row + 16 * k;
-      const float A = a.obja[off], ph = a.objp[off];
+    for (int k = 0; k < 16; ++k) xb[m.line * 272 + m.slot + 16 * k] = so[o][k];
+    __syncthreads();
+    float Ar[16], Pr[16];
+    float2 gv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 4 * wv + (i >> 2), xx = lane + 64 * (i & 3);
+      const size_t off = ((size_t)o * a.Ny + g0.x + s * kL + r) * a.Nx + g0.y + xx;
+      Ar[i] = a.obja[off];
+      Pr[i] = a.objp[off];
+      gv[i] = xb[r * 272 + xx];
+    }
+    fence_sched();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 4 * wv + (i >> 2), xx = lane + 64 * (i & 3);
+      const size_t off = ((size_t)o * a.Ny + g0.x + s * kL + r) * a.Nx + g0.y + xx;
+      const float A = Ar[i], ph = Pr[i];
       float sn, cs;
       phase_sincos(ph, &sn, &cs);
-      const float2 gO = cscale(so[o][k], c);
+      const float2 gO = cscale(gv[i], c);
       if (a.d_obja) atomicAdd(a.d_obja + off, fmaf(gO.x, cs, gO.y * sn));   // Re(g_O e^{-iφ})
       if (a.d_objp) {
         float dph = A * fmaf(gO.y, cs, -gO.x * sn);                          // Im(conj(O) g_O)
@@ -396,6 +472,7 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
         atomicAdd(a.d_objp + off, dph);
       }
     }
+    __syncthreads();
   }
 }
 
@@ -415,21 +492,20 @@ __global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
   const int P = a.P;
   constexpr float two_pi_n2 = 6.283185307179586f / (float)kN2;
   float2 fp[16], acc[16];
-  const float2* F = a.Fp + (size_t)p * kN2 + kx;
+  ld16(fp, a.Fp + (size_t)p * kN2 + kx + m.slot * kN, 16 * kN);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    fp[k] = F[(m.slot + 16 * k) * kN];
-    acc[k] = make_float2(0.f, 0.f);
-  }
+  for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
   const float gx = shift_g(kx);
+  float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
+  if (gi < a.n) ld16(nxt, a.t14 + ((size_t)gi * P + p) * kN2 + m.slot * kN + kx, 16 * kN);
   for (int j = gi; j < a.n; j += a.groups) {
     const int sidx = scan_of(a, j);
     const float sy = a.shifts[2 * sidx], sx = a.shifts[2 * sidx + 1];
     const float c = a.coef[(size_t)a.bid[j] * kNCoef + a.ci];
-    const float2* in = a.t14 + ((size_t)j * P + p) * kN2 + m.slot * kN + kx;
     float2 v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = in[16 * r * kN];
+    for (int r = 0; r < 16; ++r) v[r] = nxt[r];
+    if (j + a.groups < a.n) ld16(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2 + m.slot * kN + kx, 16 * kN);
     fft_line<-1, true>(v, m, xb, tw);
     const float2 wx = f3::cis_rev(-sx * gx);
     float sy_acc = 0.f, sim = 0.f;

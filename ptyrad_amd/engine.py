@@ -59,16 +59,16 @@ class LossConfig:
                    bool(sp["state"]), float(sp.get("weight", 0.1)), int(sp.get("ln_order", 1)),
                    bool(pb["state"]), float(pb.get("weight", 0.5)), float(pb.get("dp_pow", 0.2)))
 
-    def to_c(self, grad_scale: float, max_batch: int = 0) -> _lib.LossCfg:
+    def to_c(self, grad_scale: float, max_batch: int = 0, prep: int = 0) -> _lib.LossCfg:
         if self.pacbed_on and not (self.single_on or self.poissn_on):
             # the engine needs one data term: a zero-weight loss_single (adds nothing)
             return _lib.LossCfg(1, 0.0, self.single_q, 0, self.poissn_w, self.poissn_q, self.poissn_eps,
                                 int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale),
-                                int(max_batch))
+                                int(max_batch), int(prep))
         return _lib.LossCfg(int(self.single_on), self.single_w, self.single_q,
                             int(self.poissn_on), self.poissn_w, self.poissn_q, self.poissn_eps,
                             int(self.sparse_on), self.sparse_w, int(self.sparse_n), float(grad_scale),
-                            int(max_batch))
+                            int(max_batch), int(prep))
 
 
 class Plan:
@@ -203,7 +203,7 @@ class Plan:
         return dp_out
 
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
-                          grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None):
+                          grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None, prep=0):
         """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5).
 
         batch_offsets on the host (numpy / list / CPU tensor) let calls larger than the plan's
@@ -232,7 +232,7 @@ class Plan:
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
                                   t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0),
                                   t.get("meas_rows"))
-        cfg = loss_cfg.to_c(grad_scale, max_batch)
+        cfg = loss_cfg.to_c(grad_scale, max_batch, prep)
         g = self._grads(grads)
         _lib.check(self.lib.ptyx_forward_loss_grad(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
@@ -272,6 +272,7 @@ class Plan:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
         idx_t = self._idx(idx)
         b0 = 0
+        prep = _lib.PTYX_PREP_FULL     # the object / probe are prepared once for all the pieces
         while b0 < nb:
             b1 = b0 + 1
             while b1 < nb and off[b1 + 1] - off[b0] <= cap:
@@ -280,7 +281,8 @@ class Plan:
             sub_idx = idx_t[int(off[b0]):int(off[b1])]
             sub_dp = None if dp_out is None else dp_out[int(off[b0]):int(off[b1])]
             self.forward_loss_grad(t, sub_idx, sub_off, loss_cfg, grads, grad_scale=grad_scale,
-                                   loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch)
+                                   loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch, prep=prep)
+            prep = _lib.PTYX_PREP_REUSE
             b0 = b1
         return loss_terms
 

@@ -169,3 +169,21 @@ def test_c1_shape_trajectory_matches_reference():
         assert float(np.sqrt(np.mean((got - ref) ** 2))) < 1e-5, k
     prb = torch.view_as_complex(model.opt_probe.detach()).cpu().numpy()
     assert rel(prb, z["final_probe"]) < 1e-5
+
+
+def test_c5_shape_call_split_by_stripe_capacity(monkeypatch):
+    """A call larger than the stripe engine's per-call capacity (PTYX_STRIPE_MB) is split at
+    mini-batch boundaries; the pieces after the first reuse the first one's object / probe
+    preparation (PTYX_PREP_FULL then PTYX_PREP_REUSE).  Same results as the oracle."""
+    monkeypatch.setenv("PTYX_STRIPE_MB", "12")        # (P ψ⁰ + P T1 + P·O T2) · 512 KiB = 6 MiB a pattern
+    d = config_problem(4, 1, True, seed=13)
+    batches = [np.array([0, 4]), np.array([8, 1]), np.array([5, 2]), np.array([6, 3]), np.array([7])]
+    ks = {}
+    terms, dp, g, plan = run_fused(d, dev(), batches, meas_f16=True, kernels=ks)
+    assert plan.register_capacity == 2 and ks["k_s3"][0] == 5          # five calls (one mini-batch each)
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
