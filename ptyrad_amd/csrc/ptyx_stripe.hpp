@@ -407,7 +407,7 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
       float2 v[16], ob[16];
       ld16(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot, 16);
       fft_line<+1, false>(v, m, xb, tw);
-      ld16(ob, a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);
+      ld16(ob, a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);   // (L2: re-read per p)
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const float2 g = cscale(v[k], inv_n);

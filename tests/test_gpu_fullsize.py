@@ -86,3 +86,53 @@ def test_c2_full_call_properties():
         oterms, _, _ = orc.forward_loss_grad(oa, op, probe_c[None], scan.shifts[b], scan.crop_pos[b], H,
                                              np.ones(1, np.float32), mb, [np.arange(len(b))], LP)
         np.testing.assert_allclose(t1[k], oterms[0], rtol=1e-5, atol=1e-7)
+
+
+def test_c2_geometry_gradients_of_2048_patterns_vs_oracle():
+    """Object / probe / position gradients at the full c2 geometry (1033² object, positions spread
+    over the whole 256² raster) for 64 random mini-batches of 32 (2,048 patterns; the register
+    engine with segments crossing mini-batch and workgroup boundaries) vs the complex64 oracle on
+    the same inputs."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
+    N, S = 128, 256
+    scan = syn.raster_scan(S, S, N, seed=0)
+    Ny, Nx = scan.obj_shape
+    n = S * S
+    rng = np.random.default_rng(11)
+    oa = (1.0 + 0.05 * rng.standard_normal((1, 1, Ny, Nx))).astype(np.float32)
+    op = (0.1 * rng.standard_normal((1, 1, Ny, Nx))).astype(np.float32)
+    probe_c = (syn.stem_probe(N) * np.float32(60.0)).astype(np.complex64)
+    H = syn.fresnel_propagator(N, syn.DX_ANG, 2.0)
+    sel = rng.choice(n, 2048, replace=False)
+    batches = np.array_split(sel, 64)
+    # DPs only for the selected positions (the rest are never read); rows in scan order
+    meas = torch.zeros((n, N, N), device=device)
+    m_sel = rng.random((sel.size, N, N), dtype=np.float32)
+    meas[torch.as_tensor(sel, device=device)] = torch.tensor(m_sel, device=device)
+    t = {"obja": torch.tensor(oa, device=device), "objp": torch.tensor(op, device=device),
+         "probe": torch.view_as_real(torch.tensor(probe_c, device=device)[None]).contiguous(),
+         "shifts": torch.tensor(scan.shifts, device=device), "H": torch.tensor(H, device=device),
+         "occu": torch.ones(1, device=device), "crop_pos": torch.tensor(scan.crop_pos, device=device), "meas": meas}
+    plan = Plan(N, 1, 1, 1, Ny, Nx, n, 2048, shift_probes=True, device=device)
+    grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+    plan.profile_begin()
+    terms = plan.forward_loss_grad(t, np.concatenate(batches).astype(np.int32), batch_offsets(batches),
+                                   LossConfig.from_loss_params(LP), grads, grad_scale=1.0 / 64)
+    torch.cuda.synchronize()
+    assert "k_fused" in plan.profile_end()          # the register engine (k_fused3)
+    # the oracle on the sub-problem: the 2,048 positions re-indexed 0..2047, full object
+    loc = [np.searchsorted(np.sort(sel), b) for b in batches]
+    order = np.sort(sel)
+    m_sorted = np.empty_like(m_sel)
+    m_sorted[np.searchsorted(order, sel)] = m_sel
+    oterms, _, og = orc.forward_loss_grad(oa, op, probe_c[None], scan.shifts[order], scan.crop_pos[order], H,
+                                          np.ones(1, np.float32), m_sorted, loc, LP, cdt=np.complex64,
+                                          grad_scale=1.0 / 64)
+    np.testing.assert_allclose(terms.cpu().numpy(), oterms, rtol=1e-5, atol=1e-7)
+    assert rel(grads["obja"].cpu().numpy(), og["obja"]) < 5e-5
+    assert rel(grads["objp"].cpu().numpy(), og["objp"]) < 5e-5
+    gp = grads["probe"].cpu().numpy()
+    assert rel(gp[..., 0] + 1j * gp[..., 1], og["probe"]) < 5e-5
+    assert rel(grads["shifts"].cpu().numpy()[order], og["shifts"]) < 2e-4
