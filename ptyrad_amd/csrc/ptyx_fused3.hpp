@@ -338,24 +338,32 @@ __device__ __forceinline__ void block_sum4(float (&v)[NV], float* red) {
 // compiler can no longer sink its computation towards a later use, which otherwise keeps every
 // intermediate of a 64-register pass live across barriers and spills.
 __device__ __forceinline__ void pin(float2& v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
+// The same into an accumulation register (AGPR): values parked there between passes (the ψ⁰ park
+// and the segment's probe-gradient slab of PTYX_F3_HOLD) cost one v_accvgpr move per use and no
+// memory traffic.
+__device__ __forceinline__ void pin_a(float2& v) { asm volatile("" : "+a"(v.x), "+a"(v.y)); }
 
-// Software-pipelined pass over the 64 registers in NC chunks: chunk c+1's global loads are
-// issued before chunk c is consumed, and a scheduling barrier after every chunk keeps the
-// compiler from hoisting all 64 loads at once (which would need 128+ extra VGPRs and spill).
+// Software-pipelined pass over the 64 registers in NC chunks: the global loads of chunks
+// c+1 … c+D are in flight while chunk c is consumed, and a scheduling barrier after every chunk
+// keeps the compiler from hoisting all 64 loads at once (which would need 128+ extra VGPRs and
+// spill).  D = PTYX_F3_PIPE.
+#ifndef PTYX_F3_PIPE
+#define PTYX_F3_PIPE 1
+#endif
 template <int NC, class Ld, class Use>
 __device__ __forceinline__ void pipeline(Ld&& ld, Use&& use) {
-  auto cur = ld(std::integral_constant<int, 0>{});
+  constexpr int D = PTYX_F3_PIPE < NC ? PTYX_F3_PIPE : NC - 1 > 0 ? NC - 1 : 1;
+  using T = decltype(ld(std::integral_constant<int, 0>{}));
+  T ring[D + 1];
+  rf::sfor<0, D>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i < NC) ring[i] = ld(std::integral_constant<int, i>{});
+  });
   rf::sfor<0, NC>([&](auto C) {
     constexpr int c = decltype(C)::value;
-    if constexpr (c + 1 < NC) {
-      auto nxt = ld(std::integral_constant<int, c + 1>{});
-      use(C, cur);
-      __builtin_amdgcn_sched_barrier(0);
-      cur = nxt;
-    } else {
-      use(C, cur);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    if constexpr (c + D < NC) ring[(c + D) % (D + 1)] = ld(std::integral_constant<int, c + D>{});
+    use(C, ring[c % (D + 1)]);
+    __builtin_amdgcn_sched_barrier(0);
   });
 }
 struct Ch8 {
@@ -454,8 +462,17 @@ struct Ramp {
 // Per pattern: IFFT · park ψ⁰, ×O · FFT (DP → LDS meanwhile) · loss partial sums, g_Ψ ·
 // IFFT · slot, ×conj(O) · FFT (probe-gradient spectrum) · one pass: segment slab += conj(W) G,
 // position-gradient sums, and v = F(P)·W for the next pattern (F(P) read once per pattern).
+#ifndef PTYX_F3_OCC
+#define PTYX_F3_OCC 2   // workgroups per CU k_fused3 is compiled for
+#endif
+// PTYX_F3_HOLD: ψ⁰ and the segment slab stay in the accumulation registers (AGPRs) of a
+// one-workgroup-per-CU kernel instead of the slot park and the per-pattern slab read-modify-write
+// (256 + 256 KiB of L2 / fabric traffic per pattern).
+#ifndef PTYX_F3_HOLD
+#define PTYX_F3_HOLD 0
+#endif
 template <bool SHIFT, bool SINGLE, int QM>
-__global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
+__global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(F3Args a) {
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
   __shared__ float s_red[4 * 2];
@@ -477,7 +494,16 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
   const float gy = (float)((cd.fixed + 64) & 127) * inv_n;   // ifftshifted grid of this thread's ky
 
   // ---------------------------------------------------------------- prologue: v for the first pattern
+  constexpr bool kHold = PTYX_F3_HOLD != 0;
   float2 v[64];
+  float2 psi0[kHold ? 64 : 1], slab[kHold ? 64 : 1];
+  if constexpr (kHold) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      slab[k] = make_float2(0.f, 0.f);
+      pin_a(slab[k]);
+    }
+  }
   {
     const int tid = rf::opaque(threadIdx.x);
     const int vpk = 8 * tid;
@@ -538,7 +564,12 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const int j = 8 * C + r;
-              if (!PTYX_F3_EXP_NOPARK) st2(v[j], r_slot, vslot, 2048 * j);
+              if constexpr (kHold) {
+                psi0[j] = v[j];
+                pin_a(psi0[j]);
+              } else if (!PTYX_F3_EXP_NOPARK) {
+                st2(v[j], r_slot, vslot, 2048 * j);
+              }
               v[j] = cmul(v[j], t.x[r]);
               pin(v[j]);
             }
@@ -622,7 +653,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
-              t.x[r] = PTYX_F3_EXP_NOPARK ? make_float2(1.f, 0.f) : ld2(r_slot, vslot, 2048 * j);
+              t.x[r] = (kHold || PTYX_F3_EXP_NOPARK) ? make_float2(1.f, 0.f) : ld2(r_slot, vslot, 2048 * j);
               t.y[r] = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : ld2(r_obj, vobj, ostr * j);
             }
             return t;
@@ -632,7 +663,8 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
               const float2 gv = cscale(v[j], inv_n);
-              if (!PTYX_F3_EXP_NOSLOT) st2_stream(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+              const float2 ps = kHold ? psi0[kHold ? j : 0] : t.x[r];
+              if (!PTYX_F3_EXP_NOSLOT) st2_stream(cmulc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
               v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
               pin(v[j]);
             }
@@ -646,6 +678,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
     // false) the same pass runs without the FFT and its slab / sums are never used.
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
     const bool first = pat == p0 || a.bid[pat - 1] != p.m;   // (uniform)
+    const bool last = pat == p1 - 1 || a.bid[pat + 1] != p.m;   // (uniform; PTYX_F3_HOLD flushes the slab)
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
@@ -667,7 +700,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
               t.x[r] = ld2(r_fpk, vpk, 2048 * k);
-              t.y[r] = PTYX_F3_EXP_NOSLAB ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * k);
+              t.y[r] = (kHold || PTYX_F3_EXP_NOSLAB) ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * k);
             }
             return t;
           },
@@ -681,7 +714,12 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
               const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
               sim += im;
               kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
-              if (!PTYX_F3_EXP_NOSLAB) st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
+              if constexpr (kHold) {
+                slab[kHold ? k : 0] = cadd(slab[kHold ? k : 0], cmulc(v[k], W));   // + conj(W) G (unit)
+                pin_a(slab[kHold ? k : 0]);
+              } else if (!PTYX_F3_EXP_NOSLAB) {
+                st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
+              }
               v[k] = cmul(t.x[r], cmul(An, rn.B[r]));                 // next pattern: F(P)·W_next
               pin(v[k]);
             }
@@ -706,7 +744,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
-              t.y[r] = ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
+              t.y[r] = kHold ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
             }
             return t;
           },
@@ -714,11 +752,27 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
-              st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (unit, R layout)
+              if constexpr (kHold) {
+                slab[kHold ? j : 0] = cadd(slab[kHold ? j : 0], v[j]);   // + h (unit, R layout)
+                pin_a(slab[kHold ? j : 0]);
+              } else {
+                st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (unit, R layout)
+              }
               v[j] = t.x[r];                                       // next pattern: the probe
               pin(v[j]);
             }
           });
+    }
+    if constexpr (kHold) {
+      if (last) {   // the segment is complete: its slab is written once
+        const int vpk = rf::opaque(8 * tid);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+          st2(slab[k], r_slab_st, vpk, 2048 * k);
+          slab[k] = make_float2(0.f, 0.f);
+          pin_a(slab[k]);
+        }
+      }
     }
     F3PH(11);
 #if PTYX_F3_PHASES

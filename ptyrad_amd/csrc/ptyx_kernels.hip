@@ -655,6 +655,7 @@ struct ptyx_plan {
   float2* pcoef = nullptr;
   // k_fused3 (N = 128, single mode, f32 DPs): register-resident FFT, 2 workgroups per CU
   int nwg3 = 0;
+  size_t dyn3 = 0;            // extra dynamic LDS per k_fused3 workgroup (PTYX_F3_DYNLDS: occupancy experiments)
   float2* fpk = nullptr;      // packed probe spectrum / probe
   float2* oc = nullptr;       // A e^{iφ}
   double* pref = nullptr;     // per-row prefix sums of |φ|^n (loss_sparse)
@@ -839,7 +840,10 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     long long mb = std::min<long long>(16384, (long long)(free_b / 4 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_STRIPE_MB")) mb = std::atoll(e);
     const char* ppsi = std::getenv("PTYX_S_PSI0");
-    const bool park = !(ppsi && ppsi[0] == '0');   // measured: parking ψ⁰ beats recomputing it in P4
+    // measured (profiles/r02/r02k_*): one object mode recomputes ψ⁰ in P4 (c5 221 k vs 205 k
+    // patterns/s: the park's write in P2 costs more than the row IFFT); two object modes park it
+    // (c3 66.0 k vs 59.9 k: P4 with the extra transform spills)
+    const bool park = ppsi ? ppsi[0] != '0' : d.O > 1;
     const long long per = (long long)((park ? 2 : 1) * d.P + d.P * d.O) * (long long)N2 * (long long)sizeof(float2);
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / per);
     if (cap >= 1) {
@@ -884,14 +888,15 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2));
     const char* f3 = std::getenv("PTYX_FUSED3");
+    if (const char* dl = std::getenv("PTYX_F3_DYNLDS")) pl->dyn3 = (size_t)std::max(0LL, std::atoll(dl));
     int occ3 = 0;
     if (!(f3 && f3[0] == '0') && cap > 0 &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, 0) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, pl->dyn3) == hipSuccess &&
         occ3 > 0) {
       int o2 = 0;
       for (auto kf : {f3::k_fused3<true, true, 2>, f3::k_fused3<true, false, 2>, f3::k_fused3<false, true, 0>,
                       f3::k_fused3<false, true, 2>, f3::k_fused3<false, false, 2>})
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, pl->dyn3) == hipSuccess) occ3 = std::min(occ3, o2);
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
       // segment ids = mini-batches + workgroups of a call; sized for a mean mini-batch of ≥ 8
       // patterns (PTYX_SEG_DIV); calls with more segments take the two-pass engine
@@ -1156,13 +1161,13 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
     if (a.shift) {
-      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
-      else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, 0, st, f);
-      else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, 0, st, f);
+      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, pl->dyn3, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, pl->dyn3, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, pl->dyn3, st, f);
     } else {
-      if (half) hipLaunchKernelGGL((f3::k_fused3<false, true, 0>), gr, bl, 0, st, f);
-      else if (single) hipLaunchKernelGGL((f3::k_fused3<false, true, 2>), gr, bl, 0, st, f);
-      else hipLaunchKernelGGL((f3::k_fused3<false, false, 2>), gr, bl, 0, st, f);
+      if (half) hipLaunchKernelGGL((f3::k_fused3<false, true, 0>), gr, bl, pl->dyn3, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<false, true, 2>), gr, bl, pl->dyn3, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<false, false, 2>), gr, bl, pl->dyn3, st, f);
     }
   }
   int rc = launch_status("k_fused3 launch");
@@ -1276,14 +1281,14 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   {
     ProfScope ps(pl, kKS3, st);
     const dim3 gr(n, kStripes);
-    // Ψ held in registers for P·O ≤ 2; above that the column FFTs are redone (measured faster than
-    // holding 3-4 modes at one workgroup per CU; PTYX_S3_HOLD=1 holds up to 4)
+    // Ψ of the first min(P·O, PTYX_S3_HOLD) modes stays in registers between k_s3's two sweeps,
+    // the other modes' column FFTs are redone (default 4: fits two workgroups per CU)
     const char* hl = std::getenv("PTYX_S3_HOLD");
-    const int hold_max = (hl && hl[0] == '1') ? 4 : 2;
-    const int PO = P * O <= hold_max ? P * O : 99;
+    const int hold_max = hl ? std::max(0, std::min(4, std::atoi(hl))) : 4;
+    const int H = std::min(P * O, hold_max);
     const bool half = single && s.q == 0.5f;
 #define PTYX_S3(SG, QM)                                                                                  \
-  switch (PO) {                                                                                        \
+  switch (H) {                                                                                         \
     case 1: hipLaunchKernelGGL((k_s3<SG, QM, 1>), gr, bl, 0, st, s); break;                             \
     case 2: hipLaunchKernelGGL((k_s3<SG, QM, 2>), gr, bl, 0, st, s); break;                             \
     case 3: hipLaunchKernelGGL((k_s3<SG, QM, 3>), gr, bl, 0, st, s); break;                             \

@@ -18,7 +18,8 @@
 //   P3  columns  per (p,o): column FFT → Ψ = ·/N;  I = Σ occ|Ψ|² + 1e-10 (registers);  DP read,
 //                loss partial sums, u = ∂ℓ/∂I per UNIT mini-batch coefficient;  per (p,o):
 //                g_Ψ = 2 occ Ψ u → column IFFT                                     → T23[p,o]
-//                (Ψ of every mode is held in registers when P·O ≤ 4, else its column FFT is redone)
+//                (Ψ of the first PTYX_S3_HOLD modes stays in registers, the others' column FFTs
+//                are redone)
 //   --- k_finalize: the mini-batch NRMSE coefficients c_m (losses.py:45-47) ---
 //   P4  rows     per p: per o: row IFFT → g/N;  slot_o += g·conj(ψ⁰_p);  gP += g·conj(O_o);
 //                row FFT(gP) → T4[p] (= T1's storage);  then dA, dφ (+ the sparse sign term)
@@ -114,6 +115,35 @@ __device__ __forceinline__ void ld16(float2 (&v)[16], const float2* p, int strid
   fence_sched();
 }
 
+// The 16 points of a thread in one field through a buffer resource: the field base is uniform
+// (SGPRs), the thread's byte offset one opaque VGPR, the per-point offsets constants.  With plain
+// pointers every point of a column access (32 KiB apart, beyond the immediate range) needs its
+// own 64-bit address, and those get hoisted out of the mode / pattern loops: 32 VGPRs per array,
+// the spills of k_s4.
+constexpr unsigned kFieldBytes = kN2 * 8;
+constexpr int kColStride = kL * kN * 8;   // column pass: a thread's points are 16 rows apart
+constexpr int kRowStride = kL * 8;        // row pass: 16 columns apart
+template <int STRIDE>
+__device__ __forceinline__ void ldb(float2 (&v)[16], const float2* base, unsigned bytes, int voff) {
+  const f3::Rsrc r = f3::rsrc(base, bytes);
+  const int vo = opq(voff);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = f3::ld2(r, vo, k * STRIDE);
+  fence_sched();
+}
+template <int STRIDE>
+__device__ __forceinline__ void stb(const float2 (&v)[16], float2* base, unsigned bytes, int voff) {
+  const f3::Rsrc r = f3::rsrc(base, bytes);
+  const int vo = opq(voff);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) f3::st2(v[k], r, vo, k * STRIDE);
+}
+// object window of pattern j (origin g0), mode o: base and byte size
+__device__ __forceinline__ const float2* win_base(const SArgs& a, int o, int2 g0) {
+  return a.oc + ((size_t)o * a.Ny + g0.x) * a.Nx + g0.y;
+}
+__device__ __forceinline__ unsigned win_bytes(const SArgs& a) { return (unsigned)(((kN - 1) * a.Nx + kN) * 8); }
+
 // 256-point DFT of every line of the stripe (DIR -1 forward, +1 unnormalised inverse).
 template <int DIR, bool COL>
 __device__ __forceinline__ void fft_line(float2 (&v)[16], Map m, float2* xb, const float2* tw) {
@@ -162,15 +192,13 @@ __global__ __launch_bounds__(256, 2) void k_s1(SArgs a) {
   const Map m = map_of<true>(opq(threadIdx.x));
   const int kx = s * kL + m.line;
   const float sy = a.shifts[2 * scan_of(a, j)];
-  const float2* F = a.Fp + (size_t)p * kN2 + kx;
+  const int vcol = (m.slot * kN + kx) * 8;
   float2 v[16];
-  ld16(v, F + m.slot * kN, 16 * kN);
+  ldb<kColStride>(v, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sy * shift_g(m.slot + 16 * r)));
   fft_line<+1, true>(v, m, xb, tw);
-  float2* out = a.t14 + ((size_t)j * a.P + p) * kN2 + kx;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) out[(m.slot + 16 * k) * kN] = v[k];
+  stb<kColStride>(v, a.t14 + ((size_t)j * a.P + p) * kN2, kFieldBytes, vcol);
 }
 
 // ---------------------------------------------------------------------------------- P2
@@ -191,42 +219,37 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
   const int P = a.P;
   constexpr float inv_n2 = 1.0f / kN2;
   // this stripe of the object window (O_o does not depend on the probe mode: loaded once)
+  const int vrow = (y * kN + m.slot) * 8, vwin = (y * a.Nx + m.slot) * 8;
   float2 ob[O_][16];
 #pragma unroll
-  for (int o = 0; o < O_; ++o) ld16(ob[o], a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);
+  for (int o = 0; o < O_; ++o) ldb<kRowStride>(ob[o], win_base(a, o, g0), win_bytes(a), vwin);
   // the next probe mode's T1 rows are prefetched during this mode's transforms (O = 1: the
   // registers of a second object mode would not fit beside them)
   constexpr bool PREF = O_ == 1;
   float2 nxt[16];
-  if constexpr (PREF) ld16(nxt, a.t14 + (size_t)j * P * kN2 + y * kN + m.slot, 16);
+  if constexpr (PREF) ldb<kRowStride>(nxt, a.t14 + (size_t)j * P * kN2, kFieldBytes, vrow);
   for (int p = 0; p < P; ++p) {
     float2 v[16];
     if constexpr (PREF) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = nxt[r];
-      if (p + 1 < P) ld16(nxt, a.t14 + ((size_t)j * P + p + 1) * kN2 + y * kN + m.slot, 16);
+      if (p + 1 < P) ldb<kRowStride>(nxt, a.t14 + ((size_t)j * P + p + 1) * kN2, kFieldBytes, vrow);
     } else {
-      ld16(v, a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
+      ldb<kRowStride>(v, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
     fft_line<+1, false>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n2);
-    if (a.psi0) {
-      float2* ps = a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) ps[16 * k] = v[k];
-    }
+    if (a.psi0) stb<kRowStride>(v, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
       float2 u[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) u[k] = cmul(v[k], ob[o][k]);
       fft_line<-1, false>(u, m, xb, tw);
-      float2* out = a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[16 * r] = u[r];
+      stb<kRowStride>(u, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
     });
   }
   // loss_sparse (losses.py:101): Σ |φ|ⁿ over this stripe of the window, per object mode
@@ -257,9 +280,13 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
 
 // ---------------------------------------------------------------------------------- P3
 // grid (n, kStripes): columns kx of every mode: column FFT → Ψ, intensity, loss, g_Ψ → column IFFT.
-// HOLD > 0 (= P·O): every mode's Ψ stays in registers between the two sweeps; 0: recomputed.
+// The first HOLD modes keep Ψ in registers between the two sweeps; the column FFTs of the others
+// (P·O − HOLD of them) are redone in the second sweep.
+#ifndef PTYX_S3_LB1_FROM
+#define PTYX_S3_LB1_FROM 99   // HOLD at or above which k_s3 is compiled for one workgroup per CU
+#endif
 template <bool SINGLE, int QM, int HOLD>
-__global__ __launch_bounds__(256, HOLD >= 4 ? 1 : 2) void k_s3(SArgs a) {
+__global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : 2) void k_s3(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
@@ -268,12 +295,13 @@ __global__ __launch_bounds__(256, HOLD >= 4 ? 1 : 2) void k_s3(SArgs a) {
   const int j = blockIdx.x, s = blockIdx.y;
   const Map m = map_of<true>(opq(threadIdx.x));
   const int kx = s * kL + m.line;
-  const int PO = HOLD > 0 ? HOLD : a.P * a.O;
+  const int PO = a.P * a.O;   // ≥ HOLD (host)
   const int O = a.O;
   constexpr float inv_n = 1.0f / kN;
-  float2* base = a.t23 + (size_t)j * PO * kN2 + kx;
+  float2* base = a.t23 + (size_t)j * PO * kN2;
+  const int vcol = (m.slot * kN + kx) * 8;
   auto far_field = [&](int q, float2 (&v)[16]) {
-    ld16(v, base + (size_t)q * kN2 + m.slot * kN, 16 * kN);
+    ldb<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n);
@@ -282,22 +310,19 @@ __global__ __launch_bounds__(256, HOLD >= 4 ? 1 : 2) void k_s3(SArgs a) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) I[k] = 0.f;
   float2 hold[HOLD > 0 ? HOLD : 1][16];
-  if constexpr (HOLD > 0) {
-    rf::sfor<0, HOLD>([&](auto QQ) {
-      constexpr int q = decltype(QQ)::value;
-      far_field(q, hold[q]);
-      const float occ = a.occu[q % O];
+  rf::sfor<0, HOLD>([&](auto QQ) {
+    constexpr int q = decltype(QQ)::value;
+    far_field(q, hold[q]);
+    const float occ = a.occu[q % O];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(hold[q][k]), I[k]);
-    });
-  } else {
-    for (int q = 0; q < PO; ++q) {
-      float2 v[16];
-      far_field(q, v);
-      const float occ = a.occu[q % O];
+    for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(hold[q][k]), I[k]);
+  });
+  for (int q = HOLD; q < PO; ++q) {
+    float2 v[16];
+    far_field(q, v);
+    const float occ = a.occu[q % O];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(v[k]), I[k]);
-    }
+    for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(v[k]), I[k]);
   }
   // loss at every point of the stripe (fftshifted DP index), unit-coefficient ∂ℓ/∂I
   const int sidx = scan_of(a, j);
@@ -339,22 +364,17 @@ __global__ __launch_bounds__(256, HOLD >= 4 ? 1 : 2) void k_s3(SArgs a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], c * u[k]);
     fft_line<+1, true>(v, m, xb, tw);
-    float2* out = base + (size_t)q * kN2 + m.slot * kN;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) out[16 * k * kN] = v[k];
+    stb<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);
   };
-  if constexpr (HOLD > 0) {
-    rf::sfor<0, HOLD>([&](auto QQ) {
-      constexpr int q = decltype(QQ)::value;
-      back(q, hold[q]);
-    });
-  } else {
-    for (int q = 0; q < PO; ++q) {
-      float2 v[16];
-      far_field(q, v);
-      back(q, v);
-    }
+  for (int q = HOLD; q < PO; ++q) {
+    float2 v[16];
+    far_field(q, v);
+    back(q, v);
   }
+  rf::sfor<0, HOLD>([&](auto QQ) {
+    constexpr int q = decltype(QQ)::value;
+    back(q, hold[q]);
+  });
 }
 
 // ---------------------------------------------------------------------------------- P4
@@ -368,6 +388,10 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
   // two object-mode slot accumulators fit the registers of two workgroups per CU
   constexpr bool GP_LDS = O_ > 1;
   __shared__ float2 gpl[GP_LDS ? 16 * 256 : 1];
+  // O_ = 1: the object stripe is read from HBM once and kept in LDS ([k][thread], each thread
+  // reads back only its own points: no barrier) for the P probe modes
+  constexpr bool OB_LDS = O_ == 1;
+  __shared__ float2 obl[OB_LDS ? 16 * 256 : 1];
   load_tw(tw, a.twg);
   __syncthreads();
   const int j = blockIdx.x, s = blockIdx.y;
@@ -385,12 +409,19 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
   for (int o = 0; o < O_; ++o)
 #pragma unroll
     for (int k = 0; k < 16; ++k) so[o][k] = make_float2(0.f, 0.f);
+  const int vrow = (y * kN + m.slot) * 8, vwin = (y * a.Nx + m.slot) * 8;
+  if constexpr (OB_LDS) {
+    float2 ob[16];
+    ldb<kRowStride>(ob, win_base(a, 0, g0), win_bytes(a), vwin);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) obl[k * 256 + threadIdx.x] = ob[k];
+  }
   for (int p = 0; p < P; ++p) {
     float2 psi[16];
     if (a.psi0) {
-      ld16(psi, a.psi0 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
+      ldb<kRowStride>(psi, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     } else {   // ψ⁰_p = F⁻¹_x(wx · T1_p)/N² again: one row transform instead of a parked field
-      ld16(psi, a.t14 + ((size_t)j * P + p) * kN2 + y * kN + m.slot, 16);
+      ldb<kRowStride>(psi, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
 #pragma unroll
       for (int r = 0; r < 16; ++r) psi[r] = cmul(psi[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
       fft_line<+1, false>(psi, m, xb, tw);
@@ -405,9 +436,14 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
       float2 v[16], ob[16];
-      ld16(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2 + y * kN + m.slot, 16);
+      ldb<kRowStride>(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
       fft_line<+1, false>(v, m, xb, tw);
-      ld16(ob, a.oc + ((size_t)o * a.Ny + g0.x + y) * a.Nx + g0.y + m.slot, 16);   // (L2: re-read per p)
+      if constexpr (OB_LDS) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ob[k] = obl[k * 256 + threadIdx.x];
+      } else {
+        ldb<kRowStride>(ob, win_base(a, o, g0), win_bytes(a), vwin);   // (L2: re-read per p)
+      }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const float2 g = cscale(v[k], inv_n);
@@ -426,9 +462,7 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) gq[k] = GP_LDS ? gpl[k * 256 + threadIdx.x] : gp[GP_LDS ? 0 : k];
       fft_line<-1, false>(gq, m, xb, tw);
-      float2* out = a.t4 + ((size_t)j * P + p) * kN2 + y * kN + m.slot;   // over T1_p's rows (read above)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[16 * r] = gq[r];
+      stb<kRowStride>(gq, a.t4 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);   // over T1_p's rows (read above)
     }
   }
   if (!a.d_obja && !a.d_objp) return;
@@ -491,13 +525,14 @@ __global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
   const int kx = s * kL + m.line;
   const int P = a.P;
   constexpr float two_pi_n2 = 6.283185307179586f / (float)kN2;
+  const int vcol = (m.slot * kN + kx) * 8;
   float2 fp[16], acc[16];
-  ld16(fp, a.Fp + (size_t)p * kN2 + kx + m.slot * kN, 16 * kN);
+  ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
   const float gx = shift_g(kx);
   float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
-  if (gi < a.n) ld16(nxt, a.t14 + ((size_t)gi * P + p) * kN2 + m.slot * kN + kx, 16 * kN);
+  if (gi < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
   for (int j = gi; j < a.n; j += a.groups) {
     const int sidx = scan_of(a, j);
     const float sy = a.shifts[2 * sidx], sx = a.shifts[2 * sidx + 1];
@@ -505,7 +540,7 @@ __global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = nxt[r];
-    if (j + a.groups < a.n) ld16(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2 + m.slot * kN + kx, 16 * kN);
+    if (j + a.groups < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
     const float2 wx = f3::cis_rev(-sx * gx);
     float sy_acc = 0.f, sim = 0.f;
@@ -530,9 +565,7 @@ __global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
       o[1] = ds[1] * c * two_pi_n2;
     }
   }
-  float2* out = a.slabpart + ((size_t)gi * P + p) * kN2 + kx;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) out[(m.slot + 16 * k) * kN] = acc[k];
+  stb<kColStride>(acc, a.slabpart + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
 }
 
 // ---------------------------------------------------------------------------------- small kernels

@@ -60,6 +60,16 @@ def test_c5_shape_p4_fp16_dps_vs_oracle():
     check_against_oracle(d, [np.array([2, 6, 7, 3]), np.array([8, 0])], meas_f16=True)
 
 
+@pytest.mark.parametrize("hold,park", [("0", "1"), ("1", "1"), ("3", "0"), ("4", "1")])
+def test_stripe_mode_hold_and_psi0_variants(monkeypatch, hold, park):
+    """k_s3 with the first `hold` of P·O = 6 modes held in registers (the rest recomputed), and
+    k_s4 with ψ⁰ parked (1) or recomputed from T1 (0): all the same gradients."""
+    monkeypatch.setenv("PTYX_S3_HOLD", hold)
+    monkeypatch.setenv("PTYX_S_PSI0", park)
+    d = config_problem(3, 2, False, seed=13)
+    check_against_oracle(d, [np.array([1, 3, 4]), np.array([7, 2, 0])], meas_f16=False)
+
+
 # ------------------------------------------------------------------ rank-local measurements
 def test_rank_local_measurement_block_equals_full_stack():
     """PtychoHIP holding only the DPs of the positions it uses (rows in a shuffled order, via
