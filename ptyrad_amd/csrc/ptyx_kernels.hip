@@ -661,6 +661,13 @@ struct ptyx_plan {
   double* pref = nullptr;     // per-row prefix sums of |φ|^n (loss_sparse)
   float2* segslab = nullptr;  // per-segment unit probe-gradient spectra, packed
   int* segbid = nullptr;      // batch of each segment id (-1 unused)
+  // k_obj_gather candidate bins (tile of each pattern's window origin), per call
+  int nbins = 0;
+  int* bcnt = nullptr;        // (nbins) counts
+  int* boff = nullptr;        // (nbins + 1) offsets
+  int* bcur = nullptr;        // (nbins) fill cursors
+  int* bkey = nullptr;        // (max_patterns) bin of each pattern
+  int* blist = nullptr;       // (max_patterns) patterns by bin
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
   float2* hpk = nullptr;      // k_fused3ms: K-packed propagator
@@ -755,6 +762,18 @@ static int dalloc(ptyx_plan* pl, T** p, size_t count) {
   pl->allocs.push_back(q);
   pl->ws_bytes += count * sizeof(T);
   *p = static_cast<T*>(q);
+  return PTYX_OK;
+}
+
+// k_obj_gather's pattern bins: one per object tile
+static int alloc_bins(ptyx_plan* pl) {
+  const ptyx_dims& d = pl->d;
+  pl->nbins = ((d.Nx + kGTX - 1) / kGTX) * ((d.Ny + kGTY - 1) / kGTY);
+  int rc;
+  if ((rc = dalloc(pl, &pl->bcnt, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->boff, (size_t)pl->nbins + 1)) ||
+      (rc = dalloc(pl, &pl->bcur, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->bkey, (size_t)d.max_patterns)) ||
+      (rc = dalloc(pl, &pl->blist, (size_t)d.max_patterns)))
+    return rc;
   return PTYX_OK;
 }
 
@@ -911,7 +930,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
           (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
-          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2))) {
+          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2)) || (rc = alloc_bins(pl))) {
         free_plan(pl);
         return rc;
       }
@@ -945,7 +964,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
           (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
-          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2))) {
+          (rc = dalloc(pl, &pl->segpart, (size_t)f3::kSegSplit * N2)) || (rc = alloc_bins(pl))) {
         free_plan(pl);
         return rc;
       }
@@ -1188,11 +1207,32 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   if ((rc = launch_status("k_finalize launch"))) return rc;
   if (gz.d_obja || gz.d_objp) {
+    // candidate bins of the gather (PTYX_GATHER_SCAN=1: every tile scans every pattern instead)
+    const char* gs = std::getenv("PTYX_GATHER_SCAN");
+    const bool binned = !(gs && gs[0] == '1');
+    if (binned) {
+      ProfScope ps(pl, kKTable, st);
+      const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
+      hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
+      if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+      const dim3 gn((a.n_idx + 255) / 256);
+      hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
+      hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
+      hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
+      hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
+    }
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
+    if (binned) {
+      g.boff = pl->boff;
+      g.blist = pl->blist;
+    }
     g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse ? cfg->sparse_n : 1;
     g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
     const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    // fewer than 64 candidates per tile on average (c4's 8,192-pattern calls over 13,340 tiles:
+    // ≈ 17): 4 waves a tile instead of kGWaves
+    const bool sparse_tiles = binned && (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
     ProfScope ps(pl, kKGather, st);
     const size_t plane = (size_t)d.Ny * d.Nx;
     g.nz = Nz;
@@ -1203,7 +1243,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
       g.objp = a.objp + z * plane;
       g.d_obja = gz.d_obja ? gz.d_obja + z * plane : nullptr;
       g.d_objp = gz.d_objp ? gz.d_objp + z * plane : nullptr;
-      hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, true, 4>), dim3(tiles), dim3(64 * 4), 0, st, g);
+      else hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
     }
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
@@ -1282,9 +1323,10 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKS3, st);
     const dim3 gr(n, kStripes);
     // Ψ of the first min(P·O, PTYX_S3_HOLD) modes stays in registers between k_s3's two sweeps,
-    // the other modes' column FFTs are redone (default 4: fits two workgroups per CU)
+    // the other modes' column FFTs are redone.  Default (profiles/r02/ab/r02n_*): 2 of P·O ≤ 4
+    // (c5: three workgroups per CU beat the saved re-reads), 4 above (c3)
     const char* hl = std::getenv("PTYX_S3_HOLD");
-    const int hold_max = hl ? std::max(0, std::min(4, std::atoi(hl))) : 4;
+    const int hold_max = hl ? std::max(0, std::min(4, std::atoi(hl))) : (P * O <= 4 ? 2 : 4);
     const int H = std::min(P * O, hold_max);
     const bool half = single && s.q == 0.5f;
 #define PTYX_S3(SG, QM)                                                                                  \
@@ -1322,8 +1364,11 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKS4, st);
     SArgs s4 = s;
     s4.t4 = tail ? pl->st14 : nullptr;   // no probe / position gradient: skip the gP transform
-    if (O == 1) hipLaunchKernelGGL(k_s4<1>, dim3(n, kStripes), bl, 0, st, s4);
-    else hipLaunchKernelGGL(k_s4<2>, dim3(n, kStripes), bl, 0, st, s4);
+    const bool park = s4.psi0 != nullptr;
+    if (O == 1 && park) hipLaunchKernelGGL((k_s4<1, true>), dim3(n, kStripes), bl, 0, st, s4);
+    else if (O == 1) hipLaunchKernelGGL((k_s4<1, false>), dim3(n, kStripes), bl, 0, st, s4);
+    else if (park) hipLaunchKernelGGL((k_s4<2, true>), dim3(n, kStripes), bl, 0, st, s4);
+    else hipLaunchKernelGGL((k_s4<2, false>), dim3(n, kStripes), bl, 0, st, s4);
   }
   if ((rc = launch_status("k_s4 launch"))) return rc;
   if (!tail) return PTYX_OK;

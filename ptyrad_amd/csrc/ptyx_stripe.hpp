@@ -49,6 +49,26 @@ constexpr int kStripes = kN / kL;      // 16
 constexpr int kXElems = kL * 272;      // LDS exchange buffer (float2), row stride padded 256 → 272
 constexpr int kMaxO = 2;
 
+// workgroups per CU each pass is compiled for (its register budget: 512 / (4·WG) VGPRs per lane)
+#ifndef PTYX_S1_WG
+#define PTYX_S1_WG 2
+#endif
+#ifndef PTYX_S2_WG
+#define PTYX_S2_WG 2
+#endif
+#ifndef PTYX_S3_WG
+#define PTYX_S3_WG 2
+#endif
+#ifndef PTYX_S3_WG0   // k_s3 without held modes (recomputes every column FFT)
+#define PTYX_S3_WG0 2
+#endif
+#ifndef PTYX_S4_WG
+#define PTYX_S4_WG 2
+#endif
+#ifndef PTYX_S5_WG
+#define PTYX_S5_WG 2
+#endif
+
 struct SArgs {
   int n, P, O, Ny, Nx, n_scans, meas_f16;
   const int* idx;        // scan index per pattern
@@ -102,6 +122,10 @@ __device__ __forceinline__ int opq(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+__device__ __forceinline__ float opqf(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 // Scheduling fence: everything above is issued before anything below.  Used after a batch of
 // loads so that the 16 loads of a register array are all in flight before the first use (left
@@ -148,8 +172,11 @@ __device__ __forceinline__ unsigned win_bytes(const SArgs& a) { return (unsigned
 template <int DIR, bool COL>
 __device__ __forceinline__ void fft_line(float2 (&v)[16], Map m, float2* xb, const float2* tw) {
   float2 w[15];
+  // (an opaque slot: the compiler would otherwise hoist these 30 loop-invariant registers out of
+  // the mode / pattern loops of the calling pass)
+  const int sl = opq(m.slot);
 #pragma unroll
-  for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = tw[(m.slot * k2) & 255];
+  for (int k2 = 1; k2 < 16; ++k2) w[k2 - 1] = tw[(sl * k2) & 255];
   fence_sched();
   rf::dft<16, DIR>(v);   // over n2: v[k2]
 #pragma unroll
@@ -183,7 +210,7 @@ __device__ __forceinline__ void bsum(float (&v)[NV], float* red) {
 
 // ---------------------------------------------------------------------------------- P1
 // grid (n, kStripes, P): columns kx of F(P_p)·wy → column IFFT → T1[j][p]
-__global__ __launch_bounds__(256, 2) void k_s1(SArgs a) {
+__global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   load_tw(tw, a.twg);
@@ -204,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void k_s1(SArgs a) {
 // ---------------------------------------------------------------------------------- P2
 // grid (n, kStripes): rows y of every probe mode: ×wx → row IFFT → ψ⁰ (PSI0); ×O_o → row FFT → T2
 template <int O_>
-__global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
+__global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[4 * kMaxO];
@@ -238,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
       ldb<kRowStride>(v, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
+    for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-opqf(sx) * shift_g(m.slot + 16 * r)));
     fft_line<+1, false>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n2);
@@ -286,7 +313,7 @@ __global__ __launch_bounds__(256, 2) void k_s2(SArgs a) {
 #define PTYX_S3_LB1_FROM 99   // HOLD at or above which k_s3 is compiled for one workgroup per CU
 #endif
 template <bool SINGLE, int QM, int HOLD>
-__global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : 2) void k_s3(SArgs a) {
+__global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : HOLD == 0 ? PTYX_S3_WG0 : PTYX_S3_WG) void k_s3(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
@@ -380,8 +407,11 @@ __global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : 2) void k_s3(SA
 // ---------------------------------------------------------------------------------- P4
 // grid (n, kStripes): rows y: per p: per o: row IFFT → g;  slot_o += g conj(ψ⁰_p);
 // gP += g conj(O_o);  row FFT(gP) → T4.  Then the object gradient (× c_m) by f32 atomics.
-template <int O_>
-__global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
+// PARK: ψ⁰ was parked by P2 (read once per probe mode; reading it after each object mode's
+// transform instead, so that it is not live across the FFTs, measured slower: c3 k_s4 76 → 99 ms);
+// else recomputed from T1 (one row IFFT per probe mode).
+template <int O_, bool PARK>
+__global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   // O_ = 2: the per-probe-mode accumulator gP lives in LDS ([k][thread], conflict free), so the
@@ -417,16 +447,16 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
     for (int k = 0; k < 16; ++k) obl[k * 256 + threadIdx.x] = ob[k];
   }
   for (int p = 0; p < P; ++p) {
-    float2 psi[16];
-    if (a.psi0) {
-      ldb<kRowStride>(psi, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+    float2 psr[16];
+    if constexpr (PARK) {
+      ldb<kRowStride>(psr, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     } else {   // ψ⁰_p = F⁻¹_x(wx · T1_p)/N² again: one row transform instead of a parked field
-      ldb<kRowStride>(psi, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+      ldb<kRowStride>(psr, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) psi[r] = cmul(psi[r], f3::cis_rev(-sx * shift_g(m.slot + 16 * r)));
-      fft_line<+1, false>(psi, m, xb, tw);
+      for (int r = 0; r < 16; ++r) psr[r] = cmul(psr[r], f3::cis_rev(-opqf(sx) * shift_g(m.slot + 16 * r)));
+      fft_line<+1, false>(psr, m, xb, tw);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) psi[k] = cscale(psi[k], inv_n2);
+      for (int k = 0; k < 16; ++k) psr[k] = cscale(psr[k], inv_n2);
     }
     float2 gp[GP_LDS ? 1 : 16];
     if constexpr (!GP_LDS) {
@@ -438,9 +468,11 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
       float2 v[16], ob[16];
       ldb<kRowStride>(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
       fft_line<+1, false>(v, m, xb, tw);
+      const float2(&psi)[16] = psr;
       if constexpr (OB_LDS) {
+        const int t = opq(threadIdx.x);   // (not hoisted out of the p loop: 32 registers)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) ob[k] = obl[k * 256 + threadIdx.x];
+        for (int k = 0; k < 16; ++k) ob[k] = obl[k * 256 + t];
       } else {
         ldb<kRowStride>(ob, win_base(a, o, g0), win_bytes(a), vwin);   // (L2: re-read per p)
       }
@@ -514,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void k_s4(SArgs a) {
 // grid (kStripes, P, groups): block (s, p, g) sweeps patterns g, g + groups, ...: column FFT of
 // T4[p] → G;  slab += c_m conj(W_b) G (kept in registers across the sweep);  position-gradient
 // partials per pattern.  The slab stripe is written once at the end (k_slab_reduce sums groups).
-__global__ __launch_bounds__(256, 2) void k_s5(SArgs a) {
+__global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];

@@ -185,7 +185,8 @@ def test_c5_shape_call_split_by_stripe_capacity(monkeypatch):
     """A call larger than the stripe engine's per-call capacity (PTYX_STRIPE_MB) is split at
     mini-batch boundaries; the pieces after the first reuse the first one's object / probe
     preparation (PTYX_PREP_FULL then PTYX_PREP_REUSE).  Same results as the oracle."""
-    monkeypatch.setenv("PTYX_STRIPE_MB", "12")        # (P ψ⁰ + P T1 + P·O T2) · 512 KiB = 6 MiB a pattern
+    monkeypatch.setenv("PTYX_STRIPE_MB", "8")         # (P T1 + P·O T2) · 512 KiB = 4 MiB a pattern (O = 1:
+                                                      # ψ⁰ recomputed, not parked)
     d = config_problem(4, 1, True, seed=13)
     batches = [np.array([0, 4]), np.array([8, 1]), np.array([5, 2]), np.array([6, 3]), np.array([7])]
     ks = {}
