@@ -373,6 +373,128 @@ struct Ch4x2 {
   float2 x[4], y[4];
 };
 
+// ------------------------------------------------------------------ packed complex arithmetic
+// Two v_pk instructions per complex product (the scalar cmul / cmulc of ptyx_fft.hpp take four
+// VALU instructions); operand halves are routed by op_sel / neg modifiers.
+//   pcm(a, b)  = a·b        = (a.x b.x − a.y b.y, a.x b.y + a.y b.x)
+//   pcmc(a, b) = a·conj(b)  = (a.x b.x + a.y b.y, a.y b.x − a.x b.y)
+__device__ __forceinline__ float2 pcm(float2 a, float2 b) {
+  rf::v2f t, r;
+  asm("v_pk_mul_f32 %0, %2, %3 op_sel_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %1, %2, %3, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=&v"(t), "=v"(r)
+      : "v"(rf::pv(a)), "v"(rf::pv(b)));
+  return rf::pf(r);
+}
+__device__ __forceinline__ float2 pcmc(float2 a, float2 b) {
+  rf::v2f t, r;
+  asm("v_pk_mul_f32 %0, %2, %3 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %1, %2, %3, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
+      : "=&v"(t), "=v"(r)
+      : "v"(rf::pv(a)), "v"(rf::pv(b)));
+  return rf::pf(r);
+}
+__device__ __forceinline__ float2 pscale(float2 a, float s) { return rf::pf(rf::pv(a) * (rf::v2f){s, s}); }
+
+// ------------------------------------------------------------------ LDS-DMA operand ring
+// PTYX_F3_RING = 1: the operands of the point-wise passes (object window, ψ⁰ park, F(P), segment
+// slab) stream HBM/L2 → LDS by buffer_load_dwordx4 … lds into a per-wave ring in the (then free)
+// exchange buffer, D register pairs ahead of their use, and are read back with ds_read_b64.  No
+// VGPRs are held by loads in flight, so a pass keeps 8-16 KiB per wave (64-128 KiB per CU) of
+// operands in flight instead of the one 4-register chunk the register pipeline could afford; the
+// first D pairs are issued during the second half of the preceding FFT.
+//
+// The DMA is emitted as inline asm: issued through the builtin, the compiler would put a
+// vmcnt(0) in front of every later LDS read of the buffer (it cannot tell the ring slots apart),
+// which serialises the ring.  The waits are explicit (vm_wait, counts from ring_wait_count), M0 is
+// saved and restored inside the asm, and every asm carries a memory clobber so no compiler memory
+// access moves across it.  Per wave the ring is 16 KiB: wave w owns bytes [16 KiB·w, 16 KiB·(w+1))
+// of the exchange buffer, and each wave DMAs exactly the operands its own threads read, so the
+// ring needs no workgroup barrier.
+#ifndef PTYX_F3_RING
+#define PTYX_F3_RING 1
+#endif
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+// buffer descriptor as four SGPRs (raw, stride 0; word 3 as rsrc())
+__device__ __forceinline__ v4u srd(const void* base, unsigned bytes) {
+  const unsigned long long p = (unsigned long long)base;
+  return v4u{(unsigned)p, (unsigned)(p >> 32) & 0xffffu, bytes, 0x00020000u};
+}
+// 16 B per lane: LDS[m0 + 16·lane] ← mem[r + voff + SOFF]
+template <int SOFF>
+__device__ __forceinline__ void dma_c(v4u r, int voff, int m0) {
+  int t, s;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %1, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_mov_b32 %0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %5, %0 offen lds\n\t"
+      "s_mov_b32 m0, %1"
+      : "=&s"(t), "=&s"(s)
+      : "s"(m0), "i"(SOFF), "v"(voff), "s"(r)
+      : "memory");
+}
+// the same with soffset = J·os (object rows: os = 8·Nx bytes)
+template <int J>
+__device__ __forceinline__ void dma_m(v4u r, int voff, int m0, int os) {
+  int t, s;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %1, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_mul_i32 %0, %3, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %6, %0 offen lds\n\t"
+      "s_mov_b32 m0, %1"
+      : "=&s"(t), "=&s"(s)
+      : "s"(m0), "s"(os), "i"(J), "v"(voff), "s"(r)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// Vector-memory instructions a wave has issued after the DMAs of register pair Q, at the wait of
+// pair Q: D pairs are issued ahead (A DMAs each); iteration P then does S stores and the DMAs of
+// pair P + D (if any) into the slot pair P just freed.  The passes call it with S = 0: vmcnt
+// retires loads in order among themselves, but a store may be acknowledged before an older load
+// returns, so only the loads issued after pair Q's DMAs may be left outstanding.
+//
+// A wave's ring lies in the exchange buffer, which the next FFT's exchange overwrites across all
+// waves: a workgroup barrier separates the last ring read of every wave from that exchange.
+constexpr int ring_wait_count(int Q, int A, int S, int D) {
+  int n = 0;
+  if (Q < D) {
+    n = (D - 1 - Q) * A;
+    for (int P = 0; P < Q; ++P) n += S + (P + D < 32 ? A : 0);
+  } else {
+    for (int P = Q - D + 1; P < Q; ++P) n += S + (P + D < 32 ? A : 0);
+  }
+  return n;
+}
+// Per-lane DMA source offsets (μ = lane; the two halves of a wave fetch register pair (2q, 2q+1)).
+//   K-packed arrays (F(P), slab: element (t, k) at 8t + 2048k) and the ψ⁰ park: LDS image of a
+//   register = thread λ at 8λ.  Object window (element (λ, j) at row j + 64·l0, column 32w + λ/2):
+//   LDS image pos(λ) = 256(f>>4) + 32((f&15)>>1) + 16·l0 + 8(f&1), f = λ>>1 (conflict-free
+//   ds_read_b64, 16-B DMA granules = two adjacent columns of one row).
+__device__ __forceinline__ int dma_off_k(int mu, int w) { return ((mu >> 5) << 11) + (w << 9) + ((mu & 31) << 4); }
+__device__ __forceinline__ int dma_off_park(int mu, int w) {
+  return ((mu >> 5) << 11) + (((mu >> 4) & 1) << 10) + (w << 8) + ((mu & 15) << 4);
+}
+__device__ __forceinline__ int dma_off_obj(int mu, int w, int os) {
+  const int nu = mu & 31, l0 = nu & 1, i = ((nu >> 4) << 3) | ((nu >> 1) & 7);
+  return ((mu >> 5) + 64 * l0) * os + (w << 8) + (i << 4);
+}
+// ψ⁰ park store offset of thread λ (within wave w's slot bytes of each register row)
+__device__ __forceinline__ int park_off(int lam, int w) { return ((lam >> 5) << 10) + (w << 8) + ((lam & 31) << 3); }
+// float2 index of thread λ's object element in a register's LDS image
+__device__ __forceinline__ int obj_img(int lam) {
+  const int f = lam >> 1;
+  return ((f >> 4) << 5) + (((f & 15) >> 1) << 2) + ((lam & 1) << 1) + (f & 1);
+}
+
 // PTYX_F3_PHASES=1 (diagnostic builds only): s_memtime stamps at the phase boundaries of wave 0;
 // workgroups 0 and 1 printf their per-phase cycle totals at exit.
 #ifndef PTYX_F3_PHASES
@@ -398,18 +520,50 @@ struct PatInfo {
   int m, cy, cx, sidx, mi;   // mini-batch, window origin, scan index, measurement row
   float sy, sx;
 };
+// Per-pattern scalars through the scalar cache (s_load, counted by lgkmcnt).  A plain load of
+// these read-only tables is a vector load here (the kernel stores to global memory, so the
+// compiler cannot prove them unwritten), and its vmcnt(0) wait would also wait for every slot /
+// slab / park store still in flight.  Uniform addresses only.
+__device__ __forceinline__ int s_ld(const int* p) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void s_ld3(const int* pb, const int2* pg, const int* pi, int& b, int2& g, int& i) {
+  unsigned long long gg;
+  asm volatile(
+      "s_load_dword %0, %3, 0x0\n\t"
+      "s_load_dwordx2 %1, %4, 0x0\n\t"
+      "s_load_dword %2, %5, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(b), "=&s"(gg), "=&s"(i)
+      : "s"(pb), "s"(pg), "s"(pi)
+      : "memory");
+  g = make_int2((int)(unsigned)gg, (int)(unsigned)(gg >> 32));
+}
+__device__ __forceinline__ float2 s_ldf2(const float* p) {
+  unsigned long long v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
 template <bool SHIFT>
 __device__ __forceinline__ PatInfo pat_info(const F3Args& a, int pat) {
   PatInfo p;
   const int pp = min(pat, a.n_idx - 1);   // (a past-the-end "next" pattern reads a valid slot)
-  p.m = a.bid[pp];
-  const int2 g = a.geo[pp];
+  int2 g;
+  int si;
+  s_ld3(a.bid + pp, a.geo + pp, a.idx + pp, p.m, g, si);
   p.cy = g.x;
   p.cx = g.y;
-  p.sidx = min(max(a.idx[pp], 0), a.n_scans - 1);
-  p.mi = a.mrow ? a.mrow[p.sidx] : p.sidx;
-  p.sy = SHIFT ? a.shifts[2 * p.sidx] : 0.f;
-  p.sx = SHIFT ? a.shifts[2 * p.sidx + 1] : 0.f;
+  p.sidx = min(max(si, 0), a.n_scans - 1);
+  p.mi = a.mrow ? s_ld(a.mrow + p.sidx) : p.sidx;
+  if constexpr (SHIFT) {
+    const float2 s = s_ldf2(a.shifts + 2 * p.sidx);
+    p.sy = s.x;
+    p.sx = s.y;
+  } else {
+    p.sy = p.sx = 0.f;
+  }
   return p;
 }
 
@@ -481,6 +635,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #if PTYX_F3_PHASES
   unsigned long long ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ph_prev = __builtin_amdgcn_s_memtime();
+  const unsigned long long ph_t0 = ph_prev, ph_r0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
   int ph_n = 0;
 #endif
   constexpr float inv_n = 1.0f / kN, inv_n2 = 1.0f / kN2;
@@ -495,6 +650,8 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 
   // ---------------------------------------------------------------- prologue: v for the first pattern
   constexpr bool kHold = PTYX_F3_HOLD != 0;
+  constexpr bool kRing = PTYX_F3_RING && SHIFT && !kHold;
+  const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;   // LDS byte address
   float2 v[64];
   float2 psi0[kHold ? 64 : 1], slab[kHold ? 64 : 1];
   if constexpr (kHold) {
@@ -521,7 +678,9 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
           const float2 A = rp.a(C);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
+            // (the same arithmetic as the post4 pass that forms every later pattern's v)
+            if constexpr (kRing) v[4 * C + r] = pcm(t.x[r], pcm(A, rp.B[r]));
+            else v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
             pin(v[4 * C + r]);
           }
         });
@@ -541,16 +700,54 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     const Rsrc r_obj = rsrc(a.oc + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
     const int vobj0 = 8 * (64 * l0 * Nx + fx);
     const int ostr0 = 8 * Nx;
+    // ring (kRing): this wave's 16 KiB of the exchange buffer, descriptors of the streamed operands
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0w = lds0 + (wv << 14);
+    const float2* ringw = buf + (wv << 11);
+    const v4u s_obj = srd(a.oc + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
+    const v4u s_park = srd(a.slots + (size_t)pat * kN2, kN2 * 8);
+    const int os = __builtin_amdgcn_readfirstlane(ostr0);
+    // post1 ring: the object window, 16 register pairs ahead (A = 1, S = 2 park stores per pair)
+    auto issue1 = [&](auto Q, int voff) {
+      constexpr int q = decltype(Q)::value;
+      dma_m<2 * q>(s_obj, voff, m0w + (q % 16) * 1024, os);
+    };
     // ------------------------------------------------ ψ⁰ = F⁻¹(F(P)·W_b)  (R layout)
     F3PH(0);
     if constexpr (SHIFT) {
-      fft_inv(v, buf, lc, cd.wsign);
+      fft_inv(v, buf, lc, cd.wsign, [&] {
+        if constexpr (kRing) {
+          const int vo = dma_off_obj(rf::opaque(tid) & 63, wv, os);
+          rf::sfor<0, 16>([&](auto Q) { issue1(Q, vo); });
+        }
+      });
 #pragma unroll
-      for (int j = 0; j < 64; ++j) v[j] = cscale(v[j], inv_n2);
+      for (int j = 0; j < 64; ++j) v[j] = pscale(v[j], inv_n2);
     }
     F3PH(1);
     // ------------------------------------------------ park ψ⁰; ψ = ψ⁰·O
-    {
+    if constexpr (kRing) {
+      const int lam = rf::opaque(tid) & 63;
+      const int vo = dma_off_obj(lam, wv, os);
+      const int vpark = park_off(lam, wv);
+      const int io = obj_img(lam);
+      const Rsrc r_park = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
+      rf::sfor<0, 32>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        vm_wait<ring_wait_count(q, 1, 0, 16)>();
+        const float2* sl = ringw + (q % 16) * 128;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int j = 2 * q + rb;
+          const float2 O = sl[rb * 64 + io];
+          if (!PTYX_F3_EXP_NOPARK) st2(v[j], r_park, vpark, 2048 * j);
+          v[j] = pcm(v[j], PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : O);
+          pin(v[j]);
+        }
+        if constexpr (q + 16 < 32) issue1(std::integral_constant<int, q + 16>{}, vo);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
       const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
       pipeline<8>(
           [&](auto C) {
@@ -578,6 +775,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     F3PH(2);
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
     const float* dp = a.meas + (size_t)p.mi * kN2;
+    if constexpr (kRing) __syncthreads();   // every wave is done with its ring before the exchange
     fft_fwd(v, buf, lc, cd.wsign, [&] {
       const int lane = cd.lane;
       const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
@@ -597,6 +795,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     __syncthreads();
     F3PH(4);
     float S = 0.f, Ms = 0.f;
+    const float occ_n2 = occ * inv_n2, occ2_n = 2.0f * occ * inv_n;
     {
       const int r = (fx + 64) & 127;               // fftshifted DP row of ky
       const int b = 1 - l0;                        // fftshifted column half of kx = k + 64 l0
@@ -613,10 +812,10 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int k = 4 * kq + e;
-          const float2 Psi = cscale(v[k], inv_n);
-          Iv[e] = fmaf(occ, cabs2(Psi), kDpEps);
+          // Ψ = v/N with N a power of two: |Ψ|² occ = |v|² (occ/N²) and g_Ψ = v (2 occ u / N) exactly
+          Iv[e] = fmaf(occ_n2, cabs2(v[k]), kDpEps);
           const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
-          v[k] = cscale(Psi, 2.0f * occ * u);
+          v[k] = pscale(v[k], occ2_n * u);
           pin(v[k]);
         }
         {
@@ -643,9 +842,43 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     }
     F3PH(6);
     // ------------------------------------------------ back to real space
-    fft_inv(v, buf, lc, cd.wsign);
+    // post3 ring: ψ⁰ park + object window, 8 register pairs ahead (A = 2, S = 2 slot stores)
+    auto issue3 = [&](auto Q, int vpo, int voo) {
+      constexpr int q = decltype(Q)::value;
+      dma_c<4096 * q>(s_park, vpo, m0w + (q % 8) * 2048);
+      dma_m<2 * q>(s_obj, voo, m0w + (q % 8) * 2048 + 1024, os);
+    };
+    fft_inv(v, buf, lc, cd.wsign, [&] {
+      if constexpr (kRing) {
+        const int lam = rf::opaque(tid) & 63;
+        const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+        rf::sfor<0, 8>([&](auto Q) { issue3(Q, vpo, voo); });
+      }
+    });
     F3PH(7);
-    {
+    if constexpr (kRing) {
+      const int lam = rf::opaque(tid) & 63;
+      const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+      const int io = obj_img(lam);
+      const int vslot = rf::opaque(vslot0);
+      rf::sfor<0, 32>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        vm_wait<ring_wait_count(q, 2, 0, 8)>();
+        const float2* sl = ringw + (q % 8) * 256;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int j = 2 * q + rb;
+          const float2 ps = PTYX_F3_EXP_NOPARK ? make_float2(1.f, 0.f) : sl[rb * 64 + lam];
+          const float2 O = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : sl[128 + rb * 64 + io];
+          const float2 gv = pscale(v[j], inv_n);
+          if (!PTYX_F3_EXP_NOSLOT) st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+          v[j] = pcmc(gv, O);                                                          // g·conj(O)
+          pin(v[j]);
+        }
+        if constexpr (q + 8 < 32) issue3(std::integral_constant<int, q + 8>{}, vpo, voo);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
       const int vslot = rf::opaque(vslot0), vobj = rf::opaque(vobj0), ostr = rf::opaque(ostr0);
       pipeline<16>(
           [&](auto C) {
@@ -677,14 +910,82 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     // and so initialises it; later patterns accumulate.  Without probe/position gradients (tail
     // false) the same pass runs without the FFT and its slab / sums are never used.
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || a.bid[pat - 1] != p.m;   // (uniform)
-    const bool last = pat == p1 - 1 || a.bid[pat + 1] != p.m;   // (uniform; PTYX_F3_HOLD flushes the slab)
+    const bool first = pat == p0 || s_ld(a.bid + (pat - 1)) != p.m;   // (uniform)
+    const bool last = kHold && (pat == p1 - 1 || s_ld(a.bid + (pat + 1)) != p.m);   // (uniform; PTYX_F3_HOLD flushes the slab)
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
     const Rsrc r_slab_st = rsrc(segs, kN2 * 8);
     if (first && threadIdx.x == 0) a.segbid[seg] = p.m;
-    if constexpr (SHIFT) {
+    if constexpr (kRing) {
+      // post4 ring: F(P) + the segment slab, 8 register pairs ahead (A = 2, S = 2 slab stores).
+      // The first pattern of a segment streams F(P) in the slab's place (finite) and scales it by
+      // zero, which initialises the slab.
+      const v4u s_fpk = srd(a.fpk, kN2 * 8);
+      const v4u s_slab = first ? s_fpk : srd(segs, kN2 * 8);
+      const float keep = first ? 0.f : 1.f;
+      auto issue4 = [&](auto Q, int vk) {
+        constexpr int q = decltype(Q)::value;
+        dma_c<4096 * q>(s_fpk, vk, m0w + (q % 8) * 2048);
+        dma_c<4096 * q>(s_slab, vk, m0w + (q % 8) * 2048 + 1024);
+      };
+      auto pre4 = [&] {
+        const int vk = dma_off_k(rf::opaque(tid) & 63, wv);
+        rf::sfor<0, 8>([&](auto Q) { issue4(Q, vk); });
+      };
+      __syncthreads();   // every wave is done with its post3 ring before the exchange
+      // G = F(h), K layout (unconditional here: a branch around the FFT spills the 64 points;
+      // without probe / position gradients the slab and sums are simply never read)
+      fft_fwd(v, buf, lc, cd.wsign, pre4);
+      F3PH(9);
+      const int lam = rf::opaque(tid) & 63;
+      const int vk = dma_off_k(lam, wv);
+      const int vpk = rf::opaque(8 * tid);
+      const int l0b = rf::opaque(tid) & 1;
+      Ramp rc, rn;
+      rc.init(p.sy, p.sx, gy, l0b);
+      rn.init(pn.sy, pn.sx, gy, l0b);
+      float sim = 0.f, kim = 0.f;
+      float2 A = make_float2(0.f, 0.f), An = A;
+      rf::sfor<0, 32>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        vm_wait<ring_wait_count(q, 2, 0, 8)>();
+        const float2* sl = ringw + (q % 8) * 256;
+        if constexpr ((q & 1) == 0) {
+          A = rc.a(q >> 1);
+          An = rn.a(q >> 1);
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int k = 2 * q + rb;
+          const int r = k & 3;
+          const float2 F = sl[rb * 64 + lam];
+          const float2 W = pcm(A, rc.B[r]);
+          const float2 FW = pcm(F, W);
+          const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
+          sim += im;
+          kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
+          if (!PTYX_F3_EXP_NOSLAB) {
+            const float2 so = sl[128 + rb * 64 + lam];
+            const float2 gw = pcmc(v[k], W);                      // + conj(W) G (unit)
+            st2(rf::pf(__builtin_elementwise_fma((rf::v2f){keep, keep}, rf::pv(so), rf::pv(gw))), r_slab_st, vpk, 2048 * k);
+          }
+          v[k] = pcm(F, pcm(An, rn.B[r]));                        // next pattern: F(P)·W_next
+          pin(v[k]);
+        }
+        if constexpr (q + 8 < 32) issue4(std::integral_constant<int, q + 8>{}, vk);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      F3PH(10);
+      {
+        float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0b) * sim)};
+        block_sum4<2>(ds, s_red);
+        if (threadIdx.x == 0) {
+          a.dsu[2 * pat] = ds[0];
+          a.dsu[2 * pat + 1] = ds[1];
+        }
+      }
+    } else if constexpr (SHIFT) {
       if (tail) fft_fwd(v, buf, lc, cd.wsign);        // G = F(h), K layout
       F3PH(9);
       const int vpk = rf::opaque(8 * tid);
@@ -785,6 +1086,11 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
            "publish %llu ifft3 %llu post3 %llu fft4 %llu post4+pre %llu ds %llu\n",
            (int)blockIdx.x, ph_n, ph[0] / ph_n, ph[1] / ph_n, ph[2] / ph_n, ph[3] / ph_n, ph[4] / ph_n, ph[5] / ph_n,
            ph[6] / ph_n, ph[7] / ph_n, ph[8] / ph_n, ph[9] / ph_n, ph[10] / ph_n, ph[11] / ph_n);
+  if (threadIdx.x == 0 && blockIdx.x < 2) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    printf("F3CLOCK wg %d shader-clock MHz %.0f over %.1f us\n", (int)blockIdx.x,
+           100.0 * (double)(t1 - ph_t0) / (double)(r1 - ph_r0), (double)(r1 - ph_r0) / 100.0);
+  }
 #endif
 }
 
@@ -1003,7 +1309,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     }
     // ------------------------------------------------ probe / position gradient, next pattern's v
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || a.bid[pat - 1] != p.m;
+    const bool first = pat == p0 || s_ld(a.bid + (pat - 1)) != p.m;
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));

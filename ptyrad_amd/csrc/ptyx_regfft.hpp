@@ -521,14 +521,19 @@ __device__ __forceinline__ void fft_fwd(float2 (&v)[64], float2* buf, LaneCtx c,
   fft_fwd(v, buf, c, s, [] {});
 }
 // Unnormalised inverse DFT (exp(+2πi…)), K layout in, R layout out.
-__device__ __forceinline__ void fft_inv(float2 (&v)[64], float2* buf, LaneCtx c, float s) {
+template <class Mid>
+__device__ __forceinline__ void fft_inv(float2 (&v)[64], float2* buf, LaneCtx c, float s, Mid&& mid) {
   lane_pre<+1>(v, c);
   flip_odd(v, s);
   dft64<+1>(v);
   exchange_inv(v, buf);
+  mid();
   dft64<+1>(v);
   flip_odd(v, s);
   lane_post<+1>(v, c);
+}
+__device__ __forceinline__ void fft_inv(float2 (&v)[64], float2* buf, LaneCtx c, float s) {
+  fft_inv(v, buf, c, s, [] {});
 }
 
 // Thread coordinates.  R layout: (y = j + 64·l0, x = fixed); K layout: (ky = fixed, kx = k + 64·l0).
