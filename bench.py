@@ -357,9 +357,20 @@ def main():
         # the N = 256 stripe engine (k_s1..k_s5): FP32-FFT bound (c3 AI 107, c5 AI 71 flop/B)
         s_ms = sum(kstats[k][1] for k in stripe) / a.steps
         achieved = f_alg * n_local / (s_ms / 1e3) / 1e12
+        traffic, fabric = None, None
+        pmc = os.path.join(ROOT, "profiles", "pmc_stripe.json")
+        if os.path.exists(pmc):
+            # PMC bytes per pattern of the same passes (profiles/pmc_stripe.json, from the r02y
+            # rocprofv3 --pmc runs), per step: the fabric rate the passes sustain
+            with open(pmc) as f:
+                bpp = json.load(f).get(a.config, {}).get("bytes_per_pattern")
+            if bpp:
+                traffic = float(bpp) * n_local
+                fabric = round(traffic / (s_ms / 1e3) / 1e9, 1)
         roof = {"kernel": "stripe engine k_s1..k_s5", "bound": "mfma", "achieved": round(achieved, 2),
                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                "traffic": None, "alg_flops_per_step": f_alg * n_local, "engine_ms_per_step": round(s_ms, 3),
+                "traffic": traffic, "traffic_GBps": fabric, "alg_flops_per_step": f_alg * n_local,
+                "engine_ms_per_step": round(s_ms, 3),
                 "note": "FP32 vector peak = FP32 MFMA rate on gfx950; the FFTs run on the vector ALUs",
                 "hbm_alg_frac": round(b_alg * n_local / (s_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
     par = f"dp{world} (RCCL all-reduce of object+probe grads per step)" if world > 1 else "dp1"

@@ -269,6 +269,8 @@ struct FinArgs {
   float* loss_terms;
   float2* pcoef;   // optional, per pattern: (coef[ci], c_sparse) of its mini-batch (k_obj_gather)
   int ci;
+  int pcoef_O = 1;             // object modes with a pcoef plane (plane o holds c_sparse of mode o)
+  long long pcoef_stride = 0;  // patterns per plane
 };
 
 __global__ void k_finalize(FinArgs f) {
@@ -318,8 +320,10 @@ __global__ void k_finalize(FinArgs f) {
   if (f.loss_terms)
     for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
   if (f.pcoef) {
-    const float2 pc = make_float2(cf[f.ci], cf[2]);
-    for (int t = b0; t < b1; ++t) f.pcoef[t] = pc;
+    for (int o = 0; o < f.pcoef_O; ++o) {
+      const float2 pc = make_float2(cf[f.ci], cf[2 + o]);
+      for (int t = b0; t < b1; ++t) f.pcoef[o * f.pcoef_stride + t] = pc;
+    }
   }
 }
 
@@ -682,6 +686,7 @@ struct ptyx_plan {
   float* spsum = nullptr;
   float* sdsp = nullptr;
   float2* sslab = nullptr;
+  bool sgather = false;       // stripe object gradient: per-pattern slots + k_obj_gather (else f32 atomics)
   long long seg_cap = 0;      // segment ids the segslab holds
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
@@ -880,6 +885,16 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
       pl->stripe_cap = cap;
       pl->stripe_groups = groups;
+      // object gradient of two object modes: k_s4 writes per-pattern slots (over the T3 fields it
+      // has consumed) and k_obj_gather reduces them per tile (deterministic, no atomics).  One
+      // object mode keeps k_s4's f32 atomics (profiles/r02/ab/r02y_*: the epilogue costs c3 20 ms
+      // of 66 in k_s4 but c5 only 2.7 of 23, less than the slot stores plus the gather would).
+      const char* sg = std::getenv("PTYX_S_GATHER");
+      pl->sgather = sg ? sg[0] == '1' : d.O > 1;
+      if (pl->sgather && ((rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns * d.O)) || (rc = alloc_bins(pl)))) {
+        free_plan(pl);
+        return rc;
+      }
     }
   }
   if (!stripe && d.Nz == 1 && d.P * d.O > 1 && pl->fast && !std::getenv("PTYX_NO_FFC")) {
@@ -1306,6 +1321,8 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   s.t14 = pl->st14; s.psi0 = pl->spsi0; s.t23 = pl->st23; s.psum_s = pl->spsum; s.dp_out = a.dp_out;
   s.coef = pl->coef; s.ci = single ? 0 : 1;
   s.d_obja = gz.d_obja; s.d_objp = gz.d_objp;
+  const bool sgather = pl->sgather && (gz.d_obja || gz.d_objp);
+  s.oslot = sgather ? pl->st23 : nullptr;
   s.groups = std::max(1, std::min(pl->stripe_groups, n));
   s.slabpart = pl->sslab; s.dsp = pl->sdsp;
   s.twg = pl->twg;
@@ -1354,6 +1371,12 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
   fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  if (sgather) {
+    fa.pcoef = pl->pcoef;
+    fa.ci = s.ci;
+    fa.pcoef_O = O;
+    fa.pcoef_stride = n;
+  }
   {
     ProfScope ps(pl, kKFinalize, st);
     hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
@@ -1371,6 +1394,40 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     else hipLaunchKernelGGL((k_s4<2, false>), dim3(n, kStripes), bl, 0, st, s4);
   }
   if ((rc = launch_status("k_s4 launch"))) return rc;
+  if (sgather) {
+    // object gradient from the slots: candidate bins per call, then one k_obj_gather per mode
+    const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
+    {
+      ProfScope ps(pl, kKTable, st);
+      hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
+      if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+      const dim3 gn((n + 255) / 256);
+      hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, n, tiles_x, pl->bcnt, pl->bkey);
+      hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
+      hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, n, pl->bcur, pl->blist);
+      hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
+    }
+    GatherArgs g{};
+    g.ogscr = pl->st23; g.geo = pl->geo; g.n = n; g.boff = pl->boff; g.blist = pl->blist;
+    g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = tiles_x; g.sparse_n = cfg->sparse_on ? cfg->sparse_n : 1;
+    g.nz = P * O;   // slot o = field o of the pattern's P·O T3 fields
+    g.bbox = pl->bbox;
+    const int tiles = tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    const bool sparse_tiles = (long long)n * BinReach<kN>::n < 64LL * tiles;
+    const size_t plane = (size_t)d.Ny * d.Nx;
+    ProfScope ps(pl, kKGather, st);
+    for (int o = 0; o < O; ++o) {
+      g.z = o;
+      g.pcoef = pl->pcoef + (size_t)o * n;
+      g.obja = a.obja + o * plane;
+      g.objp = a.objp + o * plane;
+      g.d_obja = gz.d_obja ? gz.d_obja + o * plane : nullptr;
+      g.d_objp = gz.d_objp ? gz.d_objp + o * plane : nullptr;
+      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<kN, false, 4>), dim3(tiles), dim3(64 * 4), 0, st, g);
+      else hipLaunchKernelGGL((k_obj_gather<kN, false>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+    }
+    if ((rc = launch_status("stripe k_obj_gather launch"))) return rc;
+  }
   if (!tail) return PTYX_OK;
   {
     ProfScope ps(pl, kKS5, st);

@@ -23,7 +23,8 @@
 //   --- k_finalize: the mini-batch NRMSE coefficients c_m (losses.py:45-47) ---
 //   P4  rows     per p: per o: row IFFT → g/N;  slot_o += g·conj(ψ⁰_p);  gP += g·conj(O_o);
 //                row FFT(gP) → T4[p] (= T1's storage);  then dA, dφ (+ the sparse sign term)
-//                scaled by c_m, f32 atomics into the object gradient
+//                scaled by c_m, f32 atomics into the object gradient (O = 1), or the slot_o
+//                waves stored over T3 fields 0..O-1 for k_obj_gather (O = 2: deterministic)
 //   P5  columns  per pattern: column FFT(T4[p]) → G;  slab += c_m conj(W_b) G (registers, the
 //                block's stripe of the probe-gradient spectrum across its patterns);  position
 //                gradient Σ 2π g·Im(F(P) W conj(G)) per pattern (Parseval, no extra FFT)
@@ -94,6 +95,8 @@ struct SArgs {
   int ci;                // data-term coefficient index (0 single, 1 poissn)
   float* d_obja;
   float* d_objp;
+  float2* oslot;         // non-NULL: P4 stores the object-gradient waves (unit c_m) as slots over
+                         // T3 fields 0..O-1 of each pattern (k_obj_gather), instead of atomics
   float2* slabpart;      // (groups, P, N²) probe-gradient spectrum partials
   int groups;
   float* dsp;            // (n, kStripes·P, 2) position-gradient partials
@@ -196,6 +199,19 @@ __device__ __forceinline__ void fft_line(float2 (&v)[16], Map m, float2* xb, con
 
 __device__ __forceinline__ float shift_g(int k) { return (float)((k + kN / 2) & (kN - 1)) * (1.0f / kN); }
 
+// Sub-pixel ramps (image_proc.py:531).  A thread's points are k = slot + 16 r (slot < 16), so
+// (k + N/2) mod N wraps exactly at r = 8 for every thread:
+//   g(slot + 16 r) = slot/256 + h_r,   h_r = 1/2 + r/16 (r < 8),  (r − 8)/16 (r ≥ 8),
+// and cis(−s·g) = cis(−s·slot/256) · cis(−s·h_r): one per-thread factor and 16 factors shared by
+// the workgroup (an LDS row written by 16 threads) instead of 16 sin/cos pairs per thread.
+__device__ __forceinline__ float ramp_h(int r) { return r < 8 ? 0.5f + (float)r * (1.0f / 16) : (float)(r - 8) * (1.0f / 16); }
+// threads 0..15 write the shared factors of shift s into rl[16] (visible after the next barrier)
+__device__ __forceinline__ void ramp_row(float2* rl, float s) {
+  if (threadIdx.x < 16) rl[threadIdx.x] = f3::cis_rev(-s * ramp_h((int)threadIdx.x));
+}
+// the per-thread factor cis(−s·slot/256)
+__device__ __forceinline__ float2 ramp_t(float s, int slot) { return f3::cis_rev(-s * ((float)slot * (1.0f / kN))); }
+
 __device__ __forceinline__ void load_tw(float2* tw, const float2* twg) {
   for (int i = threadIdx.x; i < kN; i += blockDim.x) tw[i] = twg[i];
 }
@@ -213,17 +229,20 @@ __device__ __forceinline__ void bsum(float (&v)[NV], float* red) {
 __global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
-  load_tw(tw, a.twg);
-  __syncthreads();
+  __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y, p = blockIdx.z;
+  const float sy = a.shifts[2 * scan_of(a, j)];
+  load_tw(tw, a.twg);
+  ramp_row(rl, sy);
+  __syncthreads();
   const Map m = map_of<true>(opq(threadIdx.x));
   const int kx = s * kL + m.line;
-  const float sy = a.shifts[2 * scan_of(a, j)];
   const int vcol = (m.slot * kN + kx) * 8;
   float2 v[16];
   ldb<kColStride>(v, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
+  const float2 T = ramp_t(sy, m.slot);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-sy * shift_g(m.slot + 16 * r)));
+  for (int r = 0; r < 16; ++r) v[r] = f3::pcm(v[r], f3::pcm(T, rl[r]));
   fft_line<+1, true>(v, m, xb, tw);
   stb<kColStride>(v, a.t14 + ((size_t)j * a.P + p) * kN2, kFieldBytes, vcol);
 }
@@ -235,13 +254,16 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[4 * kMaxO];
-  load_tw(tw, a.twg);
-  __syncthreads();
+  __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y;
-  const Map m = map_of<false>(opq(threadIdx.x));
-  const int y = s * kL + m.line;
   const int sidx = scan_of(a, j);
   const float sx = a.shifts[2 * sidx + 1];
+  load_tw(tw, a.twg);
+  ramp_row(rl, sx);
+  __syncthreads();
+  const Map m = map_of<false>(opq(threadIdx.x));
+  const int y = s * kL + m.line;
+  const float2 T = ramp_t(sx, m.slot);
   const int2 g0 = a.geo[j];
   const int P = a.P;
   constexpr float inv_n2 = 1.0f / kN2;
@@ -264,8 +286,9 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
     } else {
       ldb<kRowStride>(v, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     }
+    const float2* rlo = rl + opq(0);   // (re-read per mode, not hoisted into 32 registers)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = cmul(v[r], f3::cis_rev(-opqf(sx) * shift_g(m.slot + 16 * r)));
+    for (int r = 0; r < 16; ++r) v[r] = f3::pcm(v[r], f3::pcm(T, rlo[r]));
     fft_line<+1, false>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n2);
@@ -422,9 +445,12 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
   // reads back only its own points: no barrier) for the P probe modes
   constexpr bool OB_LDS = O_ == 1;
   __shared__ float2 obl[OB_LDS ? 16 * 256 : 1];
-  load_tw(tw, a.twg);
-  __syncthreads();
+  __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y;
+  const float sx = a.shifts[2 * scan_of(a, j) + 1];
+  load_tw(tw, a.twg);
+  if constexpr (!PARK) ramp_row(rl, sx);
+  __syncthreads();
   const Map m = map_of<false>(opq(threadIdx.x));
   const int y = s * kL + m.line;
   const int2 g0 = a.geo[j];
@@ -432,7 +458,6 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
   const int mb = a.bid[j];
   constexpr float inv_n = 1.0f / kN;
   const bool want_t4 = a.t4 != nullptr;
-  const float sx = a.shifts[2 * scan_of(a, j) + 1];
   constexpr float inv_n2 = 1.0f / kN2;
   float2 so[O_][16];
 #pragma unroll
@@ -452,8 +477,10 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
       ldb<kRowStride>(psr, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     } else {   // ψ⁰_p = F⁻¹_x(wx · T1_p)/N² again: one row transform instead of a parked field
       ldb<kRowStride>(psr, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+      const float2 T = ramp_t(opqf(sx), m.slot);
+      const float2* rlo = rl + opq(0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) psr[r] = cmul(psr[r], f3::cis_rev(-opqf(sx) * shift_g(m.slot + 16 * r)));
+      for (int r = 0; r < 16; ++r) psr[r] = f3::pcm(psr[r], f3::pcm(T, rlo[r]));
       fft_line<+1, false>(psr, m, xb, tw);
 #pragma unroll
       for (int k = 0; k < 16; ++k) psr[k] = cscale(psr[k], inv_n2);
@@ -497,7 +524,17 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
       stb<kRowStride>(gq, a.t4 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);   // over T1_p's rows (read above)
     }
   }
+#ifdef PTYX_S4_EXP_NOGRAD   // cost-attribution build (results WRONG): no object-gradient epilogue
+  return;
+#endif
   if (!a.d_obja && !a.d_objp) return;
+  if (a.oslot) {
+    // slot o of pattern j = T3 field (p = 0, o), whose rows of this stripe were consumed above
+    // (no other workgroup touches them): natural (N, N) rows, c_m applied by k_obj_gather
+#pragma unroll
+    for (int o = 0; o < O_; ++o) stb<kRowStride>(so[o], a.oslot + ((size_t)j * P * O_ + o) * kN2, kFieldBytes, vrow);
+    return;
+  }
   // object gradient.  The slot accumulators are re-mapped through the (now free) exchange buffer
   // so that each wave owns 4 whole rows: every atomic / object load is 256 contiguous bytes per
   // wave instruction (the full-rate shape of global float atomics) instead of 4 × 64 B.
@@ -550,6 +587,7 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
+  __shared__ float2 rl[2][16];   // the shared ramp factors of the pattern in flight (double-buffered)
   load_tw(tw, a.twg);
   __syncthreads();
   const int s = blockIdx.x, p = blockIdx.y, gi = blockIdx.z;
@@ -565,22 +603,26 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   const float gx = shift_g(kx);
   float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
   if (gi < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
-  for (int j = gi; j < a.n; j += a.groups) {
+  for (int j = gi, it = 0; j < a.n; j += a.groups, ++it) {
     const int sidx = scan_of(a, j);
     const float sy = a.shifts[2 * sidx], sx = a.shifts[2 * sidx + 1];
     const float c = a.coef[(size_t)a.bid[j] * kNCoef + a.ci];
+    // (written here, read after fft_line's barriers; the other copy may still be read by threads
+    // finishing the previous pattern)
+    float2* rlj = rl[it & 1];
+    ramp_row(rlj, sy);
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = nxt[r];
     if (j + a.groups < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
-    const float2 wx = f3::cis_rev(-sx * gx);
+    const float2 TW = f3::pcm(ramp_t(sy, m.slot), f3::cis_rev(-sx * gx));   // cis(−sy·slot/N)·wx
     float sy_acc = 0.f, sim = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int ky = m.slot + 16 * k;
       const float gyk = shift_g(ky);
-      const float2 W = cmul(f3::cis_rev(-sy * gyk), wx);
+      const float2 W = f3::pcm(TW, rlj[k]);
       const float2 FW = cmul(fp[k], W);
       const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);   // Im(F(P) W conj(G))
       sy_acc = fmaf(gyk, im, sy_acc);

@@ -37,10 +37,12 @@ def config_problem(P, O, meas_f16, seed):
                 loss_params=json.loads(json.dumps(orc_default_loss())))
 
 
-def check_against_oracle(d, batches, meas_f16):
+def check_against_oracle(d, batches, meas_f16, gather=None):
     ks = {}
     terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=meas_f16, kernels=ks)
     assert {"k_s1", "k_s2", "k_s3", "k_s4", "k_s5"} <= set(ks), ks      # the N = 256 stripe engine ran
+    if gather is not None:   # object gradient by slots + k_obj_gather (else k_s4's f32 atomics)
+        assert ("k_obj_gather" in ks) == gather, ks
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"])
     assert rel(dp, np.concatenate(odps)) < TOL_DP
@@ -48,11 +50,17 @@ def check_against_oracle(d, batches, meas_f16):
     for k in ("obja", "objp", "probe"):
         assert rel(g[k], og[k]) < TOL_G, k
     assert rel(g["shifts"], og["shifts"]) < TOL_SH
+    return g
 
 
 def test_c3_shape_p8_o2_vs_oracle():
     d = config_problem(8, 2, False, seed=11)
-    check_against_oracle(d, [np.array([0, 4, 8]), np.array([5, 1])], meas_f16=False)
+    batches = [np.array([0, 4, 8]), np.array([5, 1])]
+    g1 = check_against_oracle(d, batches, meas_f16=False, gather=True)
+    # two object modes: slots + k_obj_gather, so the object gradient is bitwise reproducible
+    _, _, g2, _ = run_fused(d, dev(), batches, meas_f16=False)
+    for k in ("obja", "objp"):
+        assert np.array_equal(g1[k], g2[k]), k
 
 
 def test_c5_shape_p4_fp16_dps_vs_oracle():
@@ -68,6 +76,15 @@ def test_stripe_mode_hold_and_psi0_variants(monkeypatch, hold, park):
     monkeypatch.setenv("PTYX_S_PSI0", park)
     d = config_problem(3, 2, False, seed=13)
     check_against_oracle(d, [np.array([1, 3, 4]), np.array([7, 2, 0])], meas_f16=False)
+
+
+@pytest.mark.parametrize("O,flag", [(1, "1"), (2, "0")])
+def test_stripe_object_gradient_atomics_and_slots(monkeypatch, O, flag):
+    """k_s4's object-gradient form the mode count does not pick by default (PTYX_S_GATHER):
+    slots + k_obj_gather for one object mode, f32 atomics for two; the same gradients."""
+    monkeypatch.setenv("PTYX_S_GATHER", flag)
+    d = config_problem(2, O, False, seed=14)
+    check_against_oracle(d, [np.array([6, 2, 3]), np.array([0, 8, 4, 1])], meas_f16=False, gather=flag == "1")
 
 
 # ------------------------------------------------------------------ rank-local measurements
