@@ -173,6 +173,41 @@ __global__ void k_obj_prep(const float* obja, const float* objp, int Ny, int Nx,
   if (Nx == 0 && threadIdx.x == 0) prow[0] = 0;
 }
 
+// Columns of the row prefix sums → a summed-area table, in place: after k_obj_prep,
+// pref[z][y][x] = Σ_{r0 ≤ y' ≤ y} Σ_{x' < x} |φ(z, y', x')|^n over the prepared rows [r0, r1)
+// (all rows, or those the call's windows touch: the bbox rule of k_obj_prep).  A window's sum is
+// then four lookups per slice (k_pattern_table3) instead of one pair per window row.  fp64, in
+// two passes over chunks of kPrefChunk rows (one thread per (slice, chunk, column)): pass 1 scans
+// each chunk and keeps its total, pass 2 adds the totals of the chunks above (fixed order).
+constexpr int kPrefChunk = 32;
+__device__ __forceinline__ void pref_rows(const int* bbox, int Ny, int win, int& r0, int& r1) {
+  r0 = bbox ? max(0, bbox[0]) : 0;
+  r1 = bbox ? min(Ny, bbox[1] + win) : Ny;
+}
+__global__ void k_pref_cols1(double* pref, double* tot, int Ny, int Nx, const int* bbox, int win = kN) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
+  if (x > Nx) return;
+  int r0, r1;
+  pref_rows(bbox, Ny, win, r0, r1);
+  const int y0 = r0 + c * kPrefChunk, y1 = min(r1, y0 + kPrefChunk);
+  double* col = pref + (size_t)z * Ny * (Nx + 1) + x;
+  double acc = 0;
+  for (int y = y0; y < y1; ++y) col[(size_t)y * (Nx + 1)] = acc += col[(size_t)y * (Nx + 1)];
+  tot[((size_t)z * nch + c) * (Nx + 1) + x] = acc;   // (0 for chunks past r1)
+}
+__global__ void k_pref_cols2(double* pref, const double* tot, int Ny, int Nx, const int* bbox, int win = kN) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
+  if (x > Nx || c == 0) return;
+  int r0, r1;
+  pref_rows(bbox, Ny, win, r0, r1);
+  const int y0 = r0 + c * kPrefChunk, y1 = min(r1, y0 + kPrefChunk);
+  if (y0 >= y1) return;
+  double off = 0;
+  for (int k = 0; k < c; ++k) off += tot[((size_t)z * nch + k) * (Nx + 1) + x];
+  double* col = pref + (size_t)z * Ny * (Nx + 1) + x;
+  for (int y = y0; y < y1; ++y) col[(size_t)y * (Nx + 1)] += off;
+}
+
 // Bounding box of the call's windows: bbox = {min cy, max cy, min cx, max cx} (clamped origins);
 // initialise with k_bbox_init.  Lets k_obj_prep / k_obj_gather skip untouched object rows / tiles.
 __global__ void k_bbox_init(int* bbox) {
@@ -183,13 +218,21 @@ __global__ void k_bbox_init(int* bbox) {
     bbox[3] = -0x7fffffff;
   }
 }
-__global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int Ny, int Nx, int* bbox, int win = kN) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// Grid-stride over the patterns (launch with at most kBboxBlocks blocks of 256 threads): wave
+// reduction, then one set of four atomics per workgroup (contended atomics on four addresses
+// from every wave cost ≈ 50 µs at 65,536 patterns).
+constexpr int kBboxBlocks = 64;
+__global__ __launch_bounds__(256) void k_bbox(const int* idx, int n, const int* crop, int n_scans, int Ny, int Nx,
+                                              int* bbox, int win = kN) {
+  __shared__ int red[4][4];
   int a = 0x7fffffff, b = -0x7fffffff, c = 0x7fffffff, d = -0x7fffffff;
-  if (j < n) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const int s = min(max(idx[j], 0), n_scans - 1);
-    a = b = min(max(crop[2 * s], 0), Ny - win);
-    c = d = min(max(crop[2 * s + 1], 0), Nx - win);
+    const int cy = min(max(crop[2 * s], 0), Ny - win), cx = min(max(crop[2 * s + 1], 0), Nx - win);
+    a = min(a, cy);
+    b = max(b, cy);
+    c = min(c, cx);
+    d = max(d, cx);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -198,7 +241,21 @@ __global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int 
     c = min(c, __shfl_xor(c, o, 64));
     d = max(d, __shfl_xor(d, o, 64));
   }
+  const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    red[wv][0] = a;
+    red[wv][1] = b;
+    red[wv][2] = c;
+    red[wv][3] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      a = min(a, red[w][0]);
+      b = max(b, red[w][1]);
+      c = min(c, red[w][2]);
+      d = max(d, red[w][3]);
+    }
     atomicMin(bbox + 0, a);
     atomicMax(bbox + 1, b);
     atomicMin(bbox + 2, c);
@@ -206,11 +263,13 @@ __global__ void k_bbox(const int* idx, int n, const int* crop, int n_scans, int 
   }
 }
 
-// pattern → (mini-batch, clamped window origin) and, with pref, the loss_sparse window sum
-// Σ_{window} |φ|^n into psums[kSumBase] (fp64 over rows, fixed order).  One wave per pattern.
+// pattern → (mini-batch, clamped window origin) and, with pref (the summed-area table of
+// k_pref_cols1/2), the loss_sparse window sum Σ_{window} |φ|^n into psums[kSumBase]: four fp64
+// lookups per slice, lane z per slice, fixed-order wave sum.  bbox: the table's first row is
+// bbox[0] (PTYX_PREP_CALL), else row 0.  One wave per pattern.
 __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_batches, const int* crop,
                                  int n_scans, int Ny, int Nx, int* bid, int2* geo, const double* pref,
-                                 float* psums, int Nz = 1) {
+                                 float* psums, int Nz = 1, const int* bbox = nullptr) {
   const int j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -227,12 +286,17 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
     geo[j] = make_int2(cy, cx);
   }
   if (!pref) return;
+  const int r0 = bbox ? max(0, bbox[0]) : 0;
   double acc = 0;
-  for (int z = 0; z < Nz; ++z)
-    for (int r = lane; r < kN; r += 64) {
-      const double* prow = pref + ((size_t)z * Ny + cy + r) * (Nx + 1);
-      acc += prow[cx + kN] - prow[cx];
+  for (int z = lane; z < Nz; z += 64) {
+    const double* ps = pref + (size_t)z * Ny * (Nx + 1);
+    const double* lo = ps + (size_t)(cy + kN - 1) * (Nx + 1);   // rows r0 .. cy + N - 1
+    acc += lo[cx + kN] - lo[cx];
+    if (cy > r0) {                                              // minus rows r0 .. cy - 1
+      const double* hi = ps + (size_t)(cy - 1) * (Nx + 1);
+      acc -= hi[cx + kN] - hi[cx];
     }
+  }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) psums[(size_t)j * kNSum + kSumBase] = (float)acc;

@@ -662,7 +662,8 @@ struct ptyx_plan {
   size_t dyn3 = 0;            // extra dynamic LDS per k_fused3 workgroup (PTYX_F3_DYNLDS: occupancy experiments)
   float2* fpk = nullptr;      // packed probe spectrum / probe
   float2* oc = nullptr;       // A e^{iφ}
-  double* pref = nullptr;     // per-row prefix sums of |φ|^n (loss_sparse)
+  double* pref = nullptr;     // summed-area table of |φ|^n (loss_sparse), (Nz, Ny, Nx + 1)
+  double* preftot = nullptr;  // its per-chunk column totals, (Nz, ⌈Ny / kPrefChunk⌉, Nx + 1)
   float2* segslab = nullptr;  // per-segment unit probe-gradient spectra, packed
   int* segbid = nullptr;      // batch of each segment id (-1 unused)
   // k_obj_gather candidate bins (tile of each pattern's window origin), per call
@@ -942,6 +943,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->oc, (size_t)d.Ny * d.Nx)) ||
           (rc = dalloc(pl, &pl->bbox, 4)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Ny * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->preftot, (size_t)((d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk) * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
           (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
@@ -976,6 +978,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->fpk, N2)) || (rc = dalloc(pl, &pl->hpk, N2)) || (rc = dalloc(pl, &pl->bbox, 4)) ||
           (rc = dalloc(pl, &pl->oc, (size_t)d.Nz * d.Ny * d.Nx)) ||
           (rc = dalloc(pl, &pl->pref, (size_t)d.Nz * d.Ny * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->preftot,
+                       (size_t)d.Nz * ((d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk) * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) ||
           (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * 2)) ||
@@ -1143,7 +1147,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
                     // multi-GPU scan touches only its band of the replicated object)
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
-    hipLaunchKernelGGL(f3::k_bbox, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
+    hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (a.n_idx + 255) / 256))), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
                        d.Ny, d.Nx, pl->bbox);
   }
   if (!reuse) {
@@ -1151,12 +1155,19 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny * Nz), dim3(256), 0, st, a.obja, a.objp, d.Ny * Nz, d.Nx, pl->oc,
                        sparse ? pl->pref : nullptr, cfg->sparse_n,
                        cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, 128);
+    if (sparse) {   // row prefix sums → summed-area table (k_pattern_table3's window sums)
+      const int* bb = cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox;
+      const dim3 gp((d.Nx + 1 + 255) / 256, (d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk, Nz);
+      hipLaunchKernelGGL(f3::k_pref_cols1, gp, dim3(256), 0, st, pl->pref, pl->preftot, d.Ny, d.Nx, bb, 128);
+      hipLaunchKernelGGL(f3::k_pref_cols2, gp, dim3(256), 0, st, pl->pref, pl->preftot, d.Ny, d.Nx, bb, 128);
+    }
   }
   {
+    // (the table's first row: the bbox of the call that prepared it, PTYX_PREP_CALL only)
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
                        a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo,
-                       sparse ? pl->pref : nullptr, pl->psums, Nz);
+                       sparse ? pl->pref : nullptr, pl->psums, Nz, cfg->prep == PTYX_PREP_CALL ? pl->bbox : nullptr);
   }
   const bool single = cfg->single_on != 0;
   const int ci = single ? 0 : 1;
@@ -1303,7 +1314,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
                        a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
-    hipLaunchKernelGGL(f3::k_bbox, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
+    hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (n + 255) / 256))), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
                        pl->bbox, kN);
   }
   if (!reuse) {
