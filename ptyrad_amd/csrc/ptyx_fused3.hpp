@@ -61,7 +61,7 @@ struct F3Args {
   float* dsu;              // per-pattern position-gradient sums, unit coefficient (2 floats)
   int tail;                // probe or position gradient wanted
   float* dp_out;
-  // multislice (k_fused3ms): Nz slices, H K-packed; slots hold Nz planes per pattern (slice n
+  // multislice (k_fused3ms): Nz slices, H/N² K-packed; slots hold Nz planes per pattern (slice n
   // at slots + (pat·Nz + n)·N²), oc is (Nz, Ny, Nx)
   int Nz;
   const float2* hpk;
@@ -78,11 +78,12 @@ __device__ __forceinline__ int packed_rc(int t, int i) {
 
 // natural (N×N complex) → packed, one element per thread
 template <bool KL>
-__global__ void k_pack128(const float2* src, float2* dst) {
+__global__ void k_pack128(const float2* src, float2* dst, float scale = 1.0f) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= kN2) return;
   const int i = e >> 8, t = e & 255;
-  dst[e] = src[packed_rc<KL>(t, i)];
+  const float2 v = src[packed_rc<KL>(t, i)];
+  dst[e] = make_float2(v.x * scale, v.y * scale);
 }
 
 // Probe-gradient spectrum: Σ over segments (fixed order) of c_{m(seg)} × the segment's unit
@@ -459,6 +460,7 @@ __device__ __forceinline__ float2 pcmc(float2 a, float2 b) {
   return rf::pf(r);
 }
 __device__ __forceinline__ float2 pscale(float2 a, float s) { return rf::pf(rf::pv(a) * (rf::v2f){s, s}); }
+__device__ __forceinline__ float2 padd2(float2 a, float2 b) { return rf::pf(rf::pv(a) + rf::pv(b)); }
 
 // ------------------------------------------------------------------ LDS-DMA operand ring
 // PTYX_F3_RING = 1: the operands of the point-wise passes (object window, ψ⁰ park, F(P), segment
@@ -1207,13 +1209,14 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
           const float2 A = rp.a(C);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
+            v[4 * C + r] = SHIFT ? pcm(t.x[r], pcm(A, rp.B[r])) : t.x[r];
             pin(v[4 * C + r]);
           }
         });
   }
 
-  // K-layout pass: v ← v ⊙ (H or conj(H)) / N²
+  // K-layout pass: v ← v ⊙ (H or conj(H)) / N²  (hpk holds H/N², packed by the host: exact, N² is
+  // a power of two)
   auto prop_k = [&](bool conj_h) {
     const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
     pipeline<16>(
@@ -1227,7 +1230,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int k = 4 * C + r;
-            v[k] = cscale(conj_h ? cmulc(v[k], t.x[r]) : cmul(v[k], t.x[r]), inv_n2);
+            v[k] = conj_h ? pcmc(v[k], t.x[r]) : pcm(v[k], t.x[r]);
             pin(v[k]);
           }
         });
@@ -1241,7 +1244,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     if constexpr (SHIFT) {
       fft_inv(v, buf, lc, cd.wsign);
 #pragma unroll
-      for (int j = 0; j < 64; ++j) v[j] = cscale(v[j], inv_n2);
+      for (int j = 0; j < 64; ++j) v[j] = pscale(v[j], inv_n2);
     }
     // ------------------------------------------------ slices: park ψⁿ, ×O_n, propagate
     for (int n = 0; n < Nz; ++n) {
@@ -1263,7 +1266,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
               for (int r = 0; r < 8; ++r) {
                 const int j = 8 * C + r;
                 st2(v[j], r_slot, vslot, 2048 * j);
-                v[j] = cmul(v[j], t.x[r]);
+                v[j] = pcm(v[j], t.x[r]);
                 pin(v[j]);
               }
             });
@@ -1293,6 +1296,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float S = 0.f, Ms = 0.f;
+    const float occ_n2 = occ * inv_n2, occ2_n = 2.0f * occ * inv_n;
     {
       const int r = (fx + 64) & 127;
       const int b = 1 - l0;
@@ -1307,10 +1311,10 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int k = 4 * kq + e;
-          const float2 Psi = cscale(v[k], inv_n);
-          Iv[e] = fmaf(occ, cabs2(Psi), kDpEps);
+          // Ψ = v/N with N a power of two: occ|Ψ|² = |v|²·(occ/N²) and g_Ψ = v·(2 occ u/N), exactly
+          Iv[e] = fmaf(occ_n2, cabs2(v[k]), kDpEps);
           const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
-          v[k] = cscale(Psi, 2.0f * occ * u);
+          v[k] = pscale(v[k], occ2_n * u);
           pin(v[k]);
         }
         {
@@ -1358,9 +1362,9 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const int j = 4 * C + r;
-                const float2 gv = cscale(v[j], sc);
-                st2_stream(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // slice n: g·conj(ψⁿ)
-                v[j] = cmulc(gv, t.y[r]);                                  // g·conj(O_n)
+                const float2 gv = pscale(v[j], sc);
+                st2_stream(pcmc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // slice n: g·conj(ψⁿ)
+                v[j] = pcmc(gv, t.y[r]);                                  // g·conj(O_n)
                 pin(v[j]);
               }
             });
@@ -1403,13 +1407,13 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
-              const float2 W = cmul(A, rc.B[r]);
-              const float2 FW = cmul(t.x[r], W);
+              const float2 W = pcm(A, rc.B[r]);
+              const float2 FW = pcm(t.x[r], W);
               const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);
               sim += im;
               kim = fmaf((float)k, im, kim);
-              st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);
-              v[k] = cmul(t.x[r], cmul(An, rn.B[r]));
+              st2(padd2(t.y[r], pcmc(v[k], W)), r_slab_st, vpk, 2048 * k);
+              v[k] = pcm(t.x[r], pcm(An, rn.B[r]));
               pin(v[k]);
             }
           });

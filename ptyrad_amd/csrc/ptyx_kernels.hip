@@ -675,7 +675,7 @@ struct ptyx_plan {
   int* blist = nullptr;       // (max_patterns) patterns by bin
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
-  float2* hpk = nullptr;      // k_fused3ms: K-packed propagator
+  float2* hpk = nullptr;      // k_fused3ms: K-packed propagator / N²
   int* bbox = nullptr;        // k_fused3*: bounding box of a call's windows
   bool ms3 = false;           // k_fused3ms (multislice register engine) available
   // N = 256 stripe engine (ptyx_stripe.hpp): per-call intermediates for stripe_cap patterns
@@ -1141,7 +1141,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   if (Nz > 1 && !reuse) {
     ProfScope ps(pl, kKPack, st);
-    hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk);
+    hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk, 1.0f / N2);   // H/N²
   }
   if (pl->bbox) {   // rows / tiles outside the call's windows are skipped (a rank's shard of a
                     // multi-GPU scan touches only its band of the replicated object)

@@ -69,6 +69,9 @@ constexpr int kMaxO = 2;
 #ifndef PTYX_S5_WG
 #define PTYX_S5_WG 2
 #endif
+#ifndef PTYX_S5_FP_L2
+#define PTYX_S5_FP_L2 0
+#endif
 
 struct SArgs {
   int n, P, O, Ny, Nx, n_scans, meas_f16;
@@ -596,8 +599,13 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   const int P = a.P;
   constexpr float two_pi_n2 = 6.283185307179586f / (float)kN2;
   const int vcol = (m.slot * kN + kx) * 8;
-  float2 fp[16], acc[16];
+  // PTYX_S5_FP_L2: F(P)'s stripe is re-read from L2 after each pattern's transform instead of
+  // being held in 32 VGPRs across the sweep (fewer registers: more workgroups per CU)
+  float2 acc[16];
+#if !PTYX_S5_FP_L2
+  float2 fp[16];
   ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
+#endif
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
   const float gx = shift_g(kx);
@@ -616,6 +624,10 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
     for (int r = 0; r < 16; ++r) v[r] = nxt[r];
     if (j + a.groups < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
+#if PTYX_S5_FP_L2
+    float2 fp[16];
+    ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, opq(vcol));
+#endif
     const float2 TW = f3::pcm(ramp_t(sy, m.slot), f3::cis_rev(-sx * gx));   // cis(−sy·slot/N)·wx
     float sy_acc = 0.f, sim = 0.f;
 #pragma unroll
