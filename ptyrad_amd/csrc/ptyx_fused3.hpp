@@ -1171,7 +1171,10 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 //             n > 0:  g ← F⁻¹(conj(H) ⊙ F(g))/N²            (the propagator's adjoint)
 //   then the probe / position pass on g = ∂ℓ/∂ψ⁰ exactly as k_fused3.
 // 4·Nz FFTs per pattern, the algorithmic count: no forward is recomputed.  Each slot plane
-// first parks ψⁿ and is overwritten by slice n's object gradient.
+// first parks ψⁿ and is overwritten by slice n's object gradient.  With shifts (kRing) the 2·Nz
+// per-slice point-wise passes stream their operands through k_fused3's LDS-DMA ring: slice n's
+// object window (forward; ψⁿ parked in the ring's park layout) or its park + object window
+// (backward) are issued during the preceding inverse FFT, D register pairs ahead of their use.
 template <bool SHIFT, bool SINGLE, int QM>
 __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
   using namespace rf;
@@ -1190,6 +1193,8 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
   const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
   const Rsrc r_hpk = rsrc(a.hpk, kN2 * 8);
   const float gy = (float)((cd.fixed + 64) & 127) * inv_n;
+  constexpr bool kRing = PTYX_F3_RING && SHIFT;
+  const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;   // LDS byte address
 
   float2 v[64];
   {
@@ -1241,16 +1246,72 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
     const PatInfo p = pat_info<SHIFT>(a, pat);
+    // ring (kRing): this wave's 16 KiB of the exchange buffer; slice n's operand descriptors
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0w = lds0 + (wv << 14);
+    const float2* ringw = buf + (wv << 11);
+    const int os = __builtin_amdgcn_readfirstlane(8 * Nx);
+    const unsigned obytes = (unsigned)(((kN - 1) * Nx + kN) * 8);
+    auto s_obj = [&](int n) { return srd(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, obytes); };
+    auto s_park = [&](int n) { return srd(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8); };
+    // forward ring: the object window, 16 register pairs ahead (A = 1)
+    auto issue1 = [&](auto Q, const v4u& so, int voff) {
+      constexpr int q = decltype(Q)::value;
+      dma_m<2 * q>(so, voff, m0w + (q % 16) * 1024, os);
+    };
+    auto pre1 = [&](int n) {   // (mid() of the inverse FFT before slice n's pass)
+      if constexpr (kRing) {
+        const v4u so = s_obj(n);
+        const int vo = dma_off_obj(rf::opaque(tid) & 63, wv, os);
+        rf::sfor<0, 16>([&](auto Q) { issue1(Q, so, vo); });
+      }
+    };
+    // backward ring: slice n's park + object window, 8 register pairs ahead (A = 2)
+    auto issue3 = [&](auto Q, const v4u& sp, const v4u& so, int vpo, int voo) {
+      constexpr int q = decltype(Q)::value;
+      dma_c<4096 * q>(sp, vpo, m0w + (q % 8) * 2048);
+      dma_m<2 * q>(so, voo, m0w + (q % 8) * 2048 + 1024, os);
+    };
+    auto pre3 = [&](int n) {
+      if constexpr (kRing) {
+        const v4u sp = s_park(n), so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+        rf::sfor<0, 8>([&](auto Q) { issue3(Q, sp, so, vpo, voo); });
+      }
+    };
     if constexpr (SHIFT) {
-      fft_inv(v, buf, lc, cd.wsign);
+      fft_inv(v, buf, lc, cd.wsign, [&] { pre1(0); });
 #pragma unroll
       for (int j = 0; j < 64; ++j) v[j] = pscale(v[j], inv_n2);
     }
     // ------------------------------------------------ slices: park ψⁿ, ×O_n, propagate
     for (int n = 0; n < Nz; ++n) {
       const Rsrc r_slot = rsrc(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8);
-      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
-      {
+      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, obytes);
+      if constexpr (kRing) {
+        const v4u so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vo = dma_off_obj(lam, wv, os);
+        const int vpark = park_off(lam, wv);
+        const int io = obj_img(lam);
+        rf::sfor<0, 32>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          vm_wait<ring_wait_count(q, 1, 0, 16)>();
+          const float2* sl = ringw + (q % 16) * 128;
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const int j = 2 * q + rb;
+            const float2 O = sl[rb * 64 + io];
+            st2(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
+            v[j] = pcm(v[j], O);
+            pin(v[j]);
+          }
+          if constexpr (q + 16 < 32) issue1(std::integral_constant<int, q + 16>{}, so, vo);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();   // every wave is done with its ring before the next exchange
+      } else {
         const int tq = rf::opaque(threadIdx.x);
         const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
         const int ostr = rf::opaque(8 * Nx);
@@ -1274,7 +1335,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
       if (n + 1 < Nz) {
         fft_fwd(v, buf, lc, cd.wsign);
         prop_k(false);
-        fft_inv(v, buf, lc, cd.wsign);
+        fft_inv(v, buf, lc, cd.wsign, [&] { pre1(n + 1); });
       }
     }
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
@@ -1337,13 +1398,37 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
         ps[3 - base] = 0.f;
       }
     }
-    fft_inv(v, buf, lc, cd.wsign);
+    fft_inv(v, buf, lc, cd.wsign, [&] { pre3(Nz - 1); });
     // ------------------------------------------------ slices backwards
     for (int n = Nz - 1; n >= 0; --n) {
       const Rsrc r_slot = rsrc(a.slots + ((size_t)pat * Nz + n) * kN2, kN2 * 8);
-      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, (unsigned)(((kN - 1) * Nx + kN) * 8));
+      const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)p.cy * Nx + p.cx, obytes);
       const float sc = n == Nz - 1 ? inv_n : 1.0f;   // far-field ortho scale once; propagation scaled in K
-      {
+      if constexpr (kRing) {
+        const v4u sp = s_park(n), so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+        const int io = obj_img(lam);
+        const int vslot = 8 * ((rf::opaque(tid) & 1) * kN + fixed_of(rf::opaque(tid)));
+        rf::sfor<0, 32>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          vm_wait<ring_wait_count(q, 2, 0, 8)>();
+          const float2* sl = ringw + (q % 8) * 256;
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const int j = 2 * q + rb;
+            const float2 ps = sl[rb * 64 + lam];
+            const float2 O = sl[128 + rb * 64 + io];
+            const float2 gv = pscale(v[j], sc);
+            st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // slice n: g·conj(ψⁿ)
+            v[j] = pcmc(gv, O);                                  // g·conj(O_n)
+            pin(v[j]);
+          }
+          if constexpr (q + 8 < 32) issue3(std::integral_constant<int, q + 8>{}, sp, so, vpo, voo);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();   // every wave is done with its ring before the next exchange
+      } else {
         const int tq = rf::opaque(threadIdx.x);
         const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
         const int ostr = rf::opaque(8 * Nx);
@@ -1372,7 +1457,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
       if (n > 0) {
         fft_fwd(v, buf, lc, cd.wsign);
         prop_k(true);
-        fft_inv(v, buf, lc, cd.wsign);
+        fft_inv(v, buf, lc, cd.wsign, [&] { pre3(n - 1); });
       }
     }
     // ------------------------------------------------ probe / position gradient, next pattern's v
