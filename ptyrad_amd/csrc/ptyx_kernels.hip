@@ -686,6 +686,7 @@ struct ptyx_plan {
   float2* st23 = nullptr;
   float* spsum = nullptr;
   float* sdsp = nullptr;
+  float2* ssxy = nullptr;     // (max_patterns) per-call (sy, sx)
   float2* sslab = nullptr;
   bool sgather = false;       // stripe object gradient: per-pattern slots + k_obj_gather (else f32 atomics)
   long long seg_cap = 0;      // segment ids the segslab holds
@@ -878,6 +879,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->st23, (size_t)cap * d.P * d.O * N2)) ||
           (rc = dalloc(pl, &pl->spsum, (size_t)cap * sp::kStripes * kNSum)) ||
           (rc = dalloc(pl, &pl->sdsp, (size_t)cap * sp::kStripes * d.P * 2)) ||
+          (rc = dalloc(pl, &pl->ssxy, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->sslab, (size_t)groups * d.P * N2)) ||
           (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->oc, (size_t)d.O * d.Ny * d.Nx)) || (rc = dalloc(pl, &pl->bbox, 4))) {
@@ -1312,7 +1314,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
-                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo);
+                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.shifts, pl->ssxy);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
     hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (n + 255) / 256))), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
                        pl->bbox, kN);
@@ -1324,7 +1326,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   SArgs s{};
   s.n = n; s.P = P; s.O = O; s.Ny = d.Ny; s.Nx = d.Nx; s.n_scans = d.n_scans; s.meas_f16 = a.meas_f16;
-  s.idx = a.idx; s.bid = pl->bid; s.geo = pl->geo; s.shifts = a.shifts; s.mrow = a.mrow;
+  s.idx = a.idx; s.bid = pl->bid; s.geo = pl->geo; s.shifts = a.shifts; s.sxy = pl->ssxy; s.mrow = a.mrow;
   s.Fp = pl->Fp; s.oc = pl->oc; s.obja = a.obja; s.objp = a.objp; s.meas = a.meas; s.occu = a.occu;
   s.q = single ? cfg->single_q : cfg->poissn_q;
   s.eps2 = cfg->poissn_eps;

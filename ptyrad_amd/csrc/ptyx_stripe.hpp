@@ -79,6 +79,8 @@ struct SArgs {
   const int* bid;        // mini-batch per pattern
   const int2* geo;       // clamped window origin per pattern
   const float* shifts;   // (n_scans, 2)
+  const float2* sxy;     // (n) this call's patterns' (sy, sx), gathered by k_s_table: one load, no
+                         // idx → shifts chain in front of the passes' first barrier
   const int* mrow;       // measurement row of a scan index (NULL: the index itself)
   const float2* Fp;      // (P, N, N) F(probe), natural order
   const float2* oc;      // (O, Ny, Nx) A e^{iφ}
@@ -234,15 +236,15 @@ __global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
   __shared__ float2 tw[kN];
   __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y, p = blockIdx.z;
-  const float sy = a.shifts[2 * scan_of(a, j)];
-  load_tw(tw, a.twg);
-  ramp_row(rl, sy);
-  __syncthreads();
   const Map m = map_of<true>(opq(threadIdx.x));
   const int kx = s * kL + m.line;
   const int vcol = (m.slot * kN + kx) * 8;
   float2 v[16];
-  ldb<kColStride>(v, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
+  ldb<kColStride>(v, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);   // (in flight during the setup)
+  const float sy = a.sxy[j].x;
+  load_tw(tw, a.twg);
+  ramp_row(rl, sy);
+  __syncthreads();
   const float2 T = ramp_t(sy, m.slot);
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = f3::pcm(v[r], f3::pcm(T, rl[r]));
@@ -259,8 +261,7 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
   __shared__ float red[4 * kMaxO];
   __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y;
-  const int sidx = scan_of(a, j);
-  const float sx = a.shifts[2 * sidx + 1];
+  const float sx = a.sxy[j].y;
   load_tw(tw, a.twg);
   ramp_row(rl, sx);
   __syncthreads();
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
   __shared__ float2 obl[OB_LDS ? 16 * 256 : 1];
   __shared__ float2 rl[16];
   const int j = blockIdx.x, s = blockIdx.y;
-  const float sx = a.shifts[2 * scan_of(a, j) + 1];
+  const float sx = a.sxy[j].y;
   load_tw(tw, a.twg);
   if constexpr (!PARK) ramp_row(rl, sx);
   __syncthreads();
@@ -611,10 +612,16 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   const float gx = shift_g(kx);
   float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
   if (gi < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
+  // the next pattern's shifts and mini-batch are loaded one pattern ahead too
+  float2 sh_n = gi < a.n ? a.sxy[gi] : make_float2(0.f, 0.f);
+  int bid_n = gi < a.n ? a.bid[gi] : 0;
   for (int j = gi, it = 0; j < a.n; j += a.groups, ++it) {
-    const int sidx = scan_of(a, j);
-    const float sy = a.shifts[2 * sidx], sx = a.shifts[2 * sidx + 1];
-    const float c = a.coef[(size_t)a.bid[j] * kNCoef + a.ci];
+    const float sy = sh_n.x, sx = sh_n.y;
+    const float c = a.coef[(size_t)bid_n * kNCoef + a.ci];
+    if (j + a.groups < a.n) {
+      sh_n = a.sxy[j + a.groups];
+      bid_n = a.bid[j + a.groups];
+    }
     // (written here, read after fft_line's barriers; the other copy may still be read by threads
     // finishing the previous pattern)
     float2* rlj = rl[it & 1];
@@ -657,7 +664,7 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
 // ---------------------------------------------------------------------------------- small kernels
 // pattern → (mini-batch, clamped window origin)
 __global__ void k_s_table(const int* idx, int n, const int* boff, int n_batches, const int* crop, int n_scans, int Ny,
-                          int Nx, int* bid, int2* geo) {
+                          int Nx, int* bid, int2* geo, const float* shifts, float2* sxy) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   int lo = 0, hi = n_batches;
@@ -669,6 +676,7 @@ __global__ void k_s_table(const int* idx, int n, const int* boff, int n_batches,
   bid[j] = lo;
   const int s = min(max(idx[j], 0), n_scans - 1);
   geo[j] = make_int2(min(max(crop[2 * s], 0), Ny - kN), min(max(crop[2 * s + 1], 0), Nx - kN));
+  sxy[j] = make_float2(shifts[2 * s], shifts[2 * s + 1]);
 }
 
 // psums[j][i] = Σ_stripes psum_s[j][s][i]   (fixed order)
