@@ -561,6 +561,11 @@ __device__ __forceinline__ int obj_img(int lam) {
   return ((f >> 4) << 5) + (((f & 15) >> 1) << 2) + ((lam & 1) << 1) + (f & 1);
 }
 
+// PTYX_F3_CARRY: a pattern's scalars come from the previous pattern's post4 pass (0: reloaded)
+#ifndef PTYX_F3_CARRY
+#define PTYX_F3_CARRY 1
+#endif
+
 // PTYX_F3_PHASES=1 (diagnostic builds only): s_memtime stamps at the phase boundaries of wave 0;
 // workgroups 0 and 1 printf their per-phase cycle totals at exit.
 #ifndef PTYX_F3_PHASES
@@ -752,13 +757,18 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         });
   }
 
+  // the pattern's scalars are carried over from the previous pattern's post4 pass (which loads
+  // them for the next v), and its mini-batch for the segment test: no scalar-load round trips at
+  // the top of a pattern
+  PatInfo p_nxt = pat_info<SHIFT>(a, p0);
+  int m_prev = 0;
   for (int pat = p0; pat < p1; ++pat) {
     // per-thread bases re-derived from an opaque thread id each pattern and pass: keeps LICM /
     // CSE from holding 64 per-register offsets live across the transforms (they would spill)
     const int tid = rf::opaque(threadIdx.x);
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
-    const PatInfo p = pat_info<SHIFT>(a, pat);
+    const PatInfo p = PTYX_F3_CARRY ? p_nxt : pat_info<SHIFT>(a, pat);
     // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → offset 2048·j
     const Rsrc r_slot = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
     const int vslot0 = 8 * (l0 * kN + fx);
@@ -976,7 +986,9 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     // and so initialises it; later patterns accumulate.  Without probe/position gradients (tail
     // false) the same pass runs without the FFT and its slab / sums are never used.
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || s_ld(a.bid + (pat - 1)) != p.m;   // (uniform)
+    const bool first = pat == p0 || (PTYX_F3_CARRY ? m_prev : s_ld(a.bid + (pat - 1))) != p.m;   // (uniform)
+    m_prev = p.m;
+    p_nxt = pn;
     const bool last = kHold && (pat == p1 - 1 || s_ld(a.bid + (pat + 1)) != p.m);   // (uniform; PTYX_F3_HOLD flushes the slab)
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
@@ -1241,11 +1253,13 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
         });
   };
 
+  PatInfo p_nxt = pat_info<SHIFT>(a, p0);   // (carried over as in k_fused3)
+  int m_prev = 0;
   for (int pat = p0; pat < p1; ++pat) {
     const int tid = rf::opaque(threadIdx.x);
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
-    const PatInfo p = pat_info<SHIFT>(a, pat);
+    const PatInfo p = PTYX_F3_CARRY ? p_nxt : pat_info<SHIFT>(a, pat);
     // ring (kRing): this wave's 16 KiB of the exchange buffer; slice n's operand descriptors
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0w = lds0 + (wv << 14);
@@ -1462,7 +1476,9 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     }
     // ------------------------------------------------ probe / position gradient, next pattern's v
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || s_ld(a.bid + (pat - 1)) != p.m;
+    const bool first = pat == p0 || (PTYX_F3_CARRY ? m_prev : s_ld(a.bid + (pat - 1))) != p.m;
+    m_prev = p.m;
+    p_nxt = pn;
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
