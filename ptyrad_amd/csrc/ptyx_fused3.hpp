@@ -561,6 +561,16 @@ __device__ __forceinline__ int obj_img(int lam) {
   return ((f >> 4) << 5) + (((f & 15) >> 1) << 2) + ((lam & 1) << 1) + (f & 1);
 }
 
+// PTYX_F3_PARK_NT / PTYX_F3MS_PARK_NT: the ψ⁰ / ψⁿ park stores as non-temporal streams.
+// Measured (profiles/r02/ab/r02y_pnt_*): k_fused3 reads its park two transforms later, partly
+// from L2, and slows down (11.35-11.56 → 11.66-11.68 ms): off; k_fused3ms reads slice n's park
+// 2·(Nz − n) transforms later: 2.672 → 2.641 s per c4 step: on.
+#ifndef PTYX_F3_PARK_NT
+#define PTYX_F3_PARK_NT 0
+#endif
+#ifndef PTYX_F3MS_PARK_NT
+#define PTYX_F3MS_PARK_NT 1
+#endif
 // PTYX_F3_CARRY: a pattern's scalars come from the previous pattern's post4 pass (0: reloaded)
 #ifndef PTYX_F3_CARRY
 #define PTYX_F3_CARRY 1
@@ -816,7 +826,10 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
           const float2 O = sl[rb * 64 + io];
-          if (!PTYX_F3_EXP_NOPARK) st2(v[j], r_park, vpark, 2048 * j);
+          if (!PTYX_F3_EXP_NOPARK) {
+            if (PTYX_F3_PARK_NT) st2_stream(v[j], r_park, vpark, 2048 * j);
+            else st2(v[j], r_park, vpark, 2048 * j);
+          }
           v[j] = pcm(v[j], PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : O);
           pin(v[j]);
         }
@@ -1317,7 +1330,8 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
           for (int rb = 0; rb < 2; ++rb) {
             const int j = 2 * q + rb;
             const float2 O = sl[rb * 64 + io];
-            st2(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
+            if (PTYX_F3MS_PARK_NT) st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
+            else st2(v[j], r_slot, vpark, 2048 * j);
             v[j] = pcm(v[j], O);
             pin(v[j]);
           }

@@ -170,6 +170,34 @@ __device__ __forceinline__ void stb(const float2 (&v)[16], float2* base, unsigne
 #pragma unroll
   for (int k = 0; k < 16; ++k) f3::st2(v[k], r, vo, k * STRIDE);
 }
+// The same for the per-call intermediate fields (T1…T4, ψ⁰, slots: written once, read once by
+// another pass): PTYX_S_NT = 1 marks them non-temporal (aux "nt"), so they do not displace the
+// lines that are re-read (F(P), the object rows, the twiddles).  Measured (profiles/r02/ab/
+// r02y_nt_*): c5 222 → 229 k, c3 72.7 → 75.8 k patterns/s.
+#ifndef PTYX_S_NT
+#define PTYX_S_NT 1
+#endif
+template <int STRIDE>
+__device__ __forceinline__ void lds_(float2 (&v)[16], const float2* base, unsigned bytes, int voff) {
+  const f3::Rsrc r = f3::rsrc(base, bytes);
+  const int vo = opq(voff);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, vo + k * STRIDE, 0, PTYX_S_NT ? 2 : 0);
+    v[k] = make_float2(__uint_as_float(u[0]), __uint_as_float(u[1]));
+  }
+  fence_sched();
+}
+template <int STRIDE>
+__device__ __forceinline__ void sts_(const float2 (&v)[16], float2* base, unsigned bytes, int voff) {
+  const f3::Rsrc r = f3::rsrc(base, bytes);
+  const int vo = opq(voff);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v[k].x), __float_as_uint(v[k].y)};
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, vo + k * STRIDE, 0, PTYX_S_NT ? 2 : 0);
+  }
+}
 // object window of pattern j (origin g0), mode o: base and byte size
 __device__ __forceinline__ const float2* win_base(const SArgs& a, int o, int2 g0) {
   return a.oc + ((size_t)o * a.Ny + g0.x) * a.Nx + g0.y;
@@ -249,7 +277,7 @@ __global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = f3::pcm(v[r], f3::pcm(T, rl[r]));
   fft_line<+1, true>(v, m, xb, tw);
-  stb<kColStride>(v, a.t14 + ((size_t)j * a.P + p) * kN2, kFieldBytes, vcol);
+  sts_<kColStride>(v, a.t14 + ((size_t)j * a.P + p) * kN2, kFieldBytes, vcol);
 }
 
 // ---------------------------------------------------------------------------------- P2
@@ -280,15 +308,15 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
   // registers of a second object mode would not fit beside them)
   constexpr bool PREF = O_ == 1;
   float2 nxt[16];
-  if constexpr (PREF) ldb<kRowStride>(nxt, a.t14 + (size_t)j * P * kN2, kFieldBytes, vrow);
+  if constexpr (PREF) lds_<kRowStride>(nxt, a.t14 + (size_t)j * P * kN2, kFieldBytes, vrow);
   for (int p = 0; p < P; ++p) {
     float2 v[16];
     if constexpr (PREF) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = nxt[r];
-      if (p + 1 < P) ldb<kRowStride>(nxt, a.t14 + ((size_t)j * P + p + 1) * kN2, kFieldBytes, vrow);
+      if (p + 1 < P) lds_<kRowStride>(nxt, a.t14 + ((size_t)j * P + p + 1) * kN2, kFieldBytes, vrow);
     } else {
-      ldb<kRowStride>(v, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+      lds_<kRowStride>(v, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     }
     const float2* rlo = rl + opq(0);   // (re-read per mode, not hoisted into 32 registers)
 #pragma unroll
@@ -296,14 +324,14 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
     fft_line<+1, false>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n2);
-    if (a.psi0) stb<kRowStride>(v, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+    if (a.psi0) sts_<kRowStride>(v, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
       float2 u[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) u[k] = cmul(v[k], ob[o][k]);
       fft_line<-1, false>(u, m, xb, tw);
-      stb<kRowStride>(u, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
+      sts_<kRowStride>(u, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
     });
   }
   // loss_sparse (losses.py:101): Σ |φ|ⁿ over this stripe of the window, per object mode
@@ -355,7 +383,7 @@ __global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : HOLD == 0 ? PTY
   float2* base = a.t23 + (size_t)j * PO * kN2;
   const int vcol = (m.slot * kN + kx) * 8;
   auto far_field = [&](int q, float2 (&v)[16]) {
-    ldb<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);
+    ldb<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);   // (modes past the hold are read again)
     fft_line<-1, true>(v, m, xb, tw);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], inv_n);
@@ -418,7 +446,7 @@ __global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : HOLD == 0 ? PTY
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cscale(v[k], c * u[k]);
     fft_line<+1, true>(v, m, xb, tw);
-    stb<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);
+    sts_<kColStride>(v, base + (size_t)q * kN2, kFieldBytes, vcol);
   };
   for (int q = HOLD; q < PO; ++q) {
     float2 v[16];
@@ -478,9 +506,9 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
   for (int p = 0; p < P; ++p) {
     float2 psr[16];
     if constexpr (PARK) {
-      ldb<kRowStride>(psr, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+      lds_<kRowStride>(psr, a.psi0 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
     } else {   // ψ⁰_p = F⁻¹_x(wx · T1_p)/N² again: one row transform instead of a parked field
-      ldb<kRowStride>(psr, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
+      lds_<kRowStride>(psr, a.t14 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);
       const float2 T = ramp_t(opqf(sx), m.slot);
       const float2* rlo = rl + opq(0);
 #pragma unroll
@@ -497,7 +525,7 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
     rf::sfor<0, O_>([&](auto OO) {
       constexpr int o = decltype(OO)::value;
       float2 v[16], ob[16];
-      ldb<kRowStride>(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
+      lds_<kRowStride>(v, a.t23 + ((size_t)j * P * O_ + p * O_ + o) * kN2, kFieldBytes, vrow);
       fft_line<+1, false>(v, m, xb, tw);
       const float2(&psi)[16] = psr;
       if constexpr (OB_LDS) {
@@ -525,7 +553,7 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) gq[k] = GP_LDS ? gpl[k * 256 + threadIdx.x] : gp[GP_LDS ? 0 : k];
       fft_line<-1, false>(gq, m, xb, tw);
-      stb<kRowStride>(gq, a.t4 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);   // over T1_p's rows (read above)
+      sts_<kRowStride>(gq, a.t4 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);   // over T1_p's rows (read above)
     }
   }
 #ifdef PTYX_S4_EXP_NOGRAD   // cost-attribution build (results WRONG): no object-gradient epilogue
@@ -536,7 +564,7 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
     // slot o of pattern j = T3 field (p = 0, o), whose rows of this stripe were consumed above
     // (no other workgroup touches them): natural (N, N) rows, c_m applied by k_obj_gather
 #pragma unroll
-    for (int o = 0; o < O_; ++o) stb<kRowStride>(so[o], a.oslot + ((size_t)j * P * O_ + o) * kN2, kFieldBytes, vrow);
+    for (int o = 0; o < O_; ++o) sts_<kRowStride>(so[o], a.oslot + ((size_t)j * P * O_ + o) * kN2, kFieldBytes, vrow);
     return;
   }
   // object gradient.  The slot accumulators are re-mapped through the (now free) exchange buffer
@@ -611,7 +639,7 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
   const float gx = shift_g(kx);
   float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
-  if (gi < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
+  if (gi < a.n) lds_<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
   // the next pattern's shifts and mini-batch are loaded one pattern ahead too
   float2 sh_n = gi < a.n ? a.sxy[gi] : make_float2(0.f, 0.f);
   int bid_n = gi < a.n ? a.bid[gi] : 0;
@@ -629,7 +657,7 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = nxt[r];
-    if (j + a.groups < a.n) ldb<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
+    if (j + a.groups < a.n) lds_<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
 #if PTYX_S5_FP_L2
     float2 fp[16];
