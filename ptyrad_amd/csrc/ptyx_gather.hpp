@@ -37,6 +37,9 @@ struct GatherArgs {
   const int* boff = nullptr;   // bin offsets (tiles + 1) into blist, or NULL: scan every pattern
   const int* blist = nullptr;  // pattern indices by bin, ascending within a bin
 };
+#ifndef PTYX_GATHER_NT
+#define PTYX_GATHER_NT 0
+#endif
 #ifndef PTYX_GTY
 #define PTYX_GTY 16
 #endif
@@ -130,7 +133,17 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
       for (int r = 0; r < kGTY; ++r) {
         const int row = ty + r - cy;
         const int srow = ROWPERM ? 2 * (row & (N / 2 - 1)) + (row >> 6) : row;
-        v[r] = (colok && row >= 0 && row < N) ? src[srow * N + col] : make_float2(0.f, 0.f);
+        if (colok && row >= 0 && row < N) {
+#if PTYX_GATHER_NT   // slots are read once: non-temporal, so they do not displace the object rows
+          typedef float f2v __attribute__((ext_vector_type(2)));
+          const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(src + srow * N + col));
+          v[r] = make_float2(t.x, t.y);
+#else
+          v[r] = src[srow * N + col];
+#endif
+        } else {
+          v[r] = make_float2(0.f, 0.f);
+        }
       }
 #pragma unroll
       for (int r = 0; r < kGTY; ++r) {
