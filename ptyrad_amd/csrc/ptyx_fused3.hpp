@@ -571,6 +571,10 @@ __device__ __forceinline__ int obj_img(int lam) {
 #ifndef PTYX_F3MS_PARK_NT
 #define PTYX_F3MS_PARK_NT 1
 #endif
+// PTYX_F3_SLAB_NT: the segment slab's stores as non-temporal (it is re-read one pattern later)
+#ifndef PTYX_F3_SLAB_NT
+#define PTYX_F3_SLAB_NT 0
+#endif
 // PTYX_F3_CARRY: a pattern's scalars come from the previous pattern's post4 pass (0: reloaded)
 #ifndef PTYX_F3_CARRY
 #define PTYX_F3_CARRY 1
@@ -1059,7 +1063,9 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
           if (!PTYX_F3_EXP_NOSLAB) {
             const float2 so = sl[128 + rb * 64 + lam];
             const float2 gw = pcmc(v[k], W);                      // + conj(W) G (unit)
-            st2(rf::pf(__builtin_elementwise_fma((rf::v2f){keep, keep}, rf::pv(so), rf::pv(gw))), r_slab_st, vpk, 2048 * k);
+            const float2 sn = rf::pf(__builtin_elementwise_fma((rf::v2f){keep, keep}, rf::pv(so), rf::pv(gw)));
+            if (PTYX_F3_SLAB_NT) st2_stream(sn, r_slab_st, vpk, 2048 * k);
+            else st2(sn, r_slab_st, vpk, 2048 * k);
           }
           v[k] = pcm(F, pcm(An, rn.B[r]));                        // next pattern: F(P)·W_next
           pin(v[k]);
