@@ -118,9 +118,11 @@ def cpu_baseline(n, bsize, sample):
         res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
     pats = sum(r[0] for r in res)
-    out = {"value": round(pats / wall, 1), "unit": "patterns/s", "cores": len(jobs), "kind": "port",
+    busy = max(r[1] for r in res)     # the workers' compute (they run concurrently), pool start excluded
+    out = {"value": round(pats / busy, 1), "unit": "patterns/s", "cores": len(jobs), "kind": "port",
            "sample": f"{pats} patterns of the c2 shape ({len(jobs)} processes x mini-batches of {bsize}), N={n}, "
-                     f"P=O=Nz=1, shifts on, oracle/ptyx_oracle.py complex64 NumPy, wall {wall:.1f}s incl. pool start"}
+                     f"P=O=Nz=1, shifts on, oracle/ptyx_oracle.py complex64 NumPy; rate over the slowest worker's "
+                     f"compute time {busy:.1f}s (wall {wall:.1f}s incl. pool start: {pats / wall:.1f} patterns/s)"}
     ratio = os.path.join(ROOT, "tests", "golden", "cpu_ratio.json")
     if os.path.exists(ratio):   # reference CPU path vs this port, same cores, measured in the build container
         r = json.load(open(ratio))
@@ -337,20 +339,24 @@ def main():
     f_alg = n_fft * 5 * N * N * math.log2(N * N)
     roof = None
     stripe = [k for k in kstats if k.startswith("k_s")]
+    # HBM traffic of the dominant kernel from its PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate
+    # rocprofv3 --pmc runs of this bench command; tools/gpu_profile.sh -> profiles/make_traffic.py):
+    # measured at the commit named in `traffic_source`, not inside this run
+    tr = {}
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        tr = json.load(open(tpath)).get(a.config, {})
+    tsrc = f"{tr['source']} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE at {tr['measured_at']})" if tr else None
     if "k_fused" in kstats:
         # the register engines (k_fused3 / k_fused3ms): forward + loss + adjoint in one launch per call
         launches, dom_ms = kstats["k_fused"]
         avg_s = dom_ms / launches / 1e3
         per_launch = n_local / max(1, launches // a.steps)       # patterns per launch
         achieved = b_alg * per_launch / avg_s / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_c2.json")
-        if a.config == "c2" and os.path.exists(pmc):
-            # PMC summary of the same workload (profiles/collect_pmc.sh → summarize_pmc.py)
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch", {}).get("k_fused3")
+        traffic = round(tr["bytes_per_pattern"] * per_launch) if tr.get("bytes_per_pattern") else None
         roof = {"kernel": "k_fused3" if Nz == 1 else "k_fused3ms", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": tsrc,
                 "alg_bytes_per_launch": int(b_alg * per_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                 "fft_fp32_frac": round(f_alg * per_launch / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4)}
         g_launches, g_ms = kstats.get("k_obj_gather", (0, 0.0))
@@ -363,20 +369,15 @@ def main():
         s_ms = sum(kstats[k][1] for k in stripe) / a.steps
         achieved = f_alg * n_local / (s_ms / 1e3) / 1e12
         traffic, fabric = None, None
-        pmc = os.path.join(ROOT, "profiles", "pmc_stripe.json")
-        if os.path.exists(pmc):
-            # PMC bytes per pattern of the same passes (profiles/pmc_stripe.json, from the r02y
-            # rocprofv3 --pmc runs), per step: the fabric rate the passes sustain
-            with open(pmc) as f:
-                bpp = json.load(f).get(a.config, {}).get("bytes_per_pattern")
-            if bpp:
-                traffic = float(bpp) * n_local
-                fabric = round(traffic / (s_ms / 1e3) / 1e9, 1)
-        roof = {"kernel": "stripe engine k_s1..k_s5", "bound": "mfma", "achieved": round(achieved, 2),
+        if tr.get("bytes_per_pattern"):   # PMC bytes per pattern of the five passes, per step
+            traffic = round(tr["bytes_per_pattern"] * n_local)
+            fabric = round(traffic / (s_ms / 1e3) / 1e9, 1)
+        roof = {"kernel": "stripe engine k_s1..k_s5", "bound": "fp32-valu", "achieved": round(achieved, 2),
                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                "traffic": traffic, "traffic_GBps": fabric, "alg_flops_per_step": f_alg * n_local,
+                "traffic": traffic, "traffic_unit": "bytes per step", "traffic_GBps": fabric,
+                "traffic_source": tsrc, "alg_flops_per_step": f_alg * n_local,
                 "engine_ms_per_step": round(s_ms, 3),
-                "note": "FP32 vector peak = FP32 MFMA rate on gfx950; the FFTs run on the vector ALUs",
+                "note": "the FFTs run on the vector ALUs (no MFMA); FP32 vector peak 157.3 TF",
                 "hbm_alg_frac": round(b_alg * n_local / (s_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
     par = f"dp{world} (RCCL all-reduce of object+probe grads per step)" if world > 1 else "dp1"
     out = {
@@ -398,6 +399,7 @@ def main():
         "fft_tflops": round(value / world * f_alg / 1e12, 2) if cfg["mode"] != "strong" else
         round(value * f_alg / 1e12 / world, 2),
         "kernels_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in kstats.items()},
+        "launches_per_step": {k: v[0] // a.steps for k, v in kstats.items()},
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 201
+#define PTYX_ABI_VERSION 202
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -53,6 +53,10 @@ extern "C" {
 #define PTYX_PREP_CALL 0   /* prepare what this call's windows touch                           */
 #define PTYX_PREP_FULL 1   /* prepare the whole object, for later PTYX_PREP_REUSE calls          */
 #define PTYX_PREP_REUSE 2  /* reuse the previous call's preparation on this plan                */
+/* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
+ * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
+ * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
+ * reusing: REUSE is a hint, never a way to read stale preparation. */
 
 /* dims.flags */
 #define PTYX_SHIFT_PROBES 1u /* sub-px Fourier-shifted probes (PtychoAD.shift_probes, models.py:120) */
@@ -90,8 +94,9 @@ typedef struct ptyx_inputs {
   const float *kvec;       /* (N)          f32  propagator_grid k values (Ky[:,0] = Kx[0,:])  */
   float dz;                /* slice thickness used by the tilt ramps                           */
   /* rank-local measurement storage (the data-parallel driver keeps only the DPs of its own
-   * mini-batches): meas_rows[s] = row of `meas` holding scan position s, for every s
-   * a call touches.  NULL = row s (the whole stack).                                          */
+   * mini-batches): meas_rows[s] = row of `meas` holding scan position s.  HARD
+   * PRECONDITION: for every s a call touches, 0 <= meas_rows[s] < the rows of `meas` (the kernels
+   * do not check it; the Python mirror verifies it before the call).  NULL = row s.            */
   const int32_t *meas_rows; /* (n_scans) i32 device, or NULL                                     */
 } ptyx_inputs;
 
@@ -141,6 +146,32 @@ int ptyx_forward_loss_grad(ptyx_plan *plan, void *stream, const ptyx_inputs *in,
                            const int32_t *batch_offsets, int32_t n_batches, int32_t n_idx,
                            const ptyx_loss_cfg *cfg, float *loss_terms, float *dp_out,
                            const ptyx_grads *grads);
+
+/* The same call in two halves, for a mini-batch whose patterns are split over data-parallel ranks
+ * (the reference's split_batches, utils/common.py:63 / reconstruction.py:125-132, with the
+ * single-device NRMSE normalisation losses.py:45-47 kept exact).
+ *
+ *   _begin runs the forward model and the loss partial sums of this rank's patterns and writes,
+ *     per mini-batch of the call, PTYX_BATCH_SUMS doubles to batch_sums (n_batches, 13) f64 device:
+ *     [pattern count, Σ(I^q-M^q)², ΣM^q (loss_single), Σ(M^q log(I^q+ε)-I^q), ΣM^q (loss_poissn),
+ *      Σ|φ|^n per object mode (loss_sparse, 8 slots)].  Every quantity is additive over patterns.
+ *   the caller sums batch_sums over the ranks that hold parts of the same mini-batches (one
+ *     all-reduce of n_batches·13 doubles), in place,
+ *   _end takes the summed batch_sums, writes loss_terms (n_batches,5) for the WHOLE mini-batches
+ *     and accumulates this rank's share of the gradients; the ranks' gradients then sum (the
+ *     caller's gradient all-reduce) to the single-device gradient of the whole mini-batches.
+ *
+ * Arguments are those of ptyx_forward_loss_grad; the device arrays passed to _begin (inputs, idx,
+ * batch_offsets, gradients, dp_out) must stay valid and unchanged until _end returns, and no other
+ * compute call may run on the plan in between (PTYX_EINVAL).  The call must fit the plan in one
+ * piece (n_idx <= max_patterns and, for the register engines, <= ptyx_plan_register_capacity).
+ * ptyx_forward_loss_grad is _begin + _end with the call's own sums (no collective). */
+#define PTYX_BATCH_SUMS 13
+int ptyx_forward_loss_grad_begin(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
+                                 const int32_t *batch_offsets, int32_t n_batches, int32_t n_idx,
+                                 const ptyx_loss_cfg *cfg, float *dp_out, const ptyx_grads *grads,
+                                 double *batch_sums);
+int ptyx_forward_loss_grad_end(ptyx_plan *plan, void *stream, const double *batch_sums, float *loss_terms);
 
 /* Adjoint for an external loss: given dLdI (n_idx,N,N) = dL/d(dp_fwd) for the patterns idx,
  * accumulate the object / probe / position gradients (autograd of PtychoAD.forward). */
@@ -284,6 +315,15 @@ int ptyx_meas_finish(void *stream, const float *raw, int64_t n, int32_t H, int32
  * 0 when the plan's geometry has no register engine.  Callers with host-side batch offsets
  * split larger calls at mini-batch boundaries (gradients accumulate). */
 int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
+
+/* Engine-variant selection for tests and A/B measurements (no environment variable changes an
+ * engine): key "s3_hold" (0..4: probe/object modes k_s3 keeps in registers), "s_psi0" (0/1: the
+ * stripe engine parks ψ⁰ instead of recomputing it), "s_gather" (0/1: stripe object gradient by
+ * slots + gather instead of f32 atomics); value -1 restores the measured default.  Process-wide,
+ * read by ptyx_plan_create (s_psi0, s_gather) and by each call (s3_hold).  Every variant computes
+ * the same results.  ptyx_get_tuning returns the current value (-1 default, -2 unknown key). */
+int ptyx_set_tuning(const char *key, int64_t value);
+int64_t ptyx_get_tuning(const char *key);
 
 /* Bytes of device workspace the plan holds. */
 size_t ptyx_plan_workspace_bytes(const ptyx_plan *plan);

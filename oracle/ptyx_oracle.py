@@ -392,6 +392,111 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     return np.array(all_terms), dps, grads
 
 
+N_BATCH_SUMS = 13   # include/ptyx.h PTYX_BATCH_SUMS
+
+
+def batch_sums(dp, meas, ph, lp):
+    """The additive sums behind the loss terms of one (part of a) mini-batch, in the engine's
+    PTYX_BATCH_SUMS layout: [count, Σ(I^q-M^q)², ΣM^q (loss_single), Σ(M^q log(I^q+ε)-I^q), ΣM^q
+    (loss_poissn), Σ|φ|^n per object mode (8 slots)] — losses.py:45-47, 70-72, 101 before the means."""
+    out = np.zeros(N_BATCH_SUMS)
+    out[0] = dp.shape[0]
+    I, M = dp.astype(np.float64), meas.astype(np.float64)
+    s, p, sp = lp["loss_single"], lp["loss_poissn"], lp["loss_sparse"]
+    if s["state"]:
+        q = s.get("dp_pow", 0.5)
+        out[1], out[2] = ((I ** q - M ** q) ** 2).sum(), (M ** q).sum()
+    if p["state"]:
+        q, e = p.get("dp_pow", 1.0), p.get("eps", 1e-6)
+        Mq, Iq = M ** q, I ** q
+        out[3], out[4] = (Mq * np.log(Iq + e) - Iq).sum(), Mq.sum()
+    if sp["state"]:
+        a = np.abs(ph.astype(np.float64)) ** sp["ln_order"]
+        out[5:5 + ph.shape[1]] = a.sum(axis=(0, 2, 3, 4))
+    return out
+
+
+def terms_from_sums(sums, n, Nz, occu, lp):
+    """Loss terms and adjoint coefficients of a WHOLE mini-batch from its summed batch_sums
+    (losses.py:36-104): terms (5,), (c_single, c_poissn), c_sparse per object mode."""
+    B = sums[0]
+    K = B * n * n
+    terms = np.zeros(5)
+    c1 = c2 = 0.0
+    s, p, sp = lp["loss_single"], lp["loss_poissn"], lp["loss_sparse"]
+    if s["state"] and B > 0:
+        mu, rmse = sums[2] / K, math.sqrt(sums[1] / K)
+        terms[0] = s["weight"] * rmse / mu
+        c1 = s["weight"] / (mu * K * rmse) if rmse > 0 else 0.0
+    if p["state"] and B > 0:
+        mu = sums[4] / K
+        terms[1] = -p["weight"] * (sums[3] / K) / mu
+        c2 = -p["weight"] / (mu * K)
+    csp = np.zeros(len(occu))
+    if sp["state"] and B > 0:
+        nord, cnt = sp["ln_order"], B * Nz * n * n
+        m = sums[5:5 + len(occu)] / cnt
+        terms[3] = sp["weight"] * float((m ** (1.0 / nord) * occu).sum())
+        for o in range(len(occu)):
+            csp[o] = sp["weight"] * occu[o] * (m[o] ** (1.0 / nord - 1.0) if m[o] > 0 else 0.0) / cnt
+    return terms, (c1, c2), csp
+
+
+def forward_loss_grad_parts(obja, objp, probe, shifts, crop_pos, H, occu, meas, parts, loss_params, reduce,
+                            shift_probes=True, grad_scale=1.0, cdt=np.complex128):
+    """Oracle of ptyx_forward_loss_grad_begin → all-reduce → _end for ONE rank: ``parts[m]`` is this
+    rank's share (possibly empty) of mini-batch m, ``reduce(sums)`` sums the (n_batches, 13) batch
+    sums over the ranks in place.  Returns (terms of the whole mini-batches, grads of this rank's
+    patterns); summed over the ranks the gradients equal forward_loss_grad over the whole batches."""
+    if isinstance(loss_params, str):
+        loss_params = json.loads(loss_params)
+    n = probe.shape[-1]
+    Nz = obja.shape[1]
+    sums = np.zeros((len(parts), N_BATCH_SUMS))
+    fw = []
+    for m, idx in enumerate(parts):
+        idx = np.asarray(idx, dtype=np.int64)
+        if idx.size == 0:
+            fw.append(None)
+            continue
+        amp, ph = get_patches(obja, objp, crop_pos, idx, n)
+        cache = forward(amp, ph, get_probes(probe, shifts[idx], shift_probes, cdt), H, occu, cdt=cdt)
+        sums[m] = batch_sums(cache.dp, meas[idx], ph, loss_params)
+        fw.append((idx, amp, ph, cache))
+    reduce(sums)
+    g = dict(obja=np.zeros(obja.shape), objp=np.zeros(objp.shape), probe=np.zeros(probe.shape, np.complex128),
+             shifts=np.zeros(shifts.shape))
+    all_terms = []
+    for m, f in enumerate(fw):
+        terms, (c1, c2), csp = terms_from_sums(sums[m], n, Nz, occu, loss_params)
+        all_terms.append(terms)
+        if f is None:
+            continue
+        idx, amp, ph, cache = f
+        I, M = cache.dp.astype(np.float64), meas[idx].astype(np.float64)
+        dLdI = np.zeros_like(I)
+        s, p, sp = loss_params["loss_single"], loss_params["loss_poissn"], loss_params["loss_sparse"]
+        if s["state"]:
+            q = s.get("dp_pow", 0.5)
+            dLdI += c1 * (I ** q - M ** q) * q * I ** (q - 1)
+        if p["state"]:
+            q, e = p.get("dp_pow", 1.0), p.get("eps", 1e-6)
+            dLdI += c2 * (M ** q / (I ** q + e) - 1.0) * q * I ** (q - 1)
+        dph = np.zeros(ph.shape)
+        if sp["state"]:
+            a = np.abs(ph.astype(np.float64))
+            for o in range(ph.shape[1]):
+                dph[:, o] = csp[o] * a[:, o] ** (sp["ln_order"] - 1) * np.sign(ph[:, o])
+        dA, dP, dprobe, dshift = adjoint(cache, dLdI, dph, amp, ph, probe, shifts[idx], H, occu, shift_probes, cdt)
+        for i, sidx in enumerate(idx):
+            cy, cx = int(crop_pos[sidx, 0]), int(crop_pos[sidx, 1])
+            g["obja"][:, :, cy:cy + n, cx:cx + n] += grad_scale * dA[i]
+            g["objp"][:, :, cy:cy + n, cx:cx + n] += grad_scale * dP[i]
+            g["shifts"][sidx] += grad_scale * dshift[i]
+        g["probe"] += grad_scale * dprobe
+    return np.array(all_terms), g
+
+
 def propagator_param_grads(gH, H, dz, tilts, dx, lambd, case):
     """Chain rule from dL/dH to the optimised slice thickness / global tilts (get_propagators
     cases 1, 2A, 3, models.py:339-356): dL/dθ = Re Σ conj(gH) ∂H/∂θ, with ∂H/∂θ = i (∂φ/∂θ) H for

@@ -1,8 +1,7 @@
 #!/bin/bash
 # PMC counter passes (one counter group per rocprofv3 run; FETCH_SIZE and WRITE_SIZE in separate
 # passes, MI355X_MICROARCH.md "rocprofv3 PMC slots").  Run on the GPU box:
-#   bash profiles/collect_pmc.sh <outdir> [extra bench args]              (bench.py, the c2 workload)
-#   PMC_SCRIPT=tools/bench_configs.py bash profiles/collect_pmc.sh <outdir> --config c5 --patterns 4096
+#   bash profiles/collect_pmc.sh <outdir> [extra bench args, e.g. --config c5]
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=${1:-$R/gpurun_out/pmc}
@@ -10,9 +9,8 @@ shift || true
 mkdir -p "$OUT"
 OUT=$(cd "$OUT" && pwd)
 export TMPDIR=/tmp
-SCRIPT=${PMC_SCRIPT:-bench.py}
-EXTRA=""
-[ "$SCRIPT" = "bench.py" ] && EXTRA="--no-cpu-baseline"
+SCRIPT=bench.py
+EXTRA="--no-cpu-baseline"
 cd /tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 i=0

@@ -28,6 +28,7 @@ def summarize(d):
     out = {}
     for k, cs in agg.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}     # mean per dispatch
+        m["dispatches"] = max(len(v) for v in cs.values())
         fetch = m.get("FETCH_SIZE", 0.0) * 1024
         write = m.get("WRITE_SIZE", 0.0) * 1024
         m["fetch_bytes_raw"] = fetch

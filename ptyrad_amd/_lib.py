@@ -14,8 +14,9 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 201     # include/ptyx.h
+PTYX_ABI_VERSION = 202     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
+PTYX_BATCH_SUMS = 13      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
 PTYX_SHIFT_PROBES = 1
 PTYX_MEAS_F16 = 2
@@ -25,6 +26,7 @@ _ERRNAMES = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EUNSUPPORTED"}
 
 # every symbol include/ptyx.h declares (checked by tests/test_abi.py)
 EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+           "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning", "ptyx_get_tuning",
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
            "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
@@ -113,6 +115,12 @@ def load(path: str | None = None):
     lib.ptyx_forward.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, i32, vp]
     lib.ptyx_forward_loss_grad.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, vp, i32, i32,
                                            ctypes.POINTER(LossCfg), vp, vp, ctypes.POINTER(Grads)]
+    lib.ptyx_forward_loss_grad_begin.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, vp, i32, i32,
+                                                 ctypes.POINTER(LossCfg), vp, ctypes.POINTER(Grads), vp]
+    lib.ptyx_forward_loss_grad_end.argtypes = [vp, vp, vp, vp]
+    lib.ptyx_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    lib.ptyx_get_tuning.argtypes = [ctypes.c_char_p]
+    lib.ptyx_get_tuning.restype = ctypes.c_int64
     lib.ptyx_adjoint_dldi.argtypes = [vp, vp, ctypes.POINTER(Inputs), vp, i32, vp, f32,
                                       ctypes.POINTER(Grads)]
     lib.ptyx_profile_begin.argtypes = [vp]
@@ -151,6 +159,7 @@ def load(path: str | None = None):
     lib.ptyx_meas_stats.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp]
     lib.ptyx_meas_finish.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp, vp, i32]
     for name in ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+                 "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
                  "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish"):
@@ -179,6 +188,15 @@ def _check_abi(lib):
     for name, sz in zip(STRUCTS, sizes):
         if ctypes.sizeof(globals()[name]) != sz:
             raise ImportError(f"ctypes {name} is {ctypes.sizeof(globals()[name])} B, libptyx.so says {sz} B")
+
+
+def set_tuning(key: str, value: int) -> None:
+    """ptyx_set_tuning: select an engine variant (tests / A/B runs; -1 = the measured default)."""
+    check(load().ptyx_set_tuning(key.encode(), int(value)))
+
+
+def get_tuning(key: str) -> int:
+    return int(load().ptyx_get_tuning(key.encode()))
 
 
 def check(rc: int):

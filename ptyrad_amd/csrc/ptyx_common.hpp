@@ -4,6 +4,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include "ptyx.h"
 #include "ptyx_fft.hpp"
 
 namespace ptyx {
@@ -12,6 +13,8 @@ constexpr int kMaxModesO = 8;
 constexpr int kSumBase = 4;                    // [S_single, ΣM^q1, S_poissn, ΣM^q2] then O sparse sums
 constexpr int kNSum = kSumBase + kMaxModesO;
 constexpr int kNCoef = 2 + kMaxModesO;         // [c_single, c_poissn, c_sparse[o]...]
+constexpr int kNBatchSum = 5 + kMaxModesO;     // per mini-batch: [count, S1, ΣM^q1, S2, ΣM^q2, sparse[o]...]
+static_assert(kNBatchSum == PTYX_BATCH_SUMS, "include/ptyx.h PTYX_BATCH_SUMS");
 constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
 
 template <int N> struct Geo;

@@ -154,19 +154,9 @@ struct GlobalView {
 // stage kinds
 enum : int { kMid = 0, kFirst = 1, kLast = 2 };
 
-// PTYX_G256_TWO_STAGE: 1 = N = 256 2-D FFTs in two LDS-tiled stages (one scratch round trip),
-// 0 = four Stockham passes through the global ping-pong pair.
-#ifndef PTYX_G256_TWO_STAGE
-#define PTYX_G256_TWO_STAGE 1
-#endif
-
-// Fused pre/post element group size between scheduling barriers (0 = let the compiler
-// schedule freely).  Without it hipcc hoists every element's global loads of a 16-point
+// Fused pre/post element group size between scheduling barriers.  Without it hipcc hoists every element's global loads of a 16-point
 // epilogue ahead of the arithmetic and spills at 128 VGPRs (1024-thread workgroups).
-#ifndef PTYX_FUSE_GROUP
-#define PTYX_FUSE_GROUP 4
-#endif
-constexpr int kFuseGroup = PTYX_FUSE_GROUP;
+constexpr int kFuseGroup = 4;
 
 // twiddle table tw[m] = exp(-2πi m / N) (fp64 rounded), conj for inverse
 template <int DIR>
@@ -431,12 +421,10 @@ __device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pr
     }
   } else {
     static_assert(R2 != 1, "global ping-pong needs two passes per dimension");
-#if PTYX_G256_TWO_STAGE
     if constexpr (N == 256 && NT == 1024) {
       fft2d_g256<DIR, PRELOAD>(arr, tw, pre, post);
       return;
     }
-#endif
     const GlobalView<N> A{arr.a}, B{arr.b};
     stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, false>(A, B, tw, pre, post);
     stockham_pass<N, NT, R2, R1, true, DIR, kMid, false, false>(B, A, tw, pre, post);

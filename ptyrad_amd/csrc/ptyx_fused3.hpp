@@ -354,15 +354,13 @@ __device__ __forceinline__ void st2(float2 v, Rsrc r, int voff, int off) {
   const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v.x), __float_as_uint(v.y)};
   __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, 0);
 }
-// PTYX_F3_NT: non-temporal (aux = 2, "nt") for the streams read once much later or never again
-// in this kernel (final slot stores, the DP), so they do not evict the park / slab / object /
-// F(P) lines the next passes re-read from L2.
-#ifndef PTYX_F3_NT
-#define PTYX_F3_NT 1
-#endif
+// Non-temporal (aux = 2, "nt") for the streams read once much later or never again in this kernel
+// (final slot stores, the DP), so they do not evict the park / slab / object / F(P) lines the next
+// passes re-read from L2.
+constexpr int kNtAux = 2;
 __device__ __forceinline__ void st2_stream(float2 v, Rsrc r, int voff, int off) {
   const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v.x), __float_as_uint(v.y)};
-  __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, PTYX_F3_NT ? 2 : 0);
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, voff + off, 0, kNtAux);
 }
 
 // Wave sum in a fixed order, result in every lane: DPP adds within each 16-lane row
@@ -403,21 +401,14 @@ __device__ __forceinline__ void block_sum4(float (&v)[NV], float* red) {
 // compiler can no longer sink its computation towards a later use, which otherwise keeps every
 // intermediate of a 64-register pass live across barriers and spills.
 __device__ __forceinline__ void pin(float2& v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
-// The same into an accumulation register (AGPR): values parked there between passes (the ψ⁰ park
-// and the segment's probe-gradient slab of PTYX_F3_HOLD) cost one v_accvgpr move per use and no
-// memory traffic.
-__device__ __forceinline__ void pin_a(float2& v) { asm volatile("" : "+a"(v.x), "+a"(v.y)); }
 
 // Software-pipelined pass over the 64 registers in NC chunks: the global loads of chunks
 // c+1 … c+D are in flight while chunk c is consumed, and a scheduling barrier after every chunk
 // keeps the compiler from hoisting all 64 loads at once (which would need 128+ extra VGPRs and
-// spill).  D = PTYX_F3_PIPE.
-#ifndef PTYX_F3_PIPE
-#define PTYX_F3_PIPE 1
-#endif
+// spill).  D = 1 (deeper measured no faster at 256 VGPRs).
 template <int NC, class Ld, class Use>
 __device__ __forceinline__ void pipeline(Ld&& ld, Use&& use) {
-  constexpr int D = PTYX_F3_PIPE < NC ? PTYX_F3_PIPE : NC - 1 > 0 ? NC - 1 : 1;
+  constexpr int D = 1;
   using T = decltype(ld(std::integral_constant<int, 0>{}));
   T ring[D + 1];
   rf::sfor<0, D>([&](auto I) {
@@ -463,7 +454,7 @@ __device__ __forceinline__ float2 pscale(float2 a, float s) { return rf::pf(rf::
 __device__ __forceinline__ float2 padd2(float2 a, float2 b) { return rf::pf(rf::pv(a) + rf::pv(b)); }
 
 // ------------------------------------------------------------------ LDS-DMA operand ring
-// PTYX_F3_RING = 1: the operands of the point-wise passes (object window, ψ⁰ park, F(P), segment
+// The operands of the point-wise passes of the shifted-probe kernels (object window, ψ⁰ park, F(P), segment
 // slab) stream HBM/L2 → LDS by buffer_load_dwordx4 … lds into a per-wave ring in the (then free)
 // exchange buffer, D register pairs ahead of their use, and are read back with ds_read_b64.  No
 // VGPRs are held by loads in flight, so a pass keeps 8-16 KiB per wave (64-128 KiB per CU) of
@@ -477,9 +468,6 @@ __device__ __forceinline__ float2 padd2(float2 a, float2 b) { return rf::pf(rf::
 // access moves across it.  Per wave the ring is 16 KiB: wave w owns bytes [16 KiB·w, 16 KiB·(w+1))
 // of the exchange buffer, and each wave DMAs exactly the operands its own threads read, so the
 // ring needs no workgroup barrier.
-#ifndef PTYX_F3_RING
-#define PTYX_F3_RING 1
-#endif
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 // buffer descriptor as four SGPRs (raw, stride 0; word 3 as rsrc())
 __device__ __forceinline__ v4u srd(const void* base, unsigned bytes) {
@@ -561,44 +549,10 @@ __device__ __forceinline__ int obj_img(int lam) {
   return ((f >> 4) << 5) + (((f & 15) >> 1) << 2) + ((lam & 1) << 1) + (f & 1);
 }
 
-// PTYX_F3_PARK_NT / PTYX_F3MS_PARK_NT: the ψ⁰ / ψⁿ park stores as non-temporal streams.
-// Measured (profiles/r02/ab/r02y_pnt_*): k_fused3 reads its park two transforms later, partly
-// from L2, and slows down (11.35-11.56 → 11.66-11.68 ms): off; k_fused3ms reads slice n's park
-// 2·(Nz − n) transforms later: 2.672 → 2.641 s per c4 step: on.
-#ifndef PTYX_F3_PARK_NT
-#define PTYX_F3_PARK_NT 0
-#endif
-#ifndef PTYX_F3MS_PARK_NT
-#define PTYX_F3MS_PARK_NT 1
-#endif
-// PTYX_F3_SLAB_NT: the segment slab's stores as non-temporal (it is re-read one pattern later)
-#ifndef PTYX_F3_SLAB_NT
-#define PTYX_F3_SLAB_NT 0
-#endif
-// PTYX_F3_CARRY: a pattern's scalars come from the previous pattern's post4 pass (0: reloaded)
-#ifndef PTYX_F3_CARRY
-#define PTYX_F3_CARRY 1
-#endif
-
-// PTYX_F3_PHASES=1 (diagnostic builds only): s_memtime stamps at the phase boundaries of wave 0;
-// workgroups 0 and 1 printf their per-phase cycle totals at exit.
-#ifndef PTYX_F3_PHASES
-#define PTYX_F3_PHASES 0
-#endif
-#if PTYX_F3_PHASES
-#define F3PH(i)                                                  \
-  do {                                                           \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    ph[i] += t_ - ph_prev;                                       \
-    ph_prev = t_;                                                \
-  } while (0)
-#elif defined(PTYX_F3_MARK)
-#define F3PH(i) asm volatile("; MARK " #i)
-#else
-#define F3PH(i) \
-  do {          \
-  } while (0)
-#endif
+// Park stores: k_fused3 reads its ψ⁰ park two transforms later, partly from L2, so it stores
+// them plainly (non-temporal measured 11.35-11.56 → 11.66-11.68 ms, profiles/r02/ab/r02y_pnt_*);
+// k_fused3ms reads slice n's park 2·(Nz − n) transforms later and stores them non-temporal
+// (c4 2.672 → 2.641 s per step).  A pattern's scalars come from the previous pattern's post4 pass.
 
 // Per-pattern scalars.
 struct PatInfo {
@@ -672,22 +626,6 @@ struct Ramp {
   }
 };
 
-// Cost-attribution knobs for diagnostic builds (results are WRONG with any of them set):
-//   PTYX_F3_EXP_NOPARK  no ψ⁰ park store / reload      PTYX_F3_EXP_NOSLAB  no segment-slab load/store
-//   PTYX_F3_EXP_NOOBJ   no object loads (O = 1)          PTYX_F3_EXP_NOSLOT  no final slot store
-#ifndef PTYX_F3_EXP_NOPARK
-#define PTYX_F3_EXP_NOPARK 0
-#endif
-#ifndef PTYX_F3_EXP_NOSLAB
-#define PTYX_F3_EXP_NOSLAB 0
-#endif
-#ifndef PTYX_F3_EXP_NOOBJ
-#define PTYX_F3_EXP_NOOBJ 0
-#endif
-#ifndef PTYX_F3_EXP_NOSLOT
-#define PTYX_F3_EXP_NOSLOT 0
-#endif
-
 // QM: 0 → dp_pow q = 1/2 (sqrt / rsqrt), 2 → general q (see loss_point)
 //
 // Work split: workgroup w owns the contiguous pattern range [w·n/G, (w+1)·n/G).  Everything that
@@ -701,28 +639,17 @@ struct Ramp {
 // Per pattern: IFFT · park ψ⁰, ×O · FFT (DP → LDS meanwhile) · loss partial sums, g_Ψ ·
 // IFFT · slot, ×conj(O) · FFT (probe-gradient spectrum) · one pass: segment slab += conj(W) G,
 // position-gradient sums, and v = F(P)·W for the next pattern (F(P) read once per pattern).
-#ifndef PTYX_F3_OCC
-#define PTYX_F3_OCC 2   // workgroups per CU k_fused3 is compiled for
-#endif
-// PTYX_F3_HOLD: ψ⁰ and the segment slab stay in the accumulation registers (AGPRs) of a
-// one-workgroup-per-CU kernel instead of the slot park and the per-pattern slab read-modify-write
-// (256 + 256 KiB of L2 / fabric traffic per pattern).
-#ifndef PTYX_F3_HOLD
-#define PTYX_F3_HOLD 0
-#endif
+//
+// Two workgroups per CU (≤ 256 VGPRs).  Holding ψ⁰ and the segment slab in AGPRs at one workgroup
+// per CU instead of the park and the slab read-modify-write measured the same time
+// (profiles/r02/ab/r02l_c2hold: 12.29 vs 12.16 ms), so the kernel parks them.
 template <bool SHIFT, bool SINGLE, int QM>
-__global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(F3Args a) {
+__global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
   __shared__ float s_red[4 * 2];
   const Coord cd = coord(threadIdx.x);
   const LaneCtx lc = lane_ctx(cd.lane);
-#if PTYX_F3_PHASES
-  unsigned long long ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long ph_prev = __builtin_amdgcn_s_memtime();
-  const unsigned long long ph_t0 = ph_prev, ph_r0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-  int ph_n = 0;
-#endif
   constexpr float inv_n = 1.0f / kN, inv_n2 = 1.0f / kN2;
   const int w = blockIdx.x, G = gridDim.x;
   const int p0 = (int)((long long)w * a.n_idx / G), p1 = (int)((long long)(w + 1) * a.n_idx / G);
@@ -734,18 +661,9 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
   const float gy = (float)((cd.fixed + 64) & 127) * inv_n;   // ifftshifted grid of this thread's ky
 
   // ---------------------------------------------------------------- prologue: v for the first pattern
-  constexpr bool kHold = PTYX_F3_HOLD != 0;
-  constexpr bool kRing = PTYX_F3_RING && SHIFT && !kHold;
+  constexpr bool kRing = SHIFT;
   const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;   // LDS byte address
   float2 v[64];
-  float2 psi0[kHold ? 64 : 1], slab[kHold ? 64 : 1];
-  if constexpr (kHold) {
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-      slab[k] = make_float2(0.f, 0.f);
-      pin_a(slab[k]);
-    }
-  }
   {
     const int tid = rf::opaque(threadIdx.x);
     const int vpk = 8 * tid;
@@ -782,7 +700,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
     const int tid = rf::opaque(threadIdx.x);
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
-    const PatInfo p = PTYX_F3_CARRY ? p_nxt : pat_info<SHIFT>(a, pat);
+    const PatInfo p = p_nxt;
     // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → offset 2048·j
     const Rsrc r_slot = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
     const int vslot0 = 8 * (l0 * kN + fx);
@@ -803,7 +721,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
       dma_m<2 * q>(s_obj, voff, m0w + (q % 16) * 1024, os);
     };
     // ------------------------------------------------ ψ⁰ = F⁻¹(F(P)·W_b)  (R layout)
-    F3PH(0);
     if constexpr (SHIFT) {
       fft_inv(v, buf, lc, cd.wsign, [&] {
         if constexpr (kRing) {
@@ -814,7 +731,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
       for (int j = 0; j < 64; ++j) v[j] = pscale(v[j], inv_n2);
     }
-    F3PH(1);
     // ------------------------------------------------ park ψ⁰; ψ = ψ⁰·O
     if constexpr (kRing) {
       const int lam = rf::opaque(tid) & 63;
@@ -830,11 +746,8 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
           const float2 O = sl[rb * 64 + io];
-          if (!PTYX_F3_EXP_NOPARK) {
-            if (PTYX_F3_PARK_NT) st2_stream(v[j], r_park, vpark, 2048 * j);
-            else st2(v[j], r_park, vpark, 2048 * j);
-          }
-          v[j] = pcm(v[j], PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : O);
+          st2(v[j], r_park, vpark, 2048 * j);
+          v[j] = pcm(v[j], O);
           pin(v[j]);
         }
         if constexpr (q + 16 < 32) issue1(std::integral_constant<int, q + 16>{}, vo);
@@ -847,25 +760,19 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
             Ch8 t;
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-              t.x[r] = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : ld2(r_obj, vobj, ostr * (8 * C + r));
+              t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
             return t;
           },
           [&](auto C, const Ch8& t) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const int j = 8 * C + r;
-              if constexpr (kHold) {
-                psi0[j] = v[j];
-                pin_a(psi0[j]);
-              } else if (!PTYX_F3_EXP_NOPARK) {
-                st2(v[j], r_slot, vslot, 2048 * j);
-              }
+              st2(v[j], r_slot, vslot, 2048 * j);
               v[j] = cmul(v[j], t.x[r]);
               pin(v[j]);
             }
           });
     }
-    F3PH(2);
     // ------------------------------------------------ far field; DP → LDS during the row DFTs
     const float* dp = a.meas + (size_t)p.mi * kN2;
     if constexpr (kRing) __syncthreads();   // every wave is done with its ring before the exchange
@@ -880,13 +787,11 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
         __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
                                          (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
-                                         PTYX_F3_NT ? 2 : 0);
+                                         kNtAux);
       }
     });
-    F3PH(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    F3PH(4);
     float S = 0.f, Ms = 0.f;
     const float occ_n2 = occ * inv_n2, occ2_n = 2.0f * occ * inv_n;
     {
@@ -919,7 +824,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         if (kq & 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    F3PH(5);
     {
       // (block_sum4's first barrier also retires every wave's DP reads before the next exchange)
       float v2[2] = {S, Ms};
@@ -933,7 +837,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         ps[3 - base] = 0.f;
       }
     }
-    F3PH(6);
     // ------------------------------------------------ back to real space
     // post3 ring: ψ⁰ park + object window, 8 register pairs ahead (A = 2, S = 2 slot stores)
     auto issue3 = [&](auto Q, int vpo, int voo) {
@@ -948,7 +851,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         rf::sfor<0, 8>([&](auto Q) { issue3(Q, vpo, voo); });
       }
     });
-    F3PH(7);
     if constexpr (kRing) {
       const int lam = rf::opaque(tid) & 63;
       const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
@@ -961,10 +863,10 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
-          const float2 ps = PTYX_F3_EXP_NOPARK ? make_float2(1.f, 0.f) : sl[rb * 64 + lam];
-          const float2 O = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : sl[128 + rb * 64 + io];
+          const float2 ps = sl[rb * 64 + lam];
+          const float2 O = sl[128 + rb * 64 + io];
           const float2 gv = pscale(v[j], inv_n);
-          if (!PTYX_F3_EXP_NOSLOT) st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+          st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
           v[j] = pcmc(gv, O);                                                          // g·conj(O)
           pin(v[j]);
         }
@@ -979,8 +881,8 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
-              t.x[r] = (kHold || PTYX_F3_EXP_NOPARK) ? make_float2(1.f, 0.f) : ld2(r_slot, vslot, 2048 * j);
-              t.y[r] = PTYX_F3_EXP_NOOBJ ? make_float2(1.f, 0.f) : ld2(r_obj, vobj, ostr * j);
+              t.x[r] = ld2(r_slot, vslot, 2048 * j);
+              t.y[r] = ld2(r_obj, vobj, ostr * j);
             }
             return t;
           },
@@ -989,24 +891,21 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
               const float2 gv = cscale(v[j], inv_n);
-              const float2 ps = kHold ? psi0[kHold ? j : 0] : t.x[r];
-              if (!PTYX_F3_EXP_NOSLOT) st2_stream(cmulc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+              st2_stream(cmulc(gv, t.x[r]), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
               v[j] = cmulc(gv, t.y[r]);                  // g·conj(O)
               pin(v[j]);
             }
           });
     }
-    F3PH(8);
     // ------------------------------------------------ probe / position gradient, next pattern's v
     // Segment of this pattern: the run of the range inside mini-batch m, id m + w.  The first
     // pattern of a segment reads its slab through a zero-length buffer resource (loads return 0)
     // and so initialises it; later patterns accumulate.  Without probe/position gradients (tail
     // false) the same pass runs without the FFT and its slab / sums are never used.
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || (PTYX_F3_CARRY ? m_prev : s_ld(a.bid + (pat - 1))) != p.m;   // (uniform)
+    const bool first = pat == p0 || m_prev != p.m;   // (uniform)
     m_prev = p.m;
     p_nxt = pn;
-    const bool last = kHold && (pat == p1 - 1 || s_ld(a.bid + (pat + 1)) != p.m);   // (uniform; PTYX_F3_HOLD flushes the slab)
     const int seg = p.m + w;
     float2* segs = a.segslab + (size_t)seg * kN2;
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
@@ -1032,7 +931,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
       // G = F(h), K layout (unconditional here: a branch around the FFT spills the 64 points;
       // without probe / position gradients the slab and sums are simply never read)
       fft_fwd(v, buf, lc, cd.wsign, pre4);
-      F3PH(9);
       const int lam = rf::opaque(tid) & 63;
       const int vk = dma_off_k(lam, wv);
       const int vpk = rf::opaque(8 * tid);
@@ -1060,12 +958,11 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
           const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
           sim += im;
           kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
-          if (!PTYX_F3_EXP_NOSLAB) {
+          {
             const float2 so = sl[128 + rb * 64 + lam];
             const float2 gw = pcmc(v[k], W);                      // + conj(W) G (unit)
             const float2 sn = rf::pf(__builtin_elementwise_fma((rf::v2f){keep, keep}, rf::pv(so), rf::pv(gw)));
-            if (PTYX_F3_SLAB_NT) st2_stream(sn, r_slab_st, vpk, 2048 * k);
-            else st2(sn, r_slab_st, vpk, 2048 * k);
+            st2(sn, r_slab_st, vpk, 2048 * k);
           }
           v[k] = pcm(F, pcm(An, rn.B[r]));                        // next pattern: F(P)·W_next
           pin(v[k]);
@@ -1073,7 +970,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
         if constexpr (q + 8 < 32) issue4(std::integral_constant<int, q + 8>{}, vk);
         __builtin_amdgcn_sched_barrier(0);
       });
-      F3PH(10);
       {
         float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0b) * sim)};
         block_sum4<2>(ds, s_red);
@@ -1084,7 +980,6 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
       }
     } else if constexpr (SHIFT) {
       if (tail) fft_fwd(v, buf, lc, cd.wsign);        // G = F(h), K layout
-      F3PH(9);
       const int vpk = rf::opaque(8 * tid);
       const int l0b = rf::opaque(tid) & 1;
       Ramp rc, rn;
@@ -1098,7 +993,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
             for (int r = 0; r < 4; ++r) {
               const int k = 4 * C + r;
               t.x[r] = ld2(r_fpk, vpk, 2048 * k);
-              t.y[r] = (kHold || PTYX_F3_EXP_NOSLAB) ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * k);
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * k);
             }
             return t;
           },
@@ -1112,17 +1007,11 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
               const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);     // Im(F(P) W conj(G))
               sim += im;
               kim = fmaf((float)k, im, kim);                          // Σ k·im (k literal)
-              if constexpr (kHold) {
-                slab[kHold ? k : 0] = cadd(slab[kHold ? k : 0], cmulc(v[k], W));   // + conj(W) G (unit)
-                pin_a(slab[kHold ? k : 0]);
-              } else if (!PTYX_F3_EXP_NOSLAB) {
-                st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
-              }
+              st2(cadd(t.y[r], cmulc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G (unit)
               v[k] = cmul(t.x[r], cmul(An, rn.B[r]));                 // next pattern: F(P)·W_next
               pin(v[k]);
             }
           });
-      F3PH(10);
       {
         // Always reduced (a conditional consumer lets the compiler sink all 64 im products into
         // the branch and keep F(P)·W and G live, which spills).
@@ -1142,7 +1031,7 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
-              t.y[r] = kHold ? make_float2(0.f, 0.f) : ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
             }
             return t;
           },
@@ -1150,45 +1039,13 @@ __global__ __launch_bounds__(256, PTYX_F3_HOLD ? 1 : PTYX_F3_OCC) void k_fused3(
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 4 * C + r;
-              if constexpr (kHold) {
-                slab[kHold ? j : 0] = cadd(slab[kHold ? j : 0], v[j]);   // + h (unit, R layout)
-                pin_a(slab[kHold ? j : 0]);
-              } else {
-                st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (unit, R layout)
-              }
+              st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (unit, R layout)
               v[j] = t.x[r];                                       // next pattern: the probe
               pin(v[j]);
             }
           });
     }
-    if constexpr (kHold) {
-      if (last) {   // the segment is complete: its slab is written once
-        const int vpk = rf::opaque(8 * tid);
-#pragma unroll
-        for (int k = 0; k < 64; ++k) {
-          st2(slab[k], r_slab_st, vpk, 2048 * k);
-          slab[k] = make_float2(0.f, 0.f);
-          pin_a(slab[k]);
-        }
-      }
-    }
-    F3PH(11);
-#if PTYX_F3_PHASES
-    ++ph_n;
-#endif
   }
-#if PTYX_F3_PHASES
-  if (threadIdx.x == 0 && blockIdx.x < 2)
-    printf("F3PHASES wg %d n %d cyc/pattern: top %llu ifft1 %llu post1 %llu fft2 %llu dpwait %llu loss %llu "
-           "publish %llu ifft3 %llu post3 %llu fft4 %llu post4+pre %llu ds %llu\n",
-           (int)blockIdx.x, ph_n, ph[0] / ph_n, ph[1] / ph_n, ph[2] / ph_n, ph[3] / ph_n, ph[4] / ph_n, ph[5] / ph_n,
-           ph[6] / ph_n, ph[7] / ph_n, ph[8] / ph_n, ph[9] / ph_n, ph[10] / ph_n, ph[11] / ph_n);
-  if (threadIdx.x == 0 && blockIdx.x < 2) {
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    printf("F3CLOCK wg %d shader-clock MHz %.0f over %.1f us\n", (int)blockIdx.x,
-           100.0 * (double)(t1 - ph_t0) / (double)(r1 - ph_r0), (double)(r1 - ph_r0) / 100.0);
-  }
-#endif
 }
 
 
@@ -1224,7 +1081,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
   const Rsrc r_fpk = rsrc(a.fpk, kN2 * 8);
   const Rsrc r_hpk = rsrc(a.hpk, kN2 * 8);
   const float gy = (float)((cd.fixed + 64) & 127) * inv_n;
-  constexpr bool kRing = PTYX_F3_RING && SHIFT;
+  constexpr bool kRing = SHIFT;
   const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;   // LDS byte address
 
   float2 v[64];
@@ -1278,7 +1135,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     const int tid = rf::opaque(threadIdx.x);
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
-    const PatInfo p = PTYX_F3_CARRY ? p_nxt : pat_info<SHIFT>(a, pat);
+    const PatInfo p = p_nxt;
     // ring (kRing): this wave's 16 KiB of the exchange buffer; slice n's operand descriptors
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0w = lds0 + (wv << 14);
@@ -1336,8 +1193,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
           for (int rb = 0; rb < 2; ++rb) {
             const int j = 2 * q + rb;
             const float2 O = sl[rb * 64 + io];
-            if (PTYX_F3MS_PARK_NT) st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
-            else st2(v[j], r_slot, vpark, 2048 * j);
+            st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
             v[j] = pcm(v[j], O);
             pin(v[j]);
           }
@@ -1385,7 +1241,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
         const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
         __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
                                          (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
-                                         PTYX_F3_NT ? 2 : 0);
+                                         kNtAux);
       }
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1496,7 +1352,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     }
     // ------------------------------------------------ probe / position gradient, next pattern's v
     const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
-    const bool first = pat == p0 || (PTYX_F3_CARRY ? m_prev : s_ld(a.bid + (pat - 1))) != p.m;
+    const bool first = pat == p0 || m_prev != p.m;
     m_prev = p.m;
     p_nxt = pn;
     const int seg = p.m + w;

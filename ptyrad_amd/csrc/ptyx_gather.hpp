@@ -37,16 +37,9 @@ struct GatherArgs {
   const int* boff = nullptr;   // bin offsets (tiles + 1) into blist, or NULL: scan every pattern
   const int* blist = nullptr;  // pattern indices by bin, ascending within a bin
 };
-#ifndef PTYX_GATHER_NT
-#define PTYX_GATHER_NT 0
-#endif
-#ifndef PTYX_GTY
-#define PTYX_GTY 16
-#endif
-#ifndef PTYX_GWAVES
-#define PTYX_GWAVES 16
-#endif
-constexpr int kGTX = 64, kGTY = PTYX_GTY, kGWaves = PTYX_GWAVES;
+// 64 × 16 object tiles, 16 waves per tile (measured: 128-wide tiles and 2 patterns per round
+// were slower)
+constexpr int kGTX = 64, kGTY = 16, kGWaves = 16;
 
 // ROWPERM: slots written by k_fused3 (N = 128), row y stored at row 2(y & 63) + (y >> 6).
 // bins of a tile's candidates: home tiles (ty − kBinRows + 1 … ty) × (tx − kBinCols + 1 … tx)
@@ -134,13 +127,7 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
         const int row = ty + r - cy;
         const int srow = ROWPERM ? 2 * (row & (N / 2 - 1)) + (row >> 6) : row;
         if (colok && row >= 0 && row < N) {
-#if PTYX_GATHER_NT   // slots are read once: non-temporal, so they do not displace the object rows
-          typedef float f2v __attribute__((ext_vector_type(2)));
-          const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(src + srow * N + col));
-          v[r] = make_float2(t.x, t.y);
-#else
           v[r] = src[srow * N + col];
-#endif
         } else {
           v[r] = make_float2(0.f, 0.f);
         }

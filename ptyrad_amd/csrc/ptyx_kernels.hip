@@ -258,6 +258,10 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
 
 // =====================================================================================
 // k_finalize: one thread per mini-batch — loss terms and adjoint coefficients.
+// bsums_out: write the mini-batch's additive sums (PTYX_BATCH_SUMS doubles: count, S_single,
+// ΣM^q1, S_poissn, ΣM^q2, sparse sums per object mode) and stop (ptyx_forward_loss_grad_begin);
+// bsums_in: take them from there instead of this call's patterns (ptyx_forward_loss_grad_end: the
+// sums of a mini-batch whose patterns are split over ranks, all-reduced by the caller).
 struct FinArgs {
   const int* boff;
   int n_batches, N, Nz, O;
@@ -271,23 +275,37 @@ struct FinArgs {
   int ci;
   int pcoef_O = 1;             // object modes with a pcoef plane (plane o holds c_sparse of mode o)
   long long pcoef_stride = 0;  // patterns per plane
+  double* bsums_out = nullptr;
+  const double* bsums_in = nullptr;
 };
 
 __global__ void k_finalize(FinArgs f) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= f.n_batches) return;
   const int b0 = f.boff[m], b1 = f.boff[m + 1];
-  const double B = (double)(b1 - b0);
-  const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
+  double B = (double)(b1 - b0);
   double S1 = 0, M1 = 0, S2 = 0, M2 = 0, sp[kMaxModesO] = {0};
-  for (int t = b0; t < b1; ++t) {
-    const float* ps = f.psums + (size_t)t * kNSum;
-    S1 += ps[0];
-    M1 += ps[1];
-    S2 += ps[2];
-    M2 += ps[3];
-    for (int o = 0; o < f.O; ++o) sp[o] += ps[kSumBase + o];
+  if (f.bsums_in) {
+    const double* bs = f.bsums_in + (size_t)m * kNBatchSum;
+    B = bs[0]; S1 = bs[1]; M1 = bs[2]; S2 = bs[3]; M2 = bs[4];
+    for (int o = 0; o < f.O; ++o) sp[o] = bs[5 + o];
+  } else {
+    for (int t = b0; t < b1; ++t) {
+      const float* ps = f.psums + (size_t)t * kNSum;
+      S1 += ps[0];
+      M1 += ps[1];
+      S2 += ps[2];
+      M2 += ps[3];
+      for (int o = 0; o < f.O; ++o) sp[o] += ps[kSumBase + o];
+    }
   }
+  if (f.bsums_out) {
+    double* bs = f.bsums_out + (size_t)m * kNBatchSum;
+    bs[0] = B; bs[1] = S1; bs[2] = M1; bs[3] = S2; bs[4] = M2;
+    for (int o = 0; o < kMaxModesO; ++o) bs[5 + o] = o < f.O ? sp[o] : 0.0;
+    return;
+  }
+  const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
   float terms[5] = {0, 0, 0, 0, 0};
   float c1 = 0.f, c2 = 0.f;
   if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
@@ -633,7 +651,30 @@ struct DeviceGuard {
     if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
   }
 };
+// Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
+// variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
+enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneCount };
+const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1};
 }  // namespace
+
+extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
+  g_err.clear();
+  for (int k = 0; key && k < kTuneCount; ++k)
+    if (std::strcmp(key, kTuneNames[k]) == 0) {
+      if (value < -1 || value > kTuneMax[k]) return fail(PTYX_EINVAL, std::string("tuning value out of range: ") + key);
+      g_tuning[k] = value;
+      return PTYX_OK;
+    }
+  return fail(PTYX_EINVAL, std::string("unknown tuning key: ") + (key ? key : "(null)"));
+}
+
+extern "C" int64_t ptyx_get_tuning(const char* key) {
+  for (int k = 0; key && k < kTuneCount; ++k)
+    if (std::strcmp(key, kTuneNames[k]) == 0) return g_tuning[k];
+  return -2;
+}
 
 struct ptyx_plan {
   ptyx_dims d;
@@ -659,7 +700,6 @@ struct ptyx_plan {
   float2* pcoef = nullptr;
   // k_fused3 (N = 128, single mode, f32 DPs): register-resident FFT, 2 workgroups per CU
   int nwg3 = 0;
-  size_t dyn3 = 0;            // extra dynamic LDS per k_fused3 workgroup (PTYX_F3_DYNLDS: occupancy experiments)
   float2* fpk = nullptr;      // packed probe spectrum / probe
   float2* oc = nullptr;       // A e^{iφ}
   double* pref = nullptr;     // summed-area table of |φ|^n (loss_sparse), (Nz, Ny, Nx + 1)
@@ -693,8 +733,24 @@ struct ptyx_plan {
   long long scratch_stride = 0;
   size_t ws_bytes = 0;
   std::vector<void*> allocs;
-  // single-mode fast kernels (P = O = Nz = 1, N <= 128); PTYX_GENERIC=1 forces the general ones
-  bool fast = true;
+  // What the last PTYX_PREP_FULL call left in Fp / fpk / hpk / oc / pref: a PTYX_PREP_REUSE call
+  // that does not match it prepares in full (include/ptyx.h)
+  struct PrepRecord {
+    bool valid = false;
+    int engine = -1;
+    const void *obja = nullptr, *objp = nullptr, *probe = nullptr, *H = nullptr;
+    int sparse_on = 0, sparse_n = 0;
+  } prep;
+  // ptyx_forward_loss_grad_begin → _end: the call in flight
+  bool pend = false;
+  ptyx_inputs pend_in{};
+  ptyx_grads pend_gz{};
+  ptyx_loss_cfg pend_cfg{};
+  const int32_t* pend_idx = nullptr;
+  const int32_t* pend_boff = nullptr;
+  int32_t pend_nb = 0, pend_n = 0;
+  float* pend_dp = nullptr;
+  int pend_engine = -1;
   // ptyx_profile_begin/end: HIP events around every launch (kind, start, stop)
   bool prof = false;
   struct ProfRec {
@@ -703,6 +759,10 @@ struct ptyx_plan {
   };
   mutable std::vector<ProfRec> recs;
 };
+
+static int busy(const ptyx_plan* pl) {
+  return pl->pend ? fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting for its _end on this plan") : 0;
+}
 
 enum KernelKind {
   kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather,
@@ -831,10 +891,6 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->d = d;
   pl->device = device;
   pl->n_cu = cu;
-  {
-    const char* gen = std::getenv("PTYX_GENERIC");
-    pl->fast = !(gen && gen[0] == '1');
-  }
   pl->nwg =std::max(d.P, std::min(d.max_patterns, cu * blocks_per_cu(d.N)));
   const size_t N2 = (size_t)d.N * d.N;
   const bool lds = d.N <= 128;
@@ -854,22 +910,20 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     free_plan(pl);
     return rc;
   }
-  const bool stripe = d.N == 256 && d.Nz == 1 && d.O <= sp::kMaxO && (d.flags & PTYX_SHIFT_PROBES) && pl->fast &&
-                      !std::getenv("PTYX_NO_STRIPE");
+  const bool stripe = d.N == 256 && d.Nz == 1 && d.O <= sp::kMaxO && (d.flags & PTYX_SHIFT_PROBES);
   if (stripe) {
-    // per-call intermediates (T1/T4, ψ⁰: P fields; T2/T3: P·O fields per pattern; PTYX_S_PSI0=0
-    // drops ψ⁰ and P4 recomputes it) within PTYX_STRIPE_MB (default the smaller of 16 GiB
+    // per-call intermediates (T1/T4, ψ⁰: P fields; T2/T3: P·O fields per pattern; without the ψ⁰
+    // park, k_s4 recomputes it) within PTYX_STRIPE_MB (default the smaller of 16 GiB
     // and a quarter of the free HBM); calls beyond the capacity are split by the host at
     // mini-batch boundaries
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     long long mb = std::min<long long>(16384, (long long)(free_b / 4 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_STRIPE_MB")) mb = std::atoll(e);
-    const char* ppsi = std::getenv("PTYX_S_PSI0");
     // measured (profiles/r02/r02k_*): one object mode recomputes ψ⁰ in P4 (c5 221 k vs 205 k
     // patterns/s: the park's write in P2 costs more than the row IFFT); two object modes park it
     // (c3 66.0 k vs 59.9 k: P4 with the extra transform spills)
-    const bool park = ppsi ? ppsi[0] != '0' : d.O > 1;
+    const bool park = g_tuning[kTunePsi0] >= 0 ? g_tuning[kTunePsi0] != 0 : d.O > 1;
     const long long per = (long long)((park ? 2 : 1) * d.P + d.P * d.O) * (long long)N2 * (long long)sizeof(float2);
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / per);
     if (cap >= 1) {
@@ -892,15 +946,14 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       // has consumed) and k_obj_gather reduces them per tile (deterministic, no atomics).  One
       // object mode keeps k_s4's f32 atomics (profiles/r02/ab/r02y_*: the epilogue costs c3 20 ms
       // of 66 in k_s4 but c5 only 2.7 of 23, less than the slot stores plus the gather would).
-      const char* sg = std::getenv("PTYX_S_GATHER");
-      pl->sgather = sg ? sg[0] == '1' : d.O > 1;
+      pl->sgather = g_tuning[kTuneGather] >= 0 ? g_tuning[kTuneGather] != 0 : d.O > 1;
       if (pl->sgather && ((rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns * d.O)) || (rc = alloc_bins(pl)))) {
         free_plan(pl);
         return rc;
       }
     }
   }
-  if (!stripe && d.Nz == 1 && d.P * d.O > 1 && pl->fast && !std::getenv("PTYX_NO_FFC")) {
+  if (!stripe && d.Nz == 1 && d.P * d.O > 1) {
     // far-field cache: (P·O + P)·N² float2 per pattern of a call, within PTYX_FFC_MB (default the
     // smaller of 64 GiB and a third of the free HBM); calls beyond its capacity are split by the host
     size_t free_b = 0, total_b = 0;
@@ -918,27 +971,24 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->ffc_cap = cap;
     }
   }
-  if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast) {
+  if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16)) {
     // single-slice register engine: one g_O slot per pattern of a call (N² float2), bounded by
     // PTYX_OBJ_SCRATCH_MB; larger calls are split by the host at mini-batch boundaries
     long long mb = 16384;
     if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2));
-    const char* f3 = std::getenv("PTYX_FUSED3");
-    if (const char* dl = std::getenv("PTYX_F3_DYNLDS")) pl->dyn3 = (size_t)std::max(0LL, std::atoll(dl));
     int occ3 = 0;
-    if (!(f3 && f3[0] == '0') && cap > 0 &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, pl->dyn3) == hipSuccess &&
+    if (cap > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3<true, true, 0>, 256, 0) == hipSuccess &&
         occ3 > 0) {
       int o2 = 0;
       for (auto kf : {f3::k_fused3<true, true, 2>, f3::k_fused3<true, false, 2>, f3::k_fused3<false, true, 0>,
                       f3::k_fused3<false, true, 2>, f3::k_fused3<false, false, 2>})
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, pl->dyn3) == hipSuccess) occ3 = std::min(occ3, o2);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
       // segment ids = mini-batches + workgroups of a call; sized for a mean mini-batch of ≥ 8
-      // patterns (PTYX_SEG_DIV); calls with more segments take the two-pass engine
-      long long div = 8;
-      if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
+      // patterns; calls with more segments take the two-pass engine
+      constexpr long long div = 8;
       pl->seg_cap = pl->nwg3 + (cap + div - 1) / div;   // a call holds at most `cap` patterns
       if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
@@ -956,15 +1006,14 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->og_cap = cap;
     }
   }
-  if (d.N == 128 && d.P * d.O == 1 && d.Nz > 1 && !(d.flags & PTYX_MEAS_F16) && pl->fast) {
+  if (d.N == 128 && d.P * d.O == 1 && d.Nz > 1 && !(d.flags & PTYX_MEAS_F16)) {
     // multislice register engine: Nz slot planes per pattern (parked ψⁿ, then slice n's
     // object gradient), bounded by PTYX_OBJ_SCRATCH_MB like the single-slice slots
-    const char* f3 = std::getenv("PTYX_FUSED3");
     long long mb = 16384;
     if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2 * d.Nz));
     int occ3 = 0;
-    if (!(f3 && f3[0] == '0') && cap > 0 &&
+    if (cap > 0 &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fused3ms<true, true, 0>, 256, 0) == hipSuccess &&
         occ3 > 0) {
       int o2 = 0;
@@ -972,8 +1021,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
                       f3::k_fused3ms<false, true, 2>, f3::k_fused3ms<false, false, 2>})
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
       pl->nwg3 = std::min(cu * occ3, std::max(1, d.max_patterns));
-      long long div = 8;
-      if (const char* sd = std::getenv("PTYX_SEG_DIV")) div = std::max(1LL, std::atoll(sd));
+      constexpr long long div = 8;
       pl->seg_cap = pl->nwg3 + (cap + div - 1) / div;   // a call holds at most `cap` patterns
       if ((rc = dalloc(pl, &pl->ogscr, (size_t)cap * d.Nz * N2)) || (rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) ||
           (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) ||
@@ -1056,7 +1104,7 @@ static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) 
   ProfScope ps(pl, kKForward, st);
   const int grid = std::max(1, std::min(a.n_idx, pl->nwg));
   if constexpr (Geo<N>::kLds) {
-    if (pl->d.P * pl->d.O * pl->d.Nz == 1 && pl->fast) {
+    if (pl->d.P * pl->d.O * pl->d.Nz == 1) {
       const bool sums = a.psums != nullptr;
       if (a.shift && sums) hipLaunchKernelGGL((k_forward1<N, true, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
       else if (a.shift) hipLaunchKernelGGL((k_forward1<N, true, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
@@ -1076,7 +1124,7 @@ static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, 
   const int grid = pl->nwg;  // every workgroup zeroes its slab, so launch all of them
   const bool single = pl->d.P * pl->d.O == 1;
   if constexpr (Geo<N>::kLds) {
-    if (single && pl->d.Nz == 1 && pl->fast) {
+    if (single && pl->d.Nz == 1) {
       const dim3 gr(grid), bl(Geo<N>::NT);
       if (a.shift && ext) hipLaunchKernelGGL((k_adjoint1<N, true, true>), gr, bl, 0, st, a);
       else if (a.shift) hipLaunchKernelGGL((k_adjoint1<N, true, false>), gr, bl, 0, st, a);
@@ -1124,8 +1172,13 @@ int launch_status(const char* what) { return ::launch_status(what); }
 
 // ---------------------------------------------------------------- k_fused3 path (N = 128)
 // Launch sequence of one ptyx_forward_loss_grad call on the register-resident engine.
-static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
-                      const ptyx_grads& gz, hipStream_t st, float* loss_terms) {
+// ptyx_forward_loss_grad_begin / _end phases of one call (kPhaseAll: both, with the call's own sums)
+enum CallPhase { kPhaseAll = 0, kPhaseBegin = 1, kPhaseEnd = 2 };
+enum EngineKind { kEngTwoPass = 0, kEngFused3 = 1, kEngStripe = 2 };
+
+// Preparation, pattern table and the k_fused3 / k_fused3ms pass (everything before k_finalize).
+static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                       const ptyx_grads& gz, hipStream_t st) {
   constexpr int N = 128, N2 = N * N;
   const ptyx_dims& d = pl->d;
   const bool sparse = cfg->sparse_on != 0;
@@ -1208,17 +1261,30 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
     if (a.shift) {
-      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, pl->dyn3, st, f);
-      else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, pl->dyn3, st, f);
-      else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, pl->dyn3, st, f);
+      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, 0, st, f);
     } else {
-      if (half) hipLaunchKernelGGL((f3::k_fused3<false, true, 0>), gr, bl, pl->dyn3, st, f);
-      else if (single) hipLaunchKernelGGL((f3::k_fused3<false, true, 2>), gr, bl, pl->dyn3, st, f);
-      else hipLaunchKernelGGL((f3::k_fused3<false, false, 2>), gr, bl, pl->dyn3, st, f);
+      if (half) hipLaunchKernelGGL((f3::k_fused3<false, true, 0>), gr, bl, 0, st, f);
+      else if (single) hipLaunchKernelGGL((f3::k_fused3<false, true, 2>), gr, bl, 0, st, f);
+      else hipLaunchKernelGGL((f3::k_fused3<false, false, 2>), gr, bl, 0, st, f);
     }
   }
-  int rc = launch_status("k_fused3 launch");
-  if (rc) return rc;
+  return launch_status("k_fused3 launch");
+}
+
+static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                      const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+  constexpr int N = 128, N2 = N * N;
+  const ptyx_dims& d = pl->d;
+  const bool sparse = cfg->sparse_on != 0;
+  const int Nz = d.Nz;
+  const bool single = cfg->single_on != 0;
+  const int ci = single ? 0 : 1;
+  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int nseg = a.n_batches + G;
+  int rc = PTYX_OK;
+  if (ph != kPhaseEnd && (rc = fused3_pass(pl, in, a, cfg, gz, st))) return rc;
   FinArgs fa{};
   fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
   fa.psums = pl->psums; fa.occu = in->omode_occu;
@@ -1229,16 +1295,16 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     fa.pcoef = pl->pcoef;
     fa.ci = ci;
   }
+  fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
+  fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
     hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
   }
-  if ((rc = launch_status("k_finalize launch"))) return rc;
+  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   if (gz.d_obja || gz.d_objp) {
-    // candidate bins of the gather (PTYX_GATHER_SCAN=1: every tile scans every pattern instead)
-    const char* gs = std::getenv("PTYX_GATHER_SCAN");
-    const bool binned = !(gs && gs[0] == '1');
-    if (binned) {
+    // candidate bins of the gather: the patterns by object tile of their window origin
+    {
       ProfScope ps(pl, kKTable, st);
       const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
       hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
@@ -1251,16 +1317,14 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     }
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
-    if (binned) {
-      g.boff = pl->boff;
-      g.blist = pl->blist;
-    }
+    g.boff = pl->boff;
+    g.blist = pl->blist;
     g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse ? cfg->sparse_n : 1;
     g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
     const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
     // fewer than 64 candidates per tile on average (c4's 8,192-pattern calls over 13,340 tiles:
     // ≈ 17): 4 waves a tile instead of kGWaves
-    const bool sparse_tiles = binned && (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
+    const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
     ProfScope ps(pl, kKGather, st);
     const size_t plane = (size_t)d.Ny * d.Nx;
     g.nz = Nz;
@@ -1301,29 +1365,12 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
 
 // ---------------------------------------------------------------- stripe engine (N = 256)
 // Launch sequence of one ptyx_forward_loss_grad call on the stripe engine (ptyx_stripe.hpp).
-static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
-                      const ptyx_grads& gz, hipStream_t st, float* loss_terms) {
+// The stripe engine's per-call argument block (shared by the passes before and after k_finalize).
+static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, const ptyx_grads& gz) {
   using namespace sp;
   const ptyx_dims& d = pl->d;
   const int n = a.n_idx, P = d.P, O = d.O;
   const bool single = cfg->single_on != 0;
-  const bool tail = gz.d_probe != nullptr || gz.d_shifts != nullptr;
-  const bool any_grad = gz.d_obja || gz.d_objp || tail;
-  const bool reuse = cfg->prep == PTYX_PREP_REUSE;     // object / probe prepared by the previous call
-  if (!reuse) launch_spectrum<256>(pl, a, st);         // F(P_p), natural order
-  {
-    ProfScope ps(pl, kKTable, st);
-    hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
-                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.shifts, pl->ssxy);
-    hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
-    hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (n + 255) / 256))), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
-                       pl->bbox, kN);
-  }
-  if (!reuse) {
-    ProfScope ps(pl, kKObjPrep, st);   // O = A e^{iφ} on the rows the call's windows touch (or all)
-    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.O * d.Ny), dim3(256), 0, st, a.obja, a.objp, d.O * d.Ny, d.Nx, pl->oc,
-                       nullptr, 1, cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, kN);
-  }
   SArgs s{};
   s.n = n; s.P = P; s.O = O; s.Ny = d.Ny; s.Nx = d.Nx; s.n_scans = d.n_scans; s.meas_f16 = a.meas_f16;
   s.idx = a.idx; s.bid = pl->bid; s.geo = pl->geo; s.shifts = a.shifts; s.sxy = pl->ssxy; s.mrow = a.mrow;
@@ -1339,6 +1386,30 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   s.groups = std::max(1, std::min(pl->stripe_groups, n));
   s.slabpart = pl->sslab; s.dsp = pl->sdsp;
   s.twg = pl->twg;
+  return s;
+}
+
+// Stripe engine before k_finalize: preparation, pattern table, k_s1..k_s3, per-pattern sums.
+static int stripe_pass(ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, const sp::SArgs& s, hipStream_t st) {
+  using namespace sp;
+  const ptyx_dims& d = pl->d;
+  const int n = a.n_idx, P = d.P, O = d.O;
+  const bool single = cfg->single_on != 0;
+  const bool reuse = cfg->prep == PTYX_PREP_REUSE;     // object / probe prepared by the previous call
+  if (!reuse) launch_spectrum<256>(pl, a, st);         // F(P_p), natural order
+  {
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
+                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.shifts, pl->ssxy);
+    hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
+    hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (n + 255) / 256))), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
+                       pl->bbox, kN);
+  }
+  if (!reuse) {
+    ProfScope ps(pl, kKObjPrep, st);   // O = A e^{iφ} on the rows the call's windows touch (or all)
+    hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.O * d.Ny), dim3(256), 0, st, a.obja, a.objp, d.O * d.Ny, d.Nx, pl->oc,
+                       nullptr, 1, cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, kN);
+  }
   const dim3 bl(256);
   {
     ProfScope ps(pl, kKS1, st);
@@ -1352,11 +1423,10 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   {
     ProfScope ps(pl, kKS3, st);
     const dim3 gr(n, kStripes);
-    // Ψ of the first min(P·O, PTYX_S3_HOLD) modes stays in registers between k_s3's two sweeps,
-    // the other modes' column FFTs are redone.  Default (profiles/r02/ab/r02n_*): 2 of P·O ≤ 4
-    // (c5: three workgroups per CU beat the saved re-reads), 4 above (c3)
-    const char* hl = std::getenv("PTYX_S3_HOLD");
-    const int hold_max = hl ? std::max(0, std::min(4, std::atoi(hl))) : (P * O <= 4 ? 2 : 4);
+    // Ψ of the first min(P·O, hold) modes stays in registers between k_s3's two sweeps, the other
+    // modes' column FFTs are redone.  Default (profiles/r02/ab/r02n_*): 2 of P·O ≤ 4 (c5: three
+    // workgroups per CU beat the saved re-reads), 4 above (c3)
+    const int hold_max = g_tuning[kTuneHold] >= 0 ? std::min<int>(4, (int)g_tuning[kTuneHold]) : (P * O <= 4 ? 2 : 4);
     const int H = std::min(P * O, hold_max);
     const bool half = single && s.q == 0.5f;
 #define PTYX_S3(SG, QM)                                                                                  \
@@ -1378,6 +1448,21 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(k_s_psum, dim3((n * kNSum + 255) / 256), dim3(256), 0, st, pl->spsum, n, pl->psums);
   }
+  return launch_status("k_s_psum launch");
+}
+
+static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                      const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+  using namespace sp;
+  const ptyx_dims& d = pl->d;
+  const int n = a.n_idx, P = d.P, O = d.O;
+  const bool tail = gz.d_probe != nullptr || gz.d_shifts != nullptr;
+  const bool any_grad = gz.d_obja || gz.d_objp || tail;
+  const sp::SArgs s = stripe_args(pl, a, cfg, gz);
+  const bool sgather = s.oslot != nullptr;
+  const dim3 bl(256);
+  int rc = PTYX_OK;
+  if (ph != kPhaseEnd && (rc = stripe_pass(pl, a, cfg, s, st))) return rc;
   FinArgs fa{};
   fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = kN; fa.Nz = 1; fa.O = O;
   fa.psums = pl->psums; fa.occu = in->omode_occu;
@@ -1390,11 +1475,13 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     fa.pcoef_O = O;
     fa.pcoef_stride = n;
   }
+  fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
+  fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
     hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
   }
-  if ((rc = launch_status("k_finalize launch"))) return rc;
+  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   if (!any_grad) return PTYX_OK;
   {
     ProfScope ps(pl, kKS4, st);
@@ -1514,9 +1601,11 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
   int rc = check_inputs(pl, in, false);
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
+  if ((rc = busy(pl))) return rc;
   if (n_idx == 0) return PTYX_OK;
   if (!idx || !dp_out) return fail(PTYX_EINVAL, "idx / dp_out is null");
   DeviceGuard dg(pl->device);
+  pl->prep.valid = false;   // F(P) is rewritten
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   KArgs a = make_args(pl, in, idx, n_idx);
   a.dp_out = dp_out;
@@ -1546,12 +1635,11 @@ static int reduce_prop_grad(const ptyx_plan* pl, const KArgs& a, const ptyx_grad
   return launch_status("k_hslab_reduce launch");
 }
 
-extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
-                                      const int32_t* boff, int32_t n_batches, int32_t n_idx,
-                                      const ptyx_loss_cfg* cfg, float* loss_terms, float* dp_out,
-                                      const ptyx_grads* grads) {
-  g_err.clear();
-  if (!pl || !cfg) return fail(PTYX_EINVAL, "plan / cfg is null");
+// Validation, argument block and engine choice of one ptyx_forward_loss_grad call.
+static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, const int32_t* boff,
+                      int32_t n_batches, int32_t n_idx, const ptyx_loss_cfg* cfg, float* dp_out,
+                      const ptyx_grads& gz, KArgs* out, int* engine) {
+  if (!cfg) return fail(PTYX_EINVAL, "cfg is null");
   int rc = check_inputs(pl, in, true);
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
@@ -1560,8 +1648,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  DeviceGuard dg(pl->device);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (cfg->prep < PTYX_PREP_CALL || cfg->prep > PTYX_PREP_REUSE) return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
   a.boff = boff;
   a.n_batches = n_batches;
@@ -1575,8 +1662,6 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   a.psums = pl->psums;
   a.coef = pl->coef;
   a.dp_out = dp_out;
-  ptyx_grads gz{};
-  if (grads) gz = *grads;
   a.d_obja = gz.d_obja;
   a.d_objp = gz.d_objp;
   a.d_shifts = gz.d_shifts;
@@ -1585,57 +1670,79 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   // propagator gradients and per-position tilts: general two-pass engine only
   const bool want_H = a.hslab != nullptr || a.d_tilts != nullptr || a.d_dz != nullptr ||
                       (a.ptilt != nullptr && pl->d.Nz > 1);
-
   a.w1 = cfg->single_w;
   a.w2 = cfg->poissn_w;
   a.ws = cfg->sparse_w;
   a.grad_scale = cfg->grad_scale;
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;
-  const bool single_mode = pl->fast && pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
-  // register-resident engine (k_fused3): N = 128, f32 DPs, one data term, slots and segment
-  // slabs large enough for the call (no co-residency or max_batch condition: it never waits)
-  const bool fused3 = any_grad && single_mode && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 &&
-                      n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
-                      (cfg->single_on != 0) != (cfg->poissn_on != 0);
-  // multislice register engine (k_fused3ms): N = 128, P = O = 1, Nz ≥ 2, f32 DPs
-  const bool fused3ms = any_grad && !want_H && pl->ms3 && !std::getenv("PTYX_TWO_PASS") && pl->nwg3 > 0 && !a.meas_f16 &&
-                        n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap &&
-                        (cfg->single_on != 0) != (cfg->poissn_on != 0);
-  if (fused3 || fused3ms) {
-#ifndef PTYX_ONLY_N
-    return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
-#else
-    if (PTYX_ONLY_N == 128) return run_fused3(pl, in, a, cfg, gz, st, loss_terms);
-#endif
-  }
+  const bool one_term = (cfg->single_on != 0) != (cfg->poissn_on != 0);
+  const bool single_mode = pl->d.N <= 128 && pl->d.P * pl->d.O * pl->d.Nz == 1;
+  const bool slots_fit = n_idx <= pl->og_cap && (long long)n_batches + std::min(pl->nwg3, n_idx) <= pl->seg_cap;
+  // register-resident engines: k_fused3 (N = 128, single mode) and k_fused3ms (N = 128, P = O = 1,
+  // Nz ≥ 2); f32 DPs, one data term, slots and segment slabs large enough for the call (no
+  // co-residency or max_batch condition: they never wait)
+  const bool fused3 = any_grad && single_mode && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 && slots_fit && one_term;
+  const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit && one_term;
   // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): one data term, call within capacity
-  const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift &&
-                      (cfg->single_on != 0) != (cfg->poissn_on != 0) && !std::getenv("PTYX_TWO_PASS");
-  if (stripe) {
-#if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 256
-    return run_stripe(pl, in, a, cfg, gz, st, loss_terms);
+  const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && one_term;
+#ifdef PTYX_ONLY_N
+  *engine = (fused3 || fused3ms) && PTYX_ONLY_N == 128 ? kEngFused3 : stripe && PTYX_ONLY_N == 256 ? kEngStripe : kEngTwoPass;
+#else
+  *engine = (fused3 || fused3ms) ? kEngFused3 : stripe ? kEngStripe : kEngTwoPass;
 #endif
-  }
-
-  // two-pass engine: k_forward (dp, loss partial sums) → k_finalize → k_adjoint
-  if (a.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
-  if (any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
+  if (*engine == kEngTwoPass && any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
     a.ffc = pl->ffc;
     a.ffc_per = pl->ffc_per;
   }
-  PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
-  if ((rc = launch_status("k_forward launch"))) return rc;
+  *out = a;
+  return PTYX_OK;
+}
+
+// PTYX_PREP_REUSE only when the plan's record says a PTYX_PREP_FULL call of the same engine
+// prepared the same inputs; otherwise the call prepares in full (a call split into
+// pieces can change engine between pieces).  Updates the record.
+static void resolve_prep(ptyx_plan* pl, const ptyx_inputs* in, int engine, ptyx_loss_cfg* c) {
+  auto& r = pl->prep;
+  if (c->prep == PTYX_PREP_REUSE) {
+    const bool same = r.valid && r.engine == engine && r.obja == in->obja && r.objp == in->objp &&
+                      r.probe == in->probe && r.H == in->H && r.sparse_on == c->sparse_on &&
+                      (!c->sparse_on || r.sparse_n == c->sparse_n);
+    if (same) return;
+    c->prep = PTYX_PREP_FULL;
+  }
+  if (c->prep == PTYX_PREP_FULL) {
+    r.valid = true;
+    r.engine = engine;
+    r.obja = in->obja; r.objp = in->objp; r.probe = in->probe; r.H = in->H;
+    r.sparse_on = c->sparse_on; r.sparse_n = c->sparse_n;
+  } else {
+    r.valid = false;   // PTYX_PREP_CALL overwrites part of the preparation
+  }
+}
+
+// The two-pass engine: k_forward (dp, loss partial sums) → k_finalize → k_adjoint.
+static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                        const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+  int rc = PTYX_OK;
+  if (ph != kPhaseEnd) {
+    if (a.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+    PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+    if ((rc = launch_status("k_forward launch"))) return rc;
+  }
   FinArgs f{};
-  f.boff = boff; f.n_batches = n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
+  f.boff = a.boff; f.n_batches = a.n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
   f.psums = pl->psums; f.occu = in->omode_occu;
   f.single_on = cfg->single_on; f.pois_on = cfg->poissn_on; f.sparse_on = cfg->sparse_on;
   f.sparse_n = cfg->sparse_n; f.w1 = cfg->single_w; f.w2 = cfg->poissn_w; f.ws = cfg->sparse_w;
   f.grad_scale = cfg->grad_scale; f.coef = pl->coef; f.loss_terms = loss_terms;
+  f.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
+  f.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
-    hipLaunchKernelGGL(k_finalize, dim3((n_batches + 127) / 128), dim3(128), 0, st, f);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, f);
   }
-  if ((rc = launch_status("k_finalize launch"))) return rc;
+  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;
   if (!any_grad) return PTYX_OK;
   PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
   if ((rc = launch_status("k_adjoint launch"))) return rc;
@@ -1647,6 +1754,80 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   return PTYX_OK;
 }
 
+static int run_call(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                    const ptyx_grads& gz, int engine, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+#if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
+  if (engine == kEngFused3) return run_fused3(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
+#endif
+#if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 256
+  if (engine == kEngStripe) return run_stripe(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
+#endif
+  return run_two_pass(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
+}
+
+extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
+                                      const int32_t* boff, int32_t n_batches, int32_t n_idx,
+                                      const ptyx_loss_cfg* cfg, float* loss_terms, float* dp_out,
+                                      const ptyx_grads* grads) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  int rc = busy(pl);
+  if (rc) return rc;
+  ptyx_grads gz{};
+  if (grads) gz = *grads;
+  KArgs a{};
+  int engine = kEngTwoPass;
+  if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
+  DeviceGuard dg(pl->device);
+  ptyx_loss_cfg c = *cfg;
+  resolve_prep(pl, in, engine, &c);
+  return run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), loss_terms, kPhaseAll, nullptr);
+}
+
+extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
+                                            const int32_t* boff, int32_t n_batches, int32_t n_idx,
+                                            const ptyx_loss_cfg* cfg, float* dp_out, const ptyx_grads* grads,
+                                            double* batch_sums) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  int rc = busy(pl);
+  if (rc) return rc;
+  if (!batch_sums) return fail(PTYX_EINVAL, "batch_sums is null");
+  ptyx_grads gz{};
+  if (grads) gz = *grads;
+  KArgs a{};
+  int engine = kEngTwoPass;
+  if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
+  DeviceGuard dg(pl->device);
+  ptyx_loss_cfg c = *cfg;
+  resolve_prep(pl, in, engine, &c);
+  if ((rc = run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), nullptr, kPhaseBegin,
+                     batch_sums)))
+    return rc;
+  pl->pend = true;
+  pl->pend_in = *in; pl->pend_gz = gz; pl->pend_cfg = c;
+  pl->pend_idx = idx; pl->pend_boff = boff; pl->pend_nb = n_batches; pl->pend_n = n_idx;
+  pl->pend_dp = dp_out; pl->pend_engine = engine;
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_forward_loss_grad_end(ptyx_plan* pl, void* stream, const double* batch_sums, float* loss_terms) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (!pl->pend) return fail(PTYX_EINVAL, "no ptyx_forward_loss_grad_begin call is waiting on this plan");
+  if (!batch_sums) return fail(PTYX_EINVAL, "batch_sums is null");
+  pl->pend = false;
+  KArgs a{};
+  int engine = kEngTwoPass;
+  int rc = setup_call(pl, &pl->pend_in, pl->pend_idx, pl->pend_boff, pl->pend_nb, pl->pend_n, &pl->pend_cfg,
+                      pl->pend_dp, pl->pend_gz, &a, &engine);
+  if (rc) return rc;
+  if (engine != pl->pend_engine) return fail(PTYX_EINVAL, "internal: engine changed between _begin and _end");
+  DeviceGuard dg(pl->device);
+  return run_call(pl, &pl->pend_in, a, &pl->pend_cfg, pl->pend_gz, engine, reinterpret_cast<hipStream_t>(stream),
+                  loss_terms, kPhaseEnd, const_cast<double*>(batch_sums));
+}
+
 extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
                                  int32_t n_idx, const float* dLdI, float grad_scale, const ptyx_grads* grads) {
   g_err.clear();
@@ -1654,8 +1835,10 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   int rc = check_inputs(pl, in, false);
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
+  if ((rc = busy(pl))) return rc;
   if (n_idx == 0 || !grads) return PTYX_OK;
   if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
+  pl->prep.valid = false;   // F(P) is rewritten
   const ptyx_grads gz = *grads;
   if (!(gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz)) return PTYX_OK;
   DeviceGuard dg(pl->device);

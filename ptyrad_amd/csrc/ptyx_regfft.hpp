@@ -32,15 +32,9 @@
 
 #include <type_traits>
 
-// PTYX_RF_FENCE: 1 = scheduling barrier after every 8-register group of the FFT (keeps the
-// machine scheduler from interleaving all 64 registers' work, which needs ~70 extra VGPRs).
-#ifndef PTYX_RF_FENCE
-#define PTYX_RF_FENCE 1
-#endif
-#define PTYX_RF_SB()                                  \
-  do {                                                \
-    if (PTYX_RF_FENCE) __builtin_amdgcn_sched_barrier(0); \
-  } while (0)
+// Scheduling barrier after every 8-register group of the FFT (keeps the machine scheduler from
+// interleaving all 64 registers' work, which needs ~70 extra VGPRs).
+#define PTYX_RF_SB() __builtin_amdgcn_sched_barrier(0)
 
 namespace ptyx {
 namespace rf {
@@ -128,12 +122,8 @@ __device__ __forceinline__ float2 rot_sel(float2 v, float lf) {
 __device__ __forceinline__ float2 add2(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 sub2(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 
-// PTYX_RF_PK: 1 = packed f32 butterflies (v_pk_add/mul/fma_f32: one instruction per complex
-// add, two per complex twiddle multiply, the ±i and odd-π/4 swaps folded into op_sel / neg
-// modifiers), 0 = scalar f32.  Same arithmetic per component up to FMA contraction.
-#ifndef PTYX_RF_PK
-#define PTYX_RF_PK 1
-#endif
+// Packed f32 butterflies (v_pk_add/mul/fma_f32: one instruction per complex add, two per complex
+// twiddle multiply, the ±i and odd-π/4 swaps folded into op_sel / neg modifiers).
 typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f pv(float2 a) { return __builtin_bit_cast(v2f, a); }
 __device__ __forceinline__ float2 pf(v2f a) { return __builtin_bit_cast(float2, a); }
@@ -247,13 +237,8 @@ template <int R, int DIR>
 __device__ __forceinline__ void dft(float2 (&v)[R]) {
   if constexpr (R == 2) {
     const float2 a = v[0], b = v[1];
-#if PTYX_RF_PK
     v[0] = padd(a, b);
     v[1] = psub(a, b);
-#else
-    v[0] = add2(a, b);
-    v[1] = sub2(a, b);
-#endif
   } else {
     float2 e[R / 2], o[R / 2];
 #pragma unroll
@@ -265,13 +250,7 @@ __device__ __forceinline__ void dft(float2 (&v)[R]) {
     dft<R / 2, DIR>(o);
     sfor<0, R / 2>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-#if PTYX_RF_PK
       pbfly<R, k, DIR>(e[k], o[k], v[k], v[k + R / 2]);
-#else
-      const float2 t = rot<R, k, DIR>(o[k]);
-      v[k] = add2(e[k], t);
-      v[k + R / 2] = sub2(e[k], t);
-#endif
     });
   }
 }
@@ -287,11 +266,7 @@ __device__ __forceinline__ void dft64(float2 (&v)[64]) {
     dft<8, DIR>(t);
     sfor<0, 8>([&](auto K2) {
       constexpr int k2 = decltype(K2)::value;
-#if PTYX_RF_PK
       v[n1 + 8 * k2] = prot<64, n1 * k2, DIR>(t[k2]);
-#else
-      v[n1 + 8 * k2] = rot<64, n1 * k2, DIR>(t[k2]);
-#endif
     });
     PTYX_RF_SB();
   });
@@ -325,7 +300,6 @@ __device__ __forceinline__ LaneCtx lane_ctx(int lane) {
   return LaneCtx{1.0f - 2.0f * lf, lf};
 }
 
-#if PTYX_RF_PK
 // v·(lf ? W : 1) packed: u = v·(W − 1) (two instructions), v + lf·u (one)
 template <int M, int K, int DIR>
 __device__ __forceinline__ float2 prot_sel(float2 v, float lf) {
@@ -344,7 +318,6 @@ __device__ __forceinline__ float2 plane_mix(float2 m, float sgn) {
   const v2f x = {xl1(m.x), xl1(m.y)};
   return pf(__builtin_elementwise_fma((v2f){sgn, sgn}, pv(m), x));
 }
-#endif
 
 // DIF step: even lane a = x0 + x1, odd lane b = (x0 − x1)·W128^(DIR·j), j = register index
 template <int DIR>
@@ -352,12 +325,7 @@ __device__ __forceinline__ void lane_pre(float2 (&v)[64], LaneCtx c) {
   sfor<0, 64>([&](auto J) {
     constexpr int j = decltype(J)::value;
     const float2 m = v[j];
-#if PTYX_RF_PK
     v[j] = prot_sel<128, j, DIR>(plane_mix(m, c.sgn), c.lf);
-#else
-    const float2 t = make_float2(fmaf(c.sgn, m.x, xl1(m.x)), fmaf(c.sgn, m.y, xl1(m.y)));
-    v[j] = rot_sel<128, j, DIR>(t, c.lf);
-#endif
     if constexpr ((j & 7) == 7) PTYX_RF_SB();
   });
 }
@@ -366,12 +334,7 @@ template <int DIR>
 __device__ __forceinline__ void lane_post(float2 (&v)[64], LaneCtx c) {
   sfor<0, 64>([&](auto J) {
     constexpr int j = decltype(J)::value;
-#if PTYX_RF_PK
     v[j] = plane_mix(prot_sel<128, j, DIR>(v[j], c.lf), c.sgn);
-#else
-    const float2 m = rot_sel<128, j, DIR>(v[j], c.lf);
-    v[j] = make_float2(fmaf(c.sgn, m.x, xl1(m.x)), fmaf(c.sgn, m.y, xl1(m.y)));
-#endif
     if constexpr ((j & 7) == 7) PTYX_RF_SB();
   });
 }
@@ -399,11 +362,7 @@ __device__ __forceinline__ int swz(int r) {
 __device__ __forceinline__ void flip_odd(float2 (&v)[64], float s) {
 #pragma unroll
   for (int i = 1; i < 64; i += 2) {
-#if PTYX_RF_PK
     v[i] = pf(pv(v[i]) * (v2f){s, s});
-#else
-    v[i] = make_float2(v[i].x * s, v[i].y * s);
-#endif
   }
 }
 

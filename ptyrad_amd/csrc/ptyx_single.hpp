@@ -7,43 +7,6 @@
 // registers between its two uses (same last-pass point order), and g ⊙ conj(O) goes straight
 // into LDS for the probe-gradient FFT.  No per-workgroup global scratch.
 //
-// Which prefetches pay depends on register pressure at the 128-VGPR cap (1024 threads):
-#ifndef PTYX_ADJ_PREFETCH_OBJ
-#define PTYX_ADJ_PREFETCH_OBJ 0
-#endif
-#ifndef PTYX_ADJ_PREFETCH_FP
-#define PTYX_ADJ_PREFETCH_FP 0
-#endif
-#ifndef PTYX_ADJ_PREFETCH_SLAB
-#define PTYX_ADJ_PREFETCH_SLAB 0
-#endif
-// Cost-attribution knobs (experiments only, results are wrong with them set): drop the object
-// gradient atomics / the probe slab update from the fused kernel.
-#ifndef PTYX_EXP_NO_OBJ_ATOMIC
-#define PTYX_EXP_NO_OBJ_ATOMIC 0
-#endif
-#ifndef PTYX_EXP_NO_SLAB
-#define PTYX_EXP_NO_SLAB 0
-#endif
-// PTYX_EXP_PHASE_TIMES=1: barrier + s_memrealtime stamp at every phase boundary of k_fused1;
-// workgroups 0 and 128 printf their per-phase totals (µs) at exit.
-#ifndef PTYX_EXP_PHASE_TIMES
-#define PTYX_EXP_PHASE_TIMES 0
-#endif
-#if PTYX_EXP_PHASE_TIMES
-#define PTYX_PHASE(k)                            \
-  do {                                           \
-    __syncthreads();                             \
-    const unsigned long long _t = wall_clock64(); \
-    ph_acc[k] += _t - ph_prev;                   \
-    ph_prev = _t;                                \
-  } while (0)
-#else
-#define PTYX_PHASE(k) \
-  do {                \
-  } while (0)
-#endif
-//
 // All prefetches are unconditional and every switch that decides whether a register array is
 // written is a template parameter: a conditionally written array is loop-carried by the
 // compiler and stays live (and spilled) across the whole persistent pattern loop.
@@ -281,20 +244,13 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
           v = cscale(Psi, 2.0f * occ * dLdI);
           return true;
         });
-#if PTYX_ADJ_PREFETCH_OBJ
-    prefetch_object<N, NT>(a, g, tid, oa, op);
-#endif
     // back to real space; object gradient (scatter-add); g ⊙ conj(O) into LDS
     fft2d<N, NT, +1, true>(
         arr, s_tw, [&](int, int, float2 v, int) { return v; },
         [&](int y, int x, float2& v, int s) {
           const float2 gv = cscale(v, inv_n);
           const size_t off = obj_off(a, 0, 0, g.cy + y, g.cx + x);
-#if PTYX_ADJ_PREFETCH_OBJ
-          const float A = oa[s], ph = op[s];
-#else
           const float A = a.obja[off], ph = a.objp[off];
-#endif
           float sn, cs;
           phase_sincos(ph, &sn, &cs);
           const float2 gO = cmulc(gv, pb[s]);                                   // conj(ψ⁰) g
@@ -314,41 +270,21 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
         });
     if constexpr (SHIFT) {
       if (a.need_probe || a.d_shifts) {
-#if PTYX_ADJ_PREFETCH_FP
-        float2 fl[SL];
-#endif
-#if PTYX_ADJ_PREFETCH_SLAB
-        float2 sl[SL];
-#endif
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
           int y, x;
           PM::last(tid, s, y, x);
-#if PTYX_ADJ_PREFETCH_FP
-          fl[s] = a.Fp[y * N + x];
-#endif
-#if PTYX_ADJ_PREFETCH_SLAB
-          sl[s] = slab[y * N + x];
-#endif
         }
         float ds[2] = {0.f, 0.f};
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v, int) { return v; },
             [&](int y, int x, float2& G, int s) {
               const float2 W = cmul(s_wy[y], s_wx[x]);
-#if PTYX_ADJ_PREFETCH_FP
-              const float2 fpk = fl[s];
-#else
               const float2 fpk = a.Fp[y * N + x];
-#endif
               const float im = cmulc(cmul(fpk, W), G).y;                         // Im(conj(G) F(P) W)
               ds[0] = fmaf(6.283185307179586f * shift_g<N>(y), im, ds[0]);
               ds[1] = fmaf(6.283185307179586f * shift_g<N>(x), im, ds[1]);
-#if PTYX_ADJ_PREFETCH_SLAB
-              const float2 old = sl[s];
-#else
               const float2 old = slab[y * N + x];
-#endif
               if (a.need_probe) slab[y * N + x] = cadd(old, cmulc(G, W));          // Σ_b conj(W_b) F(g_Pb)
               return false;
             });

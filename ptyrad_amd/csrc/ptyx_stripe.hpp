@@ -18,8 +18,8 @@
 //   P3  columns  per (p,o): column FFT → Ψ = ·/N;  I = Σ occ|Ψ|² + 1e-10 (registers);  DP read,
 //                loss partial sums, u = ∂ℓ/∂I per UNIT mini-batch coefficient;  per (p,o):
 //                g_Ψ = 2 occ Ψ u → column IFFT                                     → T23[p,o]
-//                (Ψ of the first PTYX_S3_HOLD modes stays in registers, the others' column FFTs
-//                are redone)
+//                (Ψ of the first `hold` modes stays in registers, the others' column FFTs are
+//                redone; ptyx_set_tuning "s3_hold")
 //   --- k_finalize: the mini-batch NRMSE coefficients c_m (losses.py:45-47) ---
 //   P4  rows     per p: per o: row IFFT → g/N;  slot_o += g·conj(ψ⁰_p);  gP += g·conj(O_o);
 //                row FFT(gP) → T4[p] (= T1's storage);  then dA, dφ (+ the sparse sign term)
@@ -50,28 +50,10 @@ constexpr int kStripes = kN / kL;      // 16
 constexpr int kXElems = kL * 272;      // LDS exchange buffer (float2), row stride padded 256 → 272
 constexpr int kMaxO = 2;
 
-// workgroups per CU each pass is compiled for (its register budget: 512 / (4·WG) VGPRs per lane)
-#ifndef PTYX_S1_WG
-#define PTYX_S1_WG 2
-#endif
-#ifndef PTYX_S2_WG
-#define PTYX_S2_WG 2
-#endif
-#ifndef PTYX_S3_WG
-#define PTYX_S3_WG 2
-#endif
-#ifndef PTYX_S3_WG0   // k_s3 without held modes (recomputes every column FFT)
-#define PTYX_S3_WG0 2
-#endif
-#ifndef PTYX_S4_WG
-#define PTYX_S4_WG 2
-#endif
-#ifndef PTYX_S5_WG
-#define PTYX_S5_WG 2
-#endif
-#ifndef PTYX_S5_FP_L2
-#define PTYX_S5_FP_L2 0
-#endif
+// Every pass is compiled for two workgroups per CU (256 VGPRs per lane): one workgroup per CU
+// measured slower (k_s3 holding 4 modes: 28 vs 21 ms at c5), three spill (k_s5 with F(P) re-read
+// from L2 instead of held: 8.9 → 11.9 ms, profiles/r02/ab/r02y_s5_*).
+constexpr int kPassWG = 2;
 
 struct SArgs {
   int n, P, O, Ny, Nx, n_scans, meas_f16;
@@ -171,19 +153,17 @@ __device__ __forceinline__ void stb(const float2 (&v)[16], float2* base, unsigne
   for (int k = 0; k < 16; ++k) f3::st2(v[k], r, vo, k * STRIDE);
 }
 // The same for the per-call intermediate fields (T1…T4, ψ⁰, slots: written once, read once by
-// another pass): PTYX_S_NT = 1 marks them non-temporal (aux "nt"), so they do not displace the
+// another pass) are marked non-temporal (aux "nt"), so they do not displace the
 // lines that are re-read (F(P), the object rows, the twiddles).  Measured (profiles/r02/ab/
 // r02y_nt_*): c5 222 → 229 k, c3 72.7 → 75.8 k patterns/s.
-#ifndef PTYX_S_NT
-#define PTYX_S_NT 1
-#endif
+constexpr int kStreamAux = 2;
 template <int STRIDE>
 __device__ __forceinline__ void lds_(float2 (&v)[16], const float2* base, unsigned bytes, int voff) {
   const f3::Rsrc r = f3::rsrc(base, bytes);
   const int vo = opq(voff);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, vo + k * STRIDE, 0, PTYX_S_NT ? 2 : 0);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, vo + k * STRIDE, 0, kStreamAux);
     v[k] = make_float2(__uint_as_float(u[0]), __uint_as_float(u[1]));
   }
   fence_sched();
@@ -195,7 +175,7 @@ __device__ __forceinline__ void sts_(const float2 (&v)[16], float2* base, unsign
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(v[k].x), __float_as_uint(v[k].y)};
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, vo + k * STRIDE, 0, PTYX_S_NT ? 2 : 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, vo + k * STRIDE, 0, kStreamAux);
   }
 }
 // object window of pattern j (origin g0), mode o: base and byte size
@@ -259,7 +239,7 @@ __device__ __forceinline__ void bsum(float (&v)[NV], float* red) {
 
 // ---------------------------------------------------------------------------------- P1
 // grid (n, kStripes, P): columns kx of F(P_p)·wy → column IFFT → T1[j][p]
-__global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
+__global__ __launch_bounds__(256, kPassWG) void k_s1(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float2 rl[16];
@@ -283,7 +263,7 @@ __global__ __launch_bounds__(256, PTYX_S1_WG) void k_s1(SArgs a) {
 // ---------------------------------------------------------------------------------- P2
 // grid (n, kStripes): rows y of every probe mode: ×wx → row IFFT → ψ⁰ (PSI0); ×O_o → row FFT → T2
 template <int O_>
-__global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
+__global__ __launch_bounds__(256, kPassWG) void k_s2(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[4 * kMaxO];
@@ -364,11 +344,8 @@ __global__ __launch_bounds__(256, PTYX_S2_WG) void k_s2(SArgs a) {
 // grid (n, kStripes): columns kx of every mode: column FFT → Ψ, intensity, loss, g_Ψ → column IFFT.
 // The first HOLD modes keep Ψ in registers between the two sweeps; the column FFTs of the others
 // (P·O − HOLD of them) are redone in the second sweep.
-#ifndef PTYX_S3_LB1_FROM
-#define PTYX_S3_LB1_FROM 99   // HOLD at or above which k_s3 is compiled for one workgroup per CU
-#endif
 template <bool SINGLE, int QM, int HOLD>
-__global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : HOLD == 0 ? PTYX_S3_WG0 : PTYX_S3_WG) void k_s3(SArgs a) {
+__global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
@@ -466,7 +443,7 @@ __global__ __launch_bounds__(256, HOLD >= PTYX_S3_LB1_FROM ? 1 : HOLD == 0 ? PTY
 // transform instead, so that it is not live across the FFTs, measured slower: c3 k_s4 76 → 99 ms);
 // else recomputed from T1 (one row IFFT per probe mode).
 template <int O_, bool PARK>
-__global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
+__global__ __launch_bounds__(256, kPassWG) void k_s4(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   // O_ = 2: the per-probe-mode accumulator gP lives in LDS ([k][thread], conflict free), so the
@@ -556,9 +533,6 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
       sts_<kRowStride>(gq, a.t4 + ((size_t)j * P + p) * kN2, kFieldBytes, vrow);   // over T1_p's rows (read above)
     }
   }
-#ifdef PTYX_S4_EXP_NOGRAD   // cost-attribution build (results WRONG): no object-gradient epilogue
-  return;
-#endif
   if (!a.d_obja && !a.d_objp) return;
   if (a.oslot) {
     // slot o of pattern j = T3 field (p = 0, o), whose rows of this stripe were consumed above
@@ -615,7 +589,7 @@ __global__ __launch_bounds__(256, PTYX_S4_WG) void k_s4(SArgs a) {
 // grid (kStripes, P, groups): block (s, p, g) sweeps patterns g, g + groups, ...: column FFT of
 // T4[p] → G;  slab += c_m conj(W_b) G (kept in registers across the sweep);  position-gradient
 // partials per pattern.  The slab stripe is written once at the end (k_slab_reduce sums groups).
-__global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
+__global__ __launch_bounds__(256, kPassWG) void k_s5(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
   __shared__ float red[8];
@@ -628,13 +602,10 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
   const int P = a.P;
   constexpr float two_pi_n2 = 6.283185307179586f / (float)kN2;
   const int vcol = (m.slot * kN + kx) * 8;
-  // PTYX_S5_FP_L2: F(P)'s stripe is re-read from L2 after each pattern's transform instead of
-  // being held in 32 VGPRs across the sweep (fewer registers: more workgroups per CU)
+  // F(P)'s stripe is held in 32 VGPRs across the sweep
   float2 acc[16];
-#if !PTYX_S5_FP_L2
   float2 fp[16];
   ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
-#endif
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
   const float gx = shift_g(kx);
@@ -659,10 +630,6 @@ __global__ __launch_bounds__(256, PTYX_S5_WG) void k_s5(SArgs a) {
     for (int r = 0; r < 16; ++r) v[r] = nxt[r];
     if (j + a.groups < a.n) lds_<kColStride>(nxt, a.t14 + ((size_t)(j + a.groups) * P + p) * kN2, kFieldBytes, vcol);
     fft_line<-1, true>(v, m, xb, tw);
-#if PTYX_S5_FP_L2
-    float2 fp[16];
-    ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, opq(vcol));
-#endif
     const float2 TW = f3::pcm(ramp_t(sy, m.slot), f3::cis_rev(-sx * gx));   // cis(−sy·slot/N)·wx
     float sy_acc = 0.f, sim = 0.f;
 #pragma unroll

@@ -202,14 +202,38 @@ class Plan:
                                              _ptr(dp_out[a:b])))
         return dp_out
 
+    def _check_rows(self, t: dict, idx_t):
+        """meas_rows[idx] must address rows of the rank-local measurement block (include/ptyx.h:
+        the kernels do not check it).  One small device reduction and a host sync."""
+        rows = t.get("meas_rows")
+        if rows is None or idx_t.numel() == 0:
+            return
+        r = rows[idx_t.long()]
+        lo, hi = (int(v) for v in torch.aminmax(r))
+        if lo < 0 or hi >= t["meas"].shape[0]:
+            raise IndexError(f"meas_rows maps a position of this call to row {lo if lo < 0 else hi}, outside the "
+                             f"{t['meas'].shape[0]}-row measurement block")
+
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
-                          grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None, prep=0):
+                          grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None, prep=0,
+                          batch_sums_reduce=None, _rows_checked=False):
         """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5).
 
         batch_offsets on the host (numpy / list / CPU tensor) let calls larger than the plan's
         capacity (max_patterns, or the register engines' slot capacity) be split at mini-batch
         boundaries; device offsets must fit in one call.
+
+        batch_sums_reduce: the mini-batches are this rank's PARTS of mini-batches split over ranks
+        (ptyx_forward_loss_grad_begin / _end).  It is called with the (n_batches, 13) float64
+        device tensor of the parts' additive loss sums and must sum it over the ranks in place
+        (one all-reduce); the loss terms and gradient coefficients then belong to the whole
+        mini-batches.  Such a call is never split, so it must fit the plan's capacity.
         """
+        if not _rows_checked:
+            self._check_rows(t, self._idx(idx))
+        if batch_sums_reduce is not None:
+            return self._split_call(t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out,
+                                    batch_sums_reduce)
         host_off = not (isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu")
         if max_batch is None:
             if not host_off:
@@ -281,9 +305,36 @@ class Plan:
             sub_idx = idx_t[int(off[b0]):int(off[b1])]
             sub_dp = None if dp_out is None else dp_out[int(off[b0]):int(off[b1])]
             self.forward_loss_grad(t, sub_idx, sub_off, loss_cfg, grads, grad_scale=grad_scale,
-                                   loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch, prep=prep)
+                                   loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch, prep=prep,
+                                   _rows_checked=True)
             prep = _lib.PTYX_PREP_REUSE
             b0 = b1
+        return loss_terms
+
+    def _split_call(self, t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out, reduce):
+        """ptyx_forward_loss_grad_begin → reduce(batch sums) → ptyx_forward_loss_grad_end."""
+        idx_t = self._idx(idx)
+        off_t = self._idx(batch_offsets)
+        n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
+        cap = self.register_capacity
+        cap = min(cap, int(self.dims.max_patterns)) if cap > 0 else int(self.dims.max_patterns)
+        if n > cap:
+            raise ValueError(f"a split-batch call of {n} patterns exceeds the plan's capacity {cap}")
+        if loss_terms is None:
+            loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
+        sums = torch.empty((nb, _lib.PTYX_BATCH_SUMS), dtype=torch.float64, device=self.device)
+        inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
+                                  t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0),
+                                  t.get("meas_rows"))
+        cfg = loss_cfg.to_c(grad_scale, 0, _lib.PTYX_PREP_CALL)
+        g = self._grads(grads)
+        _lib.check(self.lib.ptyx_forward_loss_grad_begin(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
+                                                         _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(dp_out),
+                                                         ctypes.byref(g), _ptr(sums)))
+        try:
+            reduce(sums)
+        finally:   # always close the call (the plan refuses other work while one is open)
+            _lib.check(self.lib.ptyx_forward_loss_grad_end(self._h, self._stream(), _ptr(sums), _ptr(loss_terms)))
         return loss_terms
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):

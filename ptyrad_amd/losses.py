@@ -171,20 +171,41 @@ class CombinedLoss(torch.nn.Module):
         if held is not None and not held(flat):
             raise IndexError("mini-batch positions outside this rank's measurement block (measurements_index)")
 
-    def fused_into(self, model, batches, grad_scale=1.0):
+    def _special(self, model):
+        return (getattr(model, "detector_blur", False) or getattr(model, "preblur", False) or
+                getattr(model, "otf_meas", False) or self.loss_params.get("loss_simlar", {}).get("state", False))
+
+    def supports_batch_split(self, model) -> bool:
+        """Whether ``fused_into(..., batch_sums_reduce=...)`` can take mini-batches split over ranks:
+        every loss term must be a function of per-pattern additive sums (not loss_pacbed, whose
+        mean pattern is a per-batch N² sum, nor the autograd stages)."""
+        return not self._special(model) and not self.loss_params.get("loss_pacbed", {}).get("state", False)
+
+    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None):
         """The hot path without autograd: gradients of (Σ_m loss_m)·grad_scale are ACCUMULATED
         straight into the ``.grad`` tensors of the optimisable parameters the loss reaches
         (created, zeroed, when missing) — the engine writes them in place, no temporaries.
         Equivalent to ``(fused(model, batches)[0] * grad_scale).backward()``.  Returns the
         (n_batches, 5) loss terms.  Stages that need torch autograd (detector blur, pre-blur,
-        on-the-fly measurements, loss_simlar) run exactly that way, into the same ``.grad``."""
+        on-the-fly measurements, loss_simlar) run exactly that way, into the same ``.grad``.
+
+        batch_sums_reduce (data-parallel split of mini-batches, DistContext): ``batches[m]`` is this
+        rank's part (possibly empty) of mini-batch m, the same number of parts on every rank;
+        ``batch_sums_reduce(t)`` sums a float64 device tensor over the ranks in place.  The engine
+        normalises every loss by its WHOLE mini-batch (ptyx_forward_loss_grad_begin / _end), so the
+        ranks' gradients sum to the single-device gradient.  Rows of parts this rank does not hold
+        are zero in the returned terms."""
         names = model.engine_grad_names()
         for k in names:
             p = model.optimizable_tensors[k]
             if p.requires_grad and p.grad is None:
                 p.grad = torch.zeros_like(p)
-        special = (getattr(model, "detector_blur", False) or getattr(model, "preblur", False) or
-                   getattr(model, "otf_meas", False) or self.loss_params.get("loss_simlar", {}).get("state", False))
+        special = self._special(model)
+        if batch_sums_reduce is not None:
+            if not self.supports_batch_split(model):
+                raise NotImplementedError("mini-batches split over ranks need additive loss terms "
+                                          "(no loss_pacbed / loss_simlar / blur / on-the-fly stages)")
+            return self._split_into(model, batches, grad_scale, batch_sums_reduce)
         if special:
             total, terms = self.fused(model, batches)
             if total.requires_grad:
@@ -216,6 +237,50 @@ class CombinedLoss(torch.nn.Module):
                               model.shift_probes)
         if "H" in grads:
             torch.autograd.backward(H_rv, grads["H"])
+        return terms
+
+    def _split_into(self, model, parts, grad_scale, reduce):
+        """fused_into for this rank's parts of mini-batches split over ranks."""
+        from .engine import LossConfig as _LC
+        dev = model.opt_obja.device
+        G = len(parts)
+        parts = [np.asarray(b).reshape(-1) for b in parts]
+        held = [m for m, b in enumerate(parts) if b.size]
+        terms = torch.zeros((G, 5), dtype=torch.float32, device=dev)
+        if not held:   # nothing here: still join the reduction of the group's sums
+            reduce(torch.zeros((G, 13), dtype=torch.float64, device=dev))
+            return terms
+        local = [parts[m] for m in held]
+        flat = np.concatenate(local)
+        model._check_indices(flat)
+        self._check_held(model, flat)
+        sel = torch.as_tensor(held, dtype=torch.long, device=dev)
+
+        def group_reduce(sums):          # local rows -> the group's (G, 13) rows -> sum over ranks
+            full = torch.zeros((G, sums.shape[1]), dtype=torch.float64, device=dev)
+            full.index_copy_(0, sel, sums)
+            reduce(full)
+            sums.copy_(full.index_select(0, sel))
+
+        idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
+        H_rv = model._H_rv()
+        if model._tilts() is not None:
+            raise NotImplementedError("split mini-batches with per-position tilts are not supported")
+        t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
+             "shifts": model.opt_probe_pos_shifts.detach(), "H": H_rv.detach(), "tilts": None}
+        t.update(model._base())
+        live = lambda p: p is not None and p.requires_grad and p.grad is not None  # noqa: E731
+        grads = {k: p.grad for k, p in (("obja", model.opt_obja), ("objp", model.opt_objp),
+                                         ("probe", model.opt_probe)) if live(p)}
+        if model.shift_probes and live(model.opt_probe_pos_shifts):
+            grads["shifts"] = model.opt_probe_pos_shifts.grad
+        if H_rv.requires_grad:          # optimised dz / tilts: this rank's share of dL/dH, then autograd
+            grads["H"] = torch.zeros_like(H_rv)
+        local_terms = model.plan.forward_loss_grad(t, idx_t, batch_offsets(local), _LC.from_loss_params(self.loss_params),
+                                                   grads, grad_scale=float(grad_scale), batch_sums_reduce=group_reduce)
+        if "H" in grads:
+            torch.autograd.backward(H_rv, grads["H"])
+        terms.index_copy_(0, sel, local_terms)
         return terms
 
     PREBLUR_GROUP = 8192

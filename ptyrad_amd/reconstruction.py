@@ -10,10 +10,16 @@ accumulates Σ_m ∂loss_m/∂θ / grad_accumulation straight into ``.grad`` —
 accumulated gradient, reconstruction.py:741-760, without autograd temporaries).
 
 Multi-GPU (replaces the accelerate/DDP wrapper, utils/common.py:58-90): ``DistContext``.
-* The mini-batches of a group are dealt round-robin to ranks.  Batches are fixed for the run
-  (recon_loop never regroups, reconstruction.py:634-636), so ``DistContext.local_indices`` tells
-  each rank, before loading anything, which scan positions' DPs it needs: the rank keeps only
-  those (PtychoHIP ``measurements_index``), unlike DDP which holds and broadcasts the whole stack.
+* A group with at least as many mini-batches as ranks is dealt round-robin, whole mini-batches
+  per rank.  A group with fewer (the reference default grad_accumulation = 1) is SPLIT: every rank
+  takes a contiguous part of every mini-batch (the reference's split_batches=True,
+  utils/common.py:63), the engine's per-batch loss sums are all-reduced between its forward and
+  its adjoint (ptyx_forward_loss_grad_begin / _end), and each loss keeps the single-device
+  normalisation of its WHOLE mini-batch — exact, unlike DDP's average of per-rank losses.
+* Batches are fixed for the run (recon_loop never regroups, reconstruction.py:634-636), so
+  ``DistContext.local_indices`` tells each rank, before loading anything, which scan positions'
+  DPs it needs: the rank keeps only those (PtychoHIP ``measurements_index``), unlike DDP which
+  holds and broadcasts the whole stack.
 * The ``.grad`` of every parameter the loss reaches and that is trainable this iteration
   (``toggle_grad_requires``) is a view into ONE flat buffer; the engine accumulates into the
   views, ONE all-reduce(sum) of the buffer gives every rank the exact single-device accumulated
@@ -133,27 +139,58 @@ def loss_logger(batch_losses, niter, iter_t, verbose=True):
 class DistContext:
     """Rank/world of a torch.distributed job (backend 'nccl' = RCCL on ROCm, or 'gloo' on CPU)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, split_batches=None, always_reduce=False):
+        """split_batches: None = split a group's mini-batches over the ranks only when the group has
+        fewer mini-batches than ranks; True = always (accelerate's split_batches=True,
+        utils/common.py:63); False = never (whole mini-batches round-robin).
+        always_reduce: run the collectives even with one rank (tests that exercise RCCL on one GPU)."""
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.split_batches = split_batches
+        self.always_reduce = bool(always_reduce) and dist.is_initialized()
+
+    def _collective(self) -> bool:
+        return self.world > 1 or self.always_reduce
 
     def my_batches(self, group_batches):
         """Round-robin deal of a group's mini-batches to ranks (positions of batch b on rank b % world)."""
         return [i for i in range(len(group_batches)) if i % self.world == self.rank]
 
-    def local_batches(self, batches, grad_accumulation=1):
-        """The mini-batches this rank processes over one iteration of recon_step (fixed batches)."""
+    def splits(self, group_batches) -> bool:
+        """A group with fewer mini-batches than ranks is split within its mini-batches (same
+        decision on every rank: it depends only on the group size, the world size and the
+        split_batches setting)."""
+        if self.split_batches is not None:
+            return bool(self.split_batches)
+        return 1 < self.world and len(group_batches) < self.world
+
+    def my_part(self, batch):
+        """This rank's contiguous share of one mini-batch (np.array_split over the ranks; rank 0's
+        share is never empty for a non-empty mini-batch)."""
+        return np.array_split(np.asarray(batch).reshape(-1), self.world)[self.rank]
+
+    def local_batches(self, batches, grad_accumulation=1, split=True):
+        """The mini-batches (or parts of them) this rank processes over one iteration of recon_step.
+        split=False: the loss cannot be split (CombinedLoss.supports_batch_split), whole batches."""
         ga = max(1, int(grad_accumulation))
         out = []
         for g0 in range(0, len(batches), ga):
             group = batches[g0:g0 + ga]
-            out += [group[i] for i in self.my_batches(group)]
+            if split and self.splits(group):
+                out += [p for p in (self.my_part(b) for b in group) if p.size]
+            else:
+                out += [group[i] for i in self.my_batches(group)]
         return out
 
-    def local_indices(self, batches, grad_accumulation=1):
+    def allreduce_sums(self, t):
+        """Sum of the engine's per-mini-batch loss sums over the ranks (in place; float64)."""
+        if self._collective():
+            dist.all_reduce(t, group=self.group)
+
+    def local_indices(self, batches, grad_accumulation=1, split=True):
         """Sorted scan indices whose DPs this rank needs: its ``measurements_index`` block."""
-        mine = self.local_batches(batches, grad_accumulation)
+        mine = self.local_batches(batches, grad_accumulation, split)
         if not mine:
             return np.zeros(0, np.int64)
         return np.unique(np.concatenate([np.asarray(b).reshape(-1) for b in mine]))
@@ -172,7 +209,7 @@ class DistContext:
 
     def allreduce(self, flat):
         """ONE all-reduce(sum) of the gradient buffer (in place)."""
-        if self.world > 1 and flat is not None and flat.numel():
+        if self._collective() and flat is not None and flat.numel():
             dist.all_reduce(flat, group=self.group)
 
     def allreduce_grads(self, params):
@@ -202,7 +239,7 @@ class DistContext:
         buf = torch.zeros((n_total, 5), dtype=torch.float32, device=device)
         if len(idx_local):
             buf[torch.as_tensor(idx_local, device=device)] = terms_local.to(device)
-        if self.world > 1:
+        if self._collective():
             dist.all_reduce(buf, group=self.group)
         return buf
 
@@ -230,14 +267,30 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     # parameters whose .grad this iteration's steps fill: trainable now and reached by the loss
     reached = {id(model.optimizable_tensors[k]) for k in model.engine_grad_names()}
     live = [p for p in params if p.requires_grad and id(p) in reached]
+    split_ok = hasattr(loss_fn, "supports_batch_split") and loss_fn.supports_batch_split(model)
     for g0 in range(0, len(batches), ga):
         group = batches[g0:g0 + ga]
-        mine = ctx.my_batches(group)
         flat = ctx.grad_views(live)
-        if mine:
-            terms = loss_fn.fused_into(model, [group[i] for i in mine], grad_scale=1.0 / ga)
+        if ctx.splits(group) and split_ok:
+            # every rank holds a part of every mini-batch; the loss sums are all-reduced inside the
+            # engine call, so each mini-batch keeps its whole-batch normalisation.  Rank 0's part of
+            # every mini-batch is non-empty: its terms are the group's.
+            terms = loss_fn.fused_into(model, [ctx.my_part(b) for b in group], grad_scale=1.0 / ga,
+                                       batch_sums_reduce=ctx.allreduce_sums)
+            mine = list(range(len(group))) if ctx.rank == 0 else []
+            if ctx.rank:
+                terms = terms[:0]
         else:
-            terms = torch.zeros((0, 5), device=dev)
+            if ctx.splits(group) and not getattr(ctx, "_warned_idle", False):
+                print(f"[ptyrad_amd] warning: {len(group)} mini-batch(es) per optimizer step on {ctx.world} ranks and "
+                      "a loss that cannot be split (pacbed / simlar / blur stages): ranks without a mini-batch idle",
+                      flush=True)
+                ctx._warned_idle = True
+            mine = ctx.my_batches(group)
+            if mine:
+                terms = loss_fn.fused_into(model, [group[i] for i in mine], grad_scale=1.0 / ga)
+            else:
+                terms = torch.zeros((0, 5), device=dev)
         ctx.allreduce(flat)
         optimizer.step()
         optimizer.zero_grad(set_to_none=True)

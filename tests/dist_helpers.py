@@ -89,9 +89,31 @@ class OracleLoss:
     def __init__(self, lp):
         self.loss_params = lp
 
-    def fused_into(self, model, batches, grad_scale=1.0):
+    def supports_batch_split(self, model):
+        return not self.loss_params.get("loss_pacbed", {}).get("state", False)
+
+    def _split_grads(self, model, parts, reduce):
+        """oracle of ptyx_forward_loss_grad_begin → reduce → _end on this rank's parts."""
+        flat = np.concatenate([np.asarray(b).reshape(-1) for b in parts])
+        rows = getattr(model, "meas_rows", None)
+        if rows is not None and flat.size and np.any(rows[flat] < 0):
+            raise IndexError("a mini-batch position outside this rank's measurement block")
+        probe = (model.opt_probe[..., 0] + 1j * model.opt_probe[..., 1]).detach().numpy()
+
+        def reduce_np(sums):            # the (n_batches, 13) float64 sums, summed over the ranks in place
+            reduce(torch.from_numpy(sums))
+
+        return orc.forward_loss_grad_parts(
+            model.opt_obja.detach().numpy(), model.opt_objp.detach().numpy(), probe,
+            model.opt_probe_pos_shifts.detach().numpy(), model.crop_pos_np, model.H_np, model.occu_np,
+            model.meas_np, parts, self.loss_params, reduce_np, shift_probes=True)
+
+    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None):
         """recon_step's direct path: accumulate the oracle's gradients into the existing .grad."""
-        terms, g = _oracle_grads(model, batches, self.loss_params)
+        if batch_sums_reduce is not None:
+            terms, g = self._split_grads(model, batches, batch_sums_reduce)
+        else:
+            terms, g = _oracle_grads(model, batches, self.loss_params)
         vals = {"obja": g["obja"], "objp": g["objp"], "probe": np.stack([g["probe"].real, g["probe"].imag], -1),
                 "probe_pos_shifts": g["shifts"]}
         for k in model.engine_grad_names():

@@ -7,7 +7,9 @@ Both legs run the c2 hot path shape (N = 128, P = O = Nz = 1, sub-pixel shifts o
 q = 0.5 + loss_sparse L1, mini-batches of 32) on the same number of host cores:
   reference  PtychoAD.forward + CombinedLoss + backward (models.py:422, losses.py:143, autograd),
              torch CPU with torch.set_num_threads(cores);
-  port       bench.cpu_baseline(): oracle/ptyx_oracle.py complex64 NumPy in `cores` processes.
+  port       bench.cpu_baseline(): oracle/ptyx_oracle.py complex64 NumPy in `cores` processes, the
+             SAME function and the same default sample per core (110 · 20 patterns) as on the GPU
+             box, its rate taken over the workers' compute time (pool start excluded) on both.
 Harness: one warm-up pass, then the median of 3 timed passes of the whole sample.
 Writes tests/golden/cpu_ratio.json (numbers only), which bench.py reports as
 cpu_baseline.ratio_to_reference: reference patterns/s ≈ port patterns/s × ratio.
@@ -36,7 +38,7 @@ LOSS = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
                         "blur_std": 1}}
 
 
-def reference_rate(cores, n_batches=16, bsize=32):
+def reference_rate(cores, n_batches=64, bsize=32):
     models, losses, _ = import_reference()
     import make_golden as mg
     from ptyrad_amd import synthetic as syn
@@ -68,7 +70,7 @@ def port_rate(cores, sample):
     bench_cores = os.environ.get("PTYX_CPU_CORES")
     os.environ["PTYX_CPU_CORES"] = str(cores)
     try:
-        bench.cpu_baseline(128, 32, sample // 4)          # warm-up (pool start, imports)
+        bench.cpu_baseline(128, 32, max(1024, sample // 4))   # warm-up (pool start, imports)
         rs = [bench.cpu_baseline(128, 32, sample)["value"] for _ in range(3)]
     finally:
         if bench_cores is None:
@@ -81,9 +83,10 @@ def port_rate(cores, sample):
 def main():
     cores = len(os.sched_getaffinity(0))
     ref, _ = reference_rate(cores)
-    port = port_rate(cores, 4096)
+    port = port_rate(cores, 0)          # 0: bench.py's default sample (110 · 20 patterns per core)
     out = {"host": f"{cores} cores (build container)", "cores": cores, "workload": "c2 shape: N=128, P=O=Nz=1, "
            "shifts on, loss_single q=0.5 + loss_sparse L1, mini-batch 32",
+           "port_sample": "bench.cpu_baseline default (110 x 20 patterns per core), compute-time rate",
            "reference_patterns_per_s": round(ref, 1), "port_patterns_per_s": round(port, 1),
            "ratio_reference_over_port": round(ref / port, 4)}
     with open(os.path.join(HERE, "cpu_ratio.json"), "w") as f:

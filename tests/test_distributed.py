@@ -73,5 +73,76 @@ def test_local_indices_cover_each_rank_exactly():
         got.append(ctx.local_indices(batches, grad_accumulation=3))
     allidx = np.sort(np.concatenate(got))
     assert np.array_equal(allidx, np.arange(28))
-    # group 0 = batches 0,1,2 -> ranks 0,1,2; group 1 = 3,4,5; group 2 = batch 6 -> rank 0
-    assert np.array_equal(got[0], np.concatenate([batches[0], batches[3], batches[6]]))
+    # group 0 = batches 0,1,2 -> ranks 0,1,2; group 1 = 3,4,5; group 2 = batch 6 alone (fewer
+    # mini-batches than ranks): split, rank 0 takes its first two positions, ranks 1, 2 one each
+    assert np.array_equal(got[0], np.concatenate([batches[0], batches[3], batches[6][:2]]))
+    assert np.array_equal(got[2], np.concatenate([batches[2], batches[5], batches[6][3:]]))
+    # a loss that cannot be split (loss_pacbed): whole batches, group 2 on rank 0
+    ctx = DistContext()
+    ctx.rank, ctx.world = 0, 3
+    assert np.array_equal(ctx.local_indices(batches, 3, split=False),
+                          np.concatenate([batches[0], batches[3], batches[6]]))
+
+
+def _simulate_ranks(z, parts_of, lp):
+    """forward_loss_grad_parts for every rank of an in-process 'job': pass 1 collects each rank's
+    batch sums, pass 2 runs every rank with their sum (the all-reduce)."""
+    from oracle import ptyx_oracle as orc
+    args = (z["obja"], z["objp"], z["probe"], z["shifts"], z["crop_pos"], z["H"], z["occu"], z["meas"])
+    local = []
+    for parts in parts_of:
+        def grab(s):
+            local.append(s.copy())
+        orc.forward_loss_grad_parts(*args, parts, lp, grab)
+    total = np.sum(local, axis=0)
+
+    def put(s):
+        s[...] = total
+    return [orc.forward_loss_grad_parts(*args, parts, lp, put) for parts in parts_of]
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_oracle_split_mini_batches_equal_whole_batches(world):
+    """Every mini-batch split over `world` ranks (ragged and, at world 5 > batch size 4, empty
+    parts), per-batch sums all-reduced between forward and adjoint (ptyx_forward_loss_grad_begin /
+    _end): the loss terms are the whole mini-batches' and the ranks' gradients sum to the
+    single-device gradients (losses.py:45-47 normalisation per WHOLE mini-batch)."""
+    import json
+    from oracle import ptyx_oracle as orc
+    from tests.test_oracle_golden import load_case
+    d = load_case(os.path.join(os.path.dirname(__file__), "golden", "n32_p2o2z3_shift.npz"))   # P 2, O 2, Nz 3
+    z = {"obja": d["obja"], "objp": d["objp"], "probe": d["probe"], "shifts": d["shifts"], "crop_pos": d["crop_pos"],
+         "H": d["H"], "occu": d["occu"], "meas": d["meas"]}
+    lp = json.loads(json.dumps(d["loss_params"]))
+    for term in ("loss_single", "loss_poissn"):      # each data term (and both) with loss_sparse
+        lp[term]["state"] = True
+    rng = np.random.default_rng(0)
+    S = z["shifts"].shape[0]
+    batches = np.array_split(rng.permutation(S), max(1, S // 4))
+    whole_terms, _, whole = orc.forward_loss_grad(*z.values(), batches, lp)
+    parts_of = [[np.array_split(b, world)[r] for b in batches] for r in range(world)]
+    res = _simulate_ranks(z, parts_of, lp)
+    for terms, _ in res:
+        np.testing.assert_allclose(terms, whole_terms, rtol=1e-12, atol=1e-15)
+    for k in ("obja", "objp", "probe", "shifts"):
+        got = sum(g[k] for _, g in res)
+        np.testing.assert_allclose(got, whole[k], rtol=1e-10, atol=1e-13 * np.abs(whole[k]).max(), err_msg=k)
+
+
+def test_three_ranks_ga1_split_batches_reproduce_single_rank(tmp_path):
+    """grad_accumulation = 1 (the reference default) on 3 gloo ranks: every mini-batch of 4 is split
+    2/1/1 over the ranks, each rank holds only its parts' DPs (the rest NaN), and the trajectory
+    equals the single-rank one (fp32 summation order) and the reference's."""
+    path = [p for p in TRAJ if "traj_n64_b4_ga1" in p][0]
+    z = np.load(path, allow_pickle=False)
+    single, _ = run_recon(z)
+    out = str(tmp_path / "r.npz")
+    mp.start_processes(dist_worker, args=(3, free_port(), path, out, {"shard": True}), nprocs=3,
+                       start_method="spawn")
+    r = [np.load(out)] + [np.load(out.replace(".npz", f"_r{i}.npz")) for i in (1, 2)]
+    for k in ("obja", "objp", "probe", "shifts"):
+        assert np.all(np.isfinite(r[0][k])), k
+        assert np.array_equal(r[0][k], r[1][k]) and np.array_equal(r[0][k], r[2][k]), f"replicas diverged in {k}"
+        np.testing.assert_allclose(r[0][k], single[k], rtol=0, atol=2e-6)
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((r[0][k].astype(np.float64) - ref) ** 2))) < 1e-5

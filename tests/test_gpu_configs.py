@@ -68,23 +68,32 @@ def test_c5_shape_p4_fp16_dps_vs_oracle():
     check_against_oracle(d, [np.array([2, 6, 7, 3]), np.array([8, 0])], meas_f16=True)
 
 
-@pytest.mark.parametrize("hold,park", [("0", "1"), ("1", "1"), ("3", "0"), ("4", "1")])
-def test_stripe_mode_hold_and_psi0_variants(monkeypatch, hold, park):
+@pytest.fixture
+def tuning():
+    """ptyx_set_tuning for one test; every key back to its measured default afterwards."""
+    from ptyrad_amd import _lib
+    yield _lib.set_tuning
+    for k in ("s3_hold", "s_psi0", "s_gather"):
+        _lib.set_tuning(k, -1)
+
+
+@pytest.mark.parametrize("hold,park", [(0, 1), (1, 1), (3, 0), (4, 1)])
+def test_stripe_mode_hold_and_psi0_variants(tuning, hold, park):
     """k_s3 with the first `hold` of P·O = 6 modes held in registers (the rest recomputed), and
     k_s4 with ψ⁰ parked (1) or recomputed from T1 (0): all the same gradients."""
-    monkeypatch.setenv("PTYX_S3_HOLD", hold)
-    monkeypatch.setenv("PTYX_S_PSI0", park)
+    tuning("s3_hold", hold)
+    tuning("s_psi0", park)
     d = config_problem(3, 2, False, seed=13)
     check_against_oracle(d, [np.array([1, 3, 4]), np.array([7, 2, 0])], meas_f16=False)
 
 
-@pytest.mark.parametrize("O,flag", [(1, "1"), (2, "0")])
-def test_stripe_object_gradient_atomics_and_slots(monkeypatch, O, flag):
-    """k_s4's object-gradient form the mode count does not pick by default (PTYX_S_GATHER):
+@pytest.mark.parametrize("O,flag", [(1, 1), (2, 0)])
+def test_stripe_object_gradient_atomics_and_slots(tuning, O, flag):
+    """k_s4's object-gradient form the mode count does not pick by default (tuning "s_gather"):
     slots + k_obj_gather for one object mode, f32 atomics for two; the same gradients."""
-    monkeypatch.setenv("PTYX_S_GATHER", flag)
+    tuning("s_gather", flag)
     d = config_problem(2, O, False, seed=14)
-    check_against_oracle(d, [np.array([6, 2, 3]), np.array([0, 8, 4, 1])], meas_f16=False, gather=flag == "1")
+    check_against_oracle(d, [np.array([6, 2, 3]), np.array([0, 8, 4, 1])], meas_f16=False, gather=flag == 1)
 
 
 # ------------------------------------------------------------------ rank-local measurements

@@ -1,0 +1,216 @@
+"""Mini-batches split over data-parallel ranks (ptyx_forward_loss_grad_begin / _end), the prep
+record that guards PTYX_PREP_REUSE, and RCCL (torch.distributed 'nccl') on the MI355X.
+
+Reference: the multi-GPU path splits every mini-batch over the ranks (accelerate split_batches,
+src/ptyrad/utils/common.py:63; reconstruction.py:125-132) and normalises each loss by its mini-batch
+(losses.py:45-47).  Here a split call's per-batch loss sums are all-reduced between the engine's
+forward and its adjoint, so the ranks' gradients sum exactly to the single-device ones.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ptyx_oracle as orc
+from tests.test_gpu_parity import TOL_G, TOL_SH, TOL_TERMS, orc_default_loss, tensors
+from tests.test_oracle_golden import rel
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def problem(N, P, O, Nz, seed, ns=3, nf=4):
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(N, ns, nf, P=P, O=O, Nz=Nz, seed=seed)
+    return dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(60.0 if N == 128 else 30.0 if N == 256 else 40.0),
+                shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True,
+                loss_params=orc_default_loss())
+
+
+def plan_for(d, device, max_patterns=64):
+    """max_patterns 64: the register engines' segment slab then holds any of these calls."""
+    from ptyrad_amd.engine import Plan
+    O, Nz, Ny, Nx = d["obja"].shape
+    P, N = d["probe"].shape[:2]
+    return Plan(N, P, O, Nz, Ny, Nx, d["shifts"].shape[0], max_patterns, shift_probes=True, device=device)
+
+
+def zero_grads(t):
+    return {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+
+
+def to_np(g):
+    out = {k: v.cpu().numpy().astype(np.float64) for k, v in g.items()}
+    out["probe"] = out["probe"][..., 0] + 1j * out["probe"][..., 1]
+    return out
+
+
+# geometry -> engine that serves it: k_fused3, k_fused3ms, the N = 256 stripe engine, the two-pass engine
+GEOMS = {"fused3": (128, 1, 1, 1), "fused3ms": (128, 1, 1, 3), "stripe": (256, 2, 1, 1), "two_pass": (64, 2, 2, 2)}
+ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "stripe": "k_s3", "two_pass": "k_forward"}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("geom", sorted(GEOMS))
+def test_split_batches_sum_to_whole_call(geom, world):
+    """Every mini-batch split over `world` simulated ranks (one plan each): the loss terms are the
+    whole mini-batches' and the ranks' gradients sum to the whole call's (and the oracle's)."""
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    device = dev()
+    d = problem(*GEOMS[geom], seed=21 + world)
+    t = tensors(d, device)
+    cfg = LossConfig.from_loss_params(d["loss_params"])
+    batches = [np.array([3, 0, 9, 7, 11]), np.array([5, 1, 10, 2]), np.array([4, 8, 6])]
+    whole = zero_grads(t)
+    plan = plan_for(d, device)
+    plan.profile_begin()
+    wterms = plan.forward_loss_grad(t, np.concatenate(batches), batch_offsets(batches), cfg, whole)
+    ks = plan.profile_end()
+    assert ENGINE_KERNEL[geom] in ks, ks                          # the intended engine ran
+    parts_of = [[np.array_split(b, world)[r] for b in batches] for r in range(world)]
+    plans = [plan_for(d, device) for _ in range(world)]
+
+    def run(r, reduce):
+        parts = [p for p in parts_of[r] if p.size]
+        g = zero_grads(t)
+        terms = plans[r].forward_loss_grad(t, np.concatenate(parts), batch_offsets(parts), cfg, g,
+                                           batch_sums_reduce=reduce)
+        return terms, g
+
+    local = []
+    for r in range(world):                         # pass 1: each rank's sums (what the all-reduce sums)
+        run(r, lambda s: local.append(s.clone()))
+    total = torch.stack(local).sum(0)
+    res = [run(r, lambda s: s.copy_(total)) for r in range(world)]   # pass 2: with the summed sums
+    torch.cuda.synchronize()
+    for terms, _ in res:
+        np.testing.assert_allclose(terms.cpu().numpy(), wterms.cpu().numpy(), rtol=2e-6, atol=1e-9)
+    got = {k: sum(to_np(g)[k] for _, g in res) for k in whole}
+    ref = to_np(whole)
+    for k in ("obja", "objp", "probe"):
+        assert rel(got[k], ref[k]) < 2e-6, k
+    assert rel(got["shifts"], ref["shifts"]) < 2e-5
+    oterms, _, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                          d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(res[0][0].cpu().numpy(), oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(got[k], og[k]) < TOL_G, k
+    assert rel(got["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_plan_refuses_work_between_begin_and_end():
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    device = dev()
+    d = problem(64, 1, 1, 1, seed=3)
+    t = tensors(d, device)
+    plan = plan_for(d, device)
+    cfg = LossConfig.from_loss_params(d["loss_params"])
+    b = [np.array([0, 1, 2])]
+
+    def reduce(_s):   # while the call is open, the plan takes no other compute call
+        with pytest.raises(_lib.PtyxError, match="waiting for its _end"):
+            plan.forward_loss_grad(t, np.array([4, 5]), batch_offsets([np.array([4, 5])]), cfg, zero_grads(t))
+    plan.forward_loss_grad(t, b[0], batch_offsets(b), cfg, zero_grads(t), batch_sums_reduce=reduce)
+    plan.forward_loss_grad(t, b[0], batch_offsets(b), cfg, zero_grads(t))     # closed again
+    torch.cuda.synchronize()
+
+
+def test_prep_reuse_after_engine_change_prepares_in_full():
+    """a call split into pieces at the plan capacity whose first piece runs the
+    two-pass engine (64 one-pattern mini-batches: more segments than k_fused3's slab holds) and
+    whose second piece runs k_fused3 (two mini-batches of 32).  The second piece asks for
+    PTYX_PREP_REUSE, but k_fused3's object / probe preparation was never made: the plan's prep
+    record makes it prepare in full.  Loss terms and gradients match the oracle."""
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    device = dev()
+    pr = syn.random_problem(128, 8, 16, seed=17)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(60.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=orc_default_loss())
+    t = tensors(d, device)
+    plan = plan_for(d, device, max_patterns=64)
+    batches = [np.array([i]) for i in range(64)] + [np.arange(64, 96), np.arange(96, 128)]
+    g = zero_grads(t)
+    plan.profile_begin()
+    terms = plan.forward_loss_grad(t, np.concatenate(batches), batch_offsets(batches),
+                                   LossConfig.from_loss_params(d["loss_params"]), g)
+    ks = plan.profile_end()
+    assert "k_forward" in ks and "k_fused" in ks, ks           # both engines ran, one piece each
+    oterms, _, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                          d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(terms.cpu().numpy(), oterms, rtol=TOL_TERMS, atol=1e-7)
+    gn = to_np(g)
+    for k in ("obja", "objp", "probe"):
+        assert rel(gn[k], og[k]) < TOL_G, k
+    assert rel(gn["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_meas_rows_outside_the_block_is_refused():
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    device = dev()
+    d = problem(64, 1, 1, 1, seed=4)
+    t = tensors(d, device)
+    rows = torch.full((d["shifts"].shape[0],), -1, dtype=torch.int32, device=device)
+    rows[:4] = torch.arange(4, dtype=torch.int32, device=device)
+    t["meas"] = t["meas"][:4].contiguous()
+    t["meas_rows"] = rows
+    plan = plan_for(d, device)
+    cfg = LossConfig.from_loss_params(d["loss_params"])
+    plan.forward_loss_grad(t, np.array([0, 3]), batch_offsets([np.array([0, 3])]), cfg, zero_grads(t))
+    with pytest.raises(IndexError, match="meas_rows"):
+        plan.forward_loss_grad(t, np.array([1, 6]), batch_offsets([np.array([1, 6])]), cfg, zero_grads(t))
+    torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------ RCCL on the MI355X
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _nccl_worker(rank, port, path, out, split):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from ptyrad_amd.reconstruction import DistContext
+        from tests.dist_helpers import gpu_recon
+        assert torch.distributed.get_backend() == "nccl"
+        z = np.load(path, allow_pickle=False)
+        ctx = DistContext(split_batches=split, always_reduce=True)
+        model = gpu_recon(z, ctx, shard=True)
+        np.savez(out, obja=model.opt_obja.detach().cpu().numpy(), objp=model.opt_objp.detach().cpu().numpy(),
+                 backend=np.array(torch.distributed.get_backend()))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["split_batches", "whole_batches"])
+def test_recon_step_under_rccl_matches_reference(tmp_path, split):
+    """recon_step under init_process_group('nccl') (RCCL) on the MI355X, with every collective of the
+    data-parallel path executed (always_reduce at world size 1): the loss-sum all-reduce of split
+    mini-batches, the flat gradient all-reduce and the loss-term gather.  The reference
+    trajectory (grad_accumulation = 1) is reproduced: final object RMS < 1e-5."""
+    dev()
+    import torch.multiprocessing as mp
+    path = os.path.join(GOLDEN, "traj_n64_b4_ga1.npz")
+    out = str(tmp_path / "nccl.npz")
+    mp.start_processes(_nccl_worker, args=(_free_port(), path, out, split), nprocs=1, start_method="spawn")
+    r = np.load(out)
+    assert str(r["backend"]) == "nccl"
+    z = np.load(path, allow_pickle=False)
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((r[k].astype(np.float64) - ref) ** 2))) < 1e-5, k
