@@ -41,13 +41,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFLOPS = 157.3     # FP32 vector = FP32 MFMA rate on gfx950
 
-CONFIGS = {
-    "c2": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="weak"),
-    "c2-strong": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="strong"),
-    "c3": dict(N=256, P=8, O=2, Nz=1, f16=False, scan=512, mode="block"),
-    "c4": dict(N=128, P=1, O=1, Nz=16, f16=False, scan=1024, mode="strong"),
-    "c5": dict(N=256, P=4, O=1, Nz=1, f16=True, scan=4096, mode="block"),
-}
+from ptyrad_amd.synthetic import BENCH_CONFIGS as CONFIGS  # noqa: E402  (numpy only; no GPU)
 
 
 def parse():
@@ -67,6 +61,8 @@ def parse():
                     help="diagnostic (c2): build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
                          "(no collective) to check that per-rank work stays constant as W grows")
     ap.add_argument("--geom-rank", type=int, default=0)
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine variant for A/B runs (ptyx_set_tuning, include/ptyx.h); recorded in the output")
     return ap.parse_args()
 
 
@@ -176,47 +172,23 @@ def main():
     from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
     from ptyrad_amd.reconstruction import DistContext
 
+    tunings = {}
+    if a.tune:
+        from ptyrad_amd import _lib
+        for kv in a.tune:
+            k, v = kv.split("=")
+            _lib.set_tuning(k, int(v))
+            tunings[k] = int(v)
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ctx = DistContext()
     N, P, O, Nz, f16 = cfg["N"], cfg["P"], cfg["O"], cfg["Nz"], cfg["f16"]
-    step_px = syn.STEP_ANG / syn.DX_ANG
     gw, gr = (a.geom_world, a.geom_rank) if a.geom_world else (world, rank)
 
     # -------------------------------------------------- geometry: this rank's positions
-    if a.config == "c2":
-        S = a.scan or cfg["scan"]
-        scan = syn.raster_scan(S * gw, S, N, seed=0)
-        sl = slice(gr * S * S, (gr + 1) * S * S)
-        crop_pos, shifts, (Ny, Nx) = scan.crop_pos[sl], scan.shifts[sl], scan.obj_shape
-        desc = f"c2: synthetic 4D-STEM, {S}x{S} scan per GPU (weak scaling), 128x128 DP, P=O=Nz=1"
-    elif cfg["mode"] == "strong":     # c2-strong, c4: a fixed global scan, rows split over ranks
-        S = cfg["scan"] if a.config == "c4" else (a.scan or cfg["scan"])
-        scan = syn.raster_scan(S, S, N, seed=0)
-        r0, r1 = S * gr // gw, S * (gr + 1) // gw
-        sl = slice(r0 * S, r1 * S)
-        crop_pos, shifts, (Ny, Nx) = scan.crop_pos[sl], scan.shifts[sl], scan.obj_shape
-        desc = (f"{a.config}: {S}x{S} scan split over {gw} GPU(s) (rows {r0}-{r1} here), {N}x{N} DP, "
-                f"P={P}, O={O}, Nz={Nz}")
-    else:                             # c3 / c5: a block of --patterns positions of the rank's shard
-        S = cfg["scan"]
-        side = syn.object_side(S, N, step_px)
-        n_fast = min(S, a.patterns)
-        n_slow = max(1, a.patterns // n_fast)
-        rows_per_rank = S // max(1, gw)
-        # the block starts at this rank's first scan row of the full S x S raster
-        blk = syn.raster_scan(n_slow, n_fast, N, obj_shape=(side, side), seed=gr)
-        full_y0 = (side - ((S - 1) * step_px + N)) / 2.0
-        blk_y0 = (side - ((n_slow - 1) * step_px + N)) / 2.0
-        dy = int(round(full_y0 + gr * rows_per_rank * step_px - blk_y0))
-        crop_pos = blk.crop_pos.copy()
-        crop_pos[:, 0] = np.clip(crop_pos[:, 0] + dy, 0, side - N)
-        shifts, (Ny, Nx) = blk.shifts, (side, side)
-        desc = (f"{a.config}: {n_slow}x{n_fast} block of the {S}x{S} scan per GPU (rank shard rows from "
-                f"{gr * rows_per_rank}), object {side}x{side}, {N}x{N} DP, P={P}, O={O}, Nz={Nz}"
-                f"{', fp16 DP storage' if f16 else ''}")
+    crop_pos, shifts, (Ny, Nx), desc, n_global = syn.bench_geometry(a.config, gw, gr, a.patterns, a.scan)
     n_local = crop_pos.shape[0]
 
     # -------------------------------------------------- parameters (replicated) and this rank's DPs
@@ -325,7 +297,7 @@ def main():
         elapsed, engine_max, ar_max = (float(x) for x in e.tolist())
     else:
         engine_max, ar_max = engine_ms, ar_ms
-    total_patterns = world * n_local * a.steps if cfg["mode"] != "strong" else scan.crop_pos.shape[0] * a.steps
+    total_patterns = world * n_local * a.steps if cfg["mode"] != "strong" else n_global * a.steps
     if a.geom_world:
         total_patterns = n_local * a.steps
     value = total_patterns / elapsed
@@ -392,6 +364,11 @@ def main():
                    "N": N, "P": P, "O": O, "Nz": Nz, "dp_storage": "f16" if f16 else "f32",
                    "mini_batch": a.batch, "mini_batches_per_step": nb, "patterns_per_gpu_per_step": n_local,
                    "object": [Ny, Nx], "parallelism": par,
+                   **({"tunings": tunings} if tunings else {}),
+                   **({"capacity_env": {k: os.environ[k] for k in ("PTYX_STRIPE_MB", "PTYX_OBJ_SCRATCH_MB", "PTYX_FFC_MB")
+                                        if k in os.environ}} if any(k in os.environ for k in
+                                                                   ("PTYX_STRIPE_MB", "PTYX_OBJ_SCRATCH_MB", "PTYX_FFC_MB"))
+                      else {}),
                    **({"geometry_only": f"rank {gr} of a {gw}-GPU scan, no collective"} if a.geom_world else {})},
         "roofline": roof,
         "per_rank_ms": {"engine": round(engine_max, 3), "allreduce": round(ar_max, 3),

@@ -653,10 +653,10 @@ struct DeviceGuard {
 };
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
-enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneCount };
-const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1};
+enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneCount };
+const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -721,6 +721,10 @@ struct ptyx_plan {
   // N = 256 stripe engine (ptyx_stripe.hpp): per-call intermediates for stripe_cap patterns
   long long stripe_cap = 0;
   int stripe_groups = 0;
+  int stripe_defer_groups = 0;  // k_s5 groups of calls that defer the probe epilogue (fills the GPU once)
+  bool slab_live = false;       // k_s5 partials of earlier calls of the step await their reduction
+  int slab_live_groups = 0;
+  const float* slab_live_probe = nullptr;
   float2* st14 = nullptr;
   float2* spsi0 = nullptr;
   float2* st23 = nullptr;
@@ -942,6 +946,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
       pl->stripe_cap = cap;
       pl->stripe_groups = groups;
+      pl->stripe_defer_groups = std::max(1, std::min(groups, 2 * cu / (sp::kStripes * d.P)));
       // object gradient of two object modes: k_s4 writes per-pattern slots (over the T3 fields it
       // has consumed) and k_obj_gather reduces them per tile (deterministic, no atomics).  One
       // object mode keeps k_s4's f32 atomics (profiles/r02/ab/r02y_*: the epilogue costs c3 20 ms
@@ -1008,8 +1013,13 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   }
   if (d.N == 128 && d.P * d.O == 1 && d.Nz > 1 && !(d.flags & PTYX_MEAS_F16)) {
     // multislice register engine: Nz slot planes per pattern (parked ψⁿ, then slice n's
-    // object gradient), bounded by PTYX_OBJ_SCRATCH_MB like the single-slice slots
-    long long mb = 16384;
+    // object gradient), bounded by PTYX_OBJ_SCRATCH_MB (default the smaller of 64 GiB and a third
+    // of the free HBM).  Every call's k_obj_gather reads and writes the object band its windows
+    // reach, once per slice: fewer, larger calls cut that traffic (c4: 8,192 → 32,768 patterns
+    // per call, 128 → 32 gathers of the 16 × 3679² object per step).
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    long long mb = std::min<long long>(65536, (long long)(free_b / 3 / (1 << 20)));
     if (const char* s = std::getenv("PTYX_OBJ_SCRATCH_MB")) mb = std::max(0LL, std::atoll(s));
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (long long)(sizeof(float2) * N2 * d.Nz));
     int occ3 = 0;
@@ -1366,7 +1376,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
 // ---------------------------------------------------------------- stripe engine (N = 256)
 // Launch sequence of one ptyx_forward_loss_grad call on the stripe engine (ptyx_stripe.hpp).
 // The stripe engine's per-call argument block (shared by the passes before and after k_finalize).
-static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, const ptyx_grads& gz) {
+static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, const ptyx_grads& gz,
+                             int defer_groups) {
   using namespace sp;
   const ptyx_dims& d = pl->d;
   const int n = a.n_idx, P = d.P, O = d.O;
@@ -1384,6 +1395,12 @@ static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_los
   const bool sgather = pl->sgather && (gz.d_obja || gz.d_objp);
   s.oslot = sgather ? pl->st23 : nullptr;
   s.groups = std::max(1, std::min(pl->stripe_groups, n));
+  if (pl->slab_live) {                 // an earlier piece of the step left its k_s5 partials
+    s.groups = pl->slab_live_groups;
+    s.slab_acc = 1;
+  } else if (defer_groups > 0) {
+    s.groups = defer_groups;
+  }
   s.slabpart = pl->sslab; s.dsp = pl->sdsp;
   s.twg = pl->twg;
   return s;
@@ -1452,13 +1469,19 @@ static int stripe_pass(ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, 
 }
 
 static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
-                      const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+                      const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums, bool defer) {
   using namespace sp;
   const ptyx_dims& d = pl->d;
   const int n = a.n_idx, P = d.P, O = d.O;
   const bool tail = gz.d_probe != nullptr || gz.d_shifts != nullptr;
   const bool any_grad = gz.d_obja || gz.d_objp || tail;
-  const sp::SArgs s = stripe_args(pl, a, cfg, gz);
+  if (pl->slab_live && gz.d_probe != pl->slab_live_probe)
+    return fail(PTYX_EINVAL, "a deferred probe gradient awaits a call with the same d_probe");
+  // s_defer_groups tuning: 0 = never defer, > 0 = k_s5 groups of deferring calls
+  const long long dg = g_tuning[kTuneDeferGroups];
+  if (dg == 0 || !gz.d_probe) defer = false;
+  const int defer_groups = !defer ? 0 : dg > 0 ? (int)std::min<long long>(dg, pl->stripe_groups) : pl->stripe_defer_groups;
+  const sp::SArgs s = stripe_args(pl, a, cfg, gz, defer_groups);
   const bool sgather = s.oslot != nullptr;
   const dim3 bl(256);
   int rc = PTYX_OK;
@@ -1539,7 +1562,12 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_s_shift, dim3((n + 255) / 256), dim3(256), 0, st, pl->sdsp, n, kStripes * P, a.idx,
                        a.n_scans, gz.d_shifts);
   }
-  if (gz.d_probe) {
+  if (gz.d_probe && defer) {   // the reduction and the inverse FFT wait for the step's last piece
+    pl->slab_live = true;
+    pl->slab_live_groups = s.groups;
+    pl->slab_live_probe = gz.d_probe;
+  } else if (gz.d_probe) {
+    pl->slab_live = false;
     const long long per = (long long)P * kN2;
     {
       ProfScope ps(pl, kKSlabReduce, st);
@@ -1648,7 +1676,7 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  if (cfg->prep < PTYX_PREP_CALL || cfg->prep > PTYX_PREP_REUSE) return fail(PTYX_EINVAL, "unknown cfg.prep");
+  if ((cfg->prep & ~PTYX_PREP_DEFER_PROBE) > PTYX_PREP_REUSE || cfg->prep < 0) return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
   a.boff = boff;
   a.n_batches = n_batches;
@@ -1694,6 +1722,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
     a.ffc = pl->ffc;
     a.ffc_per = pl->ffc_per;
   }
+  if (pl->slab_live && *engine != kEngStripe)
+    return fail(PTYX_EINVAL, "a deferred stripe probe gradient awaits the step's last piece on this plan");
   *out = a;
   return PTYX_OK;
 }
@@ -1755,12 +1785,13 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
 }
 
 static int run_call(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
-                    const ptyx_grads& gz, int engine, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+                    const ptyx_grads& gz, int engine, hipStream_t st, float* loss_terms, int ph, double* bsums,
+                    bool defer) {
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
   if (engine == kEngFused3) return run_fused3(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
 #endif
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 256
-  if (engine == kEngStripe) return run_stripe(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
+  if (engine == kEngStripe) return run_stripe(pl, in, a, cfg, gz, st, loss_terms, ph, bsums, defer);
 #endif
   return run_two_pass(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
 }
@@ -1780,8 +1811,11 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;
+  const bool defer = (c.prep & PTYX_PREP_DEFER_PROBE) != 0;
+  c.prep &= ~PTYX_PREP_DEFER_PROBE;
   resolve_prep(pl, in, engine, &c);
-  return run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), loss_terms, kPhaseAll, nullptr);
+  return run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), loss_terms, kPhaseAll, nullptr,
+                  defer);
 }
 
 extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
@@ -1800,9 +1834,10 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;
+  c.prep &= ~PTYX_PREP_DEFER_PROBE;   // a split call is one piece: it closes its own probe gradient
   resolve_prep(pl, in, engine, &c);
   if ((rc = run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), nullptr, kPhaseBegin,
-                     batch_sums)))
+                     batch_sums, false)))
     return rc;
   pl->pend = true;
   pl->pend_in = *in; pl->pend_gz = gz; pl->pend_cfg = c;
@@ -1825,7 +1860,7 @@ extern "C" int ptyx_forward_loss_grad_end(ptyx_plan* pl, void* stream, const dou
   if (engine != pl->pend_engine) return fail(PTYX_EINVAL, "internal: engine changed between _begin and _end");
   DeviceGuard dg(pl->device);
   return run_call(pl, &pl->pend_in, a, &pl->pend_cfg, pl->pend_gz, engine, reinterpret_cast<hipStream_t>(stream),
-                  loss_terms, kPhaseEnd, const_cast<double*>(batch_sums));
+                  loss_terms, kPhaseEnd, const_cast<double*>(batch_sums), false);
 }
 
 extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,

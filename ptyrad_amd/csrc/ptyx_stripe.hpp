@@ -86,6 +86,7 @@ struct SArgs {
                          // T3 fields 0..O-1 of each pattern (k_obj_gather), instead of atomics
   float2* slabpart;      // (groups, P, N²) probe-gradient spectrum partials
   int groups;
+  int slab_acc;          // 1: add to the partials an earlier call of the step left (deferred epilogue)
   float* dsp;            // (n, kStripes·P, 2) position-gradient partials
   const float2* twg;     // W256^m, m = 0..255 (fp64-rounded)
 };
@@ -588,7 +589,8 @@ __global__ __launch_bounds__(256, kPassWG) void k_s4(SArgs a) {
 // ---------------------------------------------------------------------------------- P5
 // grid (kStripes, P, groups): block (s, p, g) sweeps patterns g, g + groups, ...: column FFT of
 // T4[p] → G;  slab += c_m conj(W_b) G (kept in registers across the sweep);  position-gradient
-// partials per pattern.  The slab stripe is written once at the end (k_slab_reduce sums groups).
+// partials per pattern.  The slab stripe is written once at the end (k_slab_reduce sums groups);
+// with slab_acc it starts from the partial an earlier call of the step stored there.
 __global__ __launch_bounds__(256, kPassWG) void k_s5(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
@@ -606,8 +608,12 @@ __global__ __launch_bounds__(256, kPassWG) void k_s5(SArgs a) {
   float2 acc[16];
   float2 fp[16];
   ldb<kColStride>(fp, a.Fp + (size_t)p * kN2, kFieldBytes, vcol);
+  if (a.slab_acc) {
+    ldb<kColStride>(acc, a.slabpart + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);
+  } else {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
+    for (int k = 0; k < 16; ++k) acc[k] = make_float2(0.f, 0.f);
+  }
   const float gx = shift_g(kx);
   float2 nxt[16];   // the next pattern's stripe is in flight during this pattern's transform
   if (gi < a.n) lds_<kColStride>(nxt, a.t14 + ((size_t)gi * P + p) * kN2, kFieldBytes, vcol);

@@ -295,20 +295,25 @@ class Plan:
         if loss_terms is None:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
         idx_t = self._idx(idx)
-        b0 = 0
-        prep = _lib.PTYX_PREP_FULL     # the object / probe are prepared once for all the pieces
+        pieces, b0 = [], 0
         while b0 < nb:
             b1 = b0 + 1
             while b1 < nb and off[b1 + 1] - off[b0] <= cap:
                 b1 += 1
+            pieces.append((b0, b1))
+            b0 = b1
+        for i, (b0, b1) in enumerate(pieces):
+            # the object / probe are prepared once for all the pieces; every piece but the last may
+            # leave its probe-gradient reduction to the next (PTYX_PREP_DEFER_PROBE)
+            prep = _lib.PTYX_PREP_FULL if i == 0 else _lib.PTYX_PREP_REUSE
+            if i < len(pieces) - 1:
+                prep |= _lib.PTYX_PREP_DEFER_PROBE
             sub_off = (off[b0:b1 + 1] - off[b0]).astype(np.int32)
             sub_idx = idx_t[int(off[b0]):int(off[b1])]
             sub_dp = None if dp_out is None else dp_out[int(off[b0]):int(off[b1])]
             self.forward_loss_grad(t, sub_idx, sub_off, loss_cfg, grads, grad_scale=grad_scale,
                                    loss_terms=loss_terms[b0:b1], dp_out=sub_dp, max_batch=max_batch, prep=prep,
                                    _rows_checked=True)
-            prep = _lib.PTYX_PREP_REUSE
-            b0 = b1
         return loss_terms
 
     def _split_call(self, t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out, reduce):

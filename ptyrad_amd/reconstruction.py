@@ -139,16 +139,21 @@ def loss_logger(batch_losses, niter, iter_t, verbose=True):
 class DistContext:
     """Rank/world of a torch.distributed job (backend 'nccl' = RCCL on ROCm, or 'gloo' on CPU)."""
 
-    def __init__(self, group=None, split_batches=None, always_reduce=False):
+    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=False):
         """split_batches: None = split a group's mini-batches over the ranks only when the group has
         fewer mini-batches than ranks; True = always (accelerate's split_batches=True,
         utils/common.py:63); False = never (whole mini-batches round-robin).
-        always_reduce: run the collectives even with one rank (tests that exercise RCCL on one GPU)."""
+        always_reduce: run the collectives even with one rank (tests that exercise RCCL on one GPU).
+        band_exchange: object gradients by row band (ObjectBands): each rank sends only the rows
+        its windows touched to their owners, owners run the optimizer on their band (ZeRO-1),
+        then the updated bands are all-gathered; the rest of the gradient is all-reduced."""
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.split_batches = split_batches
         self.always_reduce = bool(always_reduce) and dist.is_initialized()
+        self.band_exchange = bool(band_exchange)
+        self.bands = None
 
     def _collective(self) -> bool:
         return self.world > 1 or self.always_reduce
@@ -212,28 +217,6 @@ class DistContext:
         if self._collective() and flat is not None and flat.numel():
             dist.all_reduce(flat, group=self.group)
 
-    def allreduce_grads(self, params):
-        """All-reduce(sum) of the ``.grad`` of the trainable params (requires_grad True, a set
-        toggle_grad_requires makes identical on every rank); frozen ones keep ``.grad = None``
-        (reference zero_grad / toggle_grad_requires, reconstruction.py:739, 783-790)."""
-        if self.world == 1:
-            return
-        live = [p for p in params if p.requires_grad]
-        grads = []
-        for p in live:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            grads.append(p.grad)
-        if not grads:
-            return
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat, group=self.group)
-        off = 0
-        for g in grads:
-            n = g.numel()
-            g.copy_(flat[off:off + n].view_as(g))
-            off += n
-
     def gather_terms(self, terms_local, idx_local, n_total, device):
         """All ranks get the (n_total, 5) loss terms of the group (rows filled by their owners)."""
         buf = torch.zeros((n_total, 5), dtype=torch.float32, device=device)
@@ -242,6 +225,133 @@ class DistContext:
         if self._collective():
             dist.all_reduce(buf, group=self.group)
         return buf
+
+
+class ObjectBands:
+    """Row-band ownership of the object for the band-sized gradient exchange (the
+    ZeRO-1 option; replaces the object part of DDP's bucketed all-reduce, reconstruction.py:753).
+
+    Rank j owns rows [j·R, (j+1)·R) of every (O, Nz, Ny, Nx) object tensor, R = ⌈Ny / W⌉.  A rank's
+    windows touch rows [lo, hi) only (its shard of the scan), so its object gradient is zero
+    elsewhere:
+      reduce   each rank sends the rows of [lo, hi) that other ranks own to their owners (P2P); an
+               owner adds what it receives to its own rows, in rank order;
+      step     the caller's optimizer class, with the same hyperparameters, steps views of the
+               owned rows (optimizer state for 1/W of the object per rank);
+      gather   the updated bands are all-gathered, so every rank again holds the whole object
+               (the constraints and the next forward read any row).
+    Gradient bytes sent per rank: the touched rows outside the own band (the halo of a row-sharded
+    scan) instead of a full-object all-reduce; the all-gather moves (W − 1) / W of the object.  A
+    pixel that at most two ranks touch gets the same sum as the all-reduce bit for bit (a + b);
+    with more contributors only the fp32 summation order differs."""
+
+    def __init__(self, ctx, Ny, lo, hi, device):
+        self.ctx, self.Ny = ctx, int(Ny)
+        W = ctx.world
+        self.R = -(-self.Ny // W)
+        rng_ = torch.tensor([int(lo), int(hi)], dtype=torch.int64, device=device)
+        allr = [torch.zeros_like(rng_) for _ in range(W)]
+        if W > 1:
+            dist.all_gather(allr, rng_, group=ctx.group)
+        else:
+            allr = [rng_]
+        self.ranges = [(int(r[0]), int(r[1])) for r in allr]
+        self.b0 = min(self.Ny, ctx.rank * self.R)
+        self.b1 = min(self.Ny, (ctx.rank + 1) * self.R)
+        self.opt = None
+        self.views = {}
+
+    def band(self, j):
+        return min(self.Ny, j * self.R), min(self.Ny, (j + 1) * self.R)
+
+    def _peer(self, r):
+        return dist.get_global_rank(self.ctx.group, r) if self.ctx.group is not None else r
+
+    def sent_rows(self):
+        """Rows this rank sends in reduce() (the all-reduce would move 2·(W−1)/W of Ny)."""
+        lo, hi = self.ranges[self.ctx.rank]
+        return sum(max(0, min(hi, self.band(j)[1]) - max(lo, self.band(j)[0]))
+                   for j in range(self.ctx.world) if j != self.ctx.rank)
+
+    def reduce(self, grads):
+        """grads: (O, Nz, Ny, Nx) object-gradient tensors, in place: the owner's rows get the sum."""
+        me, W = self.ctx.rank, self.ctx.world
+        lo, hi = self.ranges[me]
+        for g in grads:
+            ops, bufs = [], []
+            for j in range(W):                     # send my touched rows of band j to its owner
+                if j == me:
+                    continue
+                a, b = max(lo, self.band(j)[0]), min(hi, self.band(j)[1])
+                if a < b:
+                    ops.append(dist.isend(g[:, :, a:b].contiguous(), self._peer(j), group=self.ctx.group))
+            for i in range(W):                     # receive rank i's rows of my band
+                if i == me:
+                    continue
+                a, b = max(self.ranges[i][0], self.b0), min(self.ranges[i][1], self.b1)
+                if a < b:
+                    buf = torch.empty(g[:, :, a:b].shape, dtype=g.dtype, device=g.device)
+                    bufs.append((a, b, buf, dist.irecv(buf, self._peer(i), group=self.ctx.group)))
+            for a, b, buf, req in bufs:            # in rank order
+                req.wait()
+                g[:, :, a:b] += buf
+            for op in ops:
+                op.wait()
+
+    def step(self, optimizer, params):
+        """Step `optimizer`'s class on the owned rows of the object params (their .grad holds the
+        reduced gradient there); the params' .grad is cleared so `optimizer` skips them."""
+        if self.opt is None:
+            groups = []
+            for gr in optimizer.param_groups:
+                mine = [p for p in gr["params"] if any(p is q for q in params)]
+                if mine:
+                    views = []
+                    for p in mine:
+                        v = torch.nn.Parameter(p.data[:, :, self.b0:self.b1])   # shares p's storage
+                        self.views[id(p)] = v
+                        views.append(v)
+                    groups.append({**{k: v for k, v in gr.items() if k != "params"}, "params": views})
+            self.opt = type(optimizer)(groups, **optimizer.defaults) if groups else None
+        for p in params:
+            v = self.views.get(id(p))
+            if v is not None:
+                v.grad = p.grad[:, :, self.b0:self.b1] if p.grad is not None else None
+        if self.opt is not None:
+            self.opt.step()
+            for v in self.views.values():
+                v.grad = None
+
+    def gather(self, params):
+        """Every rank receives every owner's updated rows."""
+        W = self.ctx.world
+        for p in params:
+            O, Nz, _, Nx = p.shape
+            mine = torch.zeros((O, Nz, self.R, Nx), dtype=p.dtype, device=p.device)
+            mine[:, :, :self.b1 - self.b0] = p.data[:, :, self.b0:self.b1]
+            out = torch.empty(W * mine.numel(), dtype=p.dtype, device=p.device)
+            if W > 1:
+                dist.all_gather_into_tensor(out, mine.reshape(-1), group=self.ctx.group)
+            else:
+                out.copy_(mine.reshape(-1))
+            out = out.view((W,) + tuple(mine.shape))
+            for j in range(W):
+                a, b = self.band(j)
+                if a < b and j != self.ctx.rank:
+                    p.data[:, :, a:b] = out[j, :, :, :b - a]
+
+
+def touched_rows(model, batches, N):
+    """Object rows [lo, hi) the windows of these mini-batches reach (crop_pos y + N)."""
+    idx = np.concatenate([np.asarray(b).reshape(-1) for b in batches]) if len(batches) else np.zeros(0, int)
+    if not idx.size:
+        return 0, 0
+    cp = getattr(model, "crop_pos", None)
+    if cp is None:
+        cp = model.crop_pos_np
+    cp = cp.cpu().numpy() if isinstance(cp, torch.Tensor) else np.asarray(cp)
+    cy = cp[idx, 0]
+    return int(cy.min()), int(cy.max()) + int(N)
 
 
 # ------------------------------------------------------------------ the reference step
@@ -268,6 +378,14 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     reached = {id(model.optimizable_tensors[k]) for k in model.engine_grad_names()}
     live = [p for p in params if p.requires_grad and id(p) in reached]
     split_ok = hasattr(loss_fn, "supports_batch_split") and loss_fn.supports_batch_split(model)
+    objs = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in live)]
+    band = ctx.band_exchange and ctx._collective() and bool(objs)
+    if band:
+        if ctx.bands is None:     # batches are fixed for the run: the touched rows are too
+            N = int(model.opt_probe.shape[1])
+            lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok), N)
+            ctx.bands = ObjectBands(ctx, model.opt_obja.shape[2], lo, hi, dev)
+        live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
     for g0 in range(0, len(batches), ga):
         group = batches[g0:g0 + ga]
         flat = ctx.grad_views(live)
@@ -291,8 +409,21 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
                 terms = loss_fn.fused_into(model, [group[i] for i in mine], grad_scale=1.0 / ga)
             else:
                 terms = torch.zeros((0, 5), device=dev)
-        ctx.allreduce(flat)
-        optimizer.step()
+        if band:
+            n_obj = sum(p.numel() for p in objs)
+            ctx.bands.reduce([p.grad for p in objs])
+            ctx.allreduce(flat[n_obj:])                # probe, positions, propagator: small
+            saved = [p.grad for p in objs]
+            for p in objs:
+                p.grad = None                          # the caller's optimizer skips the objects
+            optimizer.step()
+            for p, g in zip(objs, saved):
+                p.grad = g
+            ctx.bands.step(optimizer, objs)
+            ctx.bands.gather(objs)
+        else:
+            ctx.allreduce(flat)
+            optimizer.step()
         optimizer.zero_grad(set_to_none=True)
         all_terms = ctx.gather_terms(terms, mine, len(group), dev).cpu().numpy()   # one sync per step
         for row in all_terms:

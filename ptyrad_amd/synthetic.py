@@ -200,3 +200,57 @@ def random_problem(n: int, n_slow: int, n_fast: int, P: int = 1, O: int = 1, Nz:
         m = None
     return Problem(obja, objp, probe, H, omode_occupancy(O), scan.crop_pos, scan.shifts,
                    m, n_slow, n_fast)
+
+
+# BASELINE.json configs[1..4] as bench.py runs them (SURVEY §8d geometry): probe side N, modes,
+# slices, DP storage, the full raster side and how it is divided over the ranks
+BENCH_CONFIGS = {
+    "c2": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="weak"),
+    "c2-strong": dict(N=128, P=1, O=1, Nz=1, f16=False, scan=256, mode="strong"),
+    "c3": dict(N=256, P=8, O=2, Nz=1, f16=False, scan=512, mode="block"),
+    "c4": dict(N=128, P=1, O=1, Nz=16, f16=False, scan=1024, mode="strong"),
+    "c5": dict(N=256, P=4, O=1, Nz=1, f16=True, scan=4096, mode="block"),
+}
+
+
+def bench_geometry(config: str, world: int = 1, rank: int = 0, patterns: int = 16384, scan: int | None = None):
+    """The positions one rank of a bench.py job processes.
+
+    c2: a scan x scan raster per rank (weak scaling: the global raster is (scan·world) x scan);
+    c2-strong / c4: the config's raster split by rows over the ranks (strong scaling);
+    c3 / c5: a block of `patterns` positions of the config's raster, starting at the rank's first
+    row of the full raster (the full c5 shard is 275 GB of DPs per GPU).
+    Returns (crop_pos, shifts, (Ny, Nx), description, total positions of the job's global scan or None).
+    """
+    cfg = BENCH_CONFIGS[config]
+    N = cfg["N"]
+    step_px = STEP_ANG / DX_ANG
+    if config == "c2":
+        S = scan or cfg["scan"]
+        sc = raster_scan(S * world, S, N, seed=0)
+        sl = slice(rank * S * S, (rank + 1) * S * S)
+        return (sc.crop_pos[sl], sc.shifts[sl], sc.obj_shape,
+                f"c2: synthetic 4D-STEM, {S}x{S} scan per GPU (weak scaling), 128x128 DP, P=O=Nz=1", None)
+    if cfg["mode"] == "strong":
+        S = cfg["scan"] if config == "c4" else (scan or cfg["scan"])
+        sc = raster_scan(S, S, N, seed=0)
+        r0, r1 = S * rank // world, S * (rank + 1) // world
+        sl = slice(r0 * S, r1 * S)
+        return (sc.crop_pos[sl], sc.shifts[sl], sc.obj_shape,
+                f"{config}: {S}x{S} scan split over {world} GPU(s) (rows {r0}-{r1} here), {N}x{N} DP, "
+                f"P={cfg['P']}, O={cfg['O']}, Nz={cfg['Nz']}", sc.crop_pos.shape[0])
+    S = cfg["scan"]
+    side = object_side(S, N, step_px)
+    n_fast = min(S, patterns)
+    n_slow = max(1, patterns // n_fast)
+    rows_per_rank = S // max(1, world)
+    blk = raster_scan(n_slow, n_fast, N, obj_shape=(side, side), seed=rank)
+    full_y0 = (side - ((S - 1) * step_px + N)) / 2.0
+    blk_y0 = (side - ((n_slow - 1) * step_px + N)) / 2.0
+    dy = int(round(full_y0 + rank * rows_per_rank * step_px - blk_y0))
+    crop_pos = blk.crop_pos.copy()
+    crop_pos[:, 0] = np.clip(crop_pos[:, 0] + dy, 0, side - N)
+    return (crop_pos, blk.shifts, (side, side),
+            f"{config}: {n_slow}x{n_fast} block of the {S}x{S} scan per GPU (rank shard rows from "
+            f"{rank * rows_per_rank}), object {side}x{side}, {N}x{N} DP, P={cfg['P']}, O={cfg['O']}, "
+            f"Nz={cfg['Nz']}{', fp16 DP storage' if cfg['f16'] else ''}", None)

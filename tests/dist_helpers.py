@@ -129,7 +129,7 @@ class OracleLoss:
                                   model, batches, self.loss_params)
 
 
-def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False):
+def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band=False):
     """Run the trajectory fixture through ptyrad_amd.reconstruction.recon_step; returns final params.
 
     start_iter: per-tensor overrides (staggered toggle_grad_requires); shard: each rank keeps only
@@ -137,7 +137,7 @@ def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False):
     from ptyrad_amd.reconstruction import DistContext, recon_step
     sizes = z["batch_sizes"]
     batches = np.split(z["batches"], np.cumsum(sizes)[:-1])
-    ctx = DistContext()
+    ctx = DistContext(band_exchange=band)
     mi = ctx.local_indices(batches, int(z["grad_accumulation"])) if shard else None
     model = OracleModel(z, start_iter=start_iter, meas_index=mi)
     lp = json.loads(str(z["loss_params"]))
@@ -158,6 +158,7 @@ def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False):
                 m.opt_probe.copy_(torch.from_numpy(prm["probe"]))
     for it in range(1, (niter or int(z["niter"])) + 1):
         recon_step(batches, int(z["grad_accumulation"]), model, opt, loss, cfn, it, verbose=False, dist_ctx=ctx)
+    model._band_ctx = ctx
     return {k: v.detach().numpy().copy() for k, v in (("obja", model.opt_obja), ("objp", model.opt_objp),
                                                        ("probe", model.opt_probe),
                                                        ("shifts", model.opt_probe_pos_shifts))}, model
@@ -170,10 +171,14 @@ def dist_worker(rank, world, port, path, out_path, kw=None):
     try:
         z = np.load(path, allow_pickle=False)
         params, model = run_recon(z, **(kw or {}))
+        extra = {}
+        if (kw or {}).get("band"):
+            ctx_b = model._band_ctx if hasattr(model, "_band_ctx") else None
+            extra = {"sent_rows": np.array(ctx_b.bands.sent_rows() if ctx_b else -1)}
         if rank == 0:
-            np.savez(out_path, losses=np.array([v for _, v in model.loss_iters]), **params)
+            np.savez(out_path, losses=np.array([v for _, v in model.loss_iters]), **params, **extra)
         else:
-            np.savez(out_path.replace(".npz", f"_r{rank}.npz"), **params)
+            np.savez(out_path.replace(".npz", f"_r{rank}.npz"), **params, **extra)
     finally:
         torch.distributed.destroy_process_group()
 
