@@ -56,6 +56,12 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="patterns for the CPU baseline (0: about 20 s of the host's cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loss", default="single", choices=["single", "poissn", "both"],
+                    help="data term(s) beside loss_sparse (both: the stripe / register engines cannot take two "
+                         "data terms in one pass, so the call runs the general engine)")
+    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "band"],
+                    help="N > 1: object gradients by one flat all-reduce, or by row band (ObjectBands: halo "
+                         "rows to their owners, Adam on the owned band, bands all-gathered)")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--geom-world", type=int, default=0,
                     help="diagnostic (c2): build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
@@ -226,7 +232,7 @@ def main():
     off = batch_offsets(batches)       # host offsets: the Plan splits a call at mini-batch boundaries
     nb = len(batches)
     max_batch = max(len(b) for b in batches)
-    lcfg = LossConfig()
+    lcfg = LossConfig(single_on=a.loss in ("single", "both"), poissn_on=a.loss in ("poissn", "both"))
     # every gradient of the step in ONE flat buffer (position gradients are rank-local)
     names = ("obja", "objp", "probe")
     flat = torch.zeros(sum(t[k].numel() for k in names), device=dev)
@@ -255,6 +261,19 @@ def main():
         opt = torch.optim.Adam(groups, fused=True)
     except (RuntimeError, ValueError):
         opt = torch.optim.Adam(groups, foreach=True)
+    bands = None
+    n_obj = t["obja"].numel() + t["objp"].numel()
+    if world > 1 and a.exchange == "band":
+        from ptyrad_amd.reconstruction import ObjectBands
+        bands = ObjectBands(ctx, Ny, int(crop_pos[:, 0].min()), int(crop_pos[:, 0].max()) + N, dev)
+        objs = [t["obja"], t["objp"]]
+    # bytes each rank sends per step in the exchange (ring all-reduce / all-gather: (W-1)/W per pass)
+    if bands is None:
+        xbytes = 2 * (world - 1) / world * flat.numel() * 4 if world > 1 else 0
+    else:
+        row_b = t["obja"].shape[0] * t["obja"].shape[1] * Nx * 4
+        xbytes = (2 * bands.sent_rows() * row_b + (world - 1) / world * n_obj * 4 +
+                  2 * (world - 1) / world * (flat.numel() - n_obj) * 4)
 
     def step(timed=False):
         flat.zero_()
@@ -266,11 +285,30 @@ def main():
             e1 = torch.cuda.Event(enable_timing=True) if timed else None
             if timed:
                 e0.record(stream)
-            ctx.allreduce(flat)        # object + probe gradients: ONE RCCL all-reduce per step
+            if bands is None:
+                ctx.allreduce(flat)    # object + probe gradients: ONE RCCL all-reduce per step
+            else:
+                ctx.allreduce(flat[n_obj:])                   # probe
+                bands.reduce([grads["obja"], grads["objp"]])  # halo rows to their owners
             if timed:
                 e1.record(stream)
                 ar_ev.append((e0, e1))
-        opt.step()
+        if bands is None:
+            opt.step()
+        else:
+            for p_ in objs:
+                p_.grad = None
+            opt.step()                                        # probe, positions
+            t["obja"].grad, t["objp"].grad = grads["obja"], grads["objp"]
+            bands.step(opt, objs)                             # Adam on the owned rows
+            if timed:
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record(stream)
+            bands.gather(objs)
+            if timed:
+                e3 = torch.cuda.Event(enable_timing=True)
+                e3.record(stream)
+                ar_ev.append((e2, e3))
 
     for _ in range(a.warmup):
         step()
@@ -289,7 +327,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kstats = plan.profile_end()
     assert bool(torch.isfinite(terms).all()), "non-finite loss terms"
-    ar_ms = sum(e0.elapsed_time(e1) for e0, e1 in ar_ev) / max(1, len(ar_ev)) if ar_ev else 0.0
+    ar_ms = sum(e0.elapsed_time(e1) for e0, e1 in ar_ev) / a.steps if ar_ev else 0.0
     engine_ms = sum(v[1] for v in kstats.values()) / a.steps
     if world > 1:
         e = torch.tensor([elapsed, engine_ms, ar_ms], device=dev, dtype=torch.float64)
@@ -310,7 +348,7 @@ def main():
     n_fft = 2 * P * O * (2 * Nz - 1) + 2 * P
     f_alg = n_fft * 5 * N * N * math.log2(N * N)
     roof = None
-    stripe = [k for k in kstats if k.startswith("k_s")]
+    stripe = [k for k in kstats if k in ("k_s1", "k_s2", "k_s3", "k_s4", "k_s5")]
     # HBM traffic of the dominant kernel from its PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate
     # rocprofv3 --pmc runs of this bench command; tools/gpu_profile.sh -> profiles/make_traffic.py):
     # measured at the commit named in `traffic_source`, not inside this run
@@ -359,7 +397,9 @@ def main():
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "strong" if cfg["mode"] == "strong" else "weak", "vs_baseline": None,
         "dtype": "f32", "data": data,
-        "config": {"workload": desc + ", sub-px shifts on, loss_single(q=0.5)+loss_sparse(L1), mini-batch "
+        "config": {"workload": desc + ", sub-px shifts on, " + {"single": "loss_single(q=0.5)", "poissn": "loss_poissn",
+                                                                "both": "loss_single(q=0.5)+loss_poissn"}[a.loss]
+                   + "+loss_sparse(L1), mini-batch "
                    f"{a.batch}, one Adam step per iteration (grad_accumulation = all mini-batches; all-reduce first)",
                    "N": N, "P": P, "O": O, "Nz": Nz, "dp_storage": "f16" if f16 else "f32",
                    "mini_batch": a.batch, "mini_batches_per_step": nb, "patterns_per_gpu_per_step": n_local,
@@ -372,7 +412,8 @@ def main():
                    **({"geometry_only": f"rank {gr} of a {gw}-GPU scan, no collective"} if a.geom_world else {})},
         "roofline": roof,
         "per_rank_ms": {"engine": round(engine_max, 3), "allreduce": round(ar_max, 3),
-                        "allreduce_bytes": int(flat.numel() * 4)},
+                        "allreduce_bytes": int(flat.numel() * 4), "exchange": a.exchange if world > 1 else None,
+                        "exchange_bytes_sent_per_rank": int(xbytes)},
         "fft_tflops": round(value / world * f_alg / 1e12, 2) if cfg["mode"] != "strong" else
         round(value * f_alg / 1e12 / world, 2),
         "kernels_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in kstats.items()},

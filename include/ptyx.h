@@ -53,6 +53,13 @@ extern "C" {
 #define PTYX_PREP_CALL 0   /* prepare what this call's windows touch                           */
 #define PTYX_PREP_FULL 1   /* prepare the whole object, for later PTYX_PREP_REUSE calls          */
 #define PTYX_PREP_REUSE 2  /* reuse the previous call's preparation on this plan                */
+/* Flag bit, or'ed into loss_cfg.prep by a caller that splits one optimizer step into pieces: this
+ * piece may leave its probe-gradient reduction to a later piece (the stripe engine keeps
+ * accumulating its per-group k-space partials and runs the reduction and inverse FFT once, on the
+ * first later piece without the bit).  Until then d_probe lacks these pieces' contribution, and
+ * every call on the plan must pass the same d_probe.  Engines without a deferred epilogue
+ * ignore the bit. */
+#define PTYX_PREP_DEFER_PROBE 4
 /* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
  * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
  * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
@@ -319,7 +326,9 @@ int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
 /* Engine-variant selection for tests and A/B measurements (no environment variable changes an
  * engine): key "s3_hold" (0..4: probe/object modes k_s3 keeps in registers), "s_psi0" (0/1: the
  * stripe engine parks ψ⁰ instead of recomputing it), "s_gather" (0/1: stripe object gradient by
- * slots + gather instead of f32 atomics); value -1 restores the measured default.  Process-wide,
+ * slots + gather instead of f32 atomics), "s_defer_groups" (0: the stripe engine ignores
+ * PTYX_PREP_DEFER_PROBE; n > 0: k_s5 partial groups of deferring calls); value -1 restores the
+ * measured default.  Process-wide,
  * read by ptyx_plan_create (s_psi0, s_gather) and by each call (s3_hold).  Every variant computes
  * the same results.  ptyx_get_tuning returns the current value (-1 default, -2 unknown key). */
 int ptyx_set_tuning(const char *key, int64_t value);

@@ -14,19 +14,21 @@ import torch
 from .engine import LOSS_TERM_NAMES, LossConfig, batch_offsets
 
 
-def _engine_terms(plan, t, idx_t, off, cfg, grads, grad_scale, shift_probes):
+def _engine_terms(plan, t, idx_t, off, cfg, grads, grad_scale, shift_probes, rows_checked=False):
     """One ptyx_forward_loss_grad call (plus the pacbed loss and its adjoint when on); gradients
     are accumulated (+=) into ``grads``, scaled by ``grad_scale``.  ``off``: host batch offsets
-    (the Plan splits calls beyond its capacity at mini-batch boundaries)."""
+    (the Plan splits calls beyond its capacity at mini-batch boundaries).  rows_checked: the caller
+    verified on the host that every position's DP is in the rank-local block (no device check)."""
     if cfg.pacbed_on:   # loss_pacbed (losses.py:77-89): HIP loss on the call's dp, then the HIP adjoint
         N = t["probe"].shape[1]
         dp = torch.empty((int(idx_t.numel()), N, N), dtype=torch.float32, device=t["obja"].device)
-        terms = plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale, dp_out=dp)
+        terms = plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale, dp_out=dp,
+                                       _rows_checked=rows_checked)
         dLdI = plan.loss_pacbed(t, idx_t, off, dp, cfg, terms, grad_scale=grad_scale, want_dldi=bool(grads))
         if grads:
             plan.adjoint_dldi(t, idx_t, dLdI, {k: v for k, v in grads.items() if k != "shifts" or shift_probes})
         return terms
-    return plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale)
+    return plan.forward_loss_grad(t, idx_t, off, cfg, grads, grad_scale=grad_scale, _rows_checked=rows_checked)
 
 
 class _FusedLoss(torch.autograd.Function):
@@ -234,7 +236,7 @@ class CombinedLoss(torch.nn.Module):
         if H_rv.requires_grad:          # optimised dz / tilts: dL/dH, then autograd through H(dz, tilts)
             grads["H"] = torch.zeros_like(H_rv)
         terms = _engine_terms(model.plan, t, idx_t, batch_offsets(batches), cfg, grads, float(grad_scale),
-                              model.shift_probes)
+                              model.shift_probes, rows_checked=True)    # _check_held above
         if "H" in grads:
             torch.autograd.backward(H_rv, grads["H"])
         return terms
@@ -277,7 +279,8 @@ class CombinedLoss(torch.nn.Module):
         if H_rv.requires_grad:          # optimised dz / tilts: this rank's share of dL/dH, then autograd
             grads["H"] = torch.zeros_like(H_rv)
         local_terms = model.plan.forward_loss_grad(t, idx_t, batch_offsets(local), _LC.from_loss_params(self.loss_params),
-                                                   grads, grad_scale=float(grad_scale), batch_sums_reduce=group_reduce)
+                                                   grads, grad_scale=float(grad_scale), batch_sums_reduce=group_reduce,
+                                                   _rows_checked=True)   # _check_held above
         if "H" in grads:
             torch.autograd.backward(H_rv, grads["H"])
         terms.index_copy_(0, sel, local_terms)

@@ -202,10 +202,18 @@ class DistContext:
 
     def grad_views(self, params):
         """Give each param a zeroed ``.grad`` that is a view into ONE flat f32 buffer; returns it.
-        ``params`` must be the same list, in the same order, on every rank."""
+        ``params`` must be the same list, in the same order, on every rank.  The buffer is reused
+        from step to step (zeroed on the device) while the list stays the same."""
         n = sum(p.numel() for p in params)
         dev = params[0].device if params else torch.device("cpu")
-        flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        key = tuple(id(p) for p in params)
+        cached = getattr(self, "_flat", None)
+        if cached is not None and cached[0] == key and cached[1].numel() == n and cached[1].device == dev:
+            flat = cached[1]
+            flat.zero_()
+        else:
+            flat = torch.zeros(n, dtype=torch.float32, device=dev)
+            self._flat = (key, flat)
         off = 0
         for p in params:
             p.grad = flat[off:off + p.numel()].view_as(p)
@@ -284,19 +292,20 @@ class ObjectBands:
                     continue
                 a, b = max(lo, self.band(j)[0]), min(hi, self.band(j)[1])
                 if a < b:
-                    ops.append(dist.isend(g[:, :, a:b].contiguous(), self._peer(j), group=self.ctx.group))
+                    ops.append(dist.P2POp(dist.isend, g[:, :, a:b].contiguous(), self._peer(j), self.ctx.group))
             for i in range(W):                     # receive rank i's rows of my band
                 if i == me:
                     continue
                 a, b = max(self.ranges[i][0], self.b0), min(self.ranges[i][1], self.b1)
                 if a < b:
                     buf = torch.empty(g[:, :, a:b].shape, dtype=g.dtype, device=g.device)
-                    bufs.append((a, b, buf, dist.irecv(buf, self._peer(i), group=self.ctx.group)))
-            for a, b, buf, req in bufs:            # in rank order
+                    ops.append(dist.P2POp(dist.irecv, buf, self._peer(i), self.ctx.group))
+                    bufs.append((a, b, buf))
+            # one batched group: RCCL pairs every send with its receive without ordering deadlocks
+            for req in (dist.batch_isend_irecv(ops) if ops else []):
                 req.wait()
+            for a, b, buf in bufs:                 # in rank order
                 g[:, :, a:b] += buf
-            for op in ops:
-                op.wait()
 
     def step(self, optimizer, params):
         """Step `optimizer`'s class on the owned rows of the object params (their .grad holds the
@@ -386,6 +395,7 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok), N)
             ctx.bands = ObjectBands(ctx, model.opt_obja.shape[2], lo, hi, dev)
         live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
+    rows = []
     for g0 in range(0, len(batches), ga):
         group = batches[g0:g0 + ga]
         flat = ctx.grad_views(live)
@@ -411,8 +421,8 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
                 terms = torch.zeros((0, 5), device=dev)
         if band:
             n_obj = sum(p.numel() for p in objs)
-            ctx.bands.reduce([p.grad for p in objs])
-            ctx.allreduce(flat[n_obj:])                # probe, positions, propagator: small
+            ctx.allreduce(flat[n_obj:])                # probe, positions, propagator: small (a
+            ctx.bands.reduce([p.grad for p in objs])   # collective first: RCCL's communicator)
             saved = [p.grad for p in objs]
             for p in objs:
                 p.grad = None                          # the caller's optimizer skips the objects
@@ -425,12 +435,13 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             ctx.allreduce(flat)
             optimizer.step()
         optimizer.zero_grad(set_to_none=True)
-        all_terms = ctx.gather_terms(terms, mine, len(group), dev).cpu().numpy()   # one sync per step
-        for row in all_terms:
-            for name, v in zip(LOSS_TERM_NAMES, row):
-                if name in batch_losses:
-                    batch_losses[name].append(v)
+        # the loss terms stay on the device until the iteration ends (no host sync per step)
+        rows.append(ctx.gather_terms(terms, mine, len(group), dev) if ctx._collective() else terms)
         model.clear_cache()
+    for row in (torch.cat(rows).cpu().numpy() if rows else ()):   # one sync per iteration
+        for name, v in zip(LOSS_TERM_NAMES, row):
+            if name in batch_losses:
+                batch_losses[name].append(v)
     if constraint_fn is not None:
         constraint_fn(model, niter)
     iter_t = time_sync() - t0

@@ -180,7 +180,7 @@ def _free_port():
     return p
 
 
-def _nccl_worker(rank, port, path, out, split):
+def _nccl_worker(rank, port, path, out, split, band=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -190,7 +190,7 @@ def _nccl_worker(rank, port, path, out, split):
         from tests.dist_helpers import gpu_recon
         assert torch.distributed.get_backend() == "nccl"
         z = np.load(path, allow_pickle=False)
-        ctx = DistContext(split_batches=split, always_reduce=True)
+        ctx = DistContext(split_batches=split, always_reduce=True, band_exchange=band)
         model = gpu_recon(z, ctx, shard=True)
         np.savez(out, obja=model.opt_obja.detach().cpu().numpy(), objp=model.opt_objp.detach().cpu().numpy(),
                  backend=np.array(torch.distributed.get_backend()))
@@ -198,17 +198,19 @@ def _nccl_worker(rank, port, path, out, split):
         torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("split", [True, False], ids=["split_batches", "whole_batches"])
-def test_recon_step_under_rccl_matches_reference(tmp_path, split):
+@pytest.mark.parametrize("split,band", [(True, False), (False, False), (False, True)],
+                         ids=["split_batches", "whole_batches", "band_exchange"])
+def test_recon_step_under_rccl_matches_reference(tmp_path, split, band):
     """recon_step under init_process_group('nccl') (RCCL) on the MI355X, with every collective of the
     data-parallel path executed (always_reduce at world size 1): the loss-sum all-reduce of split
     mini-batches, the flat gradient all-reduce and the loss-term gather.  The reference
-    trajectory (grad_accumulation = 1) is reproduced: final object RMS < 1e-5."""
+    trajectory (grad_accumulation = 1) is reproduced: final object RMS < 1e-5.  band_exchange: the
+    object optimizer steps run on band views (ObjectBands) and the bands are all-gathered."""
     dev()
     import torch.multiprocessing as mp
     path = os.path.join(GOLDEN, "traj_n64_b4_ga1.npz")
     out = str(tmp_path / "nccl.npz")
-    mp.start_processes(_nccl_worker, args=(_free_port(), path, out, split), nprocs=1, start_method="spawn")
+    mp.start_processes(_nccl_worker, args=(_free_port(), path, out, split, band), nprocs=1, start_method="spawn")
     r = np.load(out)
     assert str(r["backend"]) == "nccl"
     z = np.load(path, allow_pickle=False)
