@@ -265,7 +265,8 @@ def main():
     n_obj = t["obja"].numel() + t["objp"].numel()
     if world > 1 and a.exchange == "band":
         from ptyrad_amd.reconstruction import ObjectBands
-        bands = ObjectBands(ctx, Ny, int(crop_pos[:, 0].min()), int(crop_pos[:, 0].max()) + N, dev)
+        bands = ObjectBands(ctx, Ny, dev)
+        bands.set_rows(int(crop_pos[:, 0].min()), int(crop_pos[:, 0].max()) + N)
         objs = [t["obja"], t["objp"]]
     # bytes each rank sends per step in the exchange (ring all-reduce / all-gather: (W-1)/W per pass)
     if bands is None:

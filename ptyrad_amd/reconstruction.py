@@ -253,21 +253,26 @@ class ObjectBands:
     pixel that at most two ranks touch gets the same sum as the all-reduce bit for bit (a + b);
     with more contributors only the fp32 summation order differs."""
 
-    def __init__(self, ctx, Ny, lo, hi, device):
-        self.ctx, self.Ny = ctx, int(Ny)
+    def __init__(self, ctx, Ny, device):
+        self.ctx, self.Ny, self.device = ctx, int(Ny), device
         W = ctx.world
         self.R = -(-self.Ny // W)
-        rng_ = torch.tensor([int(lo), int(hi)], dtype=torch.int64, device=device)
+        self.b0 = min(self.Ny, ctx.rank * self.R)
+        self.b1 = min(self.Ny, (ctx.rank + 1) * self.R)
+        self.ranges = [(0, self.Ny)] * W
+        self.opt = None
+        self.views = {}
+
+    def set_rows(self, lo, hi):
+        """Every rank's touched rows [lo, hi), exchanged (one small all-gather; every rank calls it)."""
+        W = self.ctx.world
+        rng_ = torch.tensor([int(lo), int(hi)], dtype=torch.int64, device=self.device)
         allr = [torch.zeros_like(rng_) for _ in range(W)]
         if W > 1:
-            dist.all_gather(allr, rng_, group=ctx.group)
+            dist.all_gather(allr, rng_, group=self.ctx.group)
         else:
             allr = [rng_]
         self.ranges = [(int(r[0]), int(r[1])) for r in allr]
-        self.b0 = min(self.Ny, ctx.rank * self.R)
-        self.b1 = min(self.Ny, (ctx.rank + 1) * self.R)
-        self.opt = None
-        self.views = {}
 
     def band(self, j):
         return min(self.Ny, j * self.R), min(self.Ny, (j + 1) * self.R)
@@ -307,13 +312,16 @@ class ObjectBands:
             for a, b, buf in bufs:                 # in rank order
                 g[:, :, a:b] += buf
 
-    def step(self, optimizer, params):
+    def step(self, optimizer, params, candidates=None):
         """Step `optimizer`'s class on the owned rows of the object params (their .grad holds the
-        reduced gradient there); the params' .grad is cleared so `optimizer` skips them."""
+        reduced gradient there).  The band optimizer holds a view for every object tensor of
+        `optimizer` (`candidates`), so a tensor frozen when it was built still gets its band later;
+        a view whose tensor has no .grad this step is skipped, as Adam skips a frozen tensor."""
         if self.opt is None:
+            cand = candidates if candidates is not None else params
             groups = []
             for gr in optimizer.param_groups:
-                mine = [p for p in gr["params"] if any(p is q for q in params)]
+                mine = [p for p in gr["params"] if any(p is q for q in cand)]
                 if mine:
                     views = []
                     for p in mine:
@@ -322,6 +330,8 @@ class ObjectBands:
                         views.append(v)
                     groups.append({**{k: v for k, v in gr.items() if k != "params"}, "params": views})
             self.opt = type(optimizer)(groups, **optimizer.defaults) if groups else None
+        for v in self.views.values():
+            v.grad = None
         for p in params:
             v = self.views.get(id(p))
             if v is not None:
@@ -390,10 +400,13 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     objs = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in live)]
     band = ctx.band_exchange and ctx._collective() and bool(objs)
     if band:
-        if ctx.bands is None:     # batches are fixed for the run: the touched rows are too
-            N = int(model.opt_probe.shape[1])
-            lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok), N)
-            ctx.bands = ObjectBands(ctx, model.opt_obja.shape[2], lo, hi, dev)
+        if ctx.bands is None:
+            ctx.bands = ObjectBands(ctx, model.opt_obja.shape[2], dev)
+        # the rows this rank's windows reach this iteration (recomputed: the batches may change)
+        lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok),
+                              int(model.opt_probe.shape[1]))
+        ctx.bands.set_rows(lo, hi)
+        obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
         live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
     rows = []
     for g0 in range(0, len(batches), ga):
@@ -429,7 +442,7 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             optimizer.step()
             for p, g in zip(objs, saved):
                 p.grad = g
-            ctx.bands.step(optimizer, objs)
+            ctx.bands.step(optimizer, objs, obj_all)
             ctx.bands.gather(objs)
         else:
             ctx.allreduce(flat)
@@ -462,9 +475,20 @@ def recon_loop(model, optimizer, loss_fn, constraint_fn, batches, NITER, grad_ac
 
 
 def create_optimizer(optimizer_params, optimizable_params, verbose=True):
-    """torch.optim.<name>(param groups with per-tensor lr, **configs) (reconstruction.py:285-368)."""
+    """torch.optim.<name>(param groups with per-tensor lr, **configs) (reconstruction.py:285-368).
+
+    One deliberate difference: Adam / AdamW on device parameters default to torch's fused kernel
+    (``fused=True``) unless the configs choose ``fused`` or ``foreach``.  The update is the same
+    formula; the default foreach path issues about ten kernels per parameter group from Python,
+    which at the reference's default cadence (grad_accumulation = 1, one step per 32-pattern
+    mini-batch) costs more than the engine call (tools/recon_overhead.py)."""
     name = optimizer_params.get("name", "Adam")
     cls = getattr(torch.optim, name, None)
     if cls is None:
         raise ValueError(f"Optimizer '{name}' is not supported.")
-    return cls(optimizable_params, **(optimizer_params.get("configs") or {}))
+    configs = dict(optimizer_params.get("configs") or {})
+    params = [p for g in optimizable_params for p in (g["params"] if isinstance(g, dict) else [g])]
+    if (name in ("Adam", "AdamW") and "fused" not in configs and "foreach" not in configs and params and
+            all(p.is_cuda and p.is_floating_point() for p in params)):
+        configs["fused"] = True
+    return cls(optimizable_params, **configs)

@@ -148,18 +148,21 @@ def test_three_ranks_ga1_split_batches_reproduce_single_rank(tmp_path):
         assert float(np.sqrt(np.mean((r[0][k].astype(np.float64) - ref) ** 2))) < 1e-5
 
 
-@pytest.mark.parametrize("name", ["traj_n32_p2_ga2", "traj_n64_b4_ga1"])
-def test_band_exchange_equals_flat_allreduce(tmp_path, name):
+@pytest.mark.parametrize("name,start", [("traj_n32_p2_ga2", None), ("traj_n64_b4_ga1", None),
+                                         ("traj_n32_p2_ga2", {"objp": 2, "probe": 2})],
+                         ids=["ga2", "ga1_split", "ga2_objp_frozen_first"])
+def test_band_exchange_equals_flat_allreduce(tmp_path, name, start):
     """Object gradients by row band (each rank sends only its touched rows to their owners,
     owners run Adam on their band, bands all-gathered) vs the flat all-reduce, 2 gloo ranks with
     rank-local DPs: bitwise-identical final parameters (every pixel has at most two contributors,
-    and a + b = b + a), for whole-batch (ga 2) and split (ga 1) groups."""
+    and a + b = b + a), for whole-batch (ga 2) and split (ga 1) groups, and with the object phase
+    frozen in the first iteration (its band optimizer state must start in iteration 2)."""
     path = [p for p in TRAJ if name in p][0]
     outs = {}
     for band in (False, True):
         out = str(tmp_path / f"b{int(band)}.npz")
-        mp.start_processes(dist_worker, args=(2, free_port(), path, out, {"shard": True, "band": band}), nprocs=2,
-                           start_method="spawn")
+        kw = {"shard": True, "band": band, **({"start_iter": start} if start else {})}
+        mp.start_processes(dist_worker, args=(2, free_port(), path, out, kw), nprocs=2, start_method="spawn")
         outs[band] = (np.load(out), np.load(out.replace(".npz", "_r1.npz")))
     for k in ("obja", "objp", "probe", "shifts"):
         assert np.array_equal(outs[True][0][k], outs[True][1][k]), f"band replicas diverged in {k}"
