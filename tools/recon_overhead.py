@@ -82,6 +82,10 @@ def main():
     off_dev = [torch.as_tensor(batch_offsets([b]), device=dev) for b in batches[:a.steps]]
     out = {}
     out["engine_dev"] = timed(lambda i: plan.forward_loss_grad(t, idx_dev[i], off_dev[i], cfg, grads), a.steps)
+    plan.profile_begin()      # per-kernel GPU time of a 32-pattern call (HIP events)
+    for i in range(64):
+        plan.forward_loss_grad(t, idx_dev[i], off_dev[i], cfg, grads)
+    out["engine_kernels_ms_per_call"] = {k: round(v[1] / 64, 4) for k, v in plan.profile_end().items()}
     out["engine_host"] = timed(lambda i: plan.forward_loss_grad(t, batches[i], batch_offsets([batches[i]]), cfg,
                                                                 grads), a.steps)
     for p in (model.opt_obja, model.opt_objp, model.opt_probe, model.opt_probe_pos_shifts):
