@@ -54,8 +54,10 @@ def to_np(g):
 
 
 # geometry -> engine that serves it: k_fused3, k_fused3ms, the N = 256 stripe engine, the two-pass engine
-GEOMS = {"fused3": (128, 1, 1, 1), "fused3ms": (128, 1, 1, 3), "stripe": (256, 2, 1, 1), "two_pass": (64, 2, 2, 2)}
-ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "stripe": "k_s3", "two_pass": "k_forward"}
+GEOMS = {"fused3": (128, 1, 1, 1), "fused3ms": (128, 1, 1, 3), "stripe": (256, 2, 1, 1),
+         "stripe_o2": (256, 2, 2, 1), "two_pass": (64, 2, 2, 2)}
+ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "stripe": "k_s3", "stripe_o2": "k_obj_gather",
+                 "two_pass": "k_forward"}
 
 
 @pytest.mark.parametrize("world", [2, 3])
