@@ -374,12 +374,19 @@ def touched_rows(model, batches, N):
 
 
 # ------------------------------------------------------------------ the reference step
+GRAPH_MIN_STEPS = 4   # graph replay pays for its capture from this many optimizer steps per iteration
+
+
 def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint_fn, niter, verbose=True,
-               acc=None, dist_ctx=None):
+               acc=None, dist_ctx=None, graphs=None):
     """One iteration over ``batches`` (reconstruction.py:658-781, non-LBFGS branch).
 
     Optimizer steps happen every ``grad_accumulation`` batches and after the last one; each step's
     group of batches runs as one fused engine call (sharded over ranks when ``dist_ctx`` is given).
+
+    graphs: replay the optimizer steps from hipGraphs (``ptyrad_amd.stepgraph``; bitwise the same
+    trajectory).  None = when eligible and the iteration has ≥ GRAPH_MIN_STEPS steps; False = never;
+    True = required (raises with the reason when not eligible).
     """
     if acc is not None:
         raise NotImplementedError("accelerate is replaced by DistContext (RCCL) on this path")
@@ -409,7 +416,22 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
         live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
     rows = []
-    for g0 in range(0, len(batches), ga):
+    use_graphs = False
+    if graphs is not False and not band:
+        from .stepgraph import StepGraphs, ineligible_reason
+        why = ineligible_reason(model, optimizer, loss_fn, ctx, batches, ga)
+        if graphs and why:
+            raise RuntimeError(f"recon_step(graphs=True): {why}")
+        use_graphs = why is None and (graphs or -(-len(batches) // ga) >= GRAPH_MIN_STEPS) and bool(live)
+    if use_graphs:
+        sg = getattr(model, "_step_graphs", None)
+        if sg is None:
+            sg = model._step_graphs = StepGraphs()
+        flat = ctx.grad_views(live)
+        rows.append(sg.run(model, optimizer, loss_fn, batches, ga, live, flat))
+        optimizer.zero_grad(set_to_none=True)
+        model.clear_cache()
+    for g0 in (range(0, len(batches), ga) if not use_graphs else ()):
         group = batches[g0:g0 + ga]
         flat = ctx.grad_views(live)
         if ctx.splits(group) and split_ok:

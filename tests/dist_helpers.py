@@ -183,7 +183,7 @@ def dist_worker(rank, world, port, path, out_path, kw=None):
         torch.distributed.destroy_process_group()
 
 
-def gpu_recon(z, dist_ctx=None, shard=False, niter=None, ret_all=False):
+def gpu_recon(z, dist_ctx=None, shard=False, niter=None, ret_all=False, graphs=None):
     """The trajectory fixture through PtychoHIP + CombinedLoss + recon_step on cuda:0 (the HIP
     engine); with ``shard`` the model holds only DistContext.local_indices rows of the DPs."""
     from ptyrad_amd.losses import CombinedLoss
@@ -210,7 +210,7 @@ def gpu_recon(z, dist_ctx=None, shard=False, niter=None, ret_all=False):
     last = None
     for it in range(1, (int(z["niter"]) if niter is None else niter) + 1):
         last = recon_step(batches, int(z["grad_accumulation"]), model, opt, loss_fn, None, it, verbose=False,
-                          dist_ctx=ctx)
+                          dist_ctx=ctx, graphs=graphs)
     if ret_all:
         return model, opt, loss_fn, batches, last
     return model

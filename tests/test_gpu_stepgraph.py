@@ -1,0 +1,126 @@
+"""recon_step with its optimizer steps replayed from hipGraphs (ptyrad_amd/stepgraph.py) on MI355X.
+
+The graph replays the eager step's kernels with the same arguments, so on the deterministic
+register engine (k_fused3: slots + gather, fixed-order reductions) the trajectory is BITWISE the
+eager one; on the general engine (f32 object atomics) it agrees to fp32 summation order.  Both
+match the reference's own trajectories (tests/golden/traj_*.npz, made by running PtyRAD).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+from tests.test_oracle_golden import rel
+
+pytestmark = pytest.mark.gpu
+
+
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _params(model):
+    return {k: getattr(model, k).detach().cpu().numpy() for k in
+            ("opt_obja", "opt_objp", "opt_probe", "opt_probe_pos_shifts")}
+
+
+@pytest.mark.parametrize("name,bitwise", [("traj_c1_n128", True), ("traj_n64_b4_ga1", False),
+                                          ("traj_n32_p2_ga2", False)])
+def test_graph_replayed_trajectory_equals_eager_and_reference(name, bitwise):
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    eager, _, _, _, last_e = gpu_recon(z, graphs=False, ret_all=True)
+    graph, _, _, _, last_g = gpu_recon(z, graphs=True, ret_all=True)
+    sg = graph._step_graphs
+    assert sg.captures >= 1 and sg.replays >= 1, (sg.captures, sg.replays, sg.eager)
+    pe, pg = _params(eager), _params(graph)
+    for k in pe:
+        if bitwise:
+            assert np.array_equal(pe[k], pg[k]), k
+        else:
+            assert rel(pg[k], pe[k]) < 1e-5, k
+    for k in last_e:
+        np.testing.assert_allclose(last_g[k], last_e[k], rtol=1e-5, atol=1e-7)
+    for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
+        got = pg[k].astype(np.float64)
+        assert float(np.sqrt(np.mean((got - ref) ** 2))) < 1e-5, k
+
+
+def test_graphs_c2_like_ragged_batches_frozen_probe_then_live():
+    """32×32 raster at N = 128 (k_fused3), 31 mini-batches of 33 / 34 (two step shapes), the probe
+    frozen in iteration 1 (start_iter 2) and trainable from iteration 2 (a new live set: fresh Adam
+    state, a new capture).  Three iterations, graphs vs eager: bitwise equal."""
+    need_gpu()
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    from ptyrad_amd.reconstruction import create_optimizer, recon_step
+    dev = torch.device("cuda", 0)
+    N, S = 128, 32
+    scan = syn.raster_scan(S, S, N, seed=0)
+    n = S * S
+    Ny, Nx = scan.obj_shape
+    rng = np.random.default_rng(11)
+    meas = rng.random((n, N, N)).astype(np.float32)
+    lp = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+          "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+          "loss_pacbed": {"state": False}, "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
+          "loss_simlar": {"state": False}}
+    batches = np.array_split(np.random.default_rng(3).permutation(n), 31)
+    starts = {"obja": 1, "objp": 1, "probe": 2, "probe_pos_shifts": 1, "obj_tilts": None, "slice_thickness": None}
+    lrs = {"obja": 5e-4, "objp": 5e-4, "probe": 1e-4, "probe_pos_shifts": 1e-4, "obj_tilts": 0.0,
+           "slice_thickness": 0.0}
+
+    def run(graphs):
+        iv = {"obja": np.ones((1, 1, Ny, Nx), np.float32),
+              "objp": (1e-3 * np.random.default_rng(5).random((1, 1, Ny, Nx))).astype(np.float32), "obj": None,
+              "probe": (syn.stem_probe(N) * np.float32(60.0))[None], "probe_pos_shifts": scan.shifts,
+              "omode_occu": np.ones(1, np.float32), "H": syn.fresnel_propagator(N, syn.DX_ANG, 2.0),
+              "measurements": meas, "crop_pos": scan.crop_pos, "N_scan_slow": S, "N_scan_fast": S,
+              "slice_thickness": 2.0, "dx": syn.DX_ANG, "dk": 1.0 / (N * syn.DX_ANG),
+              "lambd": syn.electron_wavelength(syn.KV), "obj_tilts": np.zeros((1, 2), np.float32)}
+        mp = {"detector_blur_std": None, "obj_preblur_std": None,
+              "update_params": {k: {"start_iter": starts[k], "lr": v} for k, v in lrs.items()},
+              "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
+        model = PtychoHIP(iv, mp, device=dev, verbose=False)
+        opt = create_optimizer(model.optimizer_params, model.optimizable_params)
+        loss_fn = CombinedLoss(lp, device=dev)
+        hist = [recon_step(batches, 1, model, opt, loss_fn, None, it, verbose=False, graphs=graphs)
+                for it in (1, 2, 3)]
+        return model, opt, hist
+
+    me, oe, he = run(False)
+    mg, og, hg = run(True)
+    sg = mg._step_graphs
+    assert sg.captures >= 3 and sg.replays > 80, (sg.captures, sg.replays, sg.eager)   # 2 shapes × 2 live sets
+    pe, pg = _params(me), _params(mg)
+    for k in pe:
+        assert np.array_equal(pe[k], pg[k]), k
+    assert not np.array_equal(pe["opt_probe"], (syn.stem_probe(N) * np.float32(60.0))[None].view(np.float32)
+                              .reshape(pe["opt_probe"].shape))
+    for a, b in zip(he, hg):
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    # optimizer state (step counts, moments) identical too: a checkpoint taken after either is the same
+    for p_e, p_g in zip([p for g in oe.param_groups for p in g["params"]],
+                        [p for g in og.param_groups for p in g["params"]]):
+        se, sgs = oe.state.get(p_e, {}), og.state.get(p_g, {})
+        assert se.keys() == sgs.keys()
+        for k in se:
+            assert torch.equal(se[k].cpu(), sgs[k].cpu()), k
+    assert all(not g["capturable"] for g in og.param_groups)
+
+
+def test_graphs_refused_with_reason_when_ineligible():
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    from ptyrad_amd.reconstruction import recon_step
+    model, opt, loss_fn, batches, _ = gpu_recon(z, niter=0, ret_all=True)
+    sgd = torch.optim.SGD(model.optimizable_params, lr=1e-4)
+    with pytest.raises(RuntimeError, match="fused Adam"):
+        recon_step(batches, 1, model, sgd, loss_fn, None, 1, verbose=False, graphs=True)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--scan", type=int, default=256)
     ap.add_argument("--ga", type=int, nargs="+", default=[1, 16, 2048])
     ap.add_argument("--iters", type=int, default=1)
+    ap.add_argument("--graphs", choices=["auto", "on", "off"], default="auto",
+                    help="recon_step(graphs=...): hipGraph-replayed optimizer steps")
     a = ap.parse_args()
     from ptyrad_amd import synthetic as syn
     from ptyrad_amd.losses import CombinedLoss
@@ -64,15 +66,18 @@ def main():
         opt = create_optimizer(model.optimizer_params, model.optimizable_params)
         loss_fn = CombinedLoss(lp, device=dev)
         batches = make_batches(np.arange(n), scan.crop_pos, 32, mode="random", rng=np.random.default_rng(3))
-        recon_step(batches, ga, model, opt, loss_fn, None, 1, verbose=False)          # warm-up iteration
+        graphs = {"auto": None, "on": True, "off": False}[a.graphs]
+        recon_step(batches, ga, model, opt, loss_fn, None, 1, verbose=False, graphs=graphs)   # warm-up iteration
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for it in range(a.iters):
-            recon_step(batches, ga, model, opt, loss_fn, None, 2 + it, verbose=False)
+            recon_step(batches, ga, model, opt, loss_fn, None, 2 + it, verbose=False, graphs=graphs)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
-        print(json.dumps({"ga": ga, "mini_batches": len(batches), "optimizer_steps": steps,
+        sg = getattr(model, "_step_graphs", None)
+        print(json.dumps({"ga": ga, "graphs": a.graphs, "replays": sg.replays if sg else 0,
+                          "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
                           "loss": float(model.loss_iters[-1][1])}), flush=True)
