@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 202
+#define PTYX_ABI_VERSION 203
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -316,6 +316,31 @@ int ptyx_meas_stats(void *stream, const float *raw, int64_t n, int32_t H, int32_
 /* dst (n,Ho,Wo) f32 (or IEEE half with dst_f16) = _process_meas of raw, given the complete stats. */
 int ptyx_meas_finish(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
                      const double *stats, void *ws, void *dst, int32_t dst_f16);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer-step bookkeeping for graph-replayed recon_step (reconstruction.py:658-781 at
+ * grad_accumulation = 1: one step per mini-batch).  A captured step reads its mini-batch through
+ * a device step counter, so one hipGraph serves every step of the same shape.
+ *   ptyx_step_select: idx_out[i] = idx_all[istart[*cnt] + i] for i < n, and zeroes grad[0..grad_n)
+ *                     (the flat gradient buffer every trainable parameter's .grad views).
+ *   ptyx_step_store:  terms_all[rstart[*cnt] + b][k] = terms[b][k] (b < nb, k < 5), then ++*cnt
+ *                     (one workgroup: every thread reads *cnt before it is advanced).
+ * ------------------------------------------------------------------------------------------- */
+int ptyx_step_select(void *stream, const int32_t *idx_all, const int64_t *istart, const int64_t *cnt, int32_t n,
+                     int32_t *idx_out, float *grad, int64_t grad_n);
+int ptyx_step_store(void *stream, const float *terms, int32_t nb, const int64_t *rstart, int64_t *cnt,
+                    float *terms_all);
+
+/* The optimizer step PtyRAD takes after each accumulated gradient (reconstruction.py:758-760,
+ * torch.optim.Adam / AdamW, the schema default optimizer params/recon_params.py) for n tensors in
+ * one grid-filling launch (ptyrad_amd.optim): per tensor i (host arrays of device pointers, read
+ * during the call only) params[i] -= Adam update from grads[i], exp_avgs[i], exp_avg_sqs[i], the
+ * step count *steps[i] (f32 on the device, ALREADY incremented for this step) and lrs[i];
+ * numels[i] elements.  flags: 1 = decoupled weight decay (AdamW), 2 = maximize.  torch's
+ * single-tensor arithmetic (fp32 elements, fp64 bias corrections). */
+int ptyx_adam_step(void *stream, int32_t n, float *const *params, const float *const *grads, float *const *exp_avgs,
+                   float *const *exp_avg_sqs, const float *const *steps, const int64_t *numels, const double *lrs,
+                   double beta1, double beta2, double eps, double weight_decay, int32_t flags);
 
 /* Patterns one ptyx_forward_loss_grad call may hold and still run on the register-resident
  * engines (k_fused3 / k_fused3ms: slot capacity); larger calls take the general engine.

@@ -27,7 +27,7 @@ ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "lib", "libptyx.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_constraints.hip"),
-           os.path.join(HERE, "ptyx_ingest.hip")]
+           os.path.join(HERE, "ptyx_ingest.hip"), os.path.join(HERE, "ptyx_optim.hip")]
 HEADERS = glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
 DEPS = SOURCES + HEADERS
 ARCH = os.environ.get("PTYX_ARCH", "gfx950")

@@ -264,6 +264,52 @@ __global__ __launch_bounds__(256) void k_bbox(const int* idx, int n, const int* 
   }
 }
 
+// Small calls (≤ kSmallCall patterns, e.g. one 32-pattern mini-batch per optimizer step at the
+// reference's default grad_accumulation = 1): the bounding box in ONE workgroup (no init launch,
+// no atomics), which also clears the call's segment table (no memset launch).
+constexpr int kSmallCall = 256;
+__global__ __launch_bounds__(256) void k_bbox_small(const int* idx, int n, const int* crop, int n_scans, int Ny,
+                                                    int Nx, int* bbox, int win, int* segbid, int nseg) {
+  __shared__ int red[4][4];
+  int a = 0x7fffffff, b = -0x7fffffff, c = 0x7fffffff, d = -0x7fffffff;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int s = min(max(idx[j], 0), n_scans - 1);
+    const int cy = min(max(crop[2 * s], 0), Ny - win), cx = min(max(crop[2 * s + 1], 0), Nx - win);
+    a = min(a, cy);
+    b = max(b, cy);
+    c = min(c, cx);
+    d = max(d, cx);
+  }
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) segbid[i] = -1;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a = min(a, __shfl_xor(a, o, 64));
+    b = max(b, __shfl_xor(b, o, 64));
+    c = min(c, __shfl_xor(c, o, 64));
+    d = max(d, __shfl_xor(d, o, 64));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[wv][0] = a;
+    red[wv][1] = b;
+    red[wv][2] = c;
+    red[wv][3] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      a = min(a, red[w][0]);
+      b = max(b, red[w][1]);
+      c = min(c, red[w][2]);
+      d = max(d, red[w][3]);
+    }
+    bbox[0] = a;
+    bbox[1] = b;
+    bbox[2] = c;
+    bbox[3] = d;
+  }
+}
+
 // pattern → (mini-batch, clamped window origin) and, with pref (the summed-area table of
 // k_pref_cols1/2), the loss_sparse window sum Σ_{window} |φ|^n into psums[kSumBase]: four fp64
 // lookups per slice, lane z per slice, fixed-order wave sum.  bbox: the table's first row is
@@ -301,6 +347,54 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) psums[(size_t)j * kNSum + kSumBase] = (float)acc;
+}
+
+// Small calls (PTYX_PREP_CALL, ≤ kSmallCall patterns): k_pattern_table3's entries with the
+// loss_sparse window sum Σ_window |φ|^n read straight from objp — no summed-area table to build.
+// One workgroup per pattern: wave w sums rows w, w + 4, … of every slice, a lane two columns, 8
+// rows per round (16 loads in flight); fp64 lane sums, fixed-order wave reduction, waves added in
+// order through LDS (deterministic).
+__global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, int n, const int* boff, int n_batches,
+                                                              const int* crop, int n_scans, int Ny, int Nx, int* bid,
+                                                              int2* geo, const float* objp, int sparse_n, float* psums,
+                                                              int Nz) {
+  __shared__ double s_w[4];
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n_batches;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (boff[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    bid[j] = lo;
+    geo[j] = make_int2(cy, cx);
+  }
+  double acc = 0;
+  for (int z = 0; z < Nz; ++z) {
+    const float* ph = objp + ((size_t)z * Ny + cy) * Nx + cx + lane;
+    for (int r0 = wave; r0 < kN; r0 += 32) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[2 * k] = ph[(size_t)(r0 + 4 * k) * Nx];
+        v[2 * k + 1] = ph[(size_t)(r0 + 4 * k) * Nx + 64];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float a = fabsf(v[k]);
+        acc += sparse_n == 1 ? (double)a : (double)powq(a, (float)sparse_n);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) s_w[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) psums[(size_t)j * kNSum + kSumBase] = (float)(((s_w[0] + s_w[1]) + s_w[2]) + s_w[3]);
 }
 
 // Far-field loss at one point, branch-free.  Returns u = ∂ℓ/∂I per unit mini-batch coefficient

@@ -279,9 +279,14 @@ struct FinArgs {
   const double* bsums_in = nullptr;
 };
 
-__global__ void k_finalize(FinArgs f) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= f.n_batches) return;
+// One wave per mini-batch: lane l sums patterns b0 + l, b0 + l + 64, … (fp64), then a fixed
+// xor-tree over the lanes (deterministic, independent of how a call is split into pieces); lane 0
+// computes the terms and coefficients, every lane writes its share of the per-pattern coefficients.
+constexpr int kFinWaves = 2;   // mini-batches per 128-thread workgroup
+__global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
+  const int m = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= f.n_batches) return;   // (wave-uniform)
   const int b0 = f.boff[m], b1 = f.boff[m + 1];
   double B = (double)(b1 - b0);
   double S1 = 0, M1 = 0, S2 = 0, M2 = 0, sp[kMaxModesO] = {0};
@@ -290,7 +295,7 @@ __global__ void k_finalize(FinArgs f) {
     B = bs[0]; S1 = bs[1]; M1 = bs[2]; S2 = bs[3]; M2 = bs[4];
     for (int o = 0; o < f.O; ++o) sp[o] = bs[5 + o];
   } else {
-    for (int t = b0; t < b1; ++t) {
+    for (int t = b0 + lane; t < b1; t += 64) {
       const float* ps = f.psums + (size_t)t * kNSum;
       S1 += ps[0];
       M1 += ps[1];
@@ -298,49 +303,63 @@ __global__ void k_finalize(FinArgs f) {
       M2 += ps[3];
       for (int o = 0; o < f.O; ++o) sp[o] += ps[kSumBase + o];
     }
+#pragma unroll
+    for (int x = 32; x >= 1; x >>= 1) {
+      S1 += __shfl_xor(S1, x, 64);
+      M1 += __shfl_xor(M1, x, 64);
+      S2 += __shfl_xor(S2, x, 64);
+      M2 += __shfl_xor(M2, x, 64);
+      for (int o = 0; o < f.O; ++o) sp[o] += __shfl_xor(sp[o], x, 64);
+    }
   }
   if (f.bsums_out) {
-    double* bs = f.bsums_out + (size_t)m * kNBatchSum;
-    bs[0] = B; bs[1] = S1; bs[2] = M1; bs[3] = S2; bs[4] = M2;
-    for (int o = 0; o < kMaxModesO; ++o) bs[5 + o] = o < f.O ? sp[o] : 0.0;
+    if (lane == 0) {
+      double* bs = f.bsums_out + (size_t)m * kNBatchSum;
+      bs[0] = B; bs[1] = S1; bs[2] = M1; bs[3] = S2; bs[4] = M2;
+      for (int o = 0; o < kMaxModesO; ++o) bs[5 + o] = o < f.O ? sp[o] : 0.0;
+    }
     return;
   }
-  const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
-  float terms[5] = {0, 0, 0, 0, 0};
-  float c1 = 0.f, c2 = 0.f;
-  if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
-    const double mu = M1 / K, rmse = sqrt(S1 / K);
-    terms[0] = (float)(f.w1 * rmse / mu);
-    c1 = rmse > 0 ? (float)(f.w1 / (mu * K * rmse) * f.grad_scale) : 0.f;
-  }
-  if (f.pois_on && B > 0) {  // -w·mean(M^q log(I^q+eps) - I^q) / mean(M^q)   losses.py:70-72
-    const double mu = M2 / K;
-    terms[1] = (float)(-f.w2 * (S2 / K) / mu);
-    c2 = (float)(-f.w2 / (mu * K) * f.grad_scale);
-  }
-  float* cf = f.coef + (size_t)m * kNCoef;
-  cf[0] = c1;
-  cf[1] = c2;
-  if (f.sparse_on && B > 0) {  // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
-    const double cnt = B * f.Nz * f.N * f.N;
-    double t = 0;
-    for (int o = 0; o < f.O; ++o) {
-      const double mo = sp[o] / cnt;
-      const double inv = 1.0 / f.sparse_n;
-      t += f.occu[o] * pow(mo, inv);
-      const double dm = (f.sparse_n == 1) ? 1.0 : (mo > 0 ? pow(mo, inv - 1.0) : 0.0);
-      cf[2 + o] = (float)(f.ws * f.occu[o] * dm / cnt * f.grad_scale);
+  float cf[2 + kMaxModesO] = {0};
+  if (lane == 0) {
+    const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
+    float terms[5] = {0, 0, 0, 0, 0};
+    if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
+      const double mu = M1 / K, rmse = sqrt(S1 / K);
+      terms[0] = (float)(f.w1 * rmse / mu);
+      cf[0] = rmse > 0 ? (float)(f.w1 / (mu * K * rmse) * f.grad_scale) : 0.f;
     }
-    terms[3] = (float)(f.ws * t);
-  } else {
-    for (int o = 0; o < f.O; ++o) cf[2 + o] = 0.f;
+    if (f.pois_on && B > 0) {  // -w·mean(M^q log(I^q+eps) - I^q) / mean(M^q)   losses.py:70-72
+      const double mu = M2 / K;
+      terms[1] = (float)(-f.w2 * (S2 / K) / mu);
+      cf[1] = (float)(-f.w2 / (mu * K) * f.grad_scale);
+    }
+    if (f.sparse_on && B > 0) {  // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
+      const double cnt = B * f.Nz * f.N * f.N;
+      double t = 0;
+      for (int o = 0; o < f.O; ++o) {
+        const double mo = sp[o] / cnt;
+        const double inv = 1.0 / f.sparse_n;
+        t += f.occu[o] * pow(mo, inv);
+        const double dm = (f.sparse_n == 1) ? 1.0 : (mo > 0 ? pow(mo, inv - 1.0) : 0.0);
+        cf[2 + o] = (float)(f.ws * f.occu[o] * dm / cnt * f.grad_scale);
+      }
+      terms[3] = (float)(f.ws * t);
+    }
+    float* cfo = f.coef + (size_t)m * kNCoef;
+    cfo[0] = cf[0];
+    cfo[1] = cf[1];
+    for (int o = 0; o < f.O; ++o) cfo[2 + o] = cf[2 + o];
+    if (f.loss_terms)
+      for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
   }
-  if (f.loss_terms)
-    for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
-  if (f.pcoef) {
-    for (int o = 0; o < f.pcoef_O; ++o) {
-      const float2 pc = make_float2(cf[f.ci], cf[2 + o]);
-      for (int t = b0; t < b1; ++t) f.pcoef[o * f.pcoef_stride + t] = pc;
+  if (f.pcoef) {   // the coefficients of lane 0, written for every pattern of the mini-batch
+    const float c = __shfl(f.ci == 0 ? cf[0] : cf[1], 0, 64);
+#pragma unroll
+    for (int o = 0; o < kMaxModesO; ++o) {
+      if (o >= f.pcoef_O) break;
+      const float2 pc = make_float2(c, __shfl(cf[2 + o], 0, 64));
+      for (int t = b0 + lane; t < b1; t += 64) f.pcoef[o * f.pcoef_stride + t] = pc;
     }
   }
 }
@@ -1208,8 +1227,18 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk, 1.0f / N2);   // H/N²
   }
-  if (pl->bbox) {   // rows / tiles outside the call's windows are skipped (a rank's shard of a
-                    // multi-GPU scan touches only its band of the replicated object)
+  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int nseg = a.n_batches + G;
+  // small calls (one mini-batch per optimizer step): one-workgroup bbox that also clears the
+  // segment table, and direct loss_sparse window sums instead of the summed-area table
+  const bool small = a.n_idx <= f3::kSmallCall && pl->bbox;
+  const bool direct_sums = sparse && small && cfg->prep == PTYX_PREP_CALL;
+  if (small) {
+    ProfScope ps(pl, kKTable, st);
+    hipLaunchKernelGGL(f3::k_bbox_small, dim3(1), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans, d.Ny, d.Nx,
+                       pl->bbox, 128, pl->segbid, nseg);
+  } else if (pl->bbox) {   // rows / tiles outside the call's windows are skipped (a rank's shard of a
+                           // multi-GPU scan touches only its band of the replicated object)
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
     hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (a.n_idx + 255) / 256))), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans,
@@ -1218,9 +1247,9 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   if (!reuse) {
     ProfScope ps(pl, kKObjPrep, st);   // (Nz, Ny) rows: every slice's O and |φ|^n prefix sums
     hipLaunchKernelGGL(f3::k_obj_prep, dim3(d.Ny * Nz), dim3(256), 0, st, a.obja, a.objp, d.Ny * Nz, d.Nx, pl->oc,
-                       sparse ? pl->pref : nullptr, cfg->sparse_n,
+                       sparse && !direct_sums ? pl->pref : nullptr, cfg->sparse_n,
                        cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox, d.Ny, 128);
-    if (sparse) {   // row prefix sums → summed-area table (k_pattern_table3's window sums)
+    if (sparse && !direct_sums) {   // row prefix sums → summed-area table (k_pattern_table3's window sums)
       const int* bb = cfg->prep == PTYX_PREP_FULL ? nullptr : pl->bbox;
       const dim3 gp((d.Nx + 1 + 255) / 256, (d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk, Nz);
       hipLaunchKernelGGL(f3::k_pref_cols1, gp, dim3(256), 0, st, pl->pref, pl->preftot, d.Ny, d.Nx, bb, 128);
@@ -1230,16 +1259,21 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   {
     // (the table's first row: the bbox of the call that prepared it, PTYX_PREP_CALL only)
     ProfScope ps(pl, kKTable, st);
-    hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
-                       a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo,
-                       sparse ? pl->pref : nullptr, pl->psums, Nz, cfg->prep == PTYX_PREP_CALL ? pl->bbox : nullptr);
+    if (direct_sums)
+      hipLaunchKernelGGL(f3::k_pattern_table_direct, dim3(a.n_idx), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
+                         a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.objp, cfg->sparse_n,
+                         pl->psums, Nz);
+    else
+      hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
+                         a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, sparse ? pl->pref : nullptr,
+                         pl->psums, Nz, cfg->prep == PTYX_PREP_CALL ? pl->bbox : nullptr);
   }
   const bool single = cfg->single_on != 0;
   const int ci = single ? 0 : 1;
-  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
-  const int nseg = a.n_batches + G;
-  hipError_t e = hipMemsetAsync(pl->segbid, 0xFF, sizeof(int) * (size_t)nseg, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(segbid)");
+  if (!small) {
+    hipError_t e = hipMemsetAsync(pl->segbid, 0xFF, sizeof(int) * (size_t)nseg, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(segbid)");
+  }
   f3::F3Args f{};
   f.n_idx = a.n_idx; f.n_scans = a.n_scans; f.Ny = d.Ny; f.Nx = d.Nx;
   f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.shifts = a.shifts;
@@ -1309,26 +1343,28 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
-    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
   }
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
-  if (gz.d_obja || gz.d_objp) {
+  // small calls: every tile scans the call's few patterns directly (no binning launches)
+  const bool bins = a.n_idx > f3::kSmallCall;
+  if ((gz.d_obja || gz.d_objp) && bins) {
     // candidate bins of the gather: the patterns by object tile of their window origin
-    {
-      ProfScope ps(pl, kKTable, st);
-      const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
-      hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
-      if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
-      const dim3 gn((a.n_idx + 255) / 256);
-      hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
-      hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
-      hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
-      hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
-    }
+    ProfScope ps(pl, kKTable, st);
+    const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
+    hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
+    if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+    const dim3 gn((a.n_idx + 255) / 256);
+    hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
+    hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
+    hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
+  }
+  if (gz.d_obja || gz.d_objp) {
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
-    g.boff = pl->boff;
-    g.blist = pl->blist;
+    g.boff = bins ? pl->boff : nullptr;
+    g.blist = bins ? pl->blist : nullptr;
     g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse ? cfg->sparse_n : 1;
     g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
     const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
@@ -1502,7 +1538,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
-    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, fa);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
   }
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   if (!any_grad) return PTYX_OK;
@@ -1621,6 +1657,49 @@ extern "C" int ptyx_profile_end(ptyx_plan* pl, ptyx_kernel_stat* out, int32_t ca
   return rc;
 }
 
+// ---------------------------------------------------------------- graph-replayed step bookkeeping
+// (ptyrad_amd/stepgraph.py): the step's indices by a device counter, and the flat gradient zeroed,
+// in one launch; the loss terms stored and the counter advanced in another.
+__global__ void k_step_select(const int32_t* idx_all, const int64_t* istart, const int64_t* cnt, int n,
+                              int32_t* idx_out, float* grad, int64_t grad_n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  if (t < n) idx_out[t] = idx_all[istart[*cnt] + t];
+  float4* g4 = reinterpret_cast<float4*>(grad);
+  const int64_t n4 = grad_n >> 2;
+  for (int64_t i = t; i < n4; i += stride) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = 4 * n4 + t; i < grad_n; i += stride) grad[i] = 0.f;
+}
+__global__ __launch_bounds__(256) void k_step_store(const float* terms, int nb, const int64_t* rstart, int64_t* cnt,
+                                                    float* terms_all) {
+  const int64_t c = *cnt;
+  const int64_t r0 = rstart[c];
+  for (int i = threadIdx.x; i < nb * 5; i += blockDim.x) terms_all[r0 * 5 + i] = terms[i];
+  __syncthreads();   // every thread has read *cnt
+  if (threadIdx.x == 0) *cnt = c + 1;
+}
+
+extern "C" int ptyx_step_select(void* stream, const int32_t* idx_all, const int64_t* istart, const int64_t* cnt,
+                                int32_t n, int32_t* idx_out, float* grad, int64_t grad_n) {
+  g_err.clear();
+  if (!idx_all || !istart || !cnt || !idx_out || n < 0 || grad_n < 0 || (grad_n && !grad))
+    return fail(PTYX_EINVAL, "ptyx_step_select: null pointer or negative size");
+  if (reinterpret_cast<uintptr_t>(grad) % 16)
+    return fail(PTYX_EINVAL, "ptyx_step_select: grad must be 16-byte aligned");
+  const int64_t work = std::max<int64_t>(n, (grad_n + 3) / 4);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (work + 255) / 256));
+  hipLaunchKernelGGL(k_step_select, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx_all, istart, cnt, n,
+                     idx_out, grad, grad_n);
+  return launch_status("k_step_select launch");
+}
+
+extern "C" int ptyx_step_store(void* stream, const float* terms, int32_t nb, const int64_t* rstart, int64_t* cnt,
+                               float* terms_all) {
+  g_err.clear();
+  if (!terms || !rstart || !cnt || !terms_all || nb < 0)
+    return fail(PTYX_EINVAL, "ptyx_step_store: null pointer or negative size");
+  hipLaunchKernelGGL(k_step_store, dim3(1), dim3(256), 0, (hipStream_t)stream, terms, nb, rstart, cnt, terms_all);
+  return launch_status("k_step_store launch");
+}
 
 extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx, int32_t n_idx,
                             float* dp_out) {
@@ -1769,7 +1848,7 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
   f.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
   {
     ProfScope ps(pl, kKFinalize, st);
-    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + 127) / 128), dim3(128), 0, st, f);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, f);
   }
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;

@@ -1,0 +1,127 @@
+// ptyx_optim.hip — the Adam / AdamW update of every trainable tensor in ONE grid-filling launch.
+//
+// recon_step (src/ptyrad/reconstruction.py:658-781) calls optimizer.step() once per optimizer
+// step; at the reference's default grad_accumulation = 1 that is once per 32-pattern
+// mini-batch.  torch's fused Adam launches one multi_tensor_apply kernel per parameter group with
+// one workgroup per 65,536-element chunk: 17 workgroups for a 1033² object, so on 256 CUs each
+// group's update is latency-bound (≈ 130 µs per object tensor at the c2 geometry, 64 % of a
+// graph-replayed step; tools/trace_gaps.py).  Here one launch covers all groups, grid-stride over
+// the concatenated elements with enough workgroups to fill the chip, so the update streams at the
+// HBM rate (28 B per element: p, g, m, v in; p, m, v out).
+//
+// Arithmetic: torch.optim.Adam's single-tensor formula (torch/optim/adam.py, the path PtyRAD's
+// CPU runs take), fp32 element math in the same operation order with no FMA contraction, the
+// bias corrections in fp64 from the device step count (already incremented by the caller):
+//   g += wd·p (Adam) | p *= 1 − lr·wd (AdamW);   m = lerp(m, g, 1 − β1);   v = v·β2 + (1 − β2)·g·g
+//   p += (−lr / (1 − β1^t))·m / (√v / √(1 − β2^t) + ε)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "ptyx.h"
+#include "ptyx_abi.hpp"
+
+namespace ptyx {
+namespace opt {
+
+constexpr int kMaxT = 16;   // tensors per launch (more are split over launches)
+
+struct AdamArgs {
+  float* p[kMaxT];
+  const float* g[kMaxT];
+  float* m[kMaxT];
+  float* v[kMaxT];
+  const float* step[kMaxT];
+  double lr[kMaxT];
+  int64_t off[kMaxT + 1];   // prefix sums of the element counts
+  int nt;
+  float beta1, beta2, eps, wd;
+  double beta1d, beta2d;
+  int adamw, maximize;
+};
+
+__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  // the tensors' step scalars, once per workgroup (lane t of wave 0 for tensor t)
+  __shared__ float s_nstep[kMaxT], s_bc2s[kMaxT];
+  if (threadIdx.x < (unsigned)a.nt) {
+    const int t = threadIdx.x;
+    const double step = (double)*a.step[t];
+    const double bc1 = 1.0 - pow(a.beta1d, step), bc2 = 1.0 - pow(a.beta2d, step);
+    s_nstep[t] = (float)(-(a.lr[t] / bc1));
+    s_bc2s[t] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const int64_t total = a.off[a.nt];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const float w1 = (float)(1.0 - a.beta1d), c2 = (float)(1.0 - a.beta2d);
+  int t = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    while (i >= a.off[t + 1]) ++t;   // grid-stride indices only grow: the tensor index only advances
+    const int64_t j = i - a.off[t];
+    const float nstep = s_nstep[t], bc2s = s_bc2s[t];
+    float g = a.g[t][j], p = a.p[t][j];
+    if (a.maximize) g = -g;
+    if (a.wd != 0.f) {
+      if (a.adamw) p = __fmul_rn(p, (float)(1.0 - a.lr[t] * (double)a.wd));
+      else g = __fadd_rn(g, __fmul_rn(p, a.wd));
+    }
+    float m = a.m[t][j], v = a.v[t][j];
+    m = __fadd_rn(m, __fmul_rn(w1, __fsub_rn(g, m)));                      // lerp, weight < 0.5
+    v = __fadd_rn(__fmul_rn(v, a.beta2), __fmul_rn(__fmul_rn(c2, g), g));   // mul_(β2).addcmul_
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), a.eps);
+    p = __fadd_rn(p, __fdiv_rn(__fmul_rn(nstep, m), denom));                // addcdiv_
+    a.p[t][j] = p;
+    a.m[t][j] = m;
+    a.v[t][j] = v;
+  }
+}
+
+}  // namespace opt
+}  // namespace ptyx
+
+using ptyx::abi::fail;
+using ptyx::abi::launch_status;
+namespace opt = ptyx::opt;
+
+extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
+                              float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                              const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
+                              double weight_decay, int32_t flags) {
+  ptyx::abi::clear_error();
+  if (n < 0 || (n && (!params || !grads || !exp_avgs || !exp_avg_sqs || !steps || !numels || !lrs)))
+    return fail(PTYX_EINVAL, "ptyx_adam_step: null array or negative count");
+  for (int i0 = 0; i0 < n; i0 += opt::kMaxT) {
+    opt::AdamArgs a{};
+    a.nt = std::min(opt::kMaxT, n - i0);
+    a.off[0] = 0;
+    for (int k = 0; k < a.nt; ++k) {
+      const int i = i0 + k;
+      if (numels[i] < 0 || (numels[i] && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i] || !steps[i])))
+        return fail(PTYX_EINVAL, "ptyx_adam_step: null tensor pointer or negative size");
+      a.p[k] = params[i];
+      a.g[k] = grads[i];
+      a.m[k] = exp_avgs[i];
+      a.v[k] = exp_avg_sqs[i];
+      a.step[k] = steps[i];
+      a.lr[k] = lrs[i];
+      a.off[k + 1] = a.off[k] + numels[i];
+    }
+    for (int k = a.nt; k < opt::kMaxT; ++k) a.off[k + 1] = a.off[a.nt];
+    a.beta1 = (float)beta1;
+    a.beta2 = (float)beta2;
+    a.beta1d = beta1;
+    a.beta2d = beta2;
+    a.eps = (float)eps;
+    a.wd = (float)weight_decay;
+    a.adamw = flags & 1;
+    a.maximize = (flags >> 1) & 1;
+    const int64_t total = a.off[a.nt];
+    if (!total) continue;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+    hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (int rc = launch_status("k_adam launch")) return rc;
+  }
+  return PTYX_OK;
+}

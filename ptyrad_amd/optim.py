@@ -1,0 +1,99 @@
+"""torch.optim.Adam / AdamW whose update runs as one grid-filling HIP launch (ptyx_adam_step).
+
+``create_optimizer`` (reconstruction.py:285-368 of the reference) builds ``torch.optim.Adam`` with
+one parameter group per optimisable tensor.  torch's fused Adam then launches one
+multi_tensor_apply kernel per group with one workgroup per 65,536-element chunk — 17 workgroups
+for a 1033² object — so at the reference's default cadence (one optimizer step per 32-pattern
+mini-batch) the update is latency-bound and costs more GPU time than the engine call
+(ptyrad_amd/csrc/ptyx_optim.hip).  These classes ARE torch.optim.Adam / AdamW (same constructor,
+param_groups, state layout — 'step', 'exp_avg', 'exp_avg_sq' — and state_dict, so checkpoints
+move between them and torch's own classes); only ``step()`` differs: the step counts advance in
+one ``torch._foreach_add_`` and every group's update runs in one ``ptyx_adam_step`` launch, in
+torch's single-tensor arithmetic (fp32, same operation order; bias corrections in fp64).
+
+Cases the kernel does not cover (amsgrad, complex or non-fp32 or sparse gradients, CPU tensors,
+tensor-valued lr / betas, differentiable) run torch's own ``step()``.  Both step paths are
+graph-capturable once the state exists (ptyrad_amd/stepgraph.py).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _eligible(group, params):
+    if group.get("amsgrad") or group.get("differentiable") or group.get("foreach") or group.get("fused"):
+        return False
+    if any(isinstance(group[k], torch.Tensor) for k in ("lr", "eps", "weight_decay")) or \
+            any(isinstance(b, torch.Tensor) for b in group["betas"]):
+        return False
+    return all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and
+               (p.grad is None or (not p.grad.is_sparse and p.grad.dtype == torch.float32 and p.grad.is_contiguous()))
+               for p in params)
+
+
+class _HipAdamMixin:
+    _decoupled = False
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        plain = []
+        batches = {}
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            if not _eligible(group, params):
+                plain.append(group)
+                continue
+            decoupled = bool(group.get("decoupled_weight_decay", self._decoupled))
+            key = (float(group["betas"][0]), float(group["betas"][1]), float(group["eps"]),
+                   float(group["weight_decay"]), decoupled, bool(group.get("maximize", False)), params[0].device)
+            b = batches.setdefault(key, [])
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                elif st["step"].device != p.device:   # a state loaded from a non-capturable torch Adam
+                    st["step"] = st["step"].to(p.device, torch.float32)
+                b.append((p, st, float(group["lr"])))
+        for (b1, b2, eps, wd, decoupled, maximize, dev), items in batches.items():
+            steps = [st["step"] for _, st, _ in items]
+            torch._foreach_add_(steps, 1)
+            n = len(items)
+            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _, _ in items])
+            G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _, _ in items])
+            M = (ctypes.c_void_p * n)(*[st["exp_avg"].data_ptr() for _, st, _ in items])
+            V = (ctypes.c_void_p * n)(*[st["exp_avg_sq"].data_ptr() for _, st, _ in items])
+            S = (ctypes.c_void_p * n)(*[st["step"].data_ptr() for _, st, _ in items])
+            NE = (ctypes.c_int64 * n)(*[p.numel() for p, _, _ in items])
+            LR = (ctypes.c_double * n)(*[lr for _, _, lr in items])
+            stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            _lib.check(_lib.load().ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd,
+                                                  (1 if decoupled else 0) | (2 if maximize else 0)))
+        if plain:
+            saved = self.param_groups
+            try:
+                self.param_groups = plain
+                super().step()
+            finally:
+                self.param_groups = saved
+        return loss
+
+
+class Adam(_HipAdamMixin, torch.optim.Adam):
+    """torch.optim.Adam with a one-launch HIP update (see the module docstring)."""
+
+
+class AdamW(_HipAdamMixin, torch.optim.AdamW):
+    """torch.optim.AdamW with a one-launch HIP update (decoupled weight decay)."""
+    _decoupled = True

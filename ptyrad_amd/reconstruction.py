@@ -499,11 +499,13 @@ def recon_loop(model, optimizer, loss_fn, constraint_fn, batches, NITER, grad_ac
 def create_optimizer(optimizer_params, optimizable_params, verbose=True):
     """torch.optim.<name>(param groups with per-tensor lr, **configs) (reconstruction.py:285-368).
 
-    One deliberate difference: Adam / AdamW on device parameters default to torch's fused kernel
-    (``fused=True``) unless the configs choose ``fused`` or ``foreach``.  The update is the same
-    formula; the default foreach path issues about ten kernels per parameter group from Python,
-    which at the reference's default cadence (grad_accumulation = 1, one step per 32-pattern
-    mini-batch) costs more than the engine call (tools/recon_overhead.py)."""
+    One deliberate difference: Adam / AdamW on device parameters, with no ``fused`` / ``foreach``
+    choice in the configs, are ``ptyrad_amd.optim.Adam`` / ``AdamW``: torch.optim.Adam / AdamW
+    themselves (same param groups, state and state_dict) whose update runs as one grid-filling
+    HIP launch.  torch's default (foreach) path issues about ten kernels per parameter group from
+    Python and its fused path one latency-bound kernel per group, and at the reference's default
+    cadence (grad_accumulation = 1, one step per 32-pattern mini-batch) either costs more than the
+    engine call (tools/recon_overhead.py, tools/trace_gaps.py)."""
     name = optimizer_params.get("name", "Adam")
     cls = getattr(torch.optim, name, None)
     if cls is None:
@@ -511,6 +513,7 @@ def create_optimizer(optimizer_params, optimizable_params, verbose=True):
     configs = dict(optimizer_params.get("configs") or {})
     params = [p for g in optimizable_params for p in (g["params"] if isinstance(g, dict) else [g])]
     if (name in ("Adam", "AdamW") and "fused" not in configs and "foreach" not in configs and params and
-            all(p.is_cuda and p.is_floating_point() for p in params)):
-        configs["fused"] = True
+            all(p.is_cuda and p.dtype == torch.float32 for p in params)):
+        from . import optim
+        cls = getattr(optim, name)
     return cls(optimizable_params, **configs)

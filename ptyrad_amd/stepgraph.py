@@ -5,8 +5,9 @@ of recon_step (reconstruction.py:658-781) is one optimizer step per 32-pattern m
 steps per iteration at the c2 geometry.  Each step is ~18 small engine launches plus the fused
 Adam kernels, and issuing them from Python costs more than the GPU needs to run them
 (0.47 ms per step, 0.18 ms of it GPU time).  ``StepGraphs`` captures ONE optimizer
-step — zero the flat gradient buffer, pick the step's indices on the device, the
-ptyx_forward_loss_grad call, ``optimizer.step()``, store the loss terms — into a hipGraph
+step — ptyx_step_select (the step's indices by a device counter, and the flat gradient buffer
+zeroed), the ptyx_forward_loss_grad call, ``optimizer.step()``, ptyx_step_store (the loss terms,
+then the counter advances) — into a hipGraph
 (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it for every later step with the same
 shape.  The step's inputs are selected on the device from a per-iteration index table by a
 step counter that the graph itself advances, so a replay needs no host work besides the launch.
@@ -16,15 +17,19 @@ Same kernels, same order, same arguments as the eager step: the trajectory is bi
 body (it creates the optimizer state a capture must not allocate), the next is captured.
 
 Eligible: one rank (no collectives inside the step), the plain fused engine path (no autograd
-stages, no loss_pacbed, no optimised propagator), Adam / AdamW with ``fused=True``
-(``create_optimizer``'s default), and every step small enough for one engine call.
+stages, no loss_pacbed, no optimised propagator), ``ptyrad_amd.optim.Adam`` / ``AdamW``
+(``create_optimizer``'s default) or torch's Adam / AdamW with ``fused=True``, and every step small
+enough for one engine call.
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 import torch
 
-from .engine import LossConfig, batch_offsets
+from . import _lib
+from .engine import LossConfig, _ptr, batch_offsets
 
 
 def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation):
@@ -39,9 +44,12 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
         return "autograd stages or loss_pacbed"
     if getattr(model, "prop_opt", False) or model._dz_t() is not None:
         return "optimised propagator (autograd through H)"
-    if not isinstance(optimizer, (torch.optim.Adam, torch.optim.AdamW)) or \
-            not all(g.get("fused") for g in optimizer.param_groups):
-        return "optimizer is not a fused Adam / AdamW"
+    from .optim import _HipAdamMixin, _eligible
+    hip_adam = isinstance(optimizer, _HipAdamMixin) and all(
+        _eligible(g, [p for p in g["params"] if p.grad is not None or p.requires_grad]) for g in optimizer.param_groups)
+    if not hip_adam and (not isinstance(optimizer, (torch.optim.Adam, torch.optim.AdamW)) or
+                         not all(g.get("fused") for g in optimizer.param_groups)):
+        return "optimizer is not ptyrad_amd.optim.Adam / AdamW or a fused torch Adam / AdamW"
     cap = model.plan.register_capacity
     cap = min(cap, int(model.plan.dims.max_patterns)) if cap > 0 else int(model.plan.dims.max_patterns)
     ga = max(1, int(grad_accumulation))
@@ -56,7 +64,7 @@ class StepGraphs:
 
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
-        self.static = {}          # key -> (idx (n,) i32, off (nb+1,) i32 device, terms (nb, 5), arange_n, arange_nb)
+        self.static = {}          # key -> (idx (n,) i32, off (nb+1,) i32 device, terms (nb, 5))
         self.pool = None
         self._table = None        # (batches fingerprint, idx_all, istart, rstart)
         self._seen = set()        # keys whose first (eager) step has run
@@ -83,22 +91,23 @@ class StepGraphs:
     def _body(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, idx_all, istart, rstart,
               terms_all):
         """Exactly recon_step's step, on static buffers: captured or run eagerly."""
-        sidx, soff, sterms, ar_n, ar_nb = self.static[key]
-        flat_grad.zero_()
-        ipos = istart.index_select(0, cnt) + ar_n
-        torch.index_select(idx_all, 0, ipos, out=sidx)
+        sidx, soff, sterms = self.static[key]
+        lib = _lib.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream(flat_grad.device).cuda_stream)
+        # the step's indices (device counter) + zeroed gradient buffer, one launch
+        _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
+                                        _ptr(flat_grad), int(flat_grad.numel())))
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
              "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(),
              "tilts": None if model._tilts() is None else model._tilts().detach().contiguous()}
         t.update(model._base())
         cfg = LossConfig.from_loss_params(loss_fn.loss_params)
-        max_batch = max(key[0])
         model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                     max_batch=max_batch, _rows_checked=True)
+                                     max_batch=max(key[0]), _rows_checked=True)
         optimizer.step()
-        rpos = rstart.index_select(0, cnt) + ar_nb
-        terms_all.index_copy_(0, rpos, sterms)
-        cnt += 1
+        # the loss terms into the iteration's table, then the counter advances (one launch)
+        _lib.check(lib.ptyx_step_store(st, _ptr(sterms), int(sterms.shape[0]), _ptr(rstart), _ptr(cnt),
+                                       _ptr(terms_all)))
 
     def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad):
         """All optimizer steps of one recon_step iteration; returns the (n_batches, 5) loss terms.
@@ -143,9 +152,7 @@ class StepGraphs:
                     n, nb = sum(sizes), len(sizes)
                     self.static[key] = (torch.zeros(n, dtype=torch.int32, device=dev),
                                         torch.as_tensor(batch_offsets([np.zeros(s) for s in sizes])).to(dev),
-                                        torch.zeros((nb, 5), dtype=torch.float32, device=dev),
-                                        torch.arange(n, dtype=torch.int64, device=dev),
-                                        torch.arange(nb, dtype=torch.int64, device=dev))
+                                        torch.zeros((nb, 5), dtype=torch.float32, device=dev))
                 args = (model, optimizer, loss_fn, flat_grad, grads, key, 1.0 / ga, cnt, idx_all, istart, rstart,
                         terms_all)
                 gr = self.graphs.get(key)

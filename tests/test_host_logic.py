@@ -94,3 +94,23 @@ def test_make_batches_sparse_matches_reference_greedy_rule():
     assert np.array_equal(np.sort(np.concatenate(got)), idx)
     bs = make_batches(idx, pos, 10, mode="sparse", random_state=0)
     assert np.array_equal(np.sort(np.concatenate(bs)), idx)
+
+
+def test_hip_adam_class_is_torch_adam_and_runs_torch_step_on_cpu():
+    """ptyrad_amd.optim.Adam is a torch.optim.Adam; on CPU tensors (no kernel) its step() is
+    torch's own, bit for bit."""
+    import torch
+    from ptyrad_amd import optim
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(5, 7, generator=g)
+    p1, p2 = a.clone().requires_grad_(), a.clone().requires_grad_()
+    o1, o2 = optim.Adam([p1], lr=1e-2, weight_decay=0.1), torch.optim.Adam([p2], lr=1e-2, weight_decay=0.1)
+    assert isinstance(o1, torch.optim.Adam)
+    for _ in range(3):
+        gr = torch.randn(5, 7, generator=g)
+        p1.grad, p2.grad = gr.clone(), gr.clone()
+        o1.step()
+        o2.step()
+    assert torch.equal(p1, p2)
+    o3 = torch.optim.Adam([p2], lr=1e-2)
+    o3.load_state_dict(o1.state_dict())
