@@ -244,23 +244,17 @@ def main():
     terms = torch.empty((nb, 5), device=dev)
     stream = torch.cuda.current_stream(dev)
     ar_ev = []
-    # The optimizer step (reconstruction.py:756-760): torch Adam over the reconstruction's tensors,
+    # The optimizer step (reconstruction.py:756-760): Adam over the reconstruction's tensors,
     # per-tensor learning rates of demo/params/tBL_WSe2_reconstruct.yml:118-123, one step per
     # iteration (grad_accumulation = all of the rank's mini-batches).  The gradients are the views
-    # of the flat all-reduced buffer; the next step's engine call sees the updated tensors.
+    # of the flat all-reduced buffer; the next step's engine call sees the updated tensors.  The
+    # optimizer is create_optimizer's default, ptyrad_amd.optim.Adam (torch.optim.Adam with its
+    # update in one grid-filling HIP launch), one param group per tensor as the reference builds them.
+    from ptyrad_amd.reconstruction import create_optimizer
     lrs = {"obja": 5e-4, "objp": 5e-4, "probe": 1e-4, "shifts": 1e-4}
     for k in lrs:
         t[k].grad = grads[k]
-    # tensors with the same learning rate share a param group: the fused kernel runs one launch
-    # per group, each over ⌈numel / 65,536⌉ chunks (a 1033² tensor alone is 17 workgroups)
-    by_lr = {}
-    for k, lr in lrs.items():
-        by_lr.setdefault(lr, []).append(t[k])
-    groups = [{"params": ps, "lr": lr} for lr, ps in by_lr.items()]
-    try:      # fused multi-tensor kernels (the object dominates: 2 x 1.66 GB at c5)
-        opt = torch.optim.Adam(groups, fused=True)
-    except (RuntimeError, ValueError):
-        opt = torch.optim.Adam(groups, foreach=True)
+    opt = create_optimizer({"name": "Adam", "configs": {}}, [{"params": [t[k]], "lr": lr} for k, lr in lrs.items()])
     bands = None
     n_obj = t["obja"].numel() + t["objp"].numel()
     if world > 1 and a.exchange == "band":

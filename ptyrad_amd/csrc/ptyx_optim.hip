@@ -35,7 +35,8 @@ struct AdamArgs {
   float* v[kMaxT];
   const float* step[kMaxT];
   double lr[kMaxT];
-  int64_t off[kMaxT + 1];   // prefix sums of the element counts
+  int64_t off[kMaxT + 1];   // prefix sums of the tensors' UNITS (4 elements if vec, else 1)
+  int vec[kMaxT];           // p, g, m, v 16-B aligned and numel % 4 == 0: float4 units
   int nt;
   float beta1, beta2, eps, wd;
   double beta1d, beta2d;
@@ -54,27 +55,77 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   }
   __syncthreads();
   const int64_t total = a.off[a.nt];
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const float w1 = (float)(1.0 - a.beta1d), c2 = (float)(1.0 - a.beta2d);
+  // a workgroup takes chunks of 4·256 consecutive units, a thread four of them 256 apart
+  // (coalesced; 16-B units where the tensor allows); chunks grid-stride
+  constexpr int kU = 4;
+  const int64_t chunk = (int64_t)kU * blockDim.x;
   int t = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    while (i >= a.off[t + 1]) ++t;   // grid-stride indices only grow: the tensor index only advances
-    const int64_t j = i - a.off[t];
-    const float nstep = s_nstep[t], bc2s = s_bc2s[t];
-    float g = a.g[t][j], p = a.p[t][j];
-    if (a.maximize) g = -g;
-    if (a.wd != 0.f) {
-      if (a.adamw) p = __fmul_rn(p, (float)(1.0 - a.lr[t] * (double)a.wd));
-      else g = __fadd_rn(g, __fmul_rn(p, a.wd));
+  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < total; c0 += (int64_t)gridDim.x * chunk) {
+    float4 g[kU], p[kU], m[kU], v[kU];
+    int tt[kU];
+    int64_t jj[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = c0 + u * blockDim.x + threadIdx.x;
+      tt[u] = -1;
+      if (i < total) {
+        while (i >= a.off[t + 1]) ++t;   // indices only grow: the tensor index only advances
+        tt[u] = t;
+        const int64_t j = i - a.off[t];
+        jj[u] = j;
+        if (a.vec[t]) {
+          g[u] = reinterpret_cast<const float4*>(a.g[t])[j];
+          p[u] = reinterpret_cast<const float4*>(a.p[t])[j];
+          m[u] = reinterpret_cast<const float4*>(a.m[t])[j];
+          v[u] = reinterpret_cast<const float4*>(a.v[t])[j];
+        } else {
+          g[u].x = a.g[t][j];
+          p[u].x = a.p[t][j];
+          m[u].x = a.m[t][j];
+          v[u].x = a.v[t][j];
+        }
+      }
     }
-    float m = a.m[t][j], v = a.v[t][j];
-    m = __fadd_rn(m, __fmul_rn(w1, __fsub_rn(g, m)));                      // lerp, weight < 0.5
-    v = __fadd_rn(__fmul_rn(v, a.beta2), __fmul_rn(__fmul_rn(c2, g), g));   // mul_(β2).addcmul_
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), a.eps);
-    p = __fadd_rn(p, __fdiv_rn(__fmul_rn(nstep, m), denom));                // addcdiv_
-    a.p[t][j] = p;
-    a.m[t][j] = m;
-    a.v[t][j] = v;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int tu = tt[u];
+      if (tu < 0) continue;
+      const float nstep = s_nstep[tu], bc2s = s_bc2s[tu];
+      const float decay = (float)(1.0 - a.lr[tu] * (double)a.wd);
+      float* gp = &g[u].x;
+      float* pp = &p[u].x;
+      float* mp = &m[u].x;
+      float* vp = &v[u].x;
+      const int ne = a.vec[tu] ? 4 : 1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e >= ne) break;
+        float gu = gp[e], pu = pp[e], mu = mp[e], vu = vp[e];
+        if (a.maximize) gu = -gu;
+        if (a.wd != 0.f) {
+          if (a.adamw) pu = __fmul_rn(pu, decay);
+          else gu = __fadd_rn(gu, __fmul_rn(pu, a.wd));
+        }
+        mu = __fadd_rn(mu, __fmul_rn(w1, __fsub_rn(gu, mu)));                        // lerp, weight < 0.5
+        vu = __fadd_rn(__fmul_rn(vu, a.beta2), __fmul_rn(__fmul_rn(c2, gu), gu));     // mul_(β2).addcmul_
+        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vu), bc2s), a.eps);
+        pu = __fadd_rn(pu, __fdiv_rn(__fmul_rn(nstep, mu), denom));                  // addcdiv_
+        pp[e] = pu;
+        mp[e] = mu;
+        vp[e] = vu;
+      }
+      const int64_t j = jj[u];
+      if (a.vec[tu]) {
+        reinterpret_cast<float4*>(a.p[tu])[j] = p[u];
+        reinterpret_cast<float4*>(a.m[tu])[j] = m[u];
+        reinterpret_cast<float4*>(a.v[tu])[j] = v[u];
+      } else {
+        a.p[tu][j] = p[u].x;
+        a.m[tu][j] = m[u].x;
+        a.v[tu][j] = v[u].x;
+      }
+    }
   }
 }
 
@@ -106,7 +157,9 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
       a.v[k] = exp_avg_sqs[i];
       a.step[k] = steps[i];
       a.lr[k] = lrs[i];
-      a.off[k + 1] = a.off[k] + numels[i];
+      const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+      a.vec[k] = numels[i] % 4 == 0 && al16(params[i]) && al16(grads[i]) && al16(exp_avgs[i]) && al16(exp_avg_sqs[i]);
+      a.off[k + 1] = a.off[k] + (a.vec[k] ? numels[i] / 4 : numels[i]);
     }
     for (int k = a.nt; k < opt::kMaxT; ++k) a.off[k + 1] = a.off[a.nt];
     a.beta1 = (float)beta1;
@@ -119,7 +172,7 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
     a.maximize = (flags >> 1) & 1;
     const int64_t total = a.off[a.nt];
     if (!total) continue;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (total + 1023) / 1024));
     hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
     if (int rc = launch_status("k_adam launch")) return rc;
   }
