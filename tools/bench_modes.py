@@ -1,0 +1,89 @@
+"""Engine-only throughput (ptyx_forward_loss_grad, patterns/s) at the geometries of the
+reference's own demo parameter files, next to the BASELINE configs' engines:
+
+  tbl   demo/params/tBL_WSe2_reconstruct.yml:23-27   N 128, 6 probe modes, 6 slices
+  pso   demo/params/PSO_reconstruct.yml:23-34         N 256 (120 px padded on the fly to 256), 4 probe
+                                                      modes, 21 slices
+  plus single-mode / single-slice neighbours of tbl for comparison.
+
+    python tools/bench_modes.py [name ...] [--patterns 4096] [--reps 3]
+
+Synthetic raster (2.871 px step), seeded uniform DPs, random mini-batches of 32, loss_single
+(q 0.5) + loss_sparse, all gradients on.  One JSON line per geometry with the per-kernel times.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+GEOMS = {
+    "tbl": dict(N=128, P=6, O=1, Nz=6),
+    "tbl_p1": dict(N=128, P=1, O=1, Nz=6),
+    "tbl_z1": dict(N=128, P=6, O=1, Nz=1),
+    "pso": dict(N=256, P=4, O=1, Nz=21),
+}
+LP = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+      "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+      "loss_pacbed": {"state": False}, "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
+      "loss_simlar": {"state": False}}
+
+
+def run(name, g, n, reps, dev):
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
+    N, P, O, Nz = g["N"], g["P"], g["O"], g["Nz"]
+    side = int(np.ceil(np.sqrt(n)))
+    sc = syn.raster_scan(side, side, N, seed=0)
+    Ny, Nx = sc.obj_shape
+    n = side * side
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    probe = np.stack([syn.stem_probe(N) * np.float32(60.0 / (p + 1)) for p in range(P)]).astype(np.complex64)
+    t = {"obja": (1.0 + 0.05 * torch.randn((O, Nz, Ny, Nx), generator=gen, device=dev)).float(),
+         "objp": (0.1 * torch.randn((O, Nz, Ny, Nx), generator=gen, device=dev)).float(),
+         "probe": torch.view_as_real(torch.tensor(probe, device=dev)).contiguous(),
+         "shifts": torch.tensor(sc.shifts, device=dev), "H": torch.tensor(syn.fresnel_propagator(N, syn.DX_ANG, 2.0), device=dev),
+         "occu": torch.full((O,), 1.0 / O, device=dev), "crop_pos": torch.tensor(sc.crop_pos, device=dev),
+         "meas": torch.rand((n, N, N), generator=gen, device=dev)}
+    plan = Plan(N, P, O, Nz, Ny, Nx, n, n, shift_probes=True, device=dev)
+    batches = np.array_split(np.random.default_rng(2).permutation(n), n // 32)
+    idx = np.concatenate(batches).astype(np.int32)
+    off = batch_offsets(batches)
+    cfg = LossConfig.from_loss_params(LP)
+    grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe", "shifts")}
+    terms = torch.empty((len(batches), 5), device=dev)
+    plan.forward_loss_grad(t, idx, off, cfg, grads, loss_terms=terms)
+    torch.cuda.synchronize()
+    plan.profile_begin()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        plan.forward_loss_grad(t, idx, off, cfg, grads, loss_terms=terms)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    ks = {k: round(v[1] / reps, 3) for k, v in plan.profile_end().items()}
+    ok = bool(torch.isfinite(terms).all())
+    print(json.dumps({"geometry": name, **g, "patterns": n, "object": [Ny, Nx], "ms_per_call": round(ms, 3),
+                      "patterns_per_s": round(n / ms * 1e3, 1), "finite": ok, "kernels_ms": ks}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="*", default=list(GEOMS))
+    ap.add_argument("--patterns", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for name in a.names:
+        run(name, GEOMS[name], a.patterns, a.reps, dev)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
