@@ -62,6 +62,8 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
 class StepGraphs:
     """Captured optimizer steps of one (model, optimizer, loss_fn), keyed by step shape."""
 
+    MAX_GRAPHS = 16               # captured steps kept (insertion order; the oldest is dropped)
+
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
         self.static = {}          # key -> (idx (n,) i32, off (nb+1,) i32 device, terms (nb, 5))
@@ -144,10 +146,14 @@ class StepGraphs:
         saved = [g.get("capturable", False) for g in optimizer.param_groups]
         for g in optimizer.param_groups:
             g["capturable"] = True            # fused Adam keeps its step counts on the device already
+        def state_ptrs():   # the optimizer state a captured step reads and writes (replaced by a load)
+            return tuple(int(v.data_ptr()) for p in live for v in optimizer.state.get(p, {}).values()
+                         if isinstance(v, torch.Tensor))
+
         try:
             for g0 in range(0, len(batches), ga):
                 sizes = tuple(len(np.asarray(b).reshape(-1)) for b in batches[g0:g0 + ga])
-                key = (sizes, live_ids, lrs, ptrs, id(optimizer))
+                key = (sizes, live_ids, lrs, ptrs, id(optimizer), state_ptrs())
                 if key not in self.static:
                     n, nb = sum(sizes), len(sizes)
                     self.static[key] = (torch.zeros(n, dtype=torch.int32, device=dev),
@@ -169,6 +175,11 @@ class StepGraphs:
                         self._body(*args)
                     self.graphs[key] = gr
                     self.captures += 1
+                    while len(self.graphs) > self.MAX_GRAPHS:   # oldest first (e.g. a learning-rate schedule)
+                        old = next(iter(self.graphs))
+                        del self.graphs[old]
+                        self.static.pop(old, None)
+                        self._seen.discard(old)
                     gr.replay()
                     self.replays += 1
                 else:
