@@ -32,7 +32,8 @@ struct GatherArgs {
   const float* objp;
   float* d_obja;
   float* d_objp;
-  int nz = 1, z = 0;     // slots hold nz planes per pattern; this launch gathers plane z
+  int nz = 1, z = 0;     // slots hold nz planes per pattern; this launch gathers plane z, or, with
+  int zgrid = 0;         // zgrid, plane blockIdx.y (obja / objp / d_* then point at plane 0)
   const int* bbox = nullptr;   // {min cy, max cy, min cx, max cx} of the call's windows: other tiles exit
   const int* boff = nullptr;   // bin offsets (tiles + 1) into blist, or NULL: scan every pattern
   const int* blist = nullptr;  // pattern indices by bin, ascending within a bin
@@ -59,6 +60,8 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
   __shared__ int s_b0[NB], s_pre[NB + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
+  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;                        // slot plane
+  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;   // object plane
   const int ty = tyi * kGTY, tx = txi * kGTX;
   if (ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] || tx >= ga.bbox[3] + N))
     return;   // no window of this call touches the tile: its gradient contribution is zero
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
       const int cy = __shfl(o.x, b, 64), cx = __shfl(o.y, b, 64);
       const float c = __shfl(cj.x, b, 64), cs = __shfl(cj.y, b, 64);
       const int jb = __shfl(j, b, 64);
-      const float2* src = ga.ogscr + ((size_t)jb * ga.nz + ga.z) * N2;
+      const float2* src = ga.ogscr + ((size_t)jb * ga.nz + zp) * N2;
       const int col = x - cx;
       const bool colok = col >= 0 && col < N;
       float2 v[kGTY];
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
   for (int e = threadIdx.x; e < kGTY * kGTX; e += 64 * GW) {
     const int y = ty + e / kGTX, xx = tx + e % kGTX;
     if (y >= ga.Ny || xx >= ga.Nx) continue;
-    const size_t off = (size_t)y * ga.Nx + xx;
+    const size_t off = zoff + (size_t)y * ga.Nx + xx;
     const float2 S = s_acc[e];
     const float A = ga.obja[off], ph = ga.objp[off];
     float sn, cs;

@@ -1372,18 +1372,11 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     // ≈ 17): 4 waves a tile instead of kGWaves
     const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
     ProfScope ps(pl, kKGather, st);
-    const size_t plane = (size_t)d.Ny * d.Nx;
     g.nz = Nz;
     g.bbox = pl->bbox;   // also for Nz = 1
-    for (int z = 0; z < Nz; ++z) {   // one launch per slice plane of the slots
-      g.z = z;
-      g.obja = a.obja + z * plane;
-      g.objp = a.objp + z * plane;
-      g.d_obja = gz.d_obja ? gz.d_obja + z * plane : nullptr;
-      g.d_objp = gz.d_objp ? gz.d_objp + z * plane : nullptr;
-      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, true, 4>), dim3(tiles), dim3(64 * 4), 0, st, g);
-      else hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
-    }
+    g.zgrid = 1;         // every slice plane in one launch (blockIdx.y = slice)
+    if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, true, 4>), dim3(tiles, Nz), dim3(64 * 4), 0, st, g);
+    else hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles, Nz), dim3(64 * kGWaves), 0, st, g);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
   if (a.shift && gz.d_shifts) {

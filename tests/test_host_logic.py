@@ -114,3 +114,21 @@ def test_hip_adam_class_is_torch_adam_and_runs_torch_step_on_cpu():
     assert torch.equal(p1, p2)
     o3 = torch.optim.Adam([p2], lr=1e-2)
     o3.load_state_dict(o1.state_dict())
+
+
+def test_stepgraph_tables_and_eligibility_on_cpu():
+    """StepGraphs' per-iteration tables (first pattern / first mini-batch of every optimizer step)
+    and recon_step's refusal of graphs=True without a HIP device."""
+    import numpy as np
+    import torch
+    from ptyrad_amd.stepgraph import StepGraphs, ineligible_reason
+    batches = [np.array([5, 1, 9]), np.array([2, 7]), np.array([0, 3, 4]), np.array([8, 6])]
+    sg = StepGraphs()
+    idx_all, istart, rstart = sg._tables(batches, 3, torch.device("cpu"))
+    assert idx_all.tolist() == [5, 1, 9, 2, 7, 0, 3, 4, 8, 6]
+    assert istart.tolist() == [0, 8] and rstart.tolist() == [0, 3]       # steps of 3 and 1 mini-batches
+    assert sg._tables(batches, 3, torch.device("cpu"))[0] is idx_all      # cached while the batches stay
+
+    class M:
+        opt_obja = torch.zeros(1)
+    assert ineligible_reason(M(), None, None, None, batches, 1) == "no HIP device"
