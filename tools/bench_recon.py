@@ -28,10 +28,15 @@ def main():
     ap.add_argument("--scan", type=int, default=256)
     ap.add_argument("--ga", type=int, nargs="+", default=[1, 16, 2048])
     ap.add_argument("--iters", type=int, default=1)
+    ap.add_argument("--tune", action="append", default=[], help="ptyx_set_tuning key=value (A/B runs)")
     ap.add_argument("--graphs", choices=["auto", "on", "off"], default="auto",
                     help="recon_step(graphs=...): hipGraph-replayed optimizer steps")
     a = ap.parse_args()
+    from ptyrad_amd import _lib
     from ptyrad_amd import synthetic as syn
+    for kv in a.tune:
+        k, v = kv.split("=")
+        _lib.set_tuning(k, int(v))
     from ptyrad_amd.losses import CombinedLoss
     from ptyrad_amd.models import PtychoHIP
     from ptyrad_amd.reconstruction import create_optimizer, make_batches, recon_step
@@ -76,7 +81,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
         sg = getattr(model, "_step_graphs", None)
-        print(json.dumps({"ga": ga, "graphs": a.graphs, "replays": sg.replays if sg else 0,
+        print(json.dumps({"ga": ga, "graphs": a.graphs, "tune": a.tune, "replays": sg.replays if sg else 0,
                           "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
