@@ -70,7 +70,14 @@ struct KArgs {
   // and every probe mode's ψ⁰ per pattern, so k_adjoint skips the recomputed forward
   float2* ffc;
   long long ffc_per;   // float2 per pattern: (P·O + P)·N²
+  // probe-mode split (small calls, P > 1): msplit = P makes every (pattern, probe mode) its own
+  // job in k_forward / k_adjoint; k_forward then leaves Σ_o occ|Ψ_{p,o}|² per mode in Imodes
+  // ((pattern·P + p)·N² floats) and k_forward_modesum forms I, dp and the loss sums
+  int msplit = 1;
+  float* Imodes = nullptr;
 };
+// calls of at most this many patterns split their probe modes over workgroups (general engine)
+constexpr int kModeSplitCap = 128;
 
 // ---------------------------------------------------------------- small helpers
 // threadIdx.x behind an empty asm: per-pattern address arithmetic stays inside the pattern

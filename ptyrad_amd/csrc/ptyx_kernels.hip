@@ -180,8 +180,11 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
   }
   __syncthreads();
   const bool want_sums = a.psums != nullptr;
+  const int PS = SINGLE ? 1 : a.msplit;   // jobs per pattern (probe-mode split)
 
-  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
+  for (int job = blockIdx.x; job < a.n_idx * PS; job += gridDim.x) {
+    const int pat = job / PS;
+    const int pbeg = PS > 1 ? job % PS : 0, pend = PS > 1 ? pbeg + 1 : a.P;
     const PatternGeom g = pattern_geom(a, pat, N);
     if (a.shift) build_ramps<N, NT>(g, s_wy, s_wx);
     const bool tilt = a.ptilt != nullptr && a.Nz > 1;
@@ -199,10 +202,11 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
         sums[3] += Mq;
       }
     };
-    float* Ip = SINGLE ? nullptr : a.Ibuf + (size_t)pat * N2;
+    // split: this job's mode intensity Σ_o occ|Ψ_{p,o}|² in its own plane (k_forward_modesum adds)
+    float* Ip = SINGLE ? nullptr : (PS > 1 ? a.Imodes + ((size_t)pat * PS + pbeg) * N2 : a.Ibuf + (size_t)pat * N2);
     float2* psi0 = scratch_psi<N>(a);   // this workgroup's ψ⁰ park (multi-object-mode calls)
     float2* cache = (!SINGLE && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
-    for (int p = 0; p < a.P; ++p) {
+    for (int p = pbeg; p < pend; ++p) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, park0, o > 0);
         float2* ffp = cache ? cache + (size_t)(p * a.O + o) * N2 : nullptr;
         const float occ = a.occu[o];
-        const bool first = (p == 0 && o == 0);
+        const bool first = (p == pbeg && o == 0);
         // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
         fft2d<N, NT, -1, true>(
             arr, s_tw, [&](int, int, float2 v) { return v; },
@@ -236,6 +240,10 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
         }
       }
     }
+    if (PS > 1) {   // the mode planes are summed by k_forward_modesum
+      __syncthreads();
+      continue;
+    }
     if constexpr (!SINGLE) {
       // epilogue: + eps, dp_out, loss sums (Ip was written by this workgroup; barrier above)
       for (int e = opaque_tid(); e < N2; e += NT) {
@@ -253,6 +261,48 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
       }
     }
     __syncthreads();
+  }
+}
+
+// Probe-mode split: I = Σ_p (mode planes, fixed order) + eps per pattern → Ibuf (k_adjoint reads
+// it), dp_out and the loss partial sums — k_forward's epilogue, once all of a pattern's modes are in.
+template <int N>
+__global__ __launch_bounds__(Geo<N>::NT) void k_forward_modesum(KArgs a) {
+  constexpr int NT = Geo<N>::NT;
+  constexpr int N2 = N * N;
+  __shared__ float s_red[(NT / 64) * 4];
+  const int pat = blockIdx.x;
+  const PatternGeom g = pattern_geom(a, pat, N);
+  const bool want_sums = a.psums != nullptr;
+  float sums[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* Im = a.Imodes + (size_t)pat * a.msplit * N2;
+  float* Ip = a.Ibuf + (size_t)pat * N2;
+  for (int e = opaque_tid(); e < N2; e += NT) {
+    float I = Im[e];
+    for (int p = 1; p < a.msplit; ++p) I += Im[(size_t)p * N2 + e];
+    I += kDpEps;
+    Ip[e] = I;
+    if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
+    if (want_sums) {
+      const float M = meas_at(a, g.m, e, N2);
+      if (a.single_on) {
+        const float Iq = powq(I, a.q1), Mq = powq(M, a.q1), d = Iq - Mq;
+        sums[0] = fmaf(d, d, sums[0]);
+        sums[1] += Mq;
+      }
+      if (a.pois_on) {
+        const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
+        sums[2] += Mq * fast_ln(Iq + a.eps2) - Iq;
+        sums[3] += Mq;
+      }
+    }
+  }
+  if (want_sums) {
+    block_sum<NT, 4>(sums, s_red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a.psums[(size_t)pat * kNSum + i] = sums[i];
+    }
   }
 }
 
@@ -397,7 +447,10 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
     for (int e = threadIdx.x; e < N2; e += NT) hsl[e] = make_float2(0.f, 0.f);
   __syncthreads();
 
-  for (int pat = blockIdx.x; pat < a.n_idx; pat += gridDim.x) {
+  const int PS = (SINGLE || EXT) ? 1 : a.msplit;   // jobs per pattern (probe-mode split)
+  for (int job = blockIdx.x; job < a.n_idx * PS; job += gridDim.x) {
+    const int pat = job / PS;
+    const int pbeg = PS > 1 ? job % PS : 0, pend = PS > 1 ? pbeg + 1 : a.P;
     const PatternGeom g = pattern_geom(a, pat, N);
     float c1 = 0.f, c2 = 0.f;
     int m = 0;
@@ -419,7 +472,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
     float dt[2] = {0.f, 0.f};   // Σ_k Ky (resp. Kx) · Re(i conj(g_Hb) H_b)
     const float* Ip = (SINGLE || EXT) ? nullptr : a.Ibuf + (size_t)pat * N2;
 
-    for (int p = 0; p < a.P; ++p) {
+    for (int p = pbeg; p < pend; ++p) {
       for (int o = 0; o < a.O; ++o) {
         const float occ = a.occu[o];
         const float csp = (!EXT && a.sparse_on && p == 0) ? a.coef[(size_t)m * kNCoef + 2 + o] : 0.f;
@@ -705,6 +758,7 @@ struct ptyx_plan {
   float* psums = nullptr;
   float* coef = nullptr;
   float* Ibuf = nullptr;
+  float* Imodes = nullptr;    // probe-mode split: P mode-intensity planes per pattern (≤ kModeSplitCap)
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* hslab = nullptr;    // PTYX_PROP_GRAD: per-workgroup dL/dH slabs
@@ -926,6 +980,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->psums, (size_t)d.max_patterns * kNSum)) ||
       (rc = dalloc(pl, &pl->coef, (size_t)d.max_patterns * kNCoef)) ||
       (rc = dalloc(pl, &pl->Ibuf, multi ? (size_t)d.max_patterns * N2 : 0)) ||
+      (rc = dalloc(pl, &pl->Imodes, d.P > 1 ? (size_t)d.P * std::min(d.max_patterns, kModeSplitCap) * N2 : 0)) ||
       (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
       (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
       (rc = dalloc(pl, &pl->hslab, prop_grad ? (size_t)pl->nwg * N2 : 0)) ||
@@ -1131,7 +1186,7 @@ static void launch_spectrum(const ptyx_plan* pl, const KArgs& a, hipStream_t st)
 template <int N>
 static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
   ProfScope ps(pl, kKForward, st);
-  const int grid = std::max(1, std::min(a.n_idx, pl->nwg));
+  const int grid = std::max(1, std::min(a.n_idx * a.msplit, pl->nwg));
   if constexpr (Geo<N>::kLds) {
     if (pl->d.P * pl->d.O * pl->d.Nz == 1) {
       const bool sums = a.psums != nullptr;
@@ -1146,6 +1201,10 @@ static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) 
     hipLaunchKernelGGL((k_forward<N, true>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
   else
     hipLaunchKernelGGL((k_forward<N, false>), dim3(grid), dim3(Geo<N>::NT), 0, st, a);
+}
+template <int N>
+static void launch_modesum(const ptyx_plan*, const KArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_forward_modesum<N>, dim3(a.n_idx), dim3(Geo<N>::NT), 0, st, a);
 }
 template <int N>
 static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, bool ext) {
@@ -1826,10 +1885,22 @@ static void resolve_prep(ptyx_plan* pl, const ptyx_inputs* in, int engine, ptyx_
 static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
                         const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
   int rc = PTYX_OK;
+  // small calls with several probe modes: one job per (pattern, probe mode), so a 32-pattern
+  // mini-batch at P = 6 keeps 192 workgroups busy instead of 32 (the default grad_accumulation = 1)
+  KArgs b = a;
+  if (pl->Imodes && pl->d.P > 1 && a.n_idx <= kModeSplitCap && a.n_idx < pl->nwg) {
+    b.msplit = pl->d.P;
+    b.Imodes = pl->Imodes;
+  }
   if (ph != kPhaseEnd) {
-    if (a.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
-    PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
+    if (b.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, b, st);
+    PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, b, st);
     if ((rc = launch_status("k_forward launch"))) return rc;
+    if (b.msplit > 1) {
+      ProfScope ps(pl, kKForward, st);
+      PTYX_DISPATCH_N(pl->d.N, launch_modesum, pl, b, st);
+      if ((rc = launch_status("k_forward_modesum launch"))) return rc;
+    }
   }
   FinArgs f{};
   f.boff = a.boff; f.n_batches = a.n_batches; f.N = pl->d.N; f.Nz = pl->d.Nz; f.O = pl->d.O;
@@ -1846,7 +1917,7 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts || gz.d_H || gz.d_tilts || gz.d_dz;
   if (!any_grad) return PTYX_OK;
-  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, false);
+  PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, b, st, false);
   if ((rc = launch_status("k_adjoint launch"))) return rc;
   if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
   if (gz.d_probe) {

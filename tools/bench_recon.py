@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--scan", type=int, default=256)
     ap.add_argument("--ga", type=int, nargs="+", default=[1, 16, 2048])
     ap.add_argument("--iters", type=int, default=1)
+    ap.add_argument("--pmodes", type=int, default=1, help="probe modes (tBL_WSe2 demo: 6)")
+    ap.add_argument("--slices", type=int, default=1, help="object slices (tBL_WSe2 demo: 6)")
     ap.add_argument("--tune", action="append", default=[], help="ptyx_set_tuning key=value (A/B runs)")
     ap.add_argument("--graphs", choices=["auto", "on", "off"], default="auto",
                     help="recon_step(graphs=...): hipGraph-replayed optimizer steps")
@@ -46,7 +48,8 @@ def main():
     n = S * S
     rng = np.random.default_rng(0)
     Ny, Nx = scan.obj_shape
-    probe = syn.stem_probe(N) * np.float32(60.0)
+    P, Nz = a.pmodes, a.slices
+    probe = np.stack([syn.stem_probe(N) * np.float32(60.0 / (1 + 2 * p)) for p in range(P)])
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     meas = torch.rand((n, N, N), generator=g, device=dev)
@@ -58,9 +61,9 @@ def main():
           "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
           "loss_simlar": {"state": False}}
     for ga in a.ga:
-        iv = {"obja": np.ones((1, 1, Ny, Nx), np.float32),
-              "objp": (1e-8 * rng.random((1, 1, Ny, Nx))).astype(np.float32), "obj": None,
-              "probe": probe[None], "probe_pos_shifts": scan.shifts, "omode_occu": np.ones(1, np.float32),
+        iv = {"obja": np.ones((1, Nz, Ny, Nx), np.float32),
+              "objp": (1e-8 * rng.random((1, Nz, Ny, Nx))).astype(np.float32), "obj": None,
+              "probe": probe, "probe_pos_shifts": scan.shifts, "omode_occu": np.ones(1, np.float32),
               "H": syn.fresnel_propagator(N, syn.DX_ANG, 2.0), "measurements": meas, "crop_pos": scan.crop_pos,
               "N_scan_slow": S, "N_scan_fast": S, "slice_thickness": 2.0, "dx": syn.DX_ANG, "dk": 1.0 / (N * syn.DX_ANG),
               "lambd": syn.electron_wavelength(syn.KV), "obj_tilts": np.zeros((1, 2), np.float32)}
@@ -81,7 +84,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
         sg = getattr(model, "_step_graphs", None)
-        print(json.dumps({"ga": ga, "graphs": a.graphs, "tune": a.tune, "replays": sg.replays if sg else 0,
+        print(json.dumps({"ga": ga, "P": P, "Nz": Nz, "graphs": a.graphs, "tune": a.tune, "replays": sg.replays if sg else 0,
                           "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
