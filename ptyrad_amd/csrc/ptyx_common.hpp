@@ -69,7 +69,7 @@ struct KArgs {
   // far-field cache (general engine, Nz = 1, P·O > 1): k_forward leaves every mode's F(ψ_out)
   // and every probe mode's ψ⁰ per pattern, so k_adjoint skips the recomputed forward
   float2* ffc;
-  long long ffc_per;   // float2 per pattern: (P·O + P)·N²
+  long long ffc_per;   // float2 per pattern: (P·O + P)·N² (Nz = 1) or P·O·(1 + Nz)·N²
   // probe-mode split (small calls, P > 1): msplit = P makes every (pattern, probe mode) its own
   // job in k_forward / k_adjoint; k_forward then leaves Σ_o occ|Ψ_{p,o}|² per mode in Imodes
   // ((pattern·P + p)·N² floats) and k_forward_modesum forms I, dp and the loss sums

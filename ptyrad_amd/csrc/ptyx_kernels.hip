@@ -210,9 +210,15 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
-        float2* park0 = cache ? cache + (size_t)(a.P * a.O + p) * N2 : (a.O > 1 ? psi0 : nullptr);
-        forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
-                                    tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, park0, o > 0);
+        if (cache && a.Nz > 1) {   // the cache keeps every slice's ψⁿ of (p, o) for k_adjoint
+          float2* psis = cache + (size_t)(a.P * a.O + (p * a.O + o) * a.Nz) * N2;
+          forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psis, sparse, sp, nullptr,
+                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, a.O > 1 ? psi0 : nullptr, o > 0);
+        } else {
+          float2* park0 = cache ? cache + (size_t)(a.P * a.O + p) * N2 : (a.O > 1 ? psi0 : nullptr);
+          forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
+                                      tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, park0, o > 0);
+        }
         float2* ffp = cache ? cache + (size_t)(p * a.O + o) * N2 : nullptr;
         const float occ = a.occu[o];
         const bool first = (p == pbeg && o == 0);
@@ -502,8 +508,9 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
               return true;
             };
         const float2* cache = (!EXT && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
-        if (cache) {   // k_forward left F(ψ_out) of this (p, o) and ψ⁰ of p: no recomputed forward
-          psi_rd = cache + (size_t)(a.P * a.O + p) * N2;
+        if (cache) {   // k_forward left F(ψ_out) of this (p, o) and ψ⁰ of p (Nz = 1) or every
+                       // slice's ψⁿ of (p, o) (Nz > 1): no recomputed forward
+          psi_rd = cache + (size_t)(a.P * a.O + (a.Nz > 1 ? (p * a.O + o) * a.Nz : p)) * N2;
           const float2* ffp = cache + (size_t)(p * a.O + o) * N2;
           for (int e = opaque_tid(); e < N2; e += NT) {
             const int y = e / N, x = e % N;
@@ -762,7 +769,7 @@ struct ptyx_plan {
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* hslab = nullptr;    // PTYX_PROP_GRAD: per-workgroup dL/dH slabs
-  float2* ffc = nullptr;      // far-field cache (general engine, Nz = 1, P·O > 1)
+  float2* ffc = nullptr;      // far-field cache (general engine, P·O > 1)
   long long ffc_per = 0, ffc_cap = 0;
   float2* scratch = nullptr;
   // register engines (k_fused3 / k_fused3ms): per-pattern object-gradient slots
@@ -1032,14 +1039,16 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
     }
   }
-  if (!stripe && d.Nz == 1 && d.P * d.O > 1) {
-    // far-field cache: (P·O + P)·N² float2 per pattern of a call, within PTYX_FFC_MB (default the
-    // smaller of 64 GiB and a third of the free HBM); calls beyond its capacity are split by the host
+  if (!stripe && d.P * d.O > 1) {
+    // far-field cache: per pattern of a call the P·O far fields plus ψ⁰ of every probe mode (Nz = 1)
+    // or every slice's ψⁿ of every (p, o) (Nz > 1) — (P·O + P)·N² or P·O·(1 + Nz)·N² float2 —
+    // within PTYX_FFC_MB (default the smaller of 64 GiB and a third of the free HBM); calls beyond
+    // its capacity are split by the host
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     long long mb = std::min<long long>(65536, (long long)(free_b / 3 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_FFC_MB")) mb = std::atoll(e);
-    const long long per = (long long)(d.P * d.O + d.P) * (long long)N2;
+    const long long per = (long long)(d.Nz > 1 ? d.P * d.O * (1 + d.Nz) : d.P * d.O + d.P) * (long long)N2;
     const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (per * (long long)sizeof(float2)));
     if (cap >= std::min<long long>(d.max_patterns, pl->nwg)) {
       if ((rc = dalloc(pl, &pl->ffc, (size_t)cap * per))) {
@@ -1849,7 +1858,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
 #else
   *engine = (fused3 || fused3ms) ? kEngFused3 : stripe ? kEngStripe : kEngTwoPass;
 #endif
-  if (*engine == kEngTwoPass && any_grad && pl->ffc && n_idx <= pl->ffc_cap) {   // k_forward fills it, k_adjoint reads it
+  // (not with propagator gradients: k_adjoint's recomputed forward is what parks their Xⁿ)
+  if (*engine == kEngTwoPass && any_grad && pl->ffc && n_idx <= pl->ffc_cap && !a.hslab && !a.d_tilts && !a.d_dz) {
     a.ffc = pl->ffc;
     a.ffc_per = pl->ffc_per;
   }
