@@ -66,8 +66,9 @@ struct KArgs {
   float dz;
   float* d_tilts;
   float* d_dz;      // ramp part of dL/d(dz) with per-position tilts
-  // far-field cache (general engine, Nz = 1, P·O > 1): k_forward leaves every mode's F(ψ_out)
-  // and every probe mode's ψ⁰ per pattern, so k_adjoint skips the recomputed forward
+  // far-field cache (general engine, P·O > 1): k_forward leaves every mode's F(ψ_out) and ψ⁰ of
+  // every probe mode (Nz = 1) or every slice's ψⁿ (Nz > 1) per pattern, so k_adjoint skips the
+  // recomputed forward
   float2* ffc;
   long long ffc_per;   // float2 per pattern: (P·O + P)·N² (Nz = 1) or P·O·(1 + Nz)·N²
   // probe-mode split (small calls, P > 1): msplit = P makes every (pattern, probe mode) its own
@@ -75,6 +76,10 @@ struct KArgs {
   // ((pattern·P + p)·N² floats) and k_forward_modesum forms I, dp and the loss sums
   int msplit = 1;
   float* Imodes = nullptr;
+  // N = 256 fused chains (g256_fstage): F(P_p) and H transposed, written by k_probe_spectrum,
+  // so the stages that run on the transposed array read them along its rows
+  float2* FpT = nullptr;   // (P, N, N): FpT[p][x][y] = F(P_p)[y][x]   (shifted probes)
+  float2* HT = nullptr;    // (N, N):    HT[x][y] = H[y][x]             (Nz > 1)
 };
 // calls of at most this many patterns split their probe modes over workgroups (general engine)
 constexpr int kModeSplitCap = 128;

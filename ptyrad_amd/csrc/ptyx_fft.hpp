@@ -338,14 +338,47 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
 // 64-row blocks entirely on chip (DFT16 over n2, twiddle W256^(n1·k2), LDS exchange, DFT16
 // over n1) and stores the block TRANSPOSED, so stage 2 is the same row kernel on the
 // transposed array, whose transposed store restores the natural orientation.  Both stores go
-// through an LDS tile and leave as 64 consecutive points (512 B) per line.
+// through an LDS tile and leave as 64 consecutive points (512 B) per line.  The multislice
+// chains fuse the stages of consecutive transforms further (g256_fstage).
 constexpr int kG256RowStride = 16 * 17;                 // [row][k2][n1], one pad per 16
 constexpr int kG256Elems = 64 * kG256RowStride;         // ≥ 256 × 65 (transposed tile)
 static_assert(kG256Elems >= 256 * 65, "tile too small");
 
-template <int DIR, bool FIRST, bool LAST, bool PRELOAD, class Pre, class Post>
-__device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float2* __restrict__ dst, float2* lds,
-                                           const float2* tw, Pre& pre, Post& post) {
+// One length-256 DFT along a block row held by its 16 threads: thread q holds the points
+// q + 16·n2 (n2 = 0..15) in v[n2] and gets back X[q + 16·k1] in v[k1] — the same layout, so two
+// row DFTs can follow each other with a point-wise step in between.
+template <int DIR>
+__device__ __forceinline__ void g256_row_dft(float2 (&v)[16], float2* lds, int lr, int q, const float2* tw) {
+  DFT<16, DIR>::run(v);
+#pragma unroll
+  for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, q * k2));
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) lds[lr * kG256RowStride + k2 * 17 + q] = v[k2];
+  // the exchange stays inside the wave (its 4 rows): LDS ops retired, no workgroup barrier
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) v[n1] = lds[lr * kG256RowStride + q * 17 + n1];
+  DFT<16, DIR>::run(v);                       // X[row][q + 16·k1] = v[k1]
+}
+
+struct NoMid {
+  __device__ __forceinline__ void operator()(int, int, float2&) const {}
+};
+
+// One N = 256 stage over the 64-row blocks of src: [pre] → row DFT (DIR1; 0 = none) → mid(y, x, v)
+// → row DFT (DIR2; 0 = none) → transposed store into dst (STORE), post(y, x, v) on the way out
+// (POST).  SRC_T: src holds the transposed array (its rows are columns of the natural one); pre,
+// mid and post always see natural coordinates.  A 2-D FFT is two stages; between an FFT and the
+// next inverse FFT of the multislice chain the point-wise step (×H, ×Oⁿ, the slice adjoint)
+// runs between the two row DFTs of ONE stage (the second axis of one transform and the first
+// axis of the next are the same rows), so the chain makes one round trip per transform instead
+// of two (forward_far_g256 / k_adjoint).
+template <int DIR1, int DIR2, bool SRC_T, bool FIRST, bool PRELOAD, bool STORE, bool POST, class Pre, class Mid,
+          class Post>
+__device__ __forceinline__ void g256_fstage(const float2* __restrict__ src, float2* __restrict__ dst, float2* lds,
+                                            const float2* tw, Pre& pre, Mid& mid, Post& post) {
   constexpr int N = 256;
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
@@ -355,46 +388,57 @@ __device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float
     float2 v[16];
 #pragma unroll
     for (int n2 = 0; n2 < 16; ++n2) {
-      const int x = q + 16 * n2;
+      const int j = q + 16 * n2;
+      const int y = SRC_T ? j : row, x = SRC_T ? row : j;
       if constexpr (FIRST) {
-        if constexpr (PRELOAD) v[n2] = call_pre(pre, row, x, src[row * N + x], n2);
-        else v[n2] = call_pre(pre, row, x, make_float2(0.f, 0.f), n2);
+        if constexpr (PRELOAD) v[n2] = call_pre(pre, y, x, src[row * N + j], n2);
+        else v[n2] = call_pre(pre, y, x, make_float2(0.f, 0.f), n2);
         if constexpr (kFuseGroup > 0 && !kSlotPre<Pre>) {
           if ((n2 + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
         }
       } else {
-        v[n2] = src[row * N + x];
+        v[n2] = src[row * N + j];
       }
     }
-    DFT<16, DIR>::run(v);
+    if constexpr (DIR1 != 0) g256_row_dft<DIR1>(v, lds, lr, q, tw);
+    if constexpr (!std::is_same_v<Mid, NoMid>) {
 #pragma unroll
-    for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], twiddle<DIR>(tw, q * k2));
+      for (int k = 0; k < 16; ++k) {
+        const int j = q + 16 * k;
+        mid(SRC_T ? j : row, SRC_T ? row : j, v[k]);
+        if constexpr (kFuseGroup > 0) {
+          if ((k + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    if constexpr (DIR2 != 0) g256_row_dft<DIR2>(v, lds, lr, q, tw);
+    if constexpr (STORE) {
+      __syncthreads();
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) lds[lr * kG256RowStride + k2 * 17 + q] = v[k2];
-    // the exchange stays inside the wave (its 4 rows): LDS ops retired, no workgroup barrier
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int n1 = 0; n1 < 16; ++n1) v[n1] = lds[lr * kG256RowStride + q * 17 + n1];
-    DFT<16, DIR>::run(v);                     // X[row][q + 16·k1] = v[k1]
-    __syncthreads();
-#pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) lds[(q + 16 * k1) * 65 + lr] = v[k1];
-    __syncthreads();
-    // transposed store: dst[k][r0 + c] for k = 0..255, c = 0..63, 64 consecutive per line
+      for (int k1 = 0; k1 < 16; ++k1) lds[(q + 16 * k1) * 65 + lr] = v[k1];
+      __syncthreads();
+      // transposed store: dst[k][r0 + c] for k = 0..255, c = 0..63, 64 consecutive per line
 #pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int e = tid + 1024 * i, k = e >> 6, c = e & 63;
-      float2 val = lds[k * 65 + c];
-      if constexpr (LAST) {
-        if (call_post(post, k, r0 + c, val, i)) dst[k * N + r0 + c] = val;
-      } else {
-        dst[k * N + r0 + c] = val;
+      for (int i = 0; i < 16; ++i) {
+        const int e = tid + 1024 * i, k = e >> 6, c = e & 63;
+        float2 val = lds[k * 65 + c];
+        if constexpr (POST) {
+          if (call_post(post, SRC_T ? k : r0 + c, SRC_T ? r0 + c : k, val, i)) dst[k * N + r0 + c] = val;
+        } else {
+          dst[k * N + r0 + c] = val;
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
+  if constexpr (!STORE) __syncthreads();
+}
+
+template <int DIR, bool FIRST, bool LAST, bool PRELOAD, class Pre, class Post>
+__device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float2* __restrict__ dst, float2* lds,
+                                           const float2* tw, Pre& pre, Post& post) {
+  NoMid nm;
+  g256_fstage<DIR, 0, LAST, FIRST, PRELOAD, true, LAST>(src, dst, lds, tw, pre, nm, post);
 }
 
 template <int DIR, bool PRELOAD, class Pre, class Post>

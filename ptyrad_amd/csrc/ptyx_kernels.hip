@@ -116,6 +116,82 @@ __device__ __forceinline__ void forward_chain(const KArgs& a, const Arr& arr, co
   }
 }
 
+// N = 256: forward_chain and the far-field FFT in 2·Nz + 1 stages instead of 4·Nz (shifted
+// probes).  Every inverse FFT runs columns first, so each point-wise step sits between the two
+// row DFTs of one g256_fstage: ×Oⁿ (and the ψⁿ stores) on natural rows, ×H on transposed rows
+// (HT, read along them).  ff(y, x, v) is the far field's store hook (natural coordinates, like
+// fft2d's post); returns the buffer of the scratch pair the far field went to (when ff stores).
+template <bool STORE_PSI, class FF>
+__device__ __forceinline__ float2* forward_far_g256(const KArgs& a, const GlobalPair<256>& arr, const float2* tw,
+                                                    const float2* wy, const float2* wx, const PatternGeom& g, int p,
+                                                    int o, float2* psi, bool sparse, float& sp_acc, const float2* ty,
+                                                    const float2* tx, float2* psi0, bool reuse0, FF& ff) {
+  constexpr int N = 256;
+  constexpr int N2 = N * N;
+  constexpr float inv_n2 = 1.0f / (float)N2;
+  auto mul_obj = [&](int n, int y, int x, float2 w) -> float2 {
+    const size_t off = obj_off(a, o, n, g.cy + y, g.cx + x);
+    const float A = a.obja[off], ph = a.objp[off];
+    float sn, cs;
+    phase_sincos(ph, &sn, &cs);
+    if (sparse) {
+      const float ap = fabsf(ph);
+      sp_acc += a.sparse_n == 1 ? ap : powq(ap, (float)a.sparse_n);
+    }
+    return cmul(w, make_float2(A * cs, A * sn));
+  };
+  float2* A = arr.a;
+  float2* B = arr.b;
+  float2* L = arr.lds;
+  auto id_pre = [](int, int, float2 v) { return v; };
+  auto store_all = [](int, int, float2&) { return true; };
+  NoMid none;
+  // first axis of F(ψ⁰ ⊙ O₀) → A (transposed)
+  if (a.shift && reuse0) {   // ψ⁰ of p parked by the o = 0 pass
+    auto pre = [&](int y, int x, float2 w) {
+      if (STORE_PSI && psi != psi0) psi[y * N + x] = w;
+      return mul_obj(0, y, x, w);
+    };
+    g256_fstage<-1, 0, false, true, true, true, false>(psi0, A, L, tw, pre, none, store_all);
+  } else if (a.shift) {      // ψ⁰ = F⁻¹(F(P) ⊙ W_b): columns (transposed rows of F(P)ᵀ), then rows
+    const float2* FpT = a.FpT + (size_t)p * N2;
+    auto pre = [&](int y, int x, float2) { return cmul(cmul(FpT[x * N + y], wy[y]), wx[x]); };
+    g256_fstage<+1, 0, true, true, false, true, false>(nullptr, B, L, tw, pre, none, store_all);
+    auto mid = [&](int y, int x, float2& v) {
+      const float2 w = cscale(v, inv_n2);
+      if (STORE_PSI) psi[y * N + x] = w;
+      if (psi0 && !(STORE_PSI && psi == psi0)) psi0[y * N + x] = w;
+      v = mul_obj(0, y, x, w);
+    };
+    g256_fstage<+1, -1, false, false, false, true, false>(B, A, L, tw, id_pre, mid, store_all);
+  } else {                   // broadcast probe
+    const float2* P0 = a.probe + (size_t)p * N2;
+    auto pre = [&](int y, int x, float2) {
+      const float2 w = P0[y * N + x];
+      if (STORE_PSI) psi[y * N + x] = w;
+      return mul_obj(0, y, x, w);
+    };
+    g256_fstage<-1, 0, false, true, false, true, false>(nullptr, A, L, tw, pre, none, store_all);
+  }
+  // ψⁿ = F⁻¹(H ⊙ F(ψⁿ⁻¹ ⊙ Oⁿ⁻¹))   (forward.py:60-63)
+  for (int n = 1; n < a.Nz; ++n) {
+    auto mh = [&](int y, int x, float2& v) {
+      v = cmul(v, a.HT[x * N + y]);
+      if (ty) v = cmul(v, cmul(ty[y], tx[x]));
+    };
+    g256_fstage<-1, +1, true, false, false, true, false>(A, B, L, tw, id_pre, mh, store_all);
+    auto mo = [&](int y, int x, float2& v) {
+      const float2 w = cscale(v, inv_n2);
+      if (STORE_PSI) psi[(size_t)n * N2 + y * N + x] = w;
+      v = mul_obj(n, y, x, w);
+    };
+    g256_fstage<+1, -1, false, false, false, true, false>(B, A, L, tw, id_pre, mo, store_all);
+  }
+  // second axis of the far-field FFT, stored through ff
+  g256_fstage<-1, 0, true, false, false, true, true>(A, B, L, tw, id_pre, none, ff);
+  return B;
+}
+
 // per-position tilt ramps of pattern s: ty[y] = exp(i dz Ky[y] tan(θy/1e3)), tx likewise
 // (the separable factor of exp(i dz (Ky tan θy + Kx tan θx)), models.py:330-356)
 template <int N, int NT>
@@ -138,9 +214,16 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* 
   constexpr bool LDS = Geo<N>::kLds;
   __shared__ float2 s_tw[N];
   __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
+  const int p = blockIdx.x;
+  if constexpr (N == 256) {
+    if (p == a.P) {   // the extra workgroup of a Nz > 1 call: HT = Hᵀ for the fused chains
+      for (int e = threadIdx.x; e < N * N; e += NT) a.HT[(e % N) * N + e / N] = a.H[e];
+      return;
+    }
+    if (!a.shift) return;
+  }
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   __syncthreads();
-  const int p = blockIdx.x;
   typename ArrayFor<N, LDS>::type arr;
   if constexpr (LDS) arr.p = s_buf;
   else {
@@ -154,6 +237,9 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* 
       arr, s_tw, [&](int y, int x, float2) { return P0[y * N + x]; },
       [&](int y, int x, float2& v) {
         out[y * N + x] = v;
+        if constexpr (N == 256) {
+          if (a.FpT) a.FpT[(size_t)p * N * N + x * N + y] = v;
+        }
         return false;
       });
 }
@@ -210,35 +296,38 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;
         float sp = 0.f;
-        if (cache && a.Nz > 1) {   // the cache keeps every slice's ψⁿ of (p, o) for k_adjoint
-          float2* psis = cache + (size_t)(a.P * a.O + (p * a.O + o) * a.Nz) * N2;
-          forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psis, sparse, sp, nullptr,
-                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, a.O > 1 ? psi0 : nullptr, o > 0);
-        } else {
-          float2* park0 = cache ? cache + (size_t)(a.P * a.O + p) * N2 : (a.O > 1 ? psi0 : nullptr);
-          forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr,
-                                      tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, park0, o > 0);
-        }
         float2* ffp = cache ? cache + (size_t)(p * a.O + o) * N2 : nullptr;
         const float occ = a.occu[o];
         const bool first = (p == pbeg && o == 0);
         // far field  Ψ = fftshift(F_o ψ_out)   (forward.py:79)
-        fft2d<N, NT, -1, true>(
-            arr, s_tw, [&](int, int, float2 v) { return v; },
-            [&](int y, int x, float2& v) {
-              if (ffp) ffp[y * N + x] = v;
-              const float2 Psi = cscale(v, inv_n);
-              const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
-              const float c = occ * cabs2(Psi);
-              if constexpr (SINGLE) {
-                const float I = c + kDpEps;
-                if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
-                if (want_sums) add_sums(I, meas_at(a, g.m, e, N2));
-              } else {
-                Ip[e] = first ? c : Ip[e] + c;
-              }
-              return false;
-            });
+        auto ff = [&](int y, int x, float2& v) {
+          if (ffp) ffp[y * N + x] = v;
+          const float2 Psi = cscale(v, inv_n);
+          const int e = ((y + N / 2) % N) * N + (x + N / 2) % N;
+          const float c = occ * cabs2(Psi);
+          if constexpr (SINGLE) {
+            const float I = c + kDpEps;
+            if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
+            if (want_sums) add_sums(I, meas_at(a, g.m, e, N2));
+          } else {
+            Ip[e] = first ? c : Ip[e] + c;
+          }
+          return false;
+        };
+        // the cache keeps every slice's ψⁿ of (p, o) for k_adjoint (Nz > 1), else ψ⁰ of p
+        float2* psis = (cache && a.Nz > 1) ? cache + (size_t)(a.P * a.O + (p * a.O + o) * a.Nz) * N2 : nullptr;
+        float2* park0 = psis ? (a.O > 1 ? psi0 : nullptr)
+                             : cache ? cache + (size_t)(a.P * a.O + p) * N2 : (a.O > 1 ? psi0 : nullptr);
+        const float2* ty = tilt ? s_ty : nullptr;
+        const float2* tx = tilt ? s_tx : nullptr;
+        if constexpr (N == 256) {
+          if (psis) forward_far_g256<true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psis, sparse, sp, ty, tx, park0, o > 0, ff);
+          else forward_far_g256<false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, ty, tx, park0, o > 0, ff);
+        } else {
+          if (psis) forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psis, sparse, sp, nullptr, ty, tx, park0, o > 0);
+          else forward_chain<N, NT, false>(a, arr, s_tw, s_wy, s_wx, g, p, o, nullptr, sparse, sp, nullptr, ty, tx, park0, o > 0);
+          fft2d<N, NT, -1, true>(arr, s_tw, [&](int, int, float2 v) { return v; }, ff);
+        }
         if (sparse) {
           float v1[1] = {sp};
           block_sum<NT, 1>(v1, s_red);
@@ -507,24 +596,6 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
               v = cscale(Psi, 2.0f * occ * dLdI);
               return true;
             };
-        const float2* cache = (!EXT && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
-        if (cache) {   // k_forward left F(ψ_out) of this (p, o) and ψ⁰ of p (Nz = 1) or every
-                       // slice's ψⁿ of (p, o) (Nz > 1): no recomputed forward
-          psi_rd = cache + (size_t)(a.P * a.O + (a.Nz > 1 ? (p * a.O + o) * a.Nz : p)) * N2;
-          const float2* ffp = cache + (size_t)(p * a.O + o) * N2;
-          for (int e = opaque_tid(); e < N2; e += NT) {
-            const int y = e / N, x = e % N;
-            float2 v = ffp[e];
-            ff_post(y, x, v);
-            arr.st(y, x, v);
-          }
-          __syncthreads();
-        } else {
-          psi_rd = psi;
-          forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
-                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0);
-          fft2d<N, NT, -1, true>(arr, s_tw, [&](int, int, float2 v) { return v; }, ff_post);
-        }
         // adjoint of slice n: g_O += conj(ψ^n) g → dA, dφ; g ← g ⊙ conj(O_n)
         auto slice_adj = [&](int n, int y, int x, float2 gv) -> float2 {
           const size_t off = obj_off(a, o, n, g.cy + y, g.cx + x);
@@ -548,6 +619,69 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
           const int e = y * N + x;
           gacc[e] = (o == 0) ? gv : cadd(gacc[e], gv);
         };
+        const float2* cache = (!EXT && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
+        // k_forward left F(ψ_out) of this (p, o) and ψ⁰ of p (Nz = 1) or every slice's ψⁿ of (p, o)
+        // (Nz > 1) in the cache: no recomputed forward
+        const float2* psi_c = cache ? cache + (size_t)(a.P * a.O + (a.Nz > 1 ? (p * a.O + o) * a.Nz : p)) * N2 : nullptr;
+        if constexpr (N == 256) {
+          if (!xs) {   // fused stages (forward_far_g256): 2·Nz + 1 round trips per mode instead of 4·Nz - 1
+            const int Nz = a.Nz;
+            float2* A = arr.a;
+            float2* B = arr.b;
+            auto id_pre = [](int, int, float2 v) { return v; };
+            auto store_all = [](int, int, float2&) { return true; };
+            NoMid none;
+            // g_Ψ → A, transposed
+            if (cache) {
+              psi_rd = psi_c;
+              auto pre = [&](int y, int x, float2 v) {
+                ff_post(y, x, v);
+                return v;
+              };
+              g256_fstage<0, 0, false, true, true, true, false>(cache + (size_t)(p * a.O + o) * N2, A, arr.lds, s_tw,
+                                                                pre, none, store_all);
+            } else {
+              psi_rd = psi;
+              float2* X = forward_far_g256<true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy,
+                                                 tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0, ff_post);
+              g256_fstage<0, 0, false, false, false, true, false>(X, A, arr.lds, s_tw, id_pre, none, store_all);
+            }
+            // F_o⁻¹ columns first; each slice adjoint sits between its inverse rows and the next
+            // forward rows, each conj(H) between forward columns and inverse columns
+            g256_fstage<+1, 0, true, false, false, true, false>(A, B, arr.lds, s_tw, id_pre, none, store_all);
+            for (int n = Nz - 1; n >= 1; --n) {
+              const float sc = n == Nz - 1 ? inv_n : inv_n2;
+              auto ma = [&](int y, int x, float2& v) { v = slice_adj(n, y, x, cscale(v, sc)); };
+              g256_fstage<+1, -1, false, false, false, true, false>(B, A, arr.lds, s_tw, id_pre, ma, store_all);
+              auto mh = [&](int y, int x, float2& v) {
+                float2 Hb = a.HT[x * N + y];
+                if (tilt) Hb = cmul(Hb, cmul(s_ty[y], s_tx[x]));
+                v = cmulc(v, Hb);
+              };
+              g256_fstage<-1, +1, true, false, false, true, false>(A, B, arr.lds, s_tw, id_pre, mh, store_all);
+            }
+            const float sc0 = Nz == 1 ? inv_n : inv_n2;
+            auto m0 = [&](int y, int x, float2& v) { acc_probe(y, x, slice_adj(0, y, x, cscale(v, sc0))); };
+            g256_fstage<+1, 0, false, false, false, false, false>(B, nullptr, arr.lds, s_tw, id_pre, m0, store_all);
+            continue;
+          }
+        }
+        if (cache) {
+          psi_rd = psi_c;
+          const float2* ffp = cache + (size_t)(p * a.O + o) * N2;
+          for (int e = opaque_tid(); e < N2; e += NT) {
+            const int y = e / N, x = e % N;
+            float2 v = ffp[e];
+            ff_post(y, x, v);
+            arr.st(y, x, v);
+          }
+          __syncthreads();
+        } else {
+          psi_rd = psi;
+          forward_chain<N, NT, true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy, xs,
+                                     tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0);
+          fft2d<N, NT, -1, true>(arr, s_tw, [&](int, int, float2 v) { return v; }, ff_post);
+        }
         const int Nz = a.Nz;
         // F_o^-1 (ortho adjoint of F_o, fftshift undone by the index map above)
         fft2d<N, NT, +1, true>(
@@ -762,6 +896,8 @@ struct ptyx_plan {
   int nwg = 0;  // persistent workgroups for k_forward / k_adjoint
   float2* twg = nullptr;
   float2* Fp = nullptr;
+  float2* FpT = nullptr;      // N = 256: F(P) and H transposed for the fused chains (KArgs::FpT / HT)
+  float2* HT = nullptr;
   float* psums = nullptr;
   float* coef = nullptr;
   float* Ibuf = nullptr;
@@ -991,7 +1127,9 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       (rc = dalloc(pl, &pl->slab, (size_t)pl->nwg * d.P * N2)) ||
       (rc = dalloc(pl, &pl->Gsum, d.P * N2)) ||
       (rc = dalloc(pl, &pl->hslab, prop_grad ? (size_t)pl->nwg * N2 : 0)) ||
-      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride))) {
+      (rc = dalloc(pl, &pl->scratch, (size_t)pl->nwg * pl->scratch_stride)) ||
+      (rc = dalloc(pl, &pl->FpT, d.N == 256 && (d.flags & PTYX_SHIFT_PROBES) ? d.P * N2 : 0)) ||
+      (rc = dalloc(pl, &pl->HT, d.N == 256 && d.Nz > 1 ? N2 : 0))) {
     free_plan(pl);
     return rc;
   }
@@ -1184,13 +1322,15 @@ static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t
   a.Ibuf = pl->Ibuf;
   a.slab = pl->slab; a.scratch = pl->scratch; a.scratch_stride = pl->scratch_stride;
   a.twg = pl->twg;
+  a.FpT = pl->FpT;
+  a.HT = pl->HT;
   return a;
 }
 
 template <int N>
 static void launch_spectrum(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
   ProfScope ps(pl, kKSpectrum, st);
-  hipLaunchKernelGGL(k_probe_spectrum<N>, dim3(pl->d.P), dim3(Geo<N>::NT), 0, st, a, pl->Fp);
+  hipLaunchKernelGGL(k_probe_spectrum<N>, dim3(pl->d.P + (a.HT ? 1 : 0)), dim3(Geo<N>::NT), 0, st, a, pl->Fp);
 }
 template <int N>
 static void launch_forward(const ptyx_plan* pl, const KArgs& a, hipStream_t st) {
@@ -1510,7 +1650,11 @@ static int stripe_pass(ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, 
   const int n = a.n_idx, P = d.P, O = d.O;
   const bool single = cfg->single_on != 0;
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;     // object / probe prepared by the previous call
-  if (!reuse) launch_spectrum<256>(pl, a, st);         // F(P_p), natural order
+  if (!reuse) {                                         // F(P_p), natural order (no transposed copy)
+    KArgs b = a;
+    b.FpT = nullptr;
+    launch_spectrum<256>(pl, b, st);
+  }
   {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
@@ -1778,7 +1922,7 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
   KArgs a = make_args(pl, in, idx, n_idx);
   a.dp_out = dp_out;
   a.psums = nullptr;
-  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  if (a.shift || a.HT) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
   PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, a, st);
   return launch_status("ptyx_forward launch");
 }
@@ -1903,7 +2047,7 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
     b.Imodes = pl->Imodes;
   }
   if (ph != kPhaseEnd) {
-    if (b.shift && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, b, st);
+    if ((b.shift || b.HT) && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, b, st);
     PTYX_DISPATCH_N(pl->d.N, launch_forward, pl, b, st);
     if ((rc = launch_status("k_forward launch"))) return rc;
     if (b.msplit > 1) {
@@ -2039,7 +2183,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   a.d_shifts = gz.d_shifts;
   a.need_probe = gz.d_probe != nullptr;
   if ((rc = setup_prop_grad(pl, gz, a))) return rc;
-  if (a.shift) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
+  if (a.shift || a.HT) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, a, st);
   PTYX_DISPATCH_N(pl->d.N, launch_adjoint, pl, a, st, true);
   if ((rc = launch_status("k_adjoint(ext) launch"))) return rc;
   if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;

@@ -202,6 +202,61 @@ def test_n256_mixed_state_vs_oracle():
     assert rel(g["shifts"], og["shifts"]) < TOL_SH
 
 
+@pytest.mark.parametrize("P,O,Nz,shift", [(2, 1, 3, True), (1, 1, 3, True), (1, 2, 2, False), (2, 2, 2, True),
+                                          (1, 3, 1, True)])
+def test_n256_general_engine_vs_oracle(P, O, Nz, shift):
+    """N = 256 through the general two-pass engine (multislice, or more object modes than the
+    stripe engine takes) — the fused g256_fstage chains, with and without the far-field cache
+    (P·O > 1 vs P·O = 1), ψ⁰ parking (O > 1) and broadcast probes: ragged mini-batches vs the
+    oracle, plus ptyx_forward's DPs and the external-dL/dI adjoint."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(256, 3, 3, P=P, O=O, Nz=Nz, seed=40 + 7 * P + O + Nz)
+    d = dict(obja=pr.obja, objp=(pr.objp / Nz).astype(np.float32), probe=pr.probe * np.float32(30.0),
+             shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=shift,
+             loss_params=orc_default_loss())
+    perm = np.random.default_rng(P + O + Nz).permutation(9)
+    batches = [perm[:4], perm[4:5], perm[5:]]
+    ks = {}
+    terms, dp, g, plan = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
+    assert "k_adjoint" in ks and "k_s1" not in ks, ks
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"],
+                                             shift_probes=shift, grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    if shift:
+        assert rel(g["shifts"], og["shifts"]) < TOL_SH
+    t = tensors(d, device)
+    b = perm[:5].astype(np.int32)
+    dpf = torch.zeros((len(b), 256, 256), device=device)
+    plan.forward(t, b, dp_out=dpf)
+    torch.cuda.synchronize()
+    assert rel(dpf.cpu().numpy(), np.concatenate(odps)[:5]) < TOL_DP
+    # external dL/dI through k_adjoint<EXT> (recomputed forward, no cache)
+    amp, ph = orc.get_patches(d["obja"], d["objp"], d["crop_pos"], b, 256)
+    probes = orc.get_probes(d["probe"], d["shifts"][b], shift)
+    cache = orc.forward(amp, ph, probes, d["H"], d["occu"])
+    dLdI = np.random.default_rng(1).standard_normal(cache.dp.shape).astype(np.float32) * 1e-3
+    dA, dP, dprobe, _ = orc.adjoint(cache, dLdI, np.zeros_like(ph, np.float64), amp, ph, d["probe"],
+                                    d["shifts"][b], d["H"], d["occu"], shift)
+    gA = np.zeros(d["obja"].shape)
+    gP = np.zeros(d["objp"].shape)
+    for i, s in enumerate(b):
+        cy, cx = d["crop_pos"][s]
+        gA[:, :, cy:cy + 256, cx:cx + 256] += dA[i]
+        gP[:, :, cy:cy + 256, cx:cx + 256] += dP[i]
+    grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe")}
+    plan.adjoint_dldi(t, b, torch.tensor(dLdI, device=device), grads)
+    torch.cuda.synchronize()
+    assert rel(grads["obja"].cpu().numpy(), gA) < TOL_G
+    assert rel(grads["objp"].cpu().numpy(), gP) < TOL_G
+    gp = grads["probe"].cpu().numpy()
+    assert rel(gp[..., 0] + 1j * gp[..., 1], dprobe) < TOL_G
+
+
 def orc_default_loss():
     return {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
             "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
