@@ -18,10 +18,12 @@ static_assert(kNBatchSum == PTYX_BATCH_SUMS, "include/ptyx.h PTYX_BATCH_SUMS");
 constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
 
 template <int N> struct Geo;
-template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true; };
-template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true; };
-template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true; };
-template <> struct Geo<256> { static constexpr int NT = 1024; static constexpr bool kLds = false; };
+// kWaves: minimum waves per SIMD the general-engine kernels are compiled for (≤ 512 / kWaves
+// VGPRs); N = 256 runs two 512-thread workgroups per CU (LDS ≈ 78 KiB each)
+template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
+template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
+template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
+template <> struct Geo<256> { static constexpr int NT = kG256Threads; static constexpr bool kLds = false; static constexpr int kWaves = 4; };
 
 struct KArgs {
   int P, O, Nz, Ny, Nx, n_scans;

@@ -335,14 +335,16 @@ __device__ __forceinline__ void stockham_pass(const Src& src, const Dst& dst, co
 // ---------------------------------------------------------------- N = 256, two stages
 // A 256² complex array (512 KiB) does not fit one CU, so each 2-D FFT makes ONE round trip
 // through the workgroup's global scratch instead of one per Stockham pass: stage 1 transforms
-// 64-row blocks entirely on chip (DFT16 over n2, twiddle W256^(n1·k2), LDS exchange, DFT16
+// 32-row blocks (512 threads, 16 a row; ≈ 78 KiB of LDS, two workgroups a CU) entirely on chip (DFT16 over n2, twiddle W256^(n1·k2), LDS exchange, DFT16
 // over n1) and stores the block TRANSPOSED, so stage 2 is the same row kernel on the
 // transposed array, whose transposed store restores the natural orientation.  Both stores go
-// through an LDS tile and leave as 64 consecutive points (512 B) per line.  The multislice
+// through an LDS tile and leave as 32 consecutive points (256 B) per line.  The multislice
 // chains fuse the stages of consecutive transforms further (g256_fstage).
+constexpr int kG256Threads = 512;                       // workgroup size of the N = 256 kernels
+constexpr int kG256Rows = kG256Threads / 16;            // rows per block: 16 threads a row
 constexpr int kG256RowStride = 16 * 17;                 // [row][k2][n1], one pad per 16
-constexpr int kG256Elems = 64 * kG256RowStride;         // ≥ 256 × 65 (transposed tile)
-static_assert(kG256Elems >= 256 * 65, "tile too small");
+constexpr int kG256Tile = kG256Rows + 1;                // transposed tile [256][rows + 1]
+constexpr int kG256Elems = kG256Rows * kG256RowStride > 256 * kG256Tile ? kG256Rows * kG256RowStride : 256 * kG256Tile;
 
 // One length-256 DFT along a block row held by its 16 threads: thread q holds the points
 // q + 16·n2 (n2 = 0..15) in v[n2] and gets back X[q + 16·k1] in v[k1] — the same layout, so two
@@ -383,7 +385,7 @@ __device__ __forceinline__ void g256_fstage(const float2* __restrict__ src, floa
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
   const int lr = tid >> 4, q = tid & 15;   // block row, n1 (step 1) / k2 (step 2)
-  for (int r0 = 0; r0 < N; r0 += 64) {
+  for (int r0 = 0; r0 < N; r0 += kG256Rows) {
     const int row = r0 + lr;
     float2 v[16];
 #pragma unroll
@@ -415,13 +417,13 @@ __device__ __forceinline__ void g256_fstage(const float2* __restrict__ src, floa
     if constexpr (STORE) {
       __syncthreads();
 #pragma unroll
-      for (int k1 = 0; k1 < 16; ++k1) lds[(q + 16 * k1) * 65 + lr] = v[k1];
+      for (int k1 = 0; k1 < 16; ++k1) lds[(q + 16 * k1) * kG256Tile + lr] = v[k1];
       __syncthreads();
-      // transposed store: dst[k][r0 + c] for k = 0..255, c = 0..63, 64 consecutive per line
+      // transposed store: dst[k][r0 + c] for k = 0..255, c < kG256Rows consecutive per line
 #pragma unroll 4
       for (int i = 0; i < 16; ++i) {
-        const int e = tid + 1024 * i, k = e >> 6, c = e & 63;
-        float2 val = lds[k * 65 + c];
+        const int e = tid + kG256Threads * i, k = e / kG256Rows, c = e % kG256Rows;
+        float2 val = lds[k * kG256Tile + c];
         if constexpr (POST) {
           if (call_post(post, SRC_T ? k : r0 + c, SRC_T ? r0 + c : k, val, i)) dst[k * N + r0 + c] = val;
         } else {
@@ -465,7 +467,7 @@ __device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pr
     }
   } else {
     static_assert(R2 != 1, "global ping-pong needs two passes per dimension");
-    if constexpr (N == 256 && NT == 1024) {
+    if constexpr (N == 256 && NT == kG256Threads) {
       fft2d_g256<DIR, PRELOAD>(arr, tw, pre, post);
       return;
     }

@@ -209,7 +209,7 @@ __device__ __forceinline__ void build_tilt_ramps(const KArgs& a, int s, float2* 
 // =====================================================================================
 // k_probe_spectrum: Fp[p] = F(P_p)
 template <int N>
-__global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* Fp_out) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_spectrum(KArgs a, float2* Fp_out) {
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   __shared__ float2 s_tw[N];
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_probe_spectrum(KArgs a, float2* 
 // k_forward: I = Σ_{p,o} occ_o |S F_o ψ_out|² + eps per pattern; dp_out; loss partial sums.
 // SINGLE: P·O == 1, the loss sums are taken straight from the far-field pass.
 template <int N, bool SINGLE>
-__global__ __launch_bounds__(Geo<N>::NT) void k_forward(KArgs a) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_forward(KArgs a) {
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   constexpr int N2 = N * N;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
 // =====================================================================================
 // k_adjoint: gradients.  EXT: dL/dI supplied by the caller (ptyx_adjoint_dldi).
 template <int N, bool SINGLE, bool EXT>
-__global__ __launch_bounds__(Geo<N>::NT) void k_adjoint(KArgs a) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint(KArgs a) {
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   constexpr int N2 = N * N;
@@ -803,7 +803,7 @@ __global__ void k_slab_reduce(const float2* slab, int nwg, long long per, float2
 
 // d_probe[p] += F^-1(G_p) (shift) or G_p (no shift)
 template <int N>
-__global__ __launch_bounds__(Geo<N>::NT) void k_probe_finalize(KArgs a, const float2* G, float2* d_probe) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_finalize(KArgs a, const float2* G, float2* d_probe) {
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   constexpr int N2 = N * N;
@@ -1021,7 +1021,7 @@ static int blocks_per_cu(int N) {
     case 32: return 8;
     case 64: return 4;
     case 128: return 1;
-    default: return 1;
+    default: return 160 * 1024 / (int)(sizeof(float2) * (kG256Elems + 5 * 256) + 256);   // N = 256: 2
   }
 }
 
