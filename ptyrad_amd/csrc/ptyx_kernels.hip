@@ -624,28 +624,38 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint(KArgs a)
         // (Nz > 1) in the cache: no recomputed forward
         const float2* psi_c = cache ? cache + (size_t)(a.P * a.O + (a.Nz > 1 ? (p * a.O + o) * a.Nz : p)) * N2 : nullptr;
         if constexpr (N == 256) {
-          if (!xs) {   // fused stages (forward_far_g256): 2·Nz + 1 round trips per mode instead of 4·Nz - 1
+          if (!xs) {   // fused stages (forward_far_g256): 2·Nz + 1 round trips per mode (2 at Nz = 1) instead of 4·Nz - 1
             const int Nz = a.Nz;
             float2* A = arr.a;
             float2* B = arr.b;
             auto id_pre = [](int, int, float2 v) { return v; };
             auto store_all = [](int, int, float2&) { return true; };
             NoMid none;
-            // g_Ψ → A, transposed
+            // g_Ψ: the cached far field (ff_post applied on the way in) or the recomputed one
+            const float2* src0;
             if (cache) {
               psi_rd = psi_c;
-              auto pre = [&](int y, int x, float2 v) {
-                ff_post(y, x, v);
-                return v;
-              };
-              g256_fstage<0, 0, false, true, true, true, false>(cache + (size_t)(p * a.O + o) * N2, A, arr.lds, s_tw,
-                                                                pre, none, store_all);
+              src0 = cache + (size_t)(p * a.O + o) * N2;
             } else {
               psi_rd = psi;
-              float2* X = forward_far_g256<true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy,
-                                                 tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0, ff_post);
-              g256_fstage<0, 0, false, false, false, true, false>(X, A, arr.lds, s_tw, id_pre, none, store_all);
+              src0 = forward_far_g256<true>(a, arr, s_tw, s_wy, s_wx, g, p, o, psi, false, dummy,
+                                            tilt ? s_ty : nullptr, tilt ? s_tx : nullptr, psi, o > 0, ff_post);
             }
+            auto pre = [&](int y, int x, float2 v) {
+              if (cache) ff_post(y, x, v);
+              return v;
+            };
+            if (Nz == 1) {   // F_o⁻¹ rows, then columns with the slice adjoint in the store hook
+              g256_fstage<+1, 0, false, true, true, true, false>(src0, A, arr.lds, s_tw, pre, none, store_all);
+              auto post0 = [&](int y, int x, float2& v) {
+                acc_probe(y, x, slice_adj(0, y, x, cscale(v, inv_n)));
+                return false;
+              };
+              g256_fstage<+1, 0, true, false, false, true, true>(A, B, arr.lds, s_tw, id_pre, none, post0);
+              continue;
+            }
+            // Nz > 1: transpose g_Ψ into A, so the slice adjoints land on natural rows below
+            g256_fstage<0, 0, false, true, true, true, false>(src0, A, arr.lds, s_tw, pre, none, store_all);
             // F_o⁻¹ columns first; each slice adjoint sits between its inverse rows and the next
             // forward rows, each conj(H) between forward columns and inverse columns
             g256_fstage<+1, 0, true, false, false, true, false>(A, B, arr.lds, s_tw, id_pre, none, store_all);
@@ -660,8 +670,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint(KArgs a)
               };
               g256_fstage<-1, +1, true, false, false, true, false>(A, B, arr.lds, s_tw, id_pre, mh, store_all);
             }
-            const float sc0 = Nz == 1 ? inv_n : inv_n2;
-            auto m0 = [&](int y, int x, float2& v) { acc_probe(y, x, slice_adj(0, y, x, cscale(v, sc0))); };
+            auto m0 = [&](int y, int x, float2& v) { acc_probe(y, x, slice_adj(0, y, x, cscale(v, inv_n2))); };
             g256_fstage<+1, 0, false, false, false, false, false>(B, nullptr, arr.lds, s_tw, id_pre, m0, store_all);
             continue;
           }
@@ -1177,18 +1186,22 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
     }
   }
-  if (!stripe && d.P * d.O > 1) {
+  if (d.P * d.O > 1) {
     // far-field cache: per pattern of a call the P·O far fields plus ψ⁰ of every probe mode (Nz = 1)
     // or every slice's ψⁿ of every (p, o) (Nz > 1) — (P·O + P)·N² or P·O·(1 + Nz)·N² float2 —
     // within PTYX_FFC_MB (default the smaller of 64 GiB and a third of the free HBM); calls beyond
-    // its capacity are split by the host
+    // its capacity are split by the host.  A stripe plan keeps one for the calls the stripe engine
+    // declines (both data terms on), sized to its call size within a sixth of the free HBM
+    // (without it those calls recompute k_adjoint's forward).
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
-    long long mb = std::min<long long>(65536, (long long)(free_b / 3 / (1 << 20)));
+    long long mb = std::min<long long>(stripe ? free_b / 6 / (1 << 20) : 65536, (long long)(free_b / 3 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_FFC_MB")) mb = std::atoll(e);
     const long long per = (long long)(d.Nz > 1 ? d.P * d.O * (1 + d.Nz) : d.P * d.O + d.P) * (long long)N2;
-    const long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (per * (long long)sizeof(float2)));
-    if (cap >= std::min<long long>(d.max_patterns, pl->nwg)) {
+    const long long need = std::min<long long>(d.max_patterns, stripe ? pl->stripe_cap : pl->nwg);
+    long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (per * (long long)sizeof(float2)));
+    if (stripe) cap = std::min(cap, need);
+    if (need > 0 && cap >= need) {
       if ((rc = dalloc(pl, &pl->ffc, (size_t)cap * per))) {
         free_plan(pl);
         return rc;

@@ -202,19 +202,24 @@ def test_n256_mixed_state_vs_oracle():
     assert rel(g["shifts"], og["shifts"]) < TOL_SH
 
 
-@pytest.mark.parametrize("P,O,Nz,shift", [(2, 1, 3, True), (1, 1, 3, True), (1, 2, 2, False), (2, 2, 2, True),
-                                          (1, 3, 1, True)])
-def test_n256_general_engine_vs_oracle(P, O, Nz, shift):
-    """N = 256 through the general two-pass engine (multislice, or more object modes than the
-    stripe engine takes) — the fused g256_fstage chains, with and without the far-field cache
-    (P·O > 1 vs P·O = 1), ψ⁰ parking (O > 1) and broadcast probes: ragged mini-batches vs the
-    oracle, plus ptyx_forward's DPs and the external-dL/dI adjoint."""
+@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, False), (1, 1, 3, True, False),
+                                               (1, 2, 2, False, False), (2, 2, 2, True, False),
+                                               (1, 3, 1, True, False), (2, 2, 1, True, True)])
+def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
+    """N = 256 through the general two-pass engine (multislice, more object modes than the
+    stripe engine takes, or both data terms on a stripe plan) — the fused g256_fstage chains, with
+    and without the far-field cache (P·O > 1 vs P·O = 1), ψ⁰ parking (O > 1) and broadcast
+    probes: ragged mini-batches vs the oracle, plus ptyx_forward's DPs and the external-dL/dI
+    adjoint."""
     device = dev()
     from ptyrad_amd import synthetic as syn
     pr = syn.random_problem(256, 3, 3, P=P, O=O, Nz=Nz, seed=40 + 7 * P + O + Nz)
+    lp = orc_default_loss()
+    if both:
+        lp["loss_poissn"]["state"] = True
     d = dict(obja=pr.obja, objp=(pr.objp / Nz).astype(np.float32), probe=pr.probe * np.float32(30.0),
              shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=shift,
-             loss_params=orc_default_loss())
+             loss_params=lp)
     perm = np.random.default_rng(P + O + Nz).permutation(9)
     batches = [perm[:4], perm[4:5], perm[5:]]
     ks = {}
