@@ -211,9 +211,22 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     and without the far-field cache (P·O > 1 vs P·O = 1), ψ⁰ parking (O > 1) and broadcast
     probes: ragged mini-batches vs the oracle, plus ptyx_forward's DPs and the external-dL/dI
     adjoint."""
+    _general_engine_case(256, P, O, Nz, shift, both)
+
+
+@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, False), (1, 2, 2, False, False),
+                                               (3, 2, 1, True, False), (1, 1, 1, True, True)])
+def test_n128_general_engine_vs_oracle(P, O, Nz, shift, both):
+    """N = 128 through the general engine's LDS FFT — mixed-state multislice with the far-field
+    cache and the probe-mode split, broadcast probes, and the single-mode two-term path
+    (k_forward1 / k_adjoint1): vs the oracle as above."""
+    _general_engine_case(128, P, O, Nz, shift, both)
+
+
+def _general_engine_case(N, P, O, Nz, shift, both):
     device = dev()
     from ptyrad_amd import synthetic as syn
-    pr = syn.random_problem(256, 3, 3, P=P, O=O, Nz=Nz, seed=40 + 7 * P + O + Nz)
+    pr = syn.random_problem(N, 3, 3, P=P, O=O, Nz=Nz, seed=40 + 7 * P + O + Nz)
     lp = orc_default_loss()
     if both:
         lp["loss_poissn"]["state"] = True
@@ -224,7 +237,7 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     batches = [perm[:4], perm[4:5], perm[5:]]
     ks = {}
     terms, dp, g, plan = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
-    assert "k_adjoint" in ks and "k_s1" not in ks, ks
+    assert ("k_adjoint" in ks or "k_adjoint1" in ks) and "k_s1" not in ks and "k_fused" not in ks, ks
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"],
                                              shift_probes=shift, grad_scale=0.5)
@@ -236,12 +249,12 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
         assert rel(g["shifts"], og["shifts"]) < TOL_SH
     t = tensors(d, device)
     b = perm[:5].astype(np.int32)
-    dpf = torch.zeros((len(b), 256, 256), device=device)
+    dpf = torch.zeros((len(b), N, N), device=device)
     plan.forward(t, b, dp_out=dpf)
     torch.cuda.synchronize()
     assert rel(dpf.cpu().numpy(), np.concatenate(odps)[:5]) < TOL_DP
     # external dL/dI through k_adjoint<EXT> (recomputed forward, no cache)
-    amp, ph = orc.get_patches(d["obja"], d["objp"], d["crop_pos"], b, 256)
+    amp, ph = orc.get_patches(d["obja"], d["objp"], d["crop_pos"], b, N)
     probes = orc.get_probes(d["probe"], d["shifts"][b], shift)
     cache = orc.forward(amp, ph, probes, d["H"], d["occu"])
     dLdI = np.random.default_rng(1).standard_normal(cache.dp.shape).astype(np.float32) * 1e-3
@@ -251,8 +264,8 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     gP = np.zeros(d["objp"].shape)
     for i, s in enumerate(b):
         cy, cx = d["crop_pos"][s]
-        gA[:, :, cy:cy + 256, cx:cx + 256] += dA[i]
-        gP[:, :, cy:cy + 256, cx:cx + 256] += dP[i]
+        gA[:, :, cy:cy + N, cx:cx + N] += dA[i]
+        gP[:, :, cy:cy + N, cx:cx + N] += dP[i]
     grads = {k: torch.zeros_like(t[k]) for k in ("obja", "objp", "probe")}
     plan.adjoint_dldi(t, b, torch.tensor(dLdI, device=device), grads)
     torch.cuda.synchronize()
