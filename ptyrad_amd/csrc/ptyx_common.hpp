@@ -78,6 +78,13 @@ struct KArgs {
   // ((pattern·P + p)·N² floats) and k_forward_modesum forms I, dp and the loss sums
   int msplit = 1;
   float* Imodes = nullptr;
+  // compact probe slabs (split calls without propagator slabs): k_adjoint runs on a grid that is
+  // a multiple of P, so workgroup w only ever sees probe mode w % P and owns one slab plane
+  // (zeroed and reduced alone: k_slab_reduce over grid / P "virtual workgroups")
+  int cslab = 0;
+  // N = 128 register engines: k_probe_spectrum also leaves F(P) in their packed K layout (the
+  // layout k_pack128<true> makes), so a step launches no separate pack kernel
+  float2* fpk = nullptr;
   // N = 256 fused chains (g256_fstage): F(P_p) and H transposed, written by k_probe_spectrum,
   // so the stages that run on the transposed array read them along its rows
   float2* FpT = nullptr;   // (P, N, N): FpT[p][x][y] = F(P_p)[y][x]   (shifted probes)

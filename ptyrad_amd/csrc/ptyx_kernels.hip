@@ -240,6 +240,9 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_spectrum(K
         if constexpr (N == 256) {
           if (a.FpT) a.FpT[(size_t)p * N * N + x * N + y] = v;
         }
+        if constexpr (N == 128) {   // inverse of f3::packed_rc<true>: row y = fixed_of(t), column x = i + 64·(t & 1)
+          if (a.fpk) a.fpk[(x & 63) * 256 + ((x >> 6) | ((y & 31) << 1) | ((y >> 5) << 6))] = v;
+        }
         return false;
       });
 }
@@ -370,25 +373,64 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward_modesum(KArgs a) {
   const PatternGeom g = pattern_geom(a, pat, N);
   const bool want_sums = a.psums != nullptr;
   float sums[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* Im = a.Imodes + (size_t)pat * a.msplit * N2;
-  float* Ip = a.Ibuf + (size_t)pat * N2;
-  for (int e = opaque_tid(); e < N2; e += NT) {
-    float I = Im[e];
-    for (int p = 1; p < a.msplit; ++p) I += Im[(size_t)p * N2 + e];
-    I += kDpEps;
-    Ip[e] = I;
-    if (a.dp_out) a.dp_out[(size_t)pat * N2 + e] = I;
-    if (want_sums) {
-      const float M = meas_at(a, g.m, e, N2);
-      if (a.single_on) {
-        const float Iq = powq(I, a.q1), Mq = powq(M, a.q1), d = Iq - Mq;
-        sums[0] = fmaf(d, d, sums[0]);
-        sums[1] += Mq;
+  // float4 units, up to four a thread in flight with every mode plane's loads issued together
+  // (one workgroup a pattern: a split call is small, so latency, not bandwidth, bounds this)
+  constexpr int N4 = N2 / 4;
+  constexpr int U = (N4 + NT - 1) / NT;
+  constexpr int UB = U < 4 ? U : 4;
+  const float4* __restrict__ Im = reinterpret_cast<const float4*>(a.Imodes + (size_t)pat * a.msplit * N2);
+  float4* __restrict__ Ip = reinterpret_cast<float4*>(a.Ibuf + (size_t)pat * N2);
+  float* const dps = a.dp_out ? a.dp_out + (size_t)pat * N2 : nullptr;   // caller's array: maybe not 16-B aligned
+  const bool dp4 = (reinterpret_cast<uintptr_t>(dps) & 15) == 0;
+  const int tid = opaque_tid();
+  for (int b0 = 0; b0 < U; b0 += UB) {
+    float4 I[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e4 = tid + (b0 + u) * NT;
+      I[u] = e4 < N4 ? Im[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int p = 1; p < a.msplit; ++p) {
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e4 = tid + (b0 + u) * NT;
+        if (e4 < N4) {
+          const float4 t = Im[(size_t)p * N4 + e4];
+          I[u].x += t.x; I[u].y += t.y; I[u].z += t.z; I[u].w += t.w;
+        }
       }
-      if (a.pois_on) {
-        const float Iq = powq(I, a.q2), Mq = powq(M, a.q2);
-        sums[2] += Mq * fast_ln(Iq + a.eps2) - Iq;
-        sums[3] += Mq;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e4 = tid + (b0 + u) * NT;
+      if (e4 >= N4) continue;
+      float4 v = I[u];
+      v.x += kDpEps; v.y += kDpEps; v.z += kDpEps; v.w += kDpEps;
+      Ip[e4] = v;
+      if (dps) {
+        if (dp4) {
+          reinterpret_cast<float4*>(dps)[e4] = v;
+        } else {
+          dps[4 * e4] = v.x; dps[4 * e4 + 1] = v.y; dps[4 * e4 + 2] = v.z; dps[4 * e4 + 3] = v.w;
+        }
+      }
+      if (want_sums) {
+        const float Iv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float I1 = Iv[c];
+          const float M = meas_at(a, g.m, 4 * e4 + c, N2);
+          if (a.single_on) {
+            const float Iq = powq(I1, a.q1), Mq = powq(M, a.q1), d = Iq - Mq;
+            sums[0] = fmaf(d, d, sums[0]);
+            sums[1] += Mq;
+          }
+          if (a.pois_on) {
+            const float Iq = powq(I1, a.q2), Mq = powq(M, a.q2);
+            sums[2] += Mq * fast_ln(Iq + a.eps2) - Iq;
+            sums[3] += Mq;
+          }
+        }
       }
     }
   }
@@ -402,7 +444,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward_modesum(KArgs a) {
 }
 
 // =====================================================================================
-// k_finalize: one thread per mini-batch — loss terms and adjoint coefficients.
+// k_finalize: one wave per mini-batch — loss terms and adjoint coefficients.
 // bsums_out: write the mini-batch's additive sums (PTYX_BATCH_SUMS doubles: count, S_single,
 // ΣM^q1, S_poissn, ΣM^q2, sparse sums per object mode) and stop (ptyx_forward_loss_grad_begin);
 // bsums_in: take them from there instead of this call's patterns (ptyx_forward_loss_grad_end: the
@@ -532,12 +574,18 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint(KArgs a)
   float2* psi = scratch_psi<N>(a);
   const float2* psi_rd = psi;   // ψⁿ the slice adjoints read: scratch, or the far-field cache's ψ⁰
   float2* gacc = psi + (size_t)a.Nz * N2;
-  float2* slab = a.slab + (size_t)blockIdx.x * a.P * N2;
+  // compact slabs: workgroup w runs probe mode w % P only; its plane sits at mode w % P of the
+  // slab of "virtual workgroup" w / P (the layout k_slab_reduce sums)
+  const int cs = a.cslab ? (int)(blockIdx.x % a.P) : -1;
+  float2* slab = a.slab + (size_t)(a.cslab ? blockIdx.x / a.P : blockIdx.x) * a.P * N2;
   // propagator gradient: dL/dH += Σ_{p,o,n<Nz-1} conj(Xⁿ) ⊙ F(g^{n+1}) / N²  (ψ^{n+1} = F⁻¹(H Xⁿ))
   float2* xs = (a.hslab || a.d_tilts || a.d_dz) ? gacc + N2 : nullptr;
   float2* hsl = a.hslab ? a.hslab + (size_t)blockIdx.x * N2 : nullptr;
-  if (a.need_probe)
-    for (int e = threadIdx.x; e < a.P * N2; e += NT) slab[e] = make_float2(0.f, 0.f);
+  if (a.need_probe) {
+    float2* z = cs >= 0 ? slab + (size_t)cs * N2 : slab;
+    const int nz = cs >= 0 ? N2 : a.P * N2;
+    for (int e = threadIdx.x; e < nz; e += NT) z[e] = make_float2(0.f, 0.f);
+  }
   if (hsl)
     for (int e = threadIdx.x; e < N2; e += NT) hsl[e] = make_float2(0.f, 0.f);
   __syncthreads();
@@ -1368,10 +1416,19 @@ template <int N>
 static void launch_modesum(const ptyx_plan*, const KArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_forward_modesum<N>, dim3(a.n_idx), dim3(Geo<N>::NT), 0, st, a);
 }
+// k_adjoint's grid: every workgroup zeroes its slab, so all of them run — except with compact
+// slabs, where the grid is the split call's jobs (or the plan's workgroups) rounded down to a
+// multiple of P and k_slab_reduce sums grid / P slabs
+static int adjoint_grid(const ptyx_plan* pl, const KArgs& a) {
+  if (!a.cslab) return pl->nwg;
+  return std::max(a.P, std::min(pl->nwg, a.n_idx * a.P) / a.P * a.P);
+}
+static int adjoint_slabs(const ptyx_plan* pl, const KArgs& a) { return a.cslab ? adjoint_grid(pl, a) / a.P : pl->nwg; }
+
 template <int N>
 static void launch_adjoint(const ptyx_plan* pl, const KArgs& a, hipStream_t st, bool ext) {
   ProfScope ps(pl, kKAdjoint, st);
-  const int grid = pl->nwg;  // every workgroup zeroes its slab, so launch all of them
+  const int grid = adjoint_grid(pl, a);
   const bool single = pl->d.P * pl->d.O == 1;
   if constexpr (Geo<N>::kLds) {
     if (single && pl->d.Nz == 1) {
@@ -1436,9 +1493,9 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
   if (reuse) {
   } else if (a.shift) {
-    launch_spectrum<N>(pl, a, st);
-    ProfScope ps(pl, kKPack, st);
-    hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, pl->Fp, pl->fpk);
+    KArgs b = a;
+    b.fpk = pl->fpk;   // F(P) packed by the spectrum kernel itself
+    launch_spectrum<N>(pl, b, st);
   } else {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256), dim3(256), 0, st,
@@ -2058,6 +2115,7 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
   if (pl->Imodes && pl->d.P > 1 && a.n_idx <= kModeSplitCap && a.n_idx < pl->nwg) {
     b.msplit = pl->d.P;
     b.Imodes = pl->Imodes;
+    b.cslab = a.hslab == nullptr;   // (a propagator slab per workgroup needs every workgroup)
   }
   if (ph != kPhaseEnd) {
     if ((b.shift || b.HT) && cfg->prep != PTYX_PREP_REUSE) PTYX_DISPATCH_N(pl->d.N, launch_spectrum, pl, b, st);
@@ -2088,7 +2146,7 @@ static int run_two_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, co
   if ((rc = launch_status("k_adjoint launch"))) return rc;
   if ((rc = reduce_prop_grad(pl, a, gz, st))) return rc;
   if (gz.d_probe) {
-    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, pl->nwg);
+    PTYX_DISPATCH_N(pl->d.N, launch_probe_finalize, pl, a, st, gz.d_probe, adjoint_slabs(pl, b));
     if ((rc = launch_status("probe finalize launch"))) return rc;
   }
   return PTYX_OK;

@@ -28,6 +28,10 @@ namespace opt {
 
 constexpr int kMaxT = 16;   // tensors per launch (more are split over launches)
 
+constexpr int kU = 4;                  // units per thread of a chunk
+constexpr int kThreads = 256;
+constexpr int64_t kChunk = (int64_t)kU * kThreads;   // units per workgroup chunk
+
 struct AdamArgs {
   float* p[kMaxT];
   const float* g[kMaxT];
@@ -35,7 +39,11 @@ struct AdamArgs {
   float* v[kMaxT];
   const float* step[kMaxT];
   double lr[kMaxT];
-  int64_t off[kMaxT + 1];   // prefix sums of the tensors' UNITS (4 elements if vec, else 1)
+  // prefix sums of the tensors' unit ranges (4 elements a unit if vec, else 1), each range padded
+  // to whole chunks, so a chunk belongs to ONE tensor: the tensor index is uniform per workgroup
+  // and the per-tensor pointers and flags are scalar loads
+  int64_t off[kMaxT + 1];
+  int64_t units[kMaxT];
   int vec[kMaxT];           // p, g, m, v 16-B aligned and numel % 4 == 0: float4 units
   int nt;
   float beta1, beta2, eps, wd;
@@ -43,61 +51,74 @@ struct AdamArgs {
   int adamw, maximize;
 };
 
-__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+// β^t for the integer step count t by square-and-multiply in fp64 (a few fp64 ulps from pow(),
+// far below the fp32 rounding of the factors it feeds; pow() for a non-integer t)
+__device__ __forceinline__ double pow_step(double b, double t) {
+  if (!(t >= 0.0 && t < 9007199254740992.0 && t == floor(t))) return pow(b, t);
+  unsigned long long n = (unsigned long long)t;
+  double r = 1.0, x = b;
+  while (n) {
+    if (n & 1) r *= x;
+    x *= x;
+    n >>= 1;
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
   // the tensors' step scalars, once per workgroup (lane t of wave 0 for tensor t)
   __shared__ float s_nstep[kMaxT], s_bc2s[kMaxT];
   if (threadIdx.x < (unsigned)a.nt) {
     const int t = threadIdx.x;
     const double step = (double)*a.step[t];
-    const double bc1 = 1.0 - pow(a.beta1d, step), bc2 = 1.0 - pow(a.beta2d, step);
+    const double bc1 = 1.0 - pow_step(a.beta1d, step), bc2 = 1.0 - pow_step(a.beta2d, step);
     s_nstep[t] = (float)(-(a.lr[t] / bc1));
     s_bc2s[t] = (float)sqrt(bc2);
   }
   __syncthreads();
   const int64_t total = a.off[a.nt];
   const float w1 = (float)(1.0 - a.beta1d), c2 = (float)(1.0 - a.beta2d);
-  // a workgroup takes chunks of 4·256 consecutive units, a thread four of them 256 apart
-  // (coalesced; 16-B units where the tensor allows); chunks grid-stride
-  constexpr int kU = 4;
-  const int64_t chunk = (int64_t)kU * blockDim.x;
+  // a workgroup takes chunks of 4·256 consecutive units of one tensor, a thread four of them 256
+  // apart (coalesced; 16-B units where the tensor allows); chunks grid-stride
   int t = 0;
-  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < total; c0 += (int64_t)gridDim.x * chunk) {
+  for (int64_t c0 = (int64_t)blockIdx.x * kChunk; c0 < total; c0 += (int64_t)gridDim.x * kChunk) {
+    while (c0 >= a.off[t + 1]) ++t;   // chunk starts only grow
+    t = __builtin_amdgcn_readfirstlane(t);
+    const int64_t j0 = c0 - a.off[t], nu = a.units[t];
+    const bool vec = a.vec[t] != 0;
+    float* __restrict__ P = a.p[t];
+    const float* __restrict__ G = a.g[t];
+    float* __restrict__ M = a.m[t];
+    float* __restrict__ V = a.v[t];
+    const float nstep = s_nstep[t], bc2s = s_bc2s[t];
+    const float decay = (float)(1.0 - a.lr[t] * (double)a.wd);
     float4 g[kU], p[kU], m[kU], v[kU];
-    int tt[kU];
-    int64_t jj[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int64_t i = c0 + u * blockDim.x + threadIdx.x;
-      tt[u] = -1;
-      if (i < total) {
-        while (i >= a.off[t + 1]) ++t;   // indices only grow: the tensor index only advances
-        tt[u] = t;
-        const int64_t j = i - a.off[t];
-        jj[u] = j;
-        if (a.vec[t]) {
-          g[u] = reinterpret_cast<const float4*>(a.g[t])[j];
-          p[u] = reinterpret_cast<const float4*>(a.p[t])[j];
-          m[u] = reinterpret_cast<const float4*>(a.m[t])[j];
-          v[u] = reinterpret_cast<const float4*>(a.v[t])[j];
+      const int64_t j = j0 + u * kThreads + threadIdx.x;
+      if (j < nu) {
+        if (vec) {
+          g[u] = reinterpret_cast<const float4*>(G)[j];
+          p[u] = reinterpret_cast<const float4*>(P)[j];
+          m[u] = reinterpret_cast<const float4*>(M)[j];
+          v[u] = reinterpret_cast<const float4*>(V)[j];
         } else {
-          g[u].x = a.g[t][j];
-          p[u].x = a.p[t][j];
-          m[u].x = a.m[t][j];
-          v[u].x = a.v[t][j];
+          g[u].x = G[j];
+          p[u].x = P[j];
+          m[u].x = M[j];
+          v[u].x = V[j];
         }
       }
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int tu = tt[u];
-      if (tu < 0) continue;
-      const float nstep = s_nstep[tu], bc2s = s_bc2s[tu];
-      const float decay = (float)(1.0 - a.lr[tu] * (double)a.wd);
+      const int64_t j = j0 + u * kThreads + threadIdx.x;
+      if (j >= nu) continue;
       float* gp = &g[u].x;
       float* pp = &p[u].x;
       float* mp = &m[u].x;
       float* vp = &v[u].x;
-      const int ne = a.vec[tu] ? 4 : 1;
+      const int ne = vec ? 4 : 1;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (e >= ne) break;
@@ -115,15 +136,14 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         mp[e] = mu;
         vp[e] = vu;
       }
-      const int64_t j = jj[u];
-      if (a.vec[tu]) {
-        reinterpret_cast<float4*>(a.p[tu])[j] = p[u];
-        reinterpret_cast<float4*>(a.m[tu])[j] = m[u];
-        reinterpret_cast<float4*>(a.v[tu])[j] = v[u];
+      if (vec) {
+        reinterpret_cast<float4*>(P)[j] = p[u];
+        reinterpret_cast<float4*>(M)[j] = m[u];
+        reinterpret_cast<float4*>(V)[j] = v[u];
       } else {
-        a.p[tu][j] = p[u].x;
-        a.m[tu][j] = m[u].x;
-        a.v[tu][j] = v[u].x;
+        P[j] = p[u].x;
+        M[j] = m[u].x;
+        V[j] = v[u].x;
       }
     }
   }
@@ -159,7 +179,8 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
       a.lr[k] = lrs[i];
       const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
       a.vec[k] = numels[i] % 4 == 0 && al16(params[i]) && al16(grads[i]) && al16(exp_avgs[i]) && al16(exp_avg_sqs[i]);
-      a.off[k + 1] = a.off[k] + (a.vec[k] ? numels[i] / 4 : numels[i]);
+      a.units[k] = a.vec[k] ? numels[i] / 4 : numels[i];
+      a.off[k + 1] = a.off[k] + (a.units[k] + opt::kChunk - 1) / opt::kChunk * opt::kChunk;
     }
     for (int k = a.nt; k < opt::kMaxT; ++k) a.off[k + 1] = a.off[a.nt];
     a.beta1 = (float)beta1;
@@ -172,8 +193,8 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
     a.maximize = (flags >> 1) & 1;
     const int64_t total = a.off[a.nt];
     if (!total) continue;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (total + 1023) / 1024));
-    hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, total / opt::kChunk));
+    hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(opt::kThreads), 0, (hipStream_t)stream, a);
     if (int rc = launch_status("k_adam launch")) return rc;
   }
   return PTYX_OK;
