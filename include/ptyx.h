@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 203
+#define PTYX_ABI_VERSION 204
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -101,11 +101,22 @@ typedef struct ptyx_inputs {
   const float *kvec;       /* (N)          f32  propagator_grid k values (Ky[:,0] = Kx[0,:])  */
   float dz;                /* slice thickness used by the tilt ramps                           */
   /* rank-local measurement storage (the data-parallel driver keeps only the DPs of its own
-   * mini-batches): meas_rows[s] = row of `meas` holding scan position s.  HARD
-   * PRECONDITION: for every s a call touches, 0 <= meas_rows[s] < the rows of `meas` (the kernels
-   * do not check it; the Python mirror verifies it before the call).  NULL = row s.            */
+   * mini-batches): meas_rows[s] = row of `meas` holding scan position s, with
+   * 0 <= meas_rows[s] < meas_row_count for every s a call touches.  NULL = row s.             */
   const int32_t *meas_rows; /* (n_scans) i32 device, or NULL                                     */
+  int32_t meas_row_count;   /* rows of `meas` when meas_rows is set (>= 1), else ignored         */
 } ptyx_inputs;
+
+/* Preconditions on the device arrays of every compute call (ptyx_forward, ptyx_forward_loss_grad
+ * (_begin), ptyx_adjoint_dldi), for each pattern j of the call with s = idx[j]:
+ *   0 <= s < n_scans;  0 <= crop_pos[s] (y, x) and crop_pos[s] + N <= (Ny, Nx);
+ *   0 <= meas_rows[s] < meas_row_count (when meas_rows is set).
+ * The engines check them on the device as they read the indices (no host synchronisation): a
+ * violation is clamped (no out-of-bounds access) and flagged on the plan, and the NEXT compute call
+ * on the plan — or ptyx_plan_check — returns PTYX_EINVAL naming it (the reference raises
+ * IndexError from its advanced indexing, models.py:261-264).  ptyx_plan_check reports the flags of
+ * every call whose kernels have completed (synchronise the stream first) and clears them. */
+int ptyx_plan_check(ptyx_plan *plan);
 
 typedef struct ptyx_grads {
   float *d_obja;   /* (O,Nz,Ny,Nx)  += dL/dobja                 or NULL */
@@ -352,8 +363,9 @@ int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
  * engine): key "s3_hold" (0..4: probe/object modes k_s3 keeps in registers), "s_psi0" (0/1: the
  * stripe engine parks ψ⁰ instead of recomputing it), "s_gather" (0/1: stripe object gradient by
  * slots + gather instead of f32 atomics), "s_defer_groups" (0: the stripe engine ignores
- * PTYX_PREP_DEFER_PROBE; n > 0: k_s5 partial groups of deferring calls); value -1 restores the
- * measured default.  Process-wide,
+ * PTYX_PREP_DEFER_PROBE; n > 0: k_s5 partial groups of deferring calls), "gather_split" (n >= 1:
+ * the object-gradient gather splits every tile's candidates over n workgroups; the default splits
+ * only grids too small to fill the GPU); value -1 restores the measured default.  Process-wide,
  * read by ptyx_plan_create (s_psi0, s_gather) and by each call (s3_hold).  Every variant computes
  * the same results.  ptyx_get_tuning returns the current value (-1 default, -2 unknown key). */
 int ptyx_set_tuning(const char *key, int64_t value);

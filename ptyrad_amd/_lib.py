@@ -14,7 +14,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 203     # include/ptyx.h
+PTYX_ABI_VERSION = 204     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_PREP_DEFER_PROBE = 4  # flag bit: the probe-gradient reduction may wait for a later piece
 PTYX_BATCH_SUMS = 13      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
@@ -33,7 +33,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
-           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step")
+           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_plan_check")
 
 
 class PtyxError(RuntimeError):
@@ -58,7 +58,8 @@ class Inputs(ctypes.Structure):
     _fields_ = [("obja", ctypes.c_void_p), ("objp", ctypes.c_void_p), ("probe", ctypes.c_void_p),
                 ("shifts", ctypes.c_void_p), ("H", ctypes.c_void_p), ("omode_occu", ctypes.c_void_p),
                 ("crop_pos", ctypes.c_void_p), ("meas", ctypes.c_void_p), ("obj_tilts", ctypes.c_void_p),
-                ("kvec", ctypes.c_void_p), ("dz", ctypes.c_float), ("meas_rows", ctypes.c_void_p)]
+                ("kvec", ctypes.c_void_p), ("dz", ctypes.c_float), ("meas_rows", ctypes.c_void_p),
+                ("meas_row_count", ctypes.c_int32)]
 
 
 class Grads(ctypes.Structure):
@@ -131,6 +132,7 @@ def load(path: str | None = None):
     lib.ptyx_profile_end.restype = ctypes.c_int
     lib.ptyx_plan_workspace_bytes.argtypes = [vp]
     lib.ptyx_plan_workspace_bytes.restype = ctypes.c_size_t
+    lib.ptyx_plan_check.argtypes = [vp]
     lib.ptyx_plan_register_capacity.argtypes = [vp]
     lib.ptyx_plan_register_capacity.restype = ctypes.c_int64
     lib.ptyx_last_error.restype = ctypes.c_char_p
@@ -164,7 +166,7 @@ def load(path: str | None = None):
     lib.ptyx_step_store.argtypes = [vp, vp, i32, vp, vp, vp]
     d64 = ctypes.c_double
     lib.ptyx_adam_step.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32]
-    for name in ("ptyx_adam_step", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+    for name in ("ptyx_plan_check", "ptyx_adam_step", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
                  "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
@@ -199,6 +201,9 @@ def _check_abi(lib):
 def set_tuning(key: str, value: int) -> None:
     """ptyx_set_tuning: select an engine variant (tests / A/B runs; -1 = the measured default)."""
     check(load().ptyx_set_tuning(key.encode(), int(value)))
+
+
+TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split")   # ptyx_set_tuning's keys
 
 
 def get_tuning(key: str) -> int:

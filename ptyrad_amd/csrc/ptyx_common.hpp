@@ -60,6 +60,8 @@ struct KArgs {
   float w1, w2, ws, grad_scale;
   // rank-local measurement block: row of meas holding scan position s (NULL: row s)
   const int* mrow;
+  int mrows;        // rows of meas (the bound meas_rows entries are checked and clamped against)
+  int* err;         // the plan's input-error flags (check_pattern), host-mapped
   // propagator gradient (PTYX_PROP_GRAD): per-workgroup dL/dH slabs; F(ψⁿ⊙Oⁿ) parked after gacc
   float2* hslab;
   // per-position tilts: ramps exp(i dz k tan(θ/1e3)) along y and x, and their gradient
@@ -157,6 +159,30 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red) {
   __syncthreads();
 }
 
+// Input validation (include/ptyx.h preconditions).  The engines' table kernels check every
+// pattern of a call: a scan index outside [0, n_scans), a window crop_pos + N outside the object
+// or a measurement row outside the block sets its flag in the plan's error words (host-mapped
+// memory, plain vector stores of 1, no atomics) and the kernels go on with the value clamped, so
+// nothing is read out of bounds; the next call on the plan (or ptyx_plan_check) reports
+// PTYX_EINVAL.  No host synchronisation on the hot path.
+enum { kErrIdx = 0, kErrWindow = 1, kErrRow = 2, kErrWords = 4 };
+__device__ __forceinline__ void check_pattern(int* err, int s_raw, int n_scans, const int* crop, int Ny, int Nx, int N,
+                                              const int* mrow, int mrows) {
+  if (!err) return;
+  if (s_raw < 0 || s_raw >= n_scans) err[kErrIdx] = 1;
+  const int s = min(max(s_raw, 0), n_scans - 1);
+  const int cy = crop[2 * s], cx = crop[2 * s + 1];
+  if (cy < 0 || cx < 0 || cy > Ny - N || cx > Nx - N) err[kErrWindow] = 1;
+  if (mrow) {
+    const int m = mrow[s];
+    if (m < 0 || m >= mrows) err[kErrRow] = 1;
+  }
+}
+// measurement row of scan position s, clamped into the block
+__device__ __forceinline__ int meas_row(const int* mrow, int mrows, int s) {
+  return mrow ? min(max(mrow[s], 0), mrows - 1) : s;
+}
+
 struct PatternGeom {
   int s, m, cy, cx;   // scan index, its measurement row, clamped window origin
   float sy, sx;
@@ -164,10 +190,11 @@ struct PatternGeom {
 
 __device__ __forceinline__ PatternGeom pattern_geom(const KArgs& a, int pat, int N) {
   PatternGeom g;
-  int s = a.idx[pat];
-  s = min(max(s, 0), a.n_scans - 1);  // defensive clamp; the host validates indices
+  const int s_raw = a.idx[pat];
+  if (threadIdx.x == 0) check_pattern(a.err, s_raw, a.n_scans, a.crop, a.Ny, a.Nx, N, a.mrow, a.mrows);
+  const int s = min(max(s_raw, 0), a.n_scans - 1);   // (invalid inputs: flagged above, clamped here)
   g.s = s;
-  g.m = a.mrow ? a.mrow[s] : s;
+  g.m = meas_row(a.mrow, a.mrows, s);
   g.cy = min(max(a.crop[2 * s], 0), a.Ny - N);
   g.cx = min(max(a.crop[2 * s + 1], 0), a.Nx - N);
   g.sy = a.shifts[2 * s];

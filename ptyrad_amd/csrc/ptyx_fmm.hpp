@@ -1,0 +1,561 @@
+// ptyx_fmm.hpp — the mixed-state register engine: N = 128, P probe modes (P > 1), one object
+// mode, Nz ≥ 1 slices, on the register-resident FFT of ptyx_regfft.hpp.  The geometry of the
+// reference's own demo (tBL_WSe2: 6 probe modes × 6 slices, demo/params/tBL_WSe2_reconstruct.yml
+// :23-27).  Included by ptyx_kernels.hip after ptyx_fused3.hpp.
+//
+// k_fused3ms carries one pattern's whole forward → loss → adjoint in one workgroup's registers.
+// With P modes the loss needs I = Σ_p occ|Ψ_p|² before any mode's adjoint can start, and a second
+// 128-VGPR field per mode does not fit, so the chain is cut at the far field into three launches,
+// each a JOB per (pattern, probe mode) — P times the workgroups of a pattern-per-workgroup design,
+// which is what keeps the reference's default cadence (one 32-pattern mini-batch a step) busy:
+//
+//   k_fmm_fwd   job (b, p): ψ⁰ = F⁻¹(F(P_p)·W_b)/N²; for n: park ψⁿ (slot plane (b, n, p)), ×O_n,
+//               ×H between slices (forward.py:50-63, image_proc.py:531-532); far field
+//               v = F(ψ_out) stored K-packed (Ψ = v/N, forward.py:79)
+//   k_fmm_loss  pattern b: I = Σ_p occ|v_p|²/N² + 1e-10, dp_out, the loss partial sums and
+//               u = ∂ℓ/∂I per unit mini-batch coefficient (K-packed; losses.py:36-75)
+//   k_finalize  c_m per mini-batch
+//   k_fmm_adj   job (b, p): g = F⁻¹(v_p·2 occ u/N)/N; for n = Nz−1 … 0: slot (b, n, p) =
+//               g·conj(ψⁿ) (unit coefficient: k_obj_gather applies c_m and sums the P planes),
+//               g ← g·conj(O_n), ×conj(H) between slices; then c_m·g → probe-gradient spectrum
+//               (per-workgroup segment of one mode) and the position sums, as k_fused3ms
+//
+// 4·Nz FFTs per job, 4·Nz·P per pattern, no recomputed forward.  Slots and far fields live in the
+// plan's far-field cache: per pattern P·(Nz + 1) planes of N² float2, slot plane (b, n, p) at
+// (b·pstride + n·P + p)·N², far field of mode p at (b·pstride + Nz·P + p)·N².  Jobs are numbered
+// mode-major (job = p·n_idx + b) and workgroup w takes the contiguous range
+// [w·J/G, (w+1)·J/G): consecutive jobs share F(P_p) and the object band, and a workgroup's jobs
+// fall in at most a few probe modes (segment id p + w: unique, since every segment boundary
+// advances p or w).
+#pragma once
+#include "ptyx_fused3.hpp"
+
+namespace ptyx {
+namespace f3 {
+
+struct FmArgs {
+  F3Args f;             // fpk: P planes (K-packed F(P_p), or the probes R-packed without shifts)
+  int P;
+  long long pstride;    // float2 planes per pattern in f.slots: P·(Nz + 1)
+  float* ubuf;          // (patterns, N²) f32 K-packed: ∂ℓ/∂I per unit coefficient
+  const float* coef;    // k_finalize's per-mini-batch coefficients
+  int ci;               // data-term coefficient index (0 single, 1 poissn)
+};
+
+__device__ __forceinline__ float ld1(Rsrc r, int voff, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff + off, 0, 0));
+}
+__device__ __forceinline__ void st1(float v, Rsrc r, int voff, int off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff + off, 0, 0);
+}
+struct Ch4u {
+  float2 x[4];
+  float u[4];
+};
+
+__device__ __forceinline__ size_t fmm_slot(const FmArgs& m, int pat, int n, int p) {
+  return ((size_t)pat * m.pstride + (size_t)n * m.P + p) * kN2;
+}
+__device__ __forceinline__ size_t fmm_far(const FmArgs& m, int pat, int p) {
+  return ((size_t)pat * m.pstride + (size_t)m.f.Nz * m.P + p) * kN2;
+}
+
+// ------------------------------------------------------------------ forward: job → far field
+template <bool SHIFT>
+__global__ __launch_bounds__(256, 2) void k_fmm_fwd(FmArgs m) {
+  using namespace rf;
+  const F3Args& a = m.f;
+  __shared__ float2 buf[kLdsElems];
+  const Coord cd = coord(threadIdx.x);
+  const LaneCtx lc = lane_ctx(cd.lane);
+  constexpr float inv_n2 = 1.0f / kN2;
+  const int w = blockIdx.x, G = gridDim.x;
+  const int nj = a.n_idx * m.P;
+  const int j0 = (int)((long long)w * nj / G), j1 = (int)((long long)(w + 1) * nj / G);
+  if (j0 >= j1) return;
+  const int Nx = a.Nx, Nz = a.Nz;
+  const size_t plane = (size_t)a.Ny * a.Nx;
+  const Rsrc r_hpk = rsrc(a.hpk, kN2 * 8);
+  const float gy = (float)((cd.fixed + 64) & 127) * (1.0f / kN);
+  constexpr bool kRing = SHIFT;
+  const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;
+  float2 v[64];
+
+  auto prop_k = [&] {   // v ← v ⊙ H/N² (K layout)
+    const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_hpk, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 4 * C + r;
+            v[k] = pcm(v[k], t.x[r]);
+            pin(v[k]);
+          }
+        });
+  };
+
+  for (int job = j0; job < j1; ++job) {
+    const int p = __builtin_amdgcn_readfirstlane(job / a.n_idx);
+    const int pat = job - p * a.n_idx;
+    const int tid = rf::opaque(threadIdx.x);
+    const PatInfo pi = pat_info<SHIFT>(a, pat);
+    // v = F(P_p)·W_b (K layout), or the probe (R layout) without shifts
+    {
+      const Rsrc r_fpk = rsrc(a.fpk + (size_t)p * kN2, kN2 * 8);
+      const int vpk = 8 * tid;
+      Ramp rp;
+      rp.init(pi.sy, pi.sx, gy, tid & 1);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = rp.a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[4 * C + r] = SHIFT ? pcm(t.x[r], pcm(A, rp.B[r])) : t.x[r];
+              pin(v[4 * C + r]);
+            }
+          });
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0w = lds0 + (wv << 14);
+    const float2* ringw = buf + (wv << 11);
+    const int os = __builtin_amdgcn_readfirstlane(8 * Nx);
+    const unsigned obytes = (unsigned)(((kN - 1) * Nx + kN) * 8);
+    auto s_obj = [&](int n) { return srd(a.oc + n * plane + (size_t)pi.cy * Nx + pi.cx, obytes); };
+    auto issue1 = [&](auto Q, const v4u& so, int voff) {
+      constexpr int q = decltype(Q)::value;
+      dma_m<2 * q>(so, voff, m0w + (q % 16) * 1024, os);
+    };
+    auto pre1 = [&](int n) {
+      if constexpr (kRing) {
+        const v4u so = s_obj(n);
+        const int vo = dma_off_obj(rf::opaque(tid) & 63, wv, os);
+        rf::sfor<0, 16>([&](auto Q) { issue1(Q, so, vo); });
+      }
+    };
+    if constexpr (SHIFT) {
+      fft_inv(v, buf, lc, cd.wsign, [&] { pre1(0); });
+#pragma unroll
+      for (int j = 0; j < 64; ++j) v[j] = pscale(v[j], inv_n2);
+    }
+    // ------------------------------------------------ slices: park ψⁿ, ×O_n, propagate
+    for (int n = 0; n < Nz; ++n) {
+      const Rsrc r_slot = rsrc(a.slots + fmm_slot(m, pat, n, p), kN2 * 8);
+      if constexpr (kRing) {
+        const v4u so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vo = dma_off_obj(lam, wv, os);
+        const int vpark = park_off(lam, wv);
+        const int io = obj_img(lam);
+        rf::sfor<0, 32>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          vm_wait<ring_wait_count(q, 1, 0, 16)>();
+          const float2* sl = ringw + (q % 16) * 128;
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const int j = 2 * q + rb;
+            const float2 O = sl[rb * 64 + io];
+            st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by k_fmm_adj)
+            v[j] = pcm(v[j], O);
+            pin(v[j]);
+          }
+          if constexpr (q + 16 < 32) issue1(std::integral_constant<int, q + 16>{}, so, vo);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();   // every wave is done with its ring before the next exchange
+      } else {
+        const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)pi.cy * Nx + pi.cx, obytes);
+        const int tq = rf::opaque(threadIdx.x);
+        const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
+        const int ostr = rf::opaque(8 * Nx);
+        pipeline<8>(
+            [&](auto C) {
+              Ch8 t;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) t.x[r] = ld2(r_obj, vobj, ostr * (8 * C + r));
+              return t;
+            },
+            [&](auto C, const Ch8& t) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const int j = 8 * C + r;
+                st2(v[j], r_slot, vslot, 2048 * j);
+                v[j] = pcm(v[j], t.x[r]);
+                pin(v[j]);
+              }
+            });
+      }
+      if (n + 1 < Nz) {
+        fft_fwd(v, buf, lc, cd.wsign);
+        prop_k();
+        fft_inv(v, buf, lc, cd.wsign, [&] { pre1(n + 1); });
+      }
+    }
+    // ------------------------------------------------ far field v = F(ψ_out), K-packed
+    fft_fwd(v, buf, lc, cd.wsign);
+    {
+      const Rsrc r_far = rsrc(a.slots + fmm_far(m, pat, p), kN2 * 8);
+      const int vpk = rf::opaque(8 * tid);
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        st2_stream(v[k], r_far, vpk, 2048 * k);
+        if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ loss: pattern → u, sums
+// One workgroup per pattern: the DP streams HBM → LDS (k_fused3's swizzled image) while the P
+// far fields are read K-packed and their intensities summed in mode order.
+template <int QM, bool SINGLE>
+__global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
+  using namespace rf;
+  const F3Args& a = m.f;
+  __shared__ float2 buf[kLdsElems];
+  __shared__ float s_red[4 * 2];
+  const Coord cd = coord(threadIdx.x);
+  const int pat = blockIdx.x;
+  const PatInfo pi = pat_info<false>(a, pat);
+  const int tid = rf::opaque(threadIdx.x);
+  const int fx = fixed_of(tid), l0 = tid & 1;
+  constexpr float inv_n2 = 1.0f / kN2;
+  {
+    const float* dp = a.meas + (size_t)pi.mi * kN2;
+    const int lane = cd.lane;
+    const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int gi = wv * 16 + i;
+      const int r = 2 * gi + (lane >> 5);
+      const int sl = lane & 31;
+      const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
+      __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
+                                       (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
+                                       kNtAux);
+    }
+  }
+  const float occ_n2 = a.occp[0] * inv_n2;
+  float acc[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) acc[k] = 0.f;
+  const int vpk = 8 * tid;
+  for (int p = 0; p < m.P; ++p) {
+    const Rsrc r_far = rsrc(a.slots + fmm_far(m, pat, p), kN2 * 8);
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_far, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[4 * C + r] = fmaf(occ_n2, cabs2(t.x[r]), acc[4 * C + r]);
+        });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float S = 0.f, Ms = 0.f;
+  {
+    const int r = (fx + 64) & 127;   // fftshifted DP row of ky
+    const int b = 1 - l0;            // fftshifted column half of kx = k + 64 l0
+    const float4* row4 = reinterpret_cast<const float4*>(buf) + r * 32;
+    const Rsrc r_dp = rsrc(a.dp_out ? a.dp_out + (size_t)pat * kN2 : a.psums, a.dp_out ? kN2 * 4 : 0);
+    const int vdp = 4 * (r * kN + 64 * b);
+    const Rsrc r_u = rsrc(m.ubuf + (size_t)pat * kN2, kN2 * 4);
+    const int vu = 4 * tid;
+#pragma unroll
+    for (int kq = 0; kq < 16; ++kq) {
+      const float4 M4 = row4[(kq + 16 * b) ^ ((r & 7) | (b << 3))];
+      const float Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+      float Iv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * kq + e;
+        Iv[e] = acc[k] + kDpEps;
+        st1(loss_point<QM, SINGLE>(Iv[e], Mv[e], a.q, a.eps2, S, Ms), r_u, vu, 1024 * k);
+      }
+      const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, i4),
+                                             r_dp, vdp + 16 * kq, 0, 0);
+    }
+  }
+  float v2[2] = {S, Ms};
+  block_sum4<2>(v2, s_red);
+  if (threadIdx.x == 0) {
+    float* ps = a.psums + (size_t)pat * kNSum;
+    const int base = SINGLE ? 0 : 2;
+    ps[base] = v2[0];
+    ps[base + 1] = v2[1];
+    ps[2 - base] = 0.f;
+    ps[3 - base] = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ adjoint: job → slots, slab
+template <bool SHIFT>
+__global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
+  using namespace rf;
+  const F3Args& a = m.f;
+  __shared__ float2 buf[kLdsElems];
+  __shared__ float s_red[4 * 2];
+  const Coord cd = coord(threadIdx.x);
+  const LaneCtx lc = lane_ctx(cd.lane);
+  constexpr float inv_n = 1.0f / kN;
+  const int w = blockIdx.x, G = gridDim.x;
+  const int nj = a.n_idx * m.P;
+  const int j0 = (int)((long long)w * nj / G), j1 = (int)((long long)(w + 1) * nj / G);
+  if (j0 >= j1) return;
+  const float occ2_n = 2.0f * a.occp[0] * inv_n;
+  const bool tail = a.tail != 0;
+  const int Nx = a.Nx, Nz = a.Nz;
+  const size_t plane = (size_t)a.Ny * a.Nx;
+  const Rsrc r_hpk = rsrc(a.hpk, kN2 * 8);
+  const float gy = (float)((cd.fixed + 64) & 127) * inv_n;
+  constexpr bool kRing = SHIFT;
+  const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;
+  float2 v[64];
+
+  auto prop_kc = [&] {   // v ← v ⊙ conj(H)/N² (K layout)
+    const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
+    pipeline<16>(
+        [&](auto C) {
+          Ch4x2 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_hpk, vpk, 2048 * (4 * C + r));
+          return t;
+        },
+        [&](auto C, const Ch4x2& t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 4 * C + r;
+            v[k] = pcmc(v[k], t.x[r]);
+            pin(v[k]);
+          }
+        });
+  };
+
+  int p_prev = -1;
+  for (int job = j0; job < j1; ++job) {
+    const int p = __builtin_amdgcn_readfirstlane(job / a.n_idx);
+    const int pat = job - p * a.n_idx;
+    const int tid = rf::opaque(threadIdx.x);
+    const PatInfo pi = pat_info<SHIFT>(a, pat);
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0w = lds0 + (wv << 14);
+    const float2* ringw = buf + (wv << 11);
+    const int os = __builtin_amdgcn_readfirstlane(8 * Nx);
+    const unsigned obytes = (unsigned)(((kN - 1) * Nx + kN) * 8);
+    auto s_obj = [&](int n) { return srd(a.oc + n * plane + (size_t)pi.cy * Nx + pi.cx, obytes); };
+    auto s_park = [&](int n) { return srd(a.slots + fmm_slot(m, pat, n, p), kN2 * 8); };
+    auto issue3 = [&](auto Q, const v4u& sp, const v4u& so, int vpo, int voo) {
+      constexpr int q = decltype(Q)::value;
+      dma_c<4096 * q>(sp, vpo, m0w + (q % 8) * 2048);
+      dma_m<2 * q>(so, voo, m0w + (q % 8) * 2048 + 1024, os);
+    };
+    auto pre3 = [&](int n) {
+      if constexpr (kRing) {
+        const v4u sp = s_park(n), so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+        rf::sfor<0, 8>([&](auto Q) { issue3(Q, sp, so, vpo, voo); });
+      }
+    };
+    // g_Ψ·N = v_p·(2 occ u/N) per unit coefficient (as k_fused3's loss epilogue)
+    {
+      const Rsrc r_far = rsrc(a.slots + fmm_far(m, pat, p), kN2 * 8);
+      const Rsrc r_u = rsrc(m.ubuf + (size_t)pat * kN2, kN2 * 4);
+      const int vpk = 8 * tid, vu = 4 * tid;
+      pipeline<16>(
+          [&](auto C) {
+            Ch4u t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              t.x[r] = ld2(r_far, vpk, 2048 * (4 * C + r));
+              t.u[r] = ld1(r_u, vu, 1024 * (4 * C + r));
+            }
+            return t;
+          },
+          [&](auto C, const Ch4u& t) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[4 * C + r] = pscale(t.x[r], occ2_n * t.u[r]);
+              pin(v[4 * C + r]);
+            }
+          });
+    }
+    fft_inv(v, buf, lc, cd.wsign, [&] { pre3(Nz - 1); });
+    // ------------------------------------------------ slices backwards
+    for (int n = Nz - 1; n >= 0; --n) {
+      const Rsrc r_slot = rsrc(a.slots + fmm_slot(m, pat, n, p), kN2 * 8);
+      const float sc = n == Nz - 1 ? inv_n : 1.0f;   // far-field ortho scale once; propagation scaled in K
+      if constexpr (kRing) {
+        const v4u sp = s_park(n), so = s_obj(n);
+        const int lam = rf::opaque(tid) & 63;
+        const int vpo = dma_off_park(lam, wv), voo = dma_off_obj(lam, wv, os);
+        const int io = obj_img(lam);
+        const int vslot = 8 * ((rf::opaque(tid) & 1) * kN + fixed_of(rf::opaque(tid)));
+        rf::sfor<0, 32>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          vm_wait<ring_wait_count(q, 2, 0, 8)>();
+          const float2* sl = ringw + (q % 8) * 256;
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const int j = 2 * q + rb;
+            const float2 ps = sl[rb * 64 + lam];
+            const float2 O = sl[128 + rb * 64 + io];
+            const float2 gv = pscale(v[j], sc);
+            st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // slice n, mode p: g·conj(ψⁿ)
+            v[j] = pcmc(gv, O);                                  // g·conj(O_n)
+            pin(v[j]);
+          }
+          if constexpr (q + 8 < 32) issue3(std::integral_constant<int, q + 8>{}, sp, so, vpo, voo);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();   // every wave is done with its ring before the next exchange
+      } else {
+        const Rsrc r_obj = rsrc(a.oc + n * plane + (size_t)pi.cy * Nx + pi.cx, obytes);
+        const int tq = rf::opaque(threadIdx.x);
+        const int vslot = 8 * ((tq & 1) * kN + fixed_of(tq)), vobj = 8 * (64 * (tq & 1) * Nx + fixed_of(tq));
+        const int ostr = rf::opaque(8 * Nx);
+        pipeline<16>(
+            [&](auto C) {
+              Ch4x2 t;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 4 * C + r;
+                t.x[r] = ld2(r_slot, vslot, 2048 * j);
+                t.y[r] = ld2(r_obj, vobj, ostr * j);
+              }
+              return t;
+            },
+            [&](auto C, const Ch4x2& t) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 4 * C + r;
+                const float2 gv = pscale(v[j], sc);
+                st2_stream(pcmc(gv, t.x[r]), r_slot, vslot, 2048 * j);
+                v[j] = pcmc(gv, t.y[r]);
+                pin(v[j]);
+              }
+            });
+      }
+      if (n > 0) {
+        fft_fwd(v, buf, lc, cd.wsign);
+        prop_kc();
+        fft_inv(v, buf, lc, cd.wsign, [&] { pre3(n - 1); });
+      }
+    }
+    // ------------------------------------------------ probe / position gradient of mode p (× c_m)
+    const bool first = job == j0 || p != p_prev;
+    p_prev = p;
+    if (!tail) continue;
+    const int seg = p + w;
+    float2* segs = a.segslab + (size_t)seg * kN2;
+    const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
+    const Rsrc r_slab_st = rsrc(segs, kN2 * 8);
+    if (first && threadIdx.x == 0) a.segbid[seg] = p;
+    const float cm = m.coef[(size_t)pi.m * kNCoef + m.ci];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = pscale(v[k], cm);
+    const Rsrc r_fpk = rsrc(a.fpk + (size_t)p * kN2, kN2 * 8);
+    if constexpr (SHIFT) {
+      fft_fwd(v, buf, lc, cd.wsign);   // G = F(h), K layout
+      const int vpk = rf::opaque(8 * tid);
+      const int l0b = rf::opaque(tid) & 1;
+      Ramp rc;
+      rc.init(pi.sy, pi.sx, gy, l0b);
+      float sim = 0.f, kim = 0.f;
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              t.x[r] = ld2(r_fpk, vpk, 2048 * k);
+              t.y[r] = ld2(r_slab_ld, vpk, 2048 * k);
+            }
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = rc.a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 4 * C + r;
+              const float2 W = pcm(A, rc.B[r]);
+              const float2 FW = pcm(t.x[r], W);
+              const float im = fmaf(FW.y, v[k].x, -FW.x * v[k].y);   // Im(F(P) W conj(G))
+              sim += im;
+              kim = fmaf((float)k, im, kim);
+              st2(padd2(t.y[r], pcmc(v[k], W)), r_slab_st, vpk, 2048 * k);   // + conj(W) G
+            }
+          });
+      float ds[2] = {gy * sim, fmaf(kim, inv_n, 0.5f * (float)(1 - l0b) * sim)};
+      block_sum4<2>(ds, s_red);
+      if (threadIdx.x == 0) {
+        a.dsu[2 * job] = ds[0];
+        a.dsu[2 * job + 1] = ds[1];
+      }
+    } else {
+      const int vpk = rf::opaque(8 * tid);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.y[r] = ld2(r_slab_ld, vpk, 2048 * (4 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * C + r;
+              st2(cadd(t.y[r], v[j]), r_slab_st, vpk, 2048 * j);   // + h (R layout)
+            }
+          });
+    }
+  }
+}
+
+// Per-mode probe-gradient spectra: block (x, y, p) sums the segments y, y + SPL, … whose mode is p
+// (already scaled by c_m in k_fmm_adj) into part[p][y]; k_segslab_final (grid.y = p) adds the
+// SPL partials in order and unpacks.  Fixed order: deterministic.
+__global__ void k_segslab_reduce_modes(const float2* segslab, const int* segbid, int nseg, float2* part) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y, p = blockIdx.z;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int g = y; g < nseg; g += kSegSplit) {
+    if (segbid[g] != p) continue;
+    acc = cadd(acc, segslab[(size_t)g * kN2 + e]);
+  }
+  part[((size_t)p * kSegSplit + y) * kN2 + e] = acc;
+}
+
+// d_shifts[s] += 2π/N² · Σ_p dsu[job (p, j)]  (c_m applied by k_fmm_adj; modes in order)
+__global__ void k_shift_apply_modes(const int* idx, int n, int n_scans, int P, const float* dsu, float* d_shifts) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  float dy = 0.f, dx = 0.f;
+  for (int p = 0; p < P; ++p) {
+    dy += dsu[2 * ((size_t)p * n + j)];
+    dx += dsu[2 * ((size_t)p * n + j) + 1];
+  }
+  constexpr float k = 6.283185307179586f / kN2;
+  atomicAdd(d_shifts + 2 * s, dy * k);
+  atomicAdd(d_shifts + 2 * s + 1, dx * k);
+}
+
+}  // namespace f3
+}  // namespace ptyx

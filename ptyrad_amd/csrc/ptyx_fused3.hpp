@@ -52,6 +52,7 @@ struct F3Args {
   const float2* oc;        // A e^{iφ}, (Ny, Nx)
   const float* meas;       // (rows, 128, 128) f32, fftshifted
   const int* mrow;         // measurement row of scan position s (NULL: row s; rank-local blocks)
+  int mrows;               // rows of meas (meas_rows entries are clamped into [0, mrows))
   const float* occp;       // omode_occu (device), occ = occp[0]
   float q, eps2;
   float* psums;            // per-pattern loss partial sums (k_finalize)
@@ -77,10 +78,13 @@ __device__ __forceinline__ int packed_rc(int t, int i) {
 }
 
 // natural (N×N complex) → packed, one element per thread
+// (grid.y = mode: plane blockIdx.y of src → plane blockIdx.y of dst)
 template <bool KL>
 __global__ void k_pack128(const float2* src, float2* dst, float scale = 1.0f) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= kN2) return;
+  src += (size_t)blockIdx.y * kN2;
+  dst += (size_t)blockIdx.y * kN2;
   const int i = e >> 8, t = e & 255;
   const float2 v = src[packed_rc<KL>(t, i)];
   dst[e] = make_float2(v.x * scale, v.y * scale);
@@ -105,9 +109,12 @@ __global__ void k_segslab_reduce(const float2* segslab, const int* segbid, int n
   }
   part[(size_t)y * kN2 + e] = acc;
 }
+// (grid.y = mode p: part + p·kSegSplit·N², out + p·N²)
 template <bool KL>
 __global__ void k_segslab_final(const float2* part, float2* out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  part += (size_t)blockIdx.y * kSegSplit * kN2;
+  out += (size_t)blockIdx.y * kN2;
   float2 acc = make_float2(0.f, 0.f);
   for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[(size_t)y * kN2 + e]);
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
@@ -314,15 +321,21 @@ __global__ __launch_bounds__(256) void k_bbox_small(const int* idx, int n, const
 // k_pref_cols1/2), the loss_sparse window sum Σ_{window} |φ|^n into psums[kSumBase]: four fp64
 // lookups per slice, lane z per slice, fixed-order wave sum.  bbox: the table's first row is
 // bbox[0] (PTYX_PREP_CALL), else row 0.  One wave per pattern.
+struct TableCheck {   // input validation of the call's patterns (check_pattern)
+  int* err;
+  const int* mrow;
+  int mrows;
+};
 __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_batches, const int* crop,
                                  int n_scans, int Ny, int Nx, int* bid, int2* geo, const double* pref,
-                                 float* psums, int Nz = 1, const int* bbox = nullptr) {
+                                 float* psums, int Nz, const int* bbox, TableCheck tc) {
   const int j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
   const int s = min(max(idx[j], 0), n_scans - 1);
   const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
   if (lane == 0) {
+    check_pattern(tc.err, idx[j], n_scans, crop, Ny, Nx, kN, tc.mrow, tc.mrows);
     int lo = 0, hi = n_batches;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -357,13 +370,14 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
 __global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, int n, const int* boff, int n_batches,
                                                               const int* crop, int n_scans, int Ny, int Nx, int* bid,
                                                               int2* geo, const float* objp, int sparse_n, float* psums,
-                                                              int Nz) {
+                                                              int Nz, TableCheck tc) {
   __shared__ double s_w[4];
   const int j = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = min(max(idx[j], 0), n_scans - 1);
   const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
   if (threadIdx.x == 0) {
+    check_pattern(tc.err, idx[j], n_scans, crop, Ny, Nx, kN, tc.mrow, tc.mrows);
     int lo = 0, hi = n_batches;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -689,7 +703,7 @@ __device__ __forceinline__ PatInfo pat_info(const F3Args& a, int pat) {
   p.cy = g.x;
   p.cx = g.y;
   p.sidx = min(max(si, 0), a.n_scans - 1);
-  p.mi = a.mrow ? s_ld(a.mrow + p.sidx) : p.sidx;
+  p.mi = a.mrow ? min(max(s_ld(a.mrow + p.sidx), 0), a.mrows - 1) : p.sidx;
   if constexpr (SHIFT) {
     const float2 s = s_ldf2(a.shifts + 2 * p.sidx);
     p.sy = s.x;

@@ -34,6 +34,13 @@ struct GatherArgs {
   float* d_objp;
   int nz = 1, z = 0;     // slots hold nz planes per pattern; this launch gathers plane z, or, with
   int zgrid = 0;         // zgrid, plane blockIdx.y (obja / objp / d_* then point at plane 0)
+  int np = 1;            // MP: plane z of pattern j is the sum of np (≤ kGatherMaxNp) consecutive slot planes
+  long long pstride = 0; // slot planes per pattern (0: nz·np); plane (j, z, p) at j·pstride + z·np + p
+  // candidate split (gridDim.z = S > 1, small objects whose tiles do not fill the GPU): split s
+  // takes every S-th candidate and leaves its tile sums in part / pcnt; k_obj_gather_fin adds the
+  // S partials in order and applies the epilogue
+  float2* part = nullptr;
+  float* pcnt = nullptr;
   const int* bbox = nullptr;   // {min cy, max cy, min cx, max cx} of the call's windows: other tiles exit
   const int* boff = nullptr;   // bin offsets (tiles + 1) into blist, or NULL: scan every pattern
   const int* blist = nullptr;  // pattern indices by bin, ascending within a bin
@@ -41,6 +48,28 @@ struct GatherArgs {
 // 64 × 16 object tiles, 16 waves per tile (measured: 128-wide tiles and 2 patterns per round
 // were slower)
 constexpr int kGTX = 64, kGTY = 16, kGWaves = 16;
+constexpr int kGatherMaxNp = 8;          // probe-mode planes summed per slot (MP)
+constexpr int kGatherPartCap = 4096;     // tile partials of a split gather (× 64·16 × 12 B = 48 MiB)
+
+// d_obja / d_objp of one object pixel from its gathered S = Σ c g_O and sparse count C
+__device__ __forceinline__ void gather_apply(const GatherArgs& ga, size_t off, float2 S, float C) {
+  const float A = ga.obja[off], ph = ga.objp[off];
+  float sn, cs;
+  phase_sincos(ph, &sn, &cs);
+  if (ga.d_obja) ga.d_obja[off] += fmaf(S.x, cs, S.y * sn);
+  if (ga.d_objp) {
+    float dph = A * fmaf(S.y, cs, -S.x * sn);
+    if (C != 0.f) {
+      const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
+      dph += ga.sparse_n == 1 ? C * sg : C * powq(fabsf(ph), (float)(ga.sparse_n - 1)) * sg;
+    }
+    ga.d_objp[off] += dph;
+  }
+}
+template <int N>
+__device__ __forceinline__ bool gather_tile_skip(const GatherArgs& ga, int ty, int tx) {
+  return ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] || tx >= ga.bbox[3] + N);
+}
 
 // ROWPERM: slots written by k_fused3 (N = 128), row y stored at row 2(y & 63) + (y >> 6).
 // bins of a tile's candidates: home tiles (ty − kBinRows + 1 … ty) × (tx − kBinCols + 1 … tx)
@@ -51,7 +80,7 @@ struct BinReach {
 
 // GW: waves per tile (kGWaves for dense calls; 4 when a tile has only a few candidates, so that
 // the per-tile fixed cost, the wave-partial reduction, stays small)
-template <int N, bool ROWPERM = false, int GW = kGWaves>
+template <int N, bool ROWPERM = false, int GW = kGWaves, bool MP = false, bool SPLIT = false>
 __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
   constexpr int N2 = N * N;
   constexpr int NB = BinReach<N>::n;
@@ -63,8 +92,8 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
   const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;                        // slot plane
   const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;   // object plane
   const int ty = tyi * kGTY, tx = txi * kGTX;
-  if (ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] || tx >= ga.bbox[3] + N))
-    return;   // no window of this call touches the tile: its gradient contribution is zero
+  if (gather_tile_skip<N>(ga, ty, tx)) return;   // no window of this call touches the tile: its contribution is zero
+  const int S = SPLIT ? (int)gridDim.z : 1, s = SPLIT ? (int)blockIdx.z : 0;
   int total = ga.n;
   if (ga.boff) {
     if (threadIdx.x < NB) {
@@ -95,12 +124,12 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
     acc[r] = make_float2(0.f, 0.f);
     cnt[r] = 0.f;
   }
-  // scan: wave w takes the 64-pattern chunks w, w + GW, ...; bins: candidate i goes to wave
-  // i mod GW (a tile's few candidates spread over all its waves)
+  // scan: wave w of split s takes the 64-pattern chunks s + S·(w + GW·k); bins: candidate
+  // i = s + S·(w + GW·(lane + 64·k)) (a tile's few candidates spread over all its waves and splits)
   const bool bins = ga.boff != nullptr;
-  const int first = bins ? wave : wave * 64;
-  for (int base = first; base < total; base += 64 * GW) {
-    const int i = bins ? base + GW * lane : base + lane;
+  const int first = bins ? s + S * wave : (s + S * wave) * 64;
+  for (int base = first; base < total; base += 64 * GW * S) {
+    const int i = bins ? base + S * GW * lane : base + lane;
     int j = i;
     int2 o = make_int2(-(1 << 29), -(1 << 29));
     float2 cj = make_float2(0.f, 0.f);
@@ -121,7 +150,8 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
       const int cy = __shfl(o.x, b, 64), cx = __shfl(o.y, b, 64);
       const float c = __shfl(cj.x, b, 64), cs = __shfl(cj.y, b, 64);
       const int jb = __shfl(j, b, 64);
-      const float2* src = ga.ogscr + ((size_t)jb * ga.nz + zp) * N2;
+      const float2* src = MP ? ga.ogscr + ((size_t)jb * ga.pstride + (size_t)zp * ga.np) * N2
+                             : ga.ogscr + ((size_t)jb * ga.nz + zp) * N2;
       const int col = x - cx;
       const bool colok = col >= 0 && col < N;
       float2 v[kGTY];
@@ -130,7 +160,17 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
         const int row = ty + r - cy;
         const int srow = ROWPERM ? 2 * (row & (N / 2 - 1)) + (row >> 6) : row;
         if (colok && row >= 0 && row < N) {
-          v[r] = src[srow * N + col];
+          if constexpr (MP) {   // the probe modes' planes of this slice: loads issued together, summed in mode order
+            float2 t[kGatherMaxNp];
+#pragma unroll
+            for (int pp = 0; pp < kGatherMaxNp; ++pp)
+              t[pp] = pp < ga.np ? src[(size_t)pp * N2 + srow * N + col] : make_float2(0.f, 0.f);
+            v[r] = t[0];
+#pragma unroll
+            for (int pp = 1; pp < kGatherMaxNp; ++pp) v[r] = cadd(v[r], t[pp]);
+          } else {
+            v[r] = src[srow * N + col];
+          }
         } else {
           v[r] = make_float2(0.f, 0.f);
         }
@@ -161,24 +201,39 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
     }
     __syncthreads();
   }
+  if constexpr (SPLIT) {   // this split's tile sums; k_obj_gather_fin adds the splits in order
+    const size_t pb = (((size_t)blockIdx.y * gridDim.x + blockIdx.x) * S + s) * (kGTY * kGTX);
+    for (int e = threadIdx.x; e < kGTY * kGTX; e += 64 * GW) {
+      ga.part[pb + e] = s_acc[e];
+      ga.pcnt[pb + e] = s_cnt[e];
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < kGTY * kGTX; e += 64 * GW) {
     const int y = ty + e / kGTX, xx = tx + e % kGTX;
     if (y >= ga.Ny || xx >= ga.Nx) continue;
-    const size_t off = zoff + (size_t)y * ga.Nx + xx;
-    const float2 S = s_acc[e];
-    const float A = ga.obja[off], ph = ga.objp[off];
-    float sn, cs;
-    phase_sincos(ph, &sn, &cs);
-    if (ga.d_obja) ga.d_obja[off] += fmaf(S.x, cs, S.y * sn);
-    if (ga.d_objp) {
-      float dph = A * fmaf(S.y, cs, -S.x * sn);
-      const float C = s_cnt[e];
-      if (C != 0.f) {
-        const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
-        dph += ga.sparse_n == 1 ? C * sg : C * powq(fabsf(ph), (float)(ga.sparse_n - 1)) * sg;
-      }
-      ga.d_objp[off] += dph;
+    gather_apply(ga, zoff + (size_t)y * ga.Nx + xx, s_acc[e], s_cnt[e]);
+  }
+}
+
+// Split gather epilogue: tile (blockIdx.x, blockIdx.y) sums its S partials in split order.
+template <int N>
+__global__ __launch_bounds__(256) void k_obj_gather_fin(GatherArgs ga, int S) {
+  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
+  const int ty = tyi * kGTY, tx = txi * kGTX;
+  if (gather_tile_skip<N>(ga, ty, tx)) return;
+  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;
+  const size_t pb = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * S * (kGTY * kGTX);
+  for (int e = threadIdx.x; e < kGTY * kGTX; e += blockDim.x) {
+    const int y = ty + e / kGTX, xx = tx + e % kGTX;
+    if (y >= ga.Ny || xx >= ga.Nx) continue;
+    float2 acc = ga.part[pb + e];
+    float c = ga.pcnt[pb + e];
+    for (int s = 1; s < S; ++s) {
+      acc = cadd(acc, ga.part[pb + (size_t)s * (kGTY * kGTX) + e]);
+      c += ga.pcnt[pb + (size_t)s * (kGTY * kGTX) + e];
     }
+    gather_apply(ga, zoff + (size_t)y * ga.Nx + xx, acc, c);
   }
 }
 

@@ -32,6 +32,7 @@
 
 #include "ptyx_common.hpp"
 #include "ptyx_fused3.hpp"
+#include "ptyx_fmm.hpp"
 #include "ptyx_stripe.hpp"
 #include "ptyx_abi.hpp"
 
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_spectrum(K
           if (a.FpT) a.FpT[(size_t)p * N * N + x * N + y] = v;
         }
         if constexpr (N == 128) {   // inverse of f3::packed_rc<true>: row y = fixed_of(t), column x = i + 64·(t & 1)
-          if (a.fpk) a.fpk[(x & 63) * 256 + ((x >> 6) | ((y & 31) << 1) | ((y >> 5) << 6))] = v;
+          if (a.fpk) a.fpk[(size_t)p * N * N + (x & 63) * 256 + ((x >> 6) | ((y & 31) << 1) | ((y >> 5) << 6))] = v;
         }
         return false;
       });
@@ -923,10 +924,10 @@ struct DeviceGuard {
 };
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
-enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneCount };
-const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1};
+enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneCount };
+const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -986,11 +987,16 @@ struct ptyx_plan {
   int* bcur = nullptr;        // (nbins) fill cursors
   int* bkey = nullptr;        // (max_patterns) bin of each pattern
   int* blist = nullptr;       // (max_patterns) patterns by bin
+  float2* gpart = nullptr;    // split gather: tile partials (kGatherPartCap × 64·16)
+  float* gpcnt = nullptr;
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
   float2* hpk = nullptr;      // k_fused3ms: K-packed propagator / N²
   int* bbox = nullptr;        // k_fused3*: bounding box of a call's windows
   bool ms3 = false;           // k_fused3ms (multislice register engine) available
+  bool fmm = false;           // k_fmm_* (mixed-state register engine, N = 128, P > 1, O = 1) available
+  int* err_host = nullptr;    // input-error flags (kErrWords ints, host-mapped; the kernels write 1s)
+  int* err_dev = nullptr;     // their device address
   // N = 256 stripe engine (ptyx_stripe.hpp): per-call intermediates for stripe_cap patterns
   long long stripe_cap = 0;
   int stripe_groups = 0;
@@ -1116,12 +1122,38 @@ static int alloc_bins(ptyx_plan* pl) {
   int rc;
   if ((rc = dalloc(pl, &pl->bcnt, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->boff, (size_t)pl->nbins + 1)) ||
       (rc = dalloc(pl, &pl->bcur, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->bkey, (size_t)d.max_patterns)) ||
-      (rc = dalloc(pl, &pl->blist, (size_t)d.max_patterns)))
+      (rc = dalloc(pl, &pl->blist, (size_t)d.max_patterns)) ||
+      (rc = dalloc(pl, &pl->gpart, (size_t)kGatherPartCap * kGTY * kGTX)) ||
+      (rc = dalloc(pl, &pl->gpcnt, (size_t)kGatherPartCap * kGTY * kGTX)))
     return rc;
   return PTYX_OK;
 }
 
+// k_obj_gather over `tiles` × `nzg` tile planes.  A grid that cannot fill the GPU (a small object:
+// the tBL demo's 370² has 144 tiles a slice) splits every tile's candidates over S workgroups whose
+// partial sums k_obj_gather_fin adds in split order (deterministic for a given call shape).
+template <int N, bool ROWPERM, bool MP>
+static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg, bool sparse_tiles, hipStream_t st) {
+  const int parts = tiles * nzg;
+  int S = 1;
+  if (parts < 1024 && pl->gpart) S = std::max(1, std::min({8, (2048 + parts - 1) / parts, kGatherPartCap / parts}));
+  if (g_tuning[kTuneGatherSplit] >= 1 && pl->gpart)
+    S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], kGatherPartCap / parts));
+  g.part = pl->gpart;
+  g.pcnt = pl->gpcnt;
+  if (S == 1) {
+    if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
+    else hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
+    return;
+  }
+  const dim3 gr(tiles, nzg, S);
+  if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, 4, MP, true>), gr, dim3(64 * 4), 0, st, g);
+  else hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, kGWaves, MP, true>), gr, dim3(64 * kGWaves), 0, st, g);
+  hipLaunchKernelGGL(k_obj_gather_fin<N>, dim3(tiles, nzg), dim3(256), 0, st, g, S);
+}
+
 static void free_plan(ptyx_plan* pl) {
+  if (pl->err_host) (void)hipHostFree(pl->err_host);
   for (void* q : pl->allocs) (void)hipFree(q);
   delete pl;
 }
@@ -1246,7 +1278,10 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     long long mb = std::min<long long>(stripe ? free_b / 6 / (1 << 20) : 65536, (long long)(free_b / 3 / (1 << 20)));
     if (const char* e = std::getenv("PTYX_FFC_MB")) mb = std::atoll(e);
     const long long per = (long long)(d.Nz > 1 ? d.P * d.O * (1 + d.Nz) : d.P * d.O + d.P) * (long long)N2;
-    const long long need = std::min<long long>(d.max_patterns, stripe ? pl->stripe_cap : pl->nwg);
+    // (the mixed-state register engine, N = 128 with one object mode and f32 DPs, keeps its slots
+    // here and works with any capacity)
+    const bool fmm_geo = d.N == 128 && d.O == 1 && d.P <= kGatherMaxNp && !(d.flags & PTYX_MEAS_F16);
+    const long long need = fmm_geo ? 1 : std::min<long long>(d.max_patterns, stripe ? pl->stripe_cap : pl->nwg);
     long long cap = std::min<long long>(d.max_patterns, (mb << 20) / (per * (long long)sizeof(float2)));
     if (stripe) cap = std::min(cap, need);
     if (need > 0 && cap >= need) {
@@ -1256,6 +1291,33 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
       pl->ffc_per = per;
       pl->ffc_cap = cap;
+    }
+  }
+  if (d.N == 128 && d.P > 1 && d.P <= kGatherMaxNp && d.O == 1 && !(d.flags & PTYX_MEAS_F16) && pl->ffc) {
+    // mixed-state register engine (ptyx_fmm.hpp): its slots (parked ψⁿ, then the object gradient)
+    // and far fields are the far-field cache's planes, P·(Nz + 1) per pattern, so it needs no
+    // per-pattern memory of its own and takes the same call sizes; jobs are (pattern, probe mode)
+    int occ3 = 0, o2 = 0;
+    bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fmm_fwd<true>, 256, 0) == hipSuccess && occ3 > 0;
+    for (auto kf : {f3::k_fmm_fwd<false>, f3::k_fmm_adj<true>, f3::k_fmm_adj<false>})
+      if (ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
+    if (ok && occ3 > 0) {
+      pl->nwg3 = (int)std::min<long long>((long long)cu * occ3, std::max<long long>(1, (long long)d.max_patterns * d.P));
+      pl->seg_cap = d.P + pl->nwg3;   // segment ids p + w
+      if ((rc = dalloc(pl, &pl->bid, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->geo, (size_t)d.max_patterns)) ||
+          (rc = dalloc(pl, &pl->pcoef, (size_t)d.max_patterns)) || (rc = dalloc(pl, &pl->fpk, (size_t)d.P * N2)) ||
+          (rc = dalloc(pl, &pl->hpk, N2)) || (rc = dalloc(pl, &pl->bbox, 4)) ||
+          (rc = dalloc(pl, &pl->oc, (size_t)d.Nz * d.Ny * d.Nx)) ||
+          (rc = dalloc(pl, &pl->pref, (size_t)d.Nz * d.Ny * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->preftot, (size_t)d.Nz * ((d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk) * (d.Nx + 1))) ||
+          (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) || (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
+          (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * d.P * 2)) ||
+          (rc = dalloc(pl, &pl->segpart, (size_t)d.P * f3::kSegSplit * N2)) || (rc = alloc_bins(pl))) {
+        free_plan(pl);
+        return rc;
+      }
+      pl->og_cap = pl->ffc_cap;
+      pl->fmm = true;
     }
   }
   if (d.N == 128 && d.P * d.O * d.Nz == 1 && !(d.flags & PTYX_MEAS_F16)) {
@@ -1333,6 +1395,15 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->ms3 = true;
     }
   }
+  // input-error flags in host-mapped memory: the kernels set them (plain stores) and the next call
+  // reads them without synchronising the stream
+  e = hipHostMalloc(reinterpret_cast<void**>(&pl->err_host), sizeof(int) * kErrWords, hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&pl->err_dev), pl->err_host, 0);
+  if (e != hipSuccess) {
+    free_plan(pl);
+    return hip_fail(e, "hipHostMalloc(error flags)");
+  }
+  for (int k = 0; k < kErrWords; ++k) pl->err_host[k] = 0;
   // fp64 twiddles rounded once to fp32: tw[m] = exp(-2πi m/N)
   std::vector<float2> tw(d.N);
   for (int m = 0; m < d.N; ++m) {
@@ -1355,8 +1426,31 @@ extern "C" int ptyx_plan_destroy(ptyx_plan* plan) {
   return PTYX_OK;
 }
 
+// The input errors an earlier call's kernels flagged (check_pattern), reported once and cleared.
+// Reads host memory the device writes: no stream synchronisation (a call still running reports at
+// a later call, or at ptyx_plan_check after the caller synchronised).
+static int take_error(ptyx_plan* pl) {
+  volatile int* e = pl->err_host;
+  if (!e || !(e[kErrIdx] | e[kErrWindow] | e[kErrRow])) return PTYX_OK;
+  std::string msg = "invalid inputs in an earlier call on this plan:";
+  if (e[kErrIdx]) msg += " a scan index outside [0, n_scans);";
+  if (e[kErrWindow]) msg += " a window crop_pos + N outside the (Ny, Nx) object;";
+  if (e[kErrRow]) msg += " a meas_rows entry outside [0, meas_row_count);";
+  msg += " the kernels clamped them, so that call's results are not valid";
+  for (int k = 0; k < kErrWords; ++k) e[k] = 0;
+  return fail(PTYX_EINVAL, msg);
+}
+
+extern "C" int ptyx_plan_check(ptyx_plan* plan) {
+  g_err.clear();
+  if (!plan) return fail(PTYX_EINVAL, "plan is null");
+  return take_error(plan);
+}
+
 static int check_inputs(const ptyx_plan* pl, const ptyx_inputs* in, bool need_meas) {
   if (!in) return fail(PTYX_EINVAL, "inputs is null");
+  if (in->meas_rows && in->meas_row_count < 1)
+    return fail(PTYX_EINVAL, "meas_row_count must give the rows of meas when meas_rows is set");
   if (!in->obja || !in->objp || !in->probe || !in->shifts || !in->omode_occu || !in->crop_pos)
     return fail(PTYX_EINVAL, "a required input pointer is null");
   if (pl->d.Nz > 1 && !in->H) return fail(PTYX_EINVAL, "H is required for Nz > 1");
@@ -1379,6 +1473,8 @@ static KArgs make_args(const ptyx_plan* pl, const ptyx_inputs* in, const int32_t
   a.occu = in->omode_occu; a.meas = in->meas;
   a.ptilt = in->obj_tilts; a.kvec = in->kvec; a.dz = in->dz;
   a.mrow = in->meas_rows;
+  a.mrows = in->meas_rows ? in->meas_row_count : d.n_scans;
+  a.err = pl->err_dev;
   a.idx = idx; a.n_idx = n_idx;
   a.Ibuf = pl->Ibuf;
   a.slab = pl->slab; a.scratch = pl->scratch; a.scratch_stride = pl->scratch_stride;
@@ -1481,32 +1577,32 @@ int launch_status(const char* what) { return ::launch_status(what); }
 // Launch sequence of one ptyx_forward_loss_grad call on the register-resident engine.
 // ptyx_forward_loss_grad_begin / _end phases of one call (kPhaseAll: both, with the call's own sums)
 enum CallPhase { kPhaseAll = 0, kPhaseBegin = 1, kPhaseEnd = 2 };
-enum EngineKind { kEngTwoPass = 0, kEngFused3 = 1, kEngStripe = 2 };
+enum EngineKind { kEngTwoPass = 0, kEngFused3 = 1, kEngStripe = 2, kEngFmm = 3 };
 
-// Preparation, pattern table and the k_fused3 / k_fused3ms pass (everything before k_finalize).
-static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
-                       const ptyx_grads& gz, hipStream_t st) {
+// Preparation shared by the register engines (k_fused3 / k_fused3ms / k_fmm_*): F(P) packed for
+// every probe mode (or the probes R-packed), H/N² packed, the call's bounding box, O = A e^{iφ}
+// and the loss_sparse tables, the pattern table; the segment table (nseg ids) cleared.
+static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                         hipStream_t st, int nseg) {
   constexpr int N = 128, N2 = N * N;
   const ptyx_dims& d = pl->d;
   const bool sparse = cfg->sparse_on != 0;
-  const int Nz = d.Nz;                 // > 1: k_fused3ms (multislice)
+  const int Nz = d.Nz;
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
   if (reuse) {
   } else if (a.shift) {
     KArgs b = a;
-    b.fpk = pl->fpk;   // F(P) packed by the spectrum kernel itself
+    b.fpk = pl->fpk;   // F(P_p) packed by the spectrum kernel itself
     launch_spectrum<N>(pl, b, st);
   } else {
     ProfScope ps(pl, kKPack, st);
-    hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256, d.P), dim3(256), 0, st,
                        reinterpret_cast<const float2*>(in->probe), pl->fpk);
   }
   if (Nz > 1 && !reuse) {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk, 1.0f / N2);   // H/N²
   }
-  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
-  const int nseg = a.n_batches + G;
   // small calls (one mini-batch per optimizer step): one-workgroup bbox that also clears the
   // segment table, and direct loss_sparse window sums instead of the summed-area table
   const bool small = a.n_idx <= f3::kSmallCall && pl->bbox;
@@ -1540,22 +1636,29 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
     if (direct_sums)
       hipLaunchKernelGGL(f3::k_pattern_table_direct, dim3(a.n_idx), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
                          a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.objp, cfg->sparse_n,
-                         pl->psums, Nz);
+                         pl->psums, Nz, f3::TableCheck{a.err, a.mrow, a.mrows});
     else
       hipLaunchKernelGGL(f3::k_pattern_table3, dim3((a.n_idx + 3) / 4), dim3(256), 0, st, a.idx, a.n_idx, a.boff,
                          a.n_batches, a.crop, a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, sparse ? pl->pref : nullptr,
-                         pl->psums, Nz, cfg->prep == PTYX_PREP_CALL ? pl->bbox : nullptr);
+                         pl->psums, Nz, cfg->prep == PTYX_PREP_CALL ? pl->bbox : nullptr,
+                         f3::TableCheck{a.err, a.mrow, a.mrows});
   }
-  const bool single = cfg->single_on != 0;
-  const int ci = single ? 0 : 1;
   if (!small) {
     hipError_t e = hipMemsetAsync(pl->segbid, 0xFF, sizeof(int) * (size_t)nseg, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(segbid)");
   }
+  return launch_status("register engine preparation");
+}
+
+// The register engines' argument block.
+static f3::F3Args register_args(const ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                                const ptyx_grads& gz) {
+  const ptyx_dims& d = pl->d;
+  const bool single = cfg->single_on != 0;
   f3::F3Args f{};
   f.n_idx = a.n_idx; f.n_scans = a.n_scans; f.Ny = d.Ny; f.Nx = d.Nx;
   f.idx = a.idx; f.bid = pl->bid; f.geo = pl->geo; f.shifts = a.shifts;
-  f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas); f.mrow = a.mrow;
+  f.fpk = pl->fpk; f.oc = pl->oc; f.meas = reinterpret_cast<const float*>(a.meas); f.mrow = a.mrow; f.mrows = a.mrows;
   f.occp = in->omode_occu;
   f.q = single ? cfg->single_q : cfg->poissn_q;
   f.eps2 = cfg->poissn_eps;
@@ -1563,8 +1666,21 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   f.slots = pl->ogscr; f.segslab = pl->segslab; f.segbid = pl->segbid; f.dsu = pl->dsu;
   f.tail = (gz.d_probe != nullptr || (a.shift && gz.d_shifts != nullptr)) ? 1 : 0;
   f.dp_out = a.dp_out;
-  f.Nz = Nz;
+  f.Nz = d.Nz;
   f.hpk = pl->hpk;
+  return f;
+}
+
+// Preparation, pattern table and the k_fused3 / k_fused3ms pass (everything before k_finalize).
+static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                       const ptyx_grads& gz, hipStream_t st) {
+  const int Nz = pl->d.Nz;                 // > 1: k_fused3ms (multislice)
+  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int nseg = a.n_batches + G;
+  int rc = register_prep(pl, in, a, cfg, st, nseg);
+  if (rc) return rc;
+  const bool single = cfg->single_on != 0;
+  const f3::F3Args f = register_args(pl, in, a, cfg, gz);
   if (Nz > 1) {
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
@@ -1653,8 +1769,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     g.nz = Nz;
     g.bbox = pl->bbox;   // also for Nz = 1
     g.zgrid = 1;         // every slice plane in one launch (blockIdx.y = slice)
-    if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, true, 4>), dim3(tiles, Nz), dim3(64 * 4), 0, st, g);
-    else hipLaunchKernelGGL((k_obj_gather<N, true>), dim3(tiles, Nz), dim3(64 * kGWaves), 0, st, g);
+    launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
   if (a.shift && gz.d_shifts) {
@@ -1680,6 +1795,119 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   return PTYX_OK;
 }
 
+// ---------------------------------------------------------------- mixed-state register engine
+// (N = 128, P > 1, O = 1; ptyx_fmm.hpp): k_fmm_fwd → k_fmm_loss → k_finalize → k_fmm_adj, then the
+// object gather over the P mode planes of each slice and the per-mode probe / position reductions.
+static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
+                   const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
+  constexpr int N = 128, N2 = N * N;
+  const ptyx_dims& d = pl->d;
+  const int P = d.P, Nz = d.Nz;
+  const bool single = cfg->single_on != 0;
+  const int ci = single ? 0 : 1;
+  const int nj = a.n_idx * P;
+  const int G = std::max(1, std::min(pl->nwg3, nj));
+  const int nseg = P + G;
+  f3::FmArgs m{};
+  m.f = register_args(pl, in, a, cfg, gz);
+  m.f.slots = pl->ffc;
+  m.P = P;
+  m.pstride = (long long)P * (Nz + 1);
+  m.ubuf = pl->Ibuf;
+  m.coef = pl->coef;
+  m.ci = ci;
+  int rc = PTYX_OK;
+  if (ph != kPhaseEnd) {
+    if ((rc = register_prep(pl, in, a, cfg, st, nseg))) return rc;
+    {
+      ProfScope ps(pl, kKFused, st);
+      if (a.shift) hipLaunchKernelGGL(f3::k_fmm_fwd<true>, dim3(G), dim3(256), 0, st, m);
+      else hipLaunchKernelGGL(f3::k_fmm_fwd<false>, dim3(G), dim3(256), 0, st, m);
+    }
+    {
+      ProfScope ps(pl, kKForward, st);
+      const dim3 gr(a.n_idx), bl(256);
+      if (single && m.f.q == 0.5f) hipLaunchKernelGGL((f3::k_fmm_loss<0, true>), gr, bl, 0, st, m);
+      else if (single) hipLaunchKernelGGL((f3::k_fmm_loss<2, true>), gr, bl, 0, st, m);
+      else hipLaunchKernelGGL((f3::k_fmm_loss<2, false>), gr, bl, 0, st, m);
+    }
+    if ((rc = launch_status("k_fmm forward launch"))) return rc;
+  }
+  FinArgs fa{};
+  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
+  fa.psums = pl->psums; fa.occu = in->omode_occu;
+  fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
+  fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
+  fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  if (gz.d_obja || gz.d_objp) {
+    fa.pcoef = pl->pcoef;
+    fa.ci = ci;
+  }
+  fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
+  fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
+  {
+    ProfScope ps(pl, kKFinalize, st);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
+  }
+  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
+  const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
+  if (!any_grad) return PTYX_OK;
+  {
+    ProfScope ps(pl, kKAdjoint, st);
+    if (a.shift) hipLaunchKernelGGL(f3::k_fmm_adj<true>, dim3(G), dim3(256), 0, st, m);
+    else hipLaunchKernelGGL(f3::k_fmm_adj<false>, dim3(G), dim3(256), 0, st, m);
+  }
+  if ((rc = launch_status("k_fmm_adj launch"))) return rc;
+  const bool bins = a.n_idx > f3::kSmallCall;
+  if ((gz.d_obja || gz.d_objp) && bins) {
+    ProfScope ps(pl, kKTable, st);
+    const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
+    hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
+    if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+    const dim3 gn((a.n_idx + 255) / 256);
+    hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
+    hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
+    hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
+  }
+  if (gz.d_obja || gz.d_objp) {
+    GatherArgs g{};
+    g.ogscr = pl->ffc; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
+    g.boff = bins ? pl->boff : nullptr;
+    g.blist = bins ? pl->blist : nullptr;
+    g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = cfg->sparse_on ? cfg->sparse_n : 1;
+    g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
+    g.nz = Nz; g.np = P; g.pstride = m.pstride;
+    g.bbox = pl->bbox;
+    g.zgrid = 1;
+    const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
+    ProfScope ps(pl, kKGather, st);
+    launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
+  }
+  if ((rc = launch_status("k_obj_gather launch"))) return rc;
+  if (a.shift && gz.d_shifts) {
+    ProfScope ps(pl, kKSlabReduce, st);
+    hipLaunchKernelGGL(f3::k_shift_apply_modes, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx,
+                       a.n_scans, P, pl->dsu, gz.d_shifts);
+  }
+  if (gz.d_probe) {
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      hipLaunchKernelGGL(f3::k_segslab_reduce_modes, dim3(N2 / 256, f3::kSegSplit, P), dim3(256), 0, st, pl->segslab,
+                         pl->segbid, nseg, pl->segpart);
+      if (a.shift)
+        hipLaunchKernelGGL(f3::k_segslab_final<true>, dim3(N2 / 256, P), dim3(256), 0, st, pl->segpart, pl->Gsum);
+      else
+        hipLaunchKernelGGL(f3::k_segslab_final<false>, dim3(N2 / 256, P), dim3(256), 0, st, pl->segpart, pl->Gsum);
+    }
+    ProfScope ps(pl, kKProbeFinalize, st);
+    hipLaunchKernelGGL(k_probe_finalize<N>, dim3(P), dim3(Geo<N>::NT), 0, st, a, pl->Gsum,
+                       reinterpret_cast<float2*>(gz.d_probe));
+  }
+  return launch_status("k_fmm probe / position reduction launch");
+}
+
 // ---------------------------------------------------------------- stripe engine (N = 256)
 // Launch sequence of one ptyx_forward_loss_grad call on the stripe engine (ptyx_stripe.hpp).
 // The stripe engine's per-call argument block (shared by the passes before and after k_finalize).
@@ -1692,6 +1920,7 @@ static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_los
   SArgs s{};
   s.n = n; s.P = P; s.O = O; s.Ny = d.Ny; s.Nx = d.Nx; s.n_scans = d.n_scans; s.meas_f16 = a.meas_f16;
   s.idx = a.idx; s.bid = pl->bid; s.geo = pl->geo; s.shifts = a.shifts; s.sxy = pl->ssxy; s.mrow = a.mrow;
+  s.mrows = a.mrows;
   s.Fp = pl->Fp; s.oc = pl->oc; s.obja = a.obja; s.objp = a.objp; s.meas = a.meas; s.occu = a.occu;
   s.q = single ? cfg->single_q : cfg->poissn_q;
   s.eps2 = cfg->poissn_eps;
@@ -1728,7 +1957,7 @@ static int stripe_pass(ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, 
   {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(k_s_table, dim3((n + 255) / 256), dim3(256), 0, st, a.idx, n, a.boff, a.n_batches, a.crop,
-                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.shifts, pl->ssxy);
+                       a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.shifts, pl->ssxy, a.err, a.mrow, a.mrows);
     hipLaunchKernelGGL(f3::k_bbox_init, dim3(1), dim3(64), 0, st, pl->bbox);
     hipLaunchKernelGGL(f3::k_bbox, dim3(std::max(1, std::min(f3::kBboxBlocks, (n + 255) / 256))), dim3(256), 0, st, a.idx, n, a.crop, a.n_scans, d.Ny, d.Nx,
                        pl->bbox, kN);
@@ -1857,8 +2086,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
       g.objp = a.objp + o * plane;
       g.d_obja = gz.d_obja ? gz.d_obja + o * plane : nullptr;
       g.d_objp = gz.d_objp ? gz.d_objp + o * plane : nullptr;
-      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<kN, false, 4>), dim3(tiles), dim3(64 * 4), 0, st, g);
-      else hipLaunchKernelGGL((k_obj_gather<kN, false>), dim3(tiles), dim3(64 * kGWaves), 0, st, g);
+      launch_gather<kN, false, false>(pl, g, tiles, 1, sparse_tiles, st);
     }
     if ((rc = launch_status("stripe k_obj_gather launch"))) return rc;
   }
@@ -1980,6 +2208,7 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
                             float* dp_out) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (int rc0 = take_error(pl)) return rc0;
   int rc = check_inputs(pl, in, false);
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
@@ -2067,10 +2296,14 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit && one_term;
   // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): one data term, call within capacity
   const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && one_term;
+  // mixed-state register engine (N = 128, P > 1, O = 1): one data term, f32 DPs, the call within
+  // the far-field cache its slots live in
+  const bool fmm = any_grad && !want_H && pl->fmm && !a.meas_f16 && one_term && n_idx <= pl->ffc_cap;
 #ifdef PTYX_ONLY_N
-  *engine = (fused3 || fused3ms) && PTYX_ONLY_N == 128 ? kEngFused3 : stripe && PTYX_ONLY_N == 256 ? kEngStripe : kEngTwoPass;
+  *engine = (fused3 || fused3ms) && PTYX_ONLY_N == 128 ? kEngFused3 : fmm && PTYX_ONLY_N == 128 ? kEngFmm
+          : stripe && PTYX_ONLY_N == 256 ? kEngStripe : kEngTwoPass;
 #else
-  *engine = (fused3 || fused3ms) ? kEngFused3 : stripe ? kEngStripe : kEngTwoPass;
+  *engine = (fused3 || fused3ms) ? kEngFused3 : fmm ? kEngFmm : stripe ? kEngStripe : kEngTwoPass;
 #endif
   // (not with propagator gradients: k_adjoint's recomputed forward is what parks their Xⁿ)
   if (*engine == kEngTwoPass && any_grad && pl->ffc && n_idx <= pl->ffc_cap && !a.hslab && !a.d_tilts && !a.d_dz) {
@@ -2157,6 +2390,7 @@ static int run_call(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const 
                     bool defer) {
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
   if (engine == kEngFused3) return run_fused3(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
+  if (engine == kEngFmm) return run_fmm(pl, in, a, cfg, gz, st, loss_terms, ph, bsums);
 #endif
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 256
   if (engine == kEngStripe) return run_stripe(pl, in, a, cfg, gz, st, loss_terms, ph, bsums, defer);
@@ -2170,6 +2404,7 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
                                       const ptyx_grads* grads) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (int rc0 = take_error(pl)) return rc0;
   int rc = busy(pl);
   if (rc) return rc;
   ptyx_grads gz{};
@@ -2192,6 +2427,7 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
                                             double* batch_sums) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (int rc0 = take_error(pl)) return rc0;
   int rc = busy(pl);
   if (rc) return rc;
   if (!batch_sums) return fail(PTYX_EINVAL, "batch_sums is null");
@@ -2235,6 +2471,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
                                  int32_t n_idx, const float* dLdI, float grad_scale, const ptyx_grads* grads) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (int rc0 = take_error(pl)) return rc0;
   int rc = check_inputs(pl, in, false);
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");

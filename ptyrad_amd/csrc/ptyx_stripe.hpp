@@ -64,6 +64,7 @@ struct SArgs {
   const float2* sxy;     // (n) this call's patterns' (sy, sx), gathered by k_s_table: one load, no
                          // idx → shifts chain in front of the passes' first barrier
   const int* mrow;       // measurement row of a scan index (NULL: the index itself)
+  int mrows;             // rows of meas (meas_rows entries are clamped into [0, mrows))
   const float2* Fp;      // (P, N, N) F(probe), natural order
   const float2* oc;      // (O, Ny, Nx) A e^{iφ}
   const float* obja;
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
   }
   // loss at every point of the stripe (fftshifted DP index), unit-coefficient ∂ℓ/∂I
   const int sidx = scan_of(a, j);
-  const size_t mi = (size_t)(a.mrow ? a.mrow[sidx] : sidx);
+  const size_t mi = (size_t)meas_row(a.mrow, a.mrows, sidx);
   const int col = (kx + kN / 2) & (kN - 1);
   float Mv[16];
 #pragma unroll
@@ -665,9 +666,11 @@ __global__ __launch_bounds__(256, kPassWG) void k_s5(SArgs a) {
 // ---------------------------------------------------------------------------------- small kernels
 // pattern → (mini-batch, clamped window origin)
 __global__ void k_s_table(const int* idx, int n, const int* boff, int n_batches, const int* crop, int n_scans, int Ny,
-                          int Nx, int* bid, int2* geo, const float* shifts, float2* sxy) {
+                          int Nx, int* bid, int2* geo, const float* shifts, float2* sxy, int* err, const int* mrow,
+                          int mrows) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
+  check_pattern(err, idx[j], n_scans, crop, Ny, Nx, kN, mrow, mrows);
   int lo = 0, hi = n_batches;
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;

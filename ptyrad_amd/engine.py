@@ -143,9 +143,10 @@ class Plan:
             _need(kvec, torch.float32, "kvec", dev)
             if tuple(tilts.shape) != (d.n_scans, 2) or tuple(kvec.shape) != (d.N,):
                 raise ValueError("per-position obj_tilts must be (n_scans, 2) and kvec (N,)")
+        rows_n = int(meas.shape[0]) if (meas is not None and meas_rows is not None) else 0
         inp = _lib.Inputs(_ptr(obja), _ptr(objp), _ptr(probe_rv), _ptr(shifts), _ptr(H), _ptr(occu),
                           _ptr(crop_pos), _ptr(meas), _ptr(tilts), _ptr(kvec if tilts is not None else None),
-                          float(dz), _ptr(meas_rows))
+                          float(dz), _ptr(meas_rows), rows_n)
         return inp, H
 
     def _idx(self, idx):
@@ -189,6 +190,7 @@ class Plan:
     def forward(self, t: dict, idx, dp_out=None):
         """ptyx_forward: dp (n, N, N) f32 = PtychoAD.forward(idx); calls larger than the plan's
         max_patterns run in pieces (patterns are independent in the forward model)."""
+        self._prev_errors()
         idx_t = self._idx(idx)
         n = int(idx_t.numel())
         if dp_out is None:
@@ -202,17 +204,20 @@ class Plan:
                                              _ptr(dp_out[a:b])))
         return dp_out
 
-    def _check_rows(self, t: dict, idx_t):
-        """meas_rows[idx] must address rows of the rank-local measurement block (include/ptyx.h:
-        the kernels do not check it).  One small device reduction and a host sync."""
-        rows = t.get("meas_rows")
-        if rows is None or idx_t.numel() == 0:
-            return
-        r = rows[idx_t.long()]
-        lo, hi = (int(v) for v in torch.aminmax(r))
-        if lo < 0 or hi >= t["meas"].shape[0]:
-            raise IndexError(f"meas_rows maps a position of this call to row {lo if lo < 0 else hi}, outside the "
-                             f"{t['meas'].shape[0]}-row measurement block")
+    def _prev_errors(self):
+        """Input errors the device flagged in an earlier call on this plan (include/ptyx.h:
+        ptyx_plan_check; a host read, no synchronisation), raised as IndexError — what the
+        reference's advanced indexing raises (models.py:261-264)."""
+        rc = self.lib.ptyx_plan_check(self._h)
+        if rc == _lib.PTYX_EINVAL:
+            raise IndexError(self.lib.ptyx_last_error().decode())
+        _lib.check(rc)
+
+    def check(self):
+        """Synchronise the plan's stream and raise IndexError if any call so far had a scan index,
+        window or meas_rows entry out of range (the device checks every pattern as it reads it)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        self._prev_errors()
 
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
                           grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None, prep=0,
@@ -229,8 +234,7 @@ class Plan:
         (one all-reduce); the loss terms and gradient coefficients then belong to the whole
         mini-batches.  Such a call is never split, so it must fit the plan's capacity.
         """
-        if not _rows_checked:
-            self._check_rows(t, self._idx(idx))
+        self._prev_errors()   # (_rows_checked: kept for callers; the device checks every call)
         if batch_sums_reduce is not None:
             return self._split_call(t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out,
                                     batch_sums_reduce)
@@ -284,6 +288,13 @@ class Plan:
         return dLdI
 
     @property
+    def call_capacity(self) -> int:
+        """Patterns one ptyx_forward_loss_grad call takes without being split: the register
+        engines' capacity, within max_patterns (what a split-batch call must fit)."""
+        cap = self.register_capacity
+        return min(cap, int(self.dims.max_patterns)) if cap > 0 else int(self.dims.max_patterns)
+
+    @property
     def register_capacity(self) -> int:
         """Patterns per call the register-resident engines take (0: none for this geometry)."""
         return int(self.lib.ptyx_plan_register_capacity(self._h))
@@ -321,9 +332,8 @@ class Plan:
         idx_t = self._idx(idx)
         off_t = self._idx(batch_offsets)
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
-        cap = self.register_capacity
-        cap = min(cap, int(self.dims.max_patterns)) if cap > 0 else int(self.dims.max_patterns)
-        if n > cap:
+        cap = self.call_capacity
+        if n > cap:   # (recon_step cuts split groups by DistContext.split_ranges, the same on every rank)
             raise ValueError(f"a split-batch call of {n} patterns exceeds the plan's capacity {cap}")
         if loss_terms is None:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
@@ -344,6 +354,7 @@ class Plan:
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):
         """ptyx_adjoint_dldi: accumulate gradients for an external dL/d(dp)."""
+        self._prev_errors()
         idx_t = self._idx(idx)
         n = int(idx_t.numel())
         _need(dLdI, torch.float32, "dLdI", self.device)

@@ -65,6 +65,19 @@ class _FusedLoss(torch.autograd.Function):
         return (*out, None, None, None, None, None, None)
 
 
+def model_stages(model_params=None, init_variables=None) -> bool:
+    """Whether a PtychoHIP built from these constructor inputs runs an autograd stage (detector blur,
+    object pre-blur, on-the-fly measurement padding / resampling: models.py:375-412) — the model
+    attributes CombinedLoss._special reads, decided from the inputs alone."""
+    mp = model_params or {}
+    iv = init_variables or {}
+    blur = any(mp.get(k) not in (None, 0) for k in ("detector_blur_std", "obj_preblur_std"))
+    sf = iv.get("on_the_fly_meas_scale_factors")
+    otf = iv.get("on_the_fly_meas_padded") is not None or (
+        sf is not None and any(float(f) != 1 for f in np.asarray(sf).reshape(-1)))
+    return bool(blur or otf)
+
+
 class CombinedLoss(torch.nn.Module):
     """Same loss_params dict and call signature as the reference CombinedLoss."""
 
@@ -177,11 +190,20 @@ class CombinedLoss(torch.nn.Module):
         return (getattr(model, "detector_blur", False) or getattr(model, "preblur", False) or
                 getattr(model, "otf_meas", False) or self.loss_params.get("loss_simlar", {}).get("state", False))
 
-    def supports_batch_split(self, model) -> bool:
+    def supports_batch_split(self, model=None, *, model_params=None, init_variables=None) -> bool:
         """Whether ``fused_into(..., batch_sums_reduce=...)`` can take mini-batches split over ranks:
         every loss term must be a function of per-pattern additive sums (not loss_pacbed, whose
-        mean pattern is a per-batch N² sum, nor the autograd stages)."""
-        return not self._special(model) and not self.loss_params.get("loss_pacbed", {}).get("state", False)
+        mean pattern is a per-batch N² sum, nor the autograd stages).
+
+        Before the model exists (a rank choosing which DPs to load, DistContext.local_indices) the
+        stages are read from the constructor's ``model_params`` / ``init_variables`` instead, by
+        the rules PtychoHIP applies, so the block and recon_step make the same decision."""
+        if self.loss_params.get("loss_pacbed", {}).get("state", False):
+            return False
+        if model is not None:
+            return not self._special(model)
+        return not (self.loss_params.get("loss_simlar", {}).get("state", False) or
+                    model_stages(model_params, init_variables))
 
     def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None):
         """The hot path without autograd: gradients of (Σ_m loss_m)·grad_scale are ACCUMULATED

@@ -29,7 +29,9 @@ run in the engine (per-pattern separable ramps, d_tilts, d_dz).
 
 Rank-local measurements (the data-parallel driver): ``init_variables["measurements"]``
 may hold only the DPs of the scan positions listed in ``init_variables["measurements_index"]``
-(e.g. ``DistContext.local_indices(batches, grad_accumulation)``); the engine reads them through a
+(``DistContext.local_indices(batches, grad_accumulation, loss_fn=..., model_params=...,
+init_variables=...)``, which makes recon_step's split decision for this loss and model); the engine
+reads them through a
 scan-index → row map (ptyx_inputs.meas_rows), and any call on a position outside the block raises.
 The reference registers the full stack on every rank (models.py:109).
 """

@@ -154,6 +154,7 @@ class DistContext:
         self.always_reduce = bool(always_reduce) and dist.is_initialized()
         self.band_exchange = bool(band_exchange)
         self.bands = None
+        self.block_split = None   # the split decision local_indices built a measurement block for
 
     def _collective(self) -> bool:
         return self.world > 1 or self.always_reduce
@@ -170,6 +171,26 @@ class DistContext:
             return bool(self.split_batches)
         return 1 < self.world and len(group_batches) < self.world
 
+    def split_ranges(self, group, cap):
+        """Consecutive mini-batch ranges [a, b) of a split group whose parts fit one engine call of
+        ``cap`` patterns on EVERY rank: decided from the whole mini-batches' sizes (rank 0's part,
+        ⌈len / world⌉, is the largest), so all ranks cut the group alike and each range is one
+        all-reduce of its loss sums on every rank.  Exact: every mini-batch keeps its own
+        normalisation.  A single part larger than ``cap`` raises on every rank alike."""
+        sizes = [-(-len(np.asarray(b).reshape(-1)) // self.world) for b in group]
+        if cap is None or cap <= 0:
+            return [(0, len(group))]
+        if max(sizes, default=0) > cap:
+            raise ValueError(f"a mini-batch part of {max(sizes)} positions exceeds the engine's call capacity {cap}")
+        out, a, n = [], 0, 0
+        for i, s in enumerate(sizes):
+            if i > a and n + s > cap:
+                out.append((a, i))
+                a, n = i, 0
+            n += s
+        out.append((a, len(group)))
+        return out
+
     def my_part(self, batch):
         """This rank's contiguous share of one mini-batch (np.array_split over the ranks; rank 0's
         share is never empty for a non-empty mini-batch)."""
@@ -179,6 +200,7 @@ class DistContext:
         """The mini-batches (or parts of them) this rank processes over one iteration of recon_step.
         split=False: the loss cannot be split (CombinedLoss.supports_batch_split), whole batches."""
         ga = max(1, int(grad_accumulation))
+        split = bool(split)
         out = []
         for g0 in range(0, len(batches), ga):
             group = batches[g0:g0 + ga]
@@ -193,20 +215,33 @@ class DistContext:
         if self._collective():
             dist.all_reduce(t, group=self.group)
 
-    def local_indices(self, batches, grad_accumulation=1, split=True):
-        """Sorted scan indices whose DPs this rank needs: its ``measurements_index`` block."""
+    def local_indices(self, batches, grad_accumulation=1, split=None, loss_fn=None, model_params=None,
+                      init_variables=None):
+        """Sorted scan indices whose DPs this rank needs: its ``measurements_index`` block.
+
+        split: whether groups with fewer mini-batches than ranks are split within the mini-batches.
+        None = the decision recon_step makes, ``loss_fn.supports_batch_split`` on the model these
+        ``model_params`` / ``init_variables`` build (True without a loss_fn).  The decision is
+        recorded; recon_step refuses (on every rank, before any collective) to run a split that
+        disagrees with it, since the block would then lack DPs the rank is given."""
+        if split is None:
+            split = loss_fn.supports_batch_split(model_params=model_params, init_variables=init_variables) \
+                if loss_fn is not None else True
+        self.block_split = bool(split)
         mine = self.local_batches(batches, grad_accumulation, split)
         if not mine:
             return np.zeros(0, np.int64)
         return np.unique(np.concatenate([np.asarray(b).reshape(-1) for b in mine]))
 
-    def grad_views(self, params):
+    def grad_views(self, params, extra=0, device=None):
         """Give each param a zeroed ``.grad`` that is a view into ONE flat f32 buffer; returns it.
         ``params`` must be the same list, in the same order, on every rank.  The buffer is reused
-        from step to step (zeroed on the device) while the list stays the same."""
-        n = sum(p.numel() for p in params)
-        dev = params[0].device if params else torch.device("cpu")
-        key = tuple(id(p) for p in params)
+        from step to step (zeroed on the device) while the list stays the same.  ``extra`` floats
+        follow the parameters' views: the step's (G, 5) loss terms ride in the same all-reduce
+        (``terms_tail``), so a step needs no separate collective for them."""
+        n = sum(p.numel() for p in params) + int(extra)
+        dev = params[0].device if params else (device or torch.device("cpu"))
+        key = (tuple(id(p) for p in params), int(extra))
         cached = getattr(self, "_flat", None)
         if cached is not None and cached[0] == key and cached[1].numel() == n and cached[1].device == dev:
             flat = cached[1]
@@ -225,14 +260,20 @@ class DistContext:
         if self._collective() and flat is not None and flat.numel():
             dist.all_reduce(flat, group=self.group)
 
-    def gather_terms(self, terms_local, idx_local, n_total, device):
-        """All ranks get the (n_total, 5) loss terms of the group (rows filled by their owners)."""
-        buf = torch.zeros((n_total, 5), dtype=torch.float32, device=device)
+    @staticmethod
+    def terms_tail(flat, extra, G):
+        """The (G, 5) loss-term rows at the start of the ``extra`` floats grad_views appended."""
+        n0 = flat.numel() - int(extra)
+        return flat[n0:n0 + 5 * G].view(G, 5)
+
+    def put_terms(self, tail, terms_local, idx_local):
+        """Rows of the group's loss terms this rank owns, into the (zeroed) tail of the flat
+        buffer: after the gradient all-reduce every rank holds the whole group's terms."""
         if len(idx_local):
-            buf[torch.as_tensor(idx_local, device=device)] = terms_local.to(device)
-        if self._collective():
-            dist.all_reduce(buf, group=self.group)
-        return buf
+            if list(idx_local) == list(range(tail.shape[0])):
+                tail.copy_(terms_local)
+            else:
+                tail[torch.as_tensor(idx_local, device=tail.device)] = terms_local.to(tail.device)
 
 
 class ObjectBands:
@@ -251,7 +292,12 @@ class ObjectBands:
     Gradient bytes sent per rank: the touched rows outside the own band (the halo of a row-sharded
     scan) instead of a full-object all-reduce; the all-gather moves (W − 1) / W of the object.  A
     pixel that at most two ranks touch gets the same sum as the all-reduce bit for bit (a + b);
-    with more contributors only the fp32 summation order differs."""
+    with more contributors only the fp32 summation order differs.
+
+    Optimizer state: the objects' moments live in this rank's band optimizer (``ObjectBands.opt``),
+    not in the caller's optimizer, so ``optimizer.state_dict()`` (save.py:110's optim_state_dict)
+    does not hold them: a run resumed from such a checkpoint restarts the object moments.  The
+    band optimizer's hyperparameters (lr, betas, …) are copied from the caller's groups every step."""
 
     def __init__(self, ctx, Ny, device):
         self.ctx, self.Ny, self.device = ctx, int(Ny), device
@@ -261,6 +307,7 @@ class ObjectBands:
         self.b1 = min(self.Ny, (ctx.rank + 1) * self.R)
         self.ranges = [(0, self.Ny)] * W
         self.opt = None
+        self._src_groups = []   # the caller's param group behind each band-optimizer group
         self.views = {}
 
     def set_rows(self, lo, hi):
@@ -329,7 +376,13 @@ class ObjectBands:
                         self.views[id(p)] = v
                         views.append(v)
                     groups.append({**{k: v for k, v in gr.items() if k != "params"}, "params": views})
+                    self._src_groups.append(gr)
             self.opt = type(optimizer)(groups, **optimizer.defaults) if groups else None
+        if self.opt is not None:   # hyperparameters follow the caller's optimizer (lr schedules, edits)
+            for bg, gr in zip(self.opt.param_groups, self._src_groups):
+                for k, v in gr.items():
+                    if k != "params":
+                        bg[k] = v
         for v in self.views.values():
             v.grad = None
         for p in params:
@@ -404,6 +457,13 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     reached = {id(model.optimizable_tensors[k]) for k in model.engine_grad_names()}
     live = [p for p in params if p.requires_grad and id(p) in reached]
     split_ok = hasattr(loss_fn, "supports_batch_split") and loss_fn.supports_batch_split(model)
+    if ctx.block_split is not None and ctx.block_split != split_ok and any(
+            ctx.splits(batches[g0:g0 + ga]) for g0 in range(0, len(batches), ga)):
+        # (the same on every rank: no rank enters a collective this iteration)
+        raise ValueError(f"the rank's measurement block was built for split_batches={ctx.block_split} "
+                         f"(DistContext.local_indices) but this loss / model {'can' if split_ok else 'cannot'} "
+                         "split mini-batches: build it with local_indices(..., loss_fn=loss_fn, model_params=..., "
+                         "init_variables=...)")
     objs = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in live)]
     band = ctx.band_exchange and ctx._collective() and bool(objs)
     if band:
@@ -423,23 +483,27 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         if graphs and why:
             raise RuntimeError(f"recon_step(graphs=True): {why}")
         use_graphs = why is None and (graphs or -(-len(batches) // ga) >= GRAPH_MIN_STEPS) and bool(live)
+    # with collectives, the step's loss terms ride in the gradient all-reduce (5·ga extra floats)
+    extra = 5 * ga if ctx._collective() else 0
     if use_graphs:
         sg = getattr(model, "_step_graphs", None)
         if sg is None:
             sg = model._step_graphs = StepGraphs()
-        flat = ctx.grad_views(live)
-        rows.append(sg.run(model, optimizer, loss_fn, batches, ga, live, flat))
+        flat = ctx.grad_views(live, extra, dev)
+        rows.append(sg.run(model, optimizer, loss_fn, batches, ga, live, flat, ctx=ctx, extra=extra))
         optimizer.zero_grad(set_to_none=True)
         model.clear_cache()
     for g0 in (range(0, len(batches), ga) if not use_graphs else ()):
         group = batches[g0:g0 + ga]
-        flat = ctx.grad_views(live)
+        flat = ctx.grad_views(live, extra, dev)
         if ctx.splits(group) and split_ok:
             # every rank holds a part of every mini-batch; the loss sums are all-reduced inside the
             # engine call, so each mini-batch keeps its whole-batch normalisation.  Rank 0's part of
             # every mini-batch is non-empty: its terms are the group's.
-            terms = loss_fn.fused_into(model, [ctx.my_part(b) for b in group], grad_scale=1.0 / ga,
-                                       batch_sums_reduce=ctx.allreduce_sums)
+            cap = model.plan.call_capacity if hasattr(model, "plan") else None
+            terms = torch.cat([loss_fn.fused_into(model, [ctx.my_part(b) for b in group[a:b]], grad_scale=1.0 / ga,
+                                                  batch_sums_reduce=ctx.allreduce_sums)
+                               for a, b in ctx.split_ranges(group, cap)])
             mine = list(range(len(group))) if ctx.rank == 0 else []
             if ctx.rank:
                 terms = terms[:0]
@@ -454,10 +518,13 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
                 terms = loss_fn.fused_into(model, [group[i] for i in mine], grad_scale=1.0 / ga)
             else:
                 terms = torch.zeros((0, 5), device=dev)
+        if extra:
+            tail = ctx.terms_tail(flat, extra, len(group))
+            ctx.put_terms(tail, terms, mine)
         if band:
             n_obj = sum(p.numel() for p in objs)
-            ctx.allreduce(flat[n_obj:])                # probe, positions, propagator: small (a
-            ctx.bands.reduce([p.grad for p in objs])   # collective first: RCCL's communicator)
+            ctx.allreduce(flat[n_obj:])                # probe, positions, propagator, loss terms:
+            ctx.bands.reduce([p.grad for p in objs])   # small (a collective first: RCCL's communicator)
             saved = [p.grad for p in objs]
             for p in objs:
                 p.grad = None                          # the caller's optimizer skips the objects
@@ -471,7 +538,7 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             optimizer.step()
         optimizer.zero_grad(set_to_none=True)
         # the loss terms stay on the device until the iteration ends (no host sync per step)
-        rows.append(ctx.gather_terms(terms, mine, len(group), dev) if ctx._collective() else terms)
+        rows.append(tail.clone() if extra else terms)
         model.clear_cache()
     for row in (torch.cat(rows).cpu().numpy() if rows else ()):   # one sync per iteration
         for name, v in zip(LOSS_TERM_NAMES, row):

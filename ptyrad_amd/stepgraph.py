@@ -16,14 +16,19 @@ Same kernels, same order, same arguments as the eager step: the trajectory is bi
 (tests/test_gpu_stepgraph.py).  The first step of every new shape runs eagerly through the same
 body (it creates the optimizer state a capture must not allocate), the next is captured.
 
-Eligible: one rank (no collectives inside the step), the plain fused engine path (no autograd
-stages, no loss_pacbed, no optimised propagator), ``ptyrad_amd.optim.Adam`` / ``AdamW``
-(``create_optimizer``'s default) or torch's Adam / AdamW with ``fused=True``, and every step small
-enough for one engine call.
+Eligible: the plain fused engine path (no autograd stages, no loss_pacbed, no optimised
+propagator), ``ptyrad_amd.optim.Adam`` / ``AdamW`` (``create_optimizer``'s default) or torch's
+Adam / AdamW with ``fused=True``, and every step small enough for one engine call.  With several
+ranks (or ``always_reduce``) the step's RCCL collectives are captured too: the all-reduce of a
+split step's per-mini-batch loss sums (between ptyx_forward_loss_grad_begin and _end) and the
+gradient all-reduce, which also carries the step's loss terms — one or two collectives a step,
+replayed with the kernels.  Needs the 'nccl' (RCCL) backend, no band exchange, and every rank
+holding a part of every mini-batch of a split step.
 """
 from __future__ import annotations
 
 import ctypes
+from dataclasses import astuple
 
 import numpy as np
 import torch
@@ -33,13 +38,31 @@ from .engine import LossConfig, _ptr, batch_offsets
 
 
 def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation):
-    """None when recon_step's steps can be graph-replayed, else why not (a short string)."""
+    """None when recon_step's steps can be graph-replayed, else why not (a short string).  The
+    answer depends only on the job's shapes and settings, never on the rank, so every rank takes
+    the same path."""
     if not torch.cuda.is_available() or model.opt_obja.device.type != "cuda":
         return "no HIP device"
-    if ctx is not None and (ctx._collective() or ctx.band_exchange):
-        return "collectives inside the step"
+    if ctx is not None and ctx.band_exchange:
+        return "band exchange (point-to-point collectives per step)"
     if not (hasattr(loss_fn, "_special") and hasattr(loss_fn, "supports_batch_split")):
         return "loss_fn is not ptyrad_amd.losses.CombinedLoss"
+    ga = max(1, int(grad_accumulation))
+    coll = ctx is not None and ctx._collective()
+    if coll:
+        import torch.distributed as dist
+        if dist.get_backend(ctx.group) != "nccl":
+            return "collectives on a backend graphs cannot capture (RCCL 'nccl' only)"
+        split_ok = loss_fn.supports_batch_split(model)
+        for g0 in range(0, len(batches), ga):
+            group = batches[g0:g0 + ga]
+            if ctx.splits(group):
+                if not split_ok:
+                    return "a split step with a loss that cannot be split"
+                if min(len(np.asarray(b).reshape(-1)) for b in group) < ctx.world:
+                    return "a mini-batch with fewer positions than ranks (empty parts)"
+            elif len(group) < ctx.world:
+                return "a step that leaves ranks without a mini-batch"
     if loss_fn._special(model) or loss_fn.loss_params.get("loss_pacbed", {}).get("state", False):
         return "autograd stages or loss_pacbed"
     if getattr(model, "prop_opt", False) or model._dz_t() is not None:
@@ -50,13 +73,36 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
     if not hip_adam and (not isinstance(optimizer, (torch.optim.Adam, torch.optim.AdamW)) or
                          not all(g.get("fused") for g in optimizer.param_groups)):
         return "optimizer is not ptyrad_amd.optim.Adam / AdamW or a fused torch Adam / AdamW"
-    cap = model.plan.register_capacity
-    cap = min(cap, int(model.plan.dims.max_patterns)) if cap > 0 else int(model.plan.dims.max_patterns)
-    ga = max(1, int(grad_accumulation))
+    cap = model.plan.call_capacity
     for g0 in range(0, len(batches), ga):
-        if sum(len(np.asarray(b).reshape(-1)) for b in batches[g0:g0 + ga]) > cap:
+        group = batches[g0:g0 + ga]
+        sizes = [len(np.asarray(b).reshape(-1)) for b in group]
+        if coll and ctx.splits(group):
+            load = sum(-(-n // ctx.world) for n in sizes)                     # rank 0's parts (the largest)
+        elif coll:
+            load = max(sum(sizes[r::ctx.world]) for r in range(ctx.world))   # whole batches round-robin
+        else:
+            load = sum(sizes)
+        if load > cap:
             return "a step larger than one engine call"
     return None
+
+
+def _local_steps(ctx, batches, ga):
+    """Per optimizer step of the iteration: (this rank's mini-batch pieces, the group size, whether
+    the group is split, the group rows this rank's terms fill).  One rank: the whole groups."""
+    out = []
+    for g0 in range(0, len(batches), ga):
+        group = batches[g0:g0 + ga]
+        if ctx is None or not ctx._collective():
+            out.append(([np.asarray(b).reshape(-1) for b in group], len(group), False, tuple(range(len(group)))))
+        elif ctx.splits(group):
+            out.append(([ctx.my_part(b) for b in group], len(group), True,
+                        tuple(range(len(group))) if ctx.rank == 0 else ()))
+        else:
+            mine = ctx.my_batches(group)
+            out.append(([np.asarray(group[i]).reshape(-1) for i in mine], len(group), False, tuple(mine)))
+    return out
 
 
 class StepGraphs:
@@ -68,7 +114,8 @@ class StepGraphs:
         self.graphs = {}          # key -> CUDAGraph
         self.static = {}          # key -> (idx (n,) i32, off (nb+1,) i32 device, terms (nb, 5))
         self.pool = None
-        self._table = None        # (batches fingerprint, idx_all, istart, rstart)
+        self._table = None        # persistent device buffers (idx_all, istart, rstart)
+        self._host = None         # the host tables last copied into them
         self._seen = set()        # keys whose first (eager) step has run
         self._cnt = None          # (1,) i64: the step the next replay runs
         self._terms = None        # (n_batches, 5) loss terms of the iteration
@@ -77,26 +124,48 @@ class StepGraphs:
         self.eager = 0
 
     # ---------------------------------------------------------------- per-iteration tables
-    def _tables(self, batches, ga, dev):
-        sizes = [len(np.asarray(b).reshape(-1)) for b in batches]
-        flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches]).astype(np.int32)
-        fp = (ga, tuple(sizes), hash(flat.tobytes()))
-        if self._table is None or self._table[0] != fp:
-            off = np.concatenate([[0], np.cumsum(sizes)])
-            istart = off[0:len(batches):ga].astype(np.int64)                 # first pattern of each step
-            rstart = np.arange(0, len(batches), ga, dtype=np.int64)          # first mini-batch of each step
-            self._table = (fp, torch.as_tensor(flat).to(dev), torch.as_tensor(istart).to(dev),
-                           torch.as_tensor(rstart).to(dev))
-        return self._table[1:]
+    def _tables(self, steps, ga, dev):
+        """The iteration's index table (every step's positions on this rank, back to back) and the
+        first pattern / mini-batch of each step, in PERSISTENT device buffers: a new batching (the
+        reference's hypertune loop reshuffles every iteration, reconstruction.py:1059) is copied
+        into them, so the captured graphs' pointers stay valid and no step is recaptured.  The
+        buffers grow (and the graphs are dropped) only when a table outgrows them."""
+        pieces = [p for st in steps for p in st[0]]
+        flat = (np.concatenate(pieces) if pieces else np.zeros(0)).astype(np.int32)
+        n_step = np.array([sum(len(p) for p in st[0]) for st in steps], np.int64)
+        istart = np.concatenate([[0], np.cumsum(n_step)[:-1]]).astype(np.int64)   # first pattern of each step
+        rstart = np.arange(0, len(steps) * ga, ga, dtype=np.int64)                 # first mini-batch of each step
+        host = (flat, istart, rstart)
+        bufs = self._table
+        if bufs is None or bufs[0].device != dev or any(b.numel() < h.size for b, h in zip(bufs, host)):
+            bufs = tuple(torch.zeros(max(h.size, 1), dtype=torch.int32 if h.dtype == np.int32 else torch.int64,
+                                     device=dev) for h in host)
+            self._table = bufs
+            self._host = None
+            self._drop_graphs()   # (their pointers were the old buffers')
+        if self._host is None or not all(h0.shape == h.shape and np.array_equal(h0, h)
+                                         for h0, h in zip(self._host, host)):
+            for b, h in zip(bufs, host):
+                b[:h.size].copy_(torch.from_numpy(h), non_blocking=False)
+            self._host = tuple(h.copy() for h in host)
+        return bufs
+
+    def _drop_graphs(self):
+        self.graphs.clear()
+        self.static.clear()
+        self._seen.clear()
 
     # ---------------------------------------------------------------- one step
     def _body(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, idx_all, istart, rstart,
-              terms_all):
-        """Exactly recon_step's step, on static buffers: captured or run eagerly."""
-        sidx, soff, sterms = self.static[key]
+              terms_all, ctx, extra, G, split):
+        """Exactly recon_step's step, on static buffers: captured or run eagerly.  With collectives
+        (RCCL, captured into the graph like the kernels): a split step all-reduces the engine's
+        per-mini-batch loss sums between its halves, and the gradient all-reduce carries the
+        step's loss terms in the flat buffer's tail."""
+        sidx, soff, sterms, mine_t = self.static[key]
         lib = _lib.load()
         st = ctypes.c_void_p(torch.cuda.current_stream(flat_grad.device).cuda_stream)
-        # the step's indices (device counter) + zeroed gradient buffer, one launch
+        # the step's indices (device counter) + zeroed gradient buffer (and terms tail), one launch
         _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
                                         _ptr(flat_grad), int(flat_grad.numel())))
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
@@ -104,21 +173,32 @@ class StepGraphs:
              "tilts": None if model._tilts() is None else model._tilts().detach().contiguous()}
         t.update(model._base())
         cfg = LossConfig.from_loss_params(loss_fn.loss_params)
-        model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                     max_batch=max(key[0]), _rows_checked=True)
+        terms = sterms
+        if split:
+            model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
+                                         batch_sums_reduce=ctx.allreduce_sums, _rows_checked=True)
+        else:
+            model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
+                                         max_batch=max(key[0]), _rows_checked=True)
+        if extra:
+            terms = ctx.terms_tail(flat_grad, extra, G)
+            if mine_t is not None:
+                terms.index_copy_(0, mine_t, sterms)
+            ctx.allreduce(flat_grad)
         optimizer.step()
         # the loss terms into the iteration's table, then the counter advances (one launch)
-        _lib.check(lib.ptyx_step_store(st, _ptr(sterms), int(sterms.shape[0]), _ptr(rstart), _ptr(cnt),
-                                       _ptr(terms_all)))
+        _lib.check(lib.ptyx_step_store(st, _ptr(terms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all)))
 
-    def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad):
+    def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad, ctx=None, extra=0):
         """All optimizer steps of one recon_step iteration; returns the (n_batches, 5) loss terms.
-        ``live``: the parameters whose ``.grad`` are views of ``flat_grad`` (DistContext.grad_views)."""
+        ``live``: the parameters whose ``.grad`` are views of ``flat_grad`` (DistContext.grad_views);
+        ``extra``: the floats after them that carry a step's loss terms through the all-reduce."""
         dev = model.opt_obja.device
         ga = max(1, int(ga))
-        idx_all, istart, rstart = self._tables(batches, ga, dev)
+        steps = _local_steps(ctx, batches, ga)
+        idx_all, istart, rstart = self._tables(steps, ga, dev)
         # every position must be held (checked once per iteration on the host, as fused_into does)
-        flat_np = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
+        flat_np = np.concatenate([p for st in steps for p in st[0]] or [np.zeros(0, np.int64)])
         model._check_indices(flat_np)
         loss_fn._check_held(model, flat_np)
         # persistent step counter and loss-term table (the graphs hold their addresses)
@@ -141,7 +221,15 @@ class StepGraphs:
                                                   model.opt_probe_pos_shifts, flat_grad, cnt,
                                                   idx_all, istart, rstart, terms_all)) + \
             tuple(int(v.data_ptr()) for v in base.values() if isinstance(v, torch.Tensor))
-        lrs = tuple(float(g["lr"]) for g in optimizer.param_groups)
+        # every value a capture bakes in besides pointers: the groups' hyperparameters (lr, betas,
+        # eps, weight_decay, maximize, ...), the loss configuration and the engine-variant tuning
+        def _hv(v):
+            return tuple(_hv(x) for x in v) if isinstance(v, (tuple, list)) else \
+                (float(v) if isinstance(v, (int, float, bool)) or torch.is_tensor(v) else repr(v))
+        hyper = tuple(tuple(sorted((k, _hv(v)) for k, v in g.items() if k not in ("params", "capturable")))
+                      for g in optimizer.param_groups)
+        lcfg = astuple(LossConfig.from_loss_params(loss_fn.loss_params))
+        tuning = tuple(_lib.get_tuning(k) for k in _lib.TUNING_KEYS)
         live_ids = tuple(id(p) for p in live)
         saved = [g.get("capturable", False) for g in optimizer.param_groups]
         for g in optimizer.param_groups:
@@ -151,16 +239,17 @@ class StepGraphs:
                          if isinstance(v, torch.Tensor))
 
         try:
-            for g0 in range(0, len(batches), ga):
-                sizes = tuple(len(np.asarray(b).reshape(-1)) for b in batches[g0:g0 + ga])
-                key = (sizes, live_ids, lrs, ptrs, id(optimizer), state_ptrs())
+            for pieces, G, split, mine in steps:
+                sizes = tuple(len(p) for p in pieces)
+                key = (sizes, G, split, mine, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs())
                 if key not in self.static:
                     n, nb = sum(sizes), len(sizes)
                     self.static[key] = (torch.zeros(n, dtype=torch.int32, device=dev),
                                         torch.as_tensor(batch_offsets([np.zeros(s) for s in sizes])).to(dev),
-                                        torch.zeros((nb, 5), dtype=torch.float32, device=dev))
+                                        torch.zeros((nb, 5), dtype=torch.float32, device=dev),
+                                        torch.as_tensor(mine, dtype=torch.long).to(dev) if (extra and mine) else None)
                 args = (model, optimizer, loss_fn, flat_grad, grads, key, 1.0 / ga, cnt, idx_all, istart, rstart,
-                        terms_all)
+                        terms_all, ctx, extra, G, split)
                 gr = self.graphs.get(key)
                 if gr is not None:
                     gr.replay()

@@ -89,7 +89,7 @@ class OracleLoss:
     def __init__(self, lp):
         self.loss_params = lp
 
-    def supports_batch_split(self, model):
+    def supports_batch_split(self, model=None, **_stages):
         return not self.loss_params.get("loss_pacbed", {}).get("state", False)
 
     def _split_grads(self, model, parts, reduce):

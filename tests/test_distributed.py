@@ -11,6 +11,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 from tests.dist_helpers import dist_worker, run_recon
@@ -82,6 +83,65 @@ def test_local_indices_cover_each_rank_exactly():
     ctx.rank, ctx.world = 0, 3
     assert np.array_equal(ctx.local_indices(batches, 3, split=False),
                           np.concatenate([batches[0], batches[3], batches[6]]))
+
+
+def test_measurement_block_and_recon_step_share_the_split_decision():
+    """the rank's DP block (local_indices) and recon_step decide the split of a group
+    with fewer mini-batches than ranks the same way.  A loss that cannot be split (loss_pacbed) or
+    a model stage that forces autograd (detector blur, on-the-fly measurements) gives whole
+    mini-batches; a block built for the other decision is refused before any collective."""
+    import os
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.reconstruction import DistContext, recon_step
+    from tests.dist_helpers import OracleLoss, OracleModel
+    batches = [np.arange(i * 4, i * 4 + 4) for i in range(4)]
+    lp = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+          "loss_poissn": {"state": False}, "loss_pacbed": {"state": True, "weight": 0.5, "dp_pow": 0.2},
+          "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1}, "loss_simlar": {"state": False}}
+    ctx = DistContext()
+    ctx.rank, ctx.world = 1, 2
+    whole = ctx.local_indices(batches, 1, loss_fn=CombinedLoss(lp, device="cpu"))
+    assert ctx.block_split is False
+    assert whole.size == 0                       # one mini-batch per step, unsplittable: rank 0 takes it
+    assert ctx.local_indices(batches, 2, loss_fn=CombinedLoss(lp, device="cpu")).size == 8   # ga 2: one each
+    lp_nopac = {**lp, "loss_pacbed": {"state": False}}
+    assert ctx.local_indices(batches, 1, loss_fn=CombinedLoss(lp_nopac, device="cpu")).size == 8   # parts of all 4
+    assert ctx.block_split is True
+    assert not CombinedLoss(lp_nopac, device="cpu").supports_batch_split(model_params={"detector_blur_std": 1.0})
+    assert not CombinedLoss(lp_nopac, device="cpu").supports_batch_split(
+        init_variables={"on_the_fly_meas_scale_factors": [2.0, 2.0]})
+    assert CombinedLoss(lp_nopac, device="cpu").supports_batch_split(
+        model_params={"detector_blur_std": None}, init_variables={"on_the_fly_meas_scale_factors": [1.0, 1.0]})
+    # a block built for split mini-batches, then a loss that cannot split: refused up front
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "traj_n64_b4_ga1.npz"), allow_pickle=False)
+    zb = np.split(z["batches"], np.cumsum(z["batch_sizes"])[:-1])
+    ctx = DistContext()
+    ctx.rank, ctx.world = 0, 2
+    mi = ctx.local_indices(zb, 1)
+    model = OracleModel(z, meas_index=mi)
+    opt = torch.optim.Adam(model.optimizable_params)
+    with pytest.raises(ValueError, match="split_batches=True"):
+        recon_step(zb, 1, model, opt, OracleLoss(lp), None, 1, verbose=False, dist_ctx=ctx)
+
+
+def test_split_ranges_cut_groups_alike_on_every_rank():
+    """a split group too large for one engine call is cut into mini-batch ranges from
+    the whole mini-batches' sizes (rank 0's parts are the largest), identically on every rank."""
+    from ptyrad_amd.reconstruction import DistContext
+    group = [np.arange(10), np.arange(7), np.arange(4), np.arange(9)]
+    got = []
+    for r in range(3):
+        ctx = DistContext()
+        ctx.rank, ctx.world = r, 3
+        got.append(ctx.split_ranges(group, 6))
+        for a, b in got[-1]:   # every rank's share of a range fits the call
+            assert sum(len(ctx.my_part(x)) for x in group[a:b]) <= 6
+    assert got[0] == got[1] == got[2] == [(0, 1), (1, 3), (3, 4)]
+    assert DistContext().split_ranges(group, None) == [(0, 4)]
+    ctx = DistContext()
+    ctx.rank, ctx.world = 2, 3
+    with pytest.raises(ValueError, match="exceeds"):
+        ctx.split_ranges(group, 3)
 
 
 def _simulate_ranks(z, parts_of, lp):

@@ -79,7 +79,7 @@ def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", 
 
 # the engine each BASELINE-config / demo-shaped fixture (make_golden.py --large) must run on
 ENGINE_OF = {"n256_p8o2z1_c3": "k_s1", "n256_p4o1z1_c5f16": "k_s1", "n128_p1o1z16_c4": "k_fused",
-             "n128_p6o1z6_tbl": "k_adjoint", "n256_p4o1z5_pso": "k_adjoint"}
+             "n128_p6o1z6_tbl": "k_fused", "n256_p4o1z5_pso": "k_adjoint"}
 
 
 @pytest.mark.parametrize("path", CASES, ids=[p.split("/")[-1][:-4] for p in CASES])
@@ -223,12 +223,13 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     _general_engine_case(256, P, O, Nz, shift, both)
 
 
-@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, False), (1, 2, 2, False, False),
+@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, True), (1, 2, 2, False, False),
                                                (3, 2, 1, True, False), (1, 1, 1, True, True)])
 def test_n128_general_engine_vs_oracle(P, O, Nz, shift, both):
-    """N = 128 through the general engine's LDS FFT — mixed-state multislice with the far-field
-    cache and the probe-mode split, broadcast probes, and the single-mode two-term path
-    (k_forward1 / k_adjoint1): vs the oracle as above."""
+    """N = 128 through the general engine's LDS FFT — mixed-state multislice with both data terms
+    (one object mode and one term takes the mixed-state register engine), several object modes with
+    the far-field cache and the probe-mode split, broadcast probes, and the single-mode two-term
+    path (k_forward1 / k_adjoint1): vs the oracle as above."""
     _general_engine_case(128, P, O, Nz, shift, both)
 
 
@@ -473,3 +474,83 @@ def test_calls_larger_than_max_patterns_are_split():
     for k in g0:
         assert rel(g1[k], g0[k]) < 1e-5, k
         assert rel(a1[k], a0[k]) < 1e-5, k
+
+
+def _mixed_state(P, Nz, shift, seed, ns=6, nf=7):
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(128, ns, nf, P=P, Nz=Nz, seed=seed)
+    return dict(obja=pr.obja, objp=(pr.objp / Nz).astype(np.float32), probe=pr.probe * np.float32(60.0),
+                shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=shift,
+                loss_params=orc_default_loss())
+
+
+@pytest.mark.parametrize("P,Nz,shift,q", [(2, 1, True, 0.5), (3, 2, True, 0.5), (6, 6, True, 0.5), (2, 3, False, 0.5),
+                                          (4, 1, False, 1.0), (2, 2, True, 0.7)])
+def test_mixed_state_register_engine_vs_oracle(P, Nz, shift, q):
+    """N = 128, P probe modes, Nz slices through the mixed-state register engine (k_fmm_fwd →
+    k_fmm_loss → k_fmm_adj, ptyx_fmm.hpp): ragged mini-batches vs the oracle — the tBL_WSe2 demo's
+    6 × 6 geometry, single slice, broadcast probes, and the general dp_pow form."""
+    device = dev()
+    d = _mixed_state(P, Nz, shift, seed=50 + 7 * P + Nz)
+    d["loss_params"]["loss_single"]["dp_pow"] = q
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(P + Nz).permutation(S)
+    cuts = [0, 9, 10, 30, S]
+    batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
+    assert "k_fused" in ks and "k_adjoint" in ks, ks
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"],
+                                             shift_probes=shift, grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    if shift:
+        assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_mixed_state_register_engine_poisson_and_binned_gather():
+    """loss_poissn as the data term, and a call of 300 patterns (> the small-call limit: binned
+    gather, summed-area-table window sums) with P = 2, Nz = 2: vs the oracle, bitwise repeatable."""
+    device = dev()
+    d = _mixed_state(2, 2, True, seed=77, ns=15, nf=20)
+    d["loss_params"]["loss_single"]["state"] = False
+    d["loss_params"]["loss_poissn"]["state"] = True
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(3).permutation(S)
+    batches = np.array_split(perm, 10)
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, batches, kernels=ks)
+    assert "k_fused" in ks and "k_obj_gather" in ks, ks
+    terms2, _, g2, _ = run_fused(d, device, batches)
+    assert np.array_equal(terms, terms2) and np.array_equal(g["obja"], g2["obja"]) and np.array_equal(g["probe"], g2["probe"])
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+def test_mixed_state_call_split_at_batch_boundaries(monkeypatch):
+    """A call larger than the far-field cache the mixed-state engine keeps its slots in is split
+    by engine.Plan at mini-batch boundaries (prep reuse across the pieces): vs the oracle."""
+    device = dev()
+    monkeypatch.setenv("PTYX_FFC_MB", "20")   # 20 MiB / (3 · 3 planes · 128 KiB) = 17 patterns per call
+    d = _mixed_state(3, 2, True, seed=81)
+    perm = np.random.default_rng(6).permutation(42)
+    cuts = [0, 9, 10, 25, 42]
+    batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    assert make_plan(d, device).register_capacity == 17
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
+    assert ks["k_fused"][0] >= 3, ks
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"], grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH

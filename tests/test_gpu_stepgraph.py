@@ -144,3 +144,40 @@ def test_graphs_follow_an_optimizer_state_reload():
         out.append(_params(model))
     for k in out[0]:
         assert np.array_equal(out[0][k], out[1][k]), k
+
+
+def test_graphs_follow_hyperparameters_and_reuse_reshuffled_tables():
+    """a captured step bakes in Adam's betas / eps / weight_decay and the loss
+    configuration besides the learning rate; changing any of them between iterations makes a new
+    capture (the trajectory stays bitwise the eager one), while reshuffled mini-batches of the same
+    shapes (hypertune, reconstruction.py:1059) are copied into the persistent index tables and
+    replay the existing graphs without a new capture."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    from ptyrad_amd.reconstruction import recon_step
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    out, caps = [], []
+    for graphs in (False, True):
+        model, opt, loss_fn, batches, _ = gpu_recon(z, niter=0, ret_all=True)
+        recon_step(batches, 1, model, opt, loss_fn, None, 1, verbose=False, graphs=graphs)
+        for g in opt.param_groups:
+            g["betas"] = (0.8, 0.99)
+            g["eps"] = 1e-7
+        recon_step(batches, 1, model, opt, loss_fn, None, 2, verbose=False, graphs=graphs)
+        loss_fn.loss_params["loss_sparse"]["weight"] = 0.2
+        recon_step(batches, 1, model, opt, loss_fn, None, 3, verbose=False, graphs=graphs)
+        out.append(_params(model))
+        if graphs:
+            sg = model._step_graphs
+            caps.append(sg.captures)
+            flat = np.concatenate(batches)
+            perm = np.random.default_rng(7).permutation(flat.size)
+            shuffled = np.split(flat[perm], np.cumsum([len(b) for b in batches])[:-1])
+            recon_step(shuffled, 1, model, opt, loss_fn, None, 4, verbose=False, graphs=True)
+            caps.append(sg.captures)
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k]), k
+    # iteration 1 (two steps) runs both eagerly: its first step creates the Adam state, so the
+    # second has a new key; iterations 2 and 3 each capture once for their new betas / loss weight
+    assert caps[0] >= 2, caps
+    assert caps[1] == caps[0], caps      # reshuffled batches: same graphs

@@ -117,17 +117,34 @@ def test_hip_adam_class_is_torch_adam_and_runs_torch_step_on_cpu():
 
 
 def test_stepgraph_tables_and_eligibility_on_cpu():
-    """StepGraphs' per-iteration tables (first pattern / first mini-batch of every optimizer step)
-    and recon_step's refusal of graphs=True without a HIP device."""
+    """StepGraphs' per-iteration tables (first pattern / first mini-batch of every optimizer step,
+    per rank: whole groups, parts of split groups or the rank's whole mini-batches), the
+    persistent buffers a reshuffled batching is copied into, and recon_step's refusal of
+    graphs=True without a HIP device."""
     import numpy as np
     import torch
-    from ptyrad_amd.stepgraph import StepGraphs, ineligible_reason
+    from ptyrad_amd.reconstruction import DistContext
+    from ptyrad_amd.stepgraph import StepGraphs, _local_steps, ineligible_reason
     batches = [np.array([5, 1, 9]), np.array([2, 7]), np.array([0, 3, 4]), np.array([8, 6])]
     sg = StepGraphs()
-    idx_all, istart, rstart = sg._tables(batches, 3, torch.device("cpu"))
+    steps = _local_steps(None, batches, 3)
+    assert [(s[1], s[2], s[3]) for s in steps] == [(3, False, (0, 1, 2)), (1, False, (0,))]
+    idx_all, istart, rstart = sg._tables(steps, 3, torch.device("cpu"))
     assert idx_all.tolist() == [5, 1, 9, 2, 7, 0, 3, 4, 8, 6]
     assert istart.tolist() == [0, 8] and rstart.tolist() == [0, 3]       # steps of 3 and 1 mini-batches
-    assert sg._tables(batches, 3, torch.device("cpu"))[0] is idx_all      # cached while the batches stay
+    assert sg._tables(steps, 3, torch.device("cpu"))[0] is idx_all       # cached while the batches stay
+    shuffled = [np.array([9, 5, 1]), np.array([7, 2]), np.array([4, 0, 3]), np.array([6, 8])]
+    again = sg._tables(_local_steps(None, shuffled, 3), 3, torch.device("cpu"))
+    assert again[0] is idx_all and idx_all.tolist() == [9, 5, 1, 7, 2, 4, 0, 3, 6, 8]   # same buffers, new table
+    # two ranks: ga = 1 splits each mini-batch (rank 1 takes the second part), ga = 2 deals whole ones
+    ctx = DistContext()
+    ctx.rank, ctx.world, ctx.always_reduce = 1, 2, True
+    st1 = _local_steps(ctx, batches, 1)
+    assert [p.tolist() for s in st1 for p in s[0]] == [[9], [7], [4], [6]] and all(s[2] and s[3] == () for s in st1)
+    st2 = _local_steps(ctx, batches, 2)
+    assert [p.tolist() for s in st2 for p in s[0]] == [[2, 7], [8, 6]] and [s[3] for s in st2] == [(1,), (1,)]
+    tab = StepGraphs()._tables(st2, 2, torch.device("cpu"))
+    assert tab[1].tolist() == [0, 2] and tab[2].tolist() == [0, 2]
 
     class M:
         opt_obja = torch.zeros(1)

@@ -6,7 +6,7 @@ reference's own demo parameter files, next to the BASELINE configs' engines:
                                                       modes, 21 slices
   plus single-mode / single-slice neighbours of tbl for comparison.
 
-    python tools/bench_modes.py [name ...] [--patterns 4096] [--reps 3]
+    python tools/bench_modes.py [name ...] [--patterns 4096] [--reps 3] [--tune key=value ...]
 
 Synthetic raster (2.871 px step), seeded uniform DPs, random mini-batches of 32, loss_single
 (q 0.5) + loss_sparse, all gradients on.  One JSON line per geometry with the per-kernel times.
@@ -33,7 +33,7 @@ LP = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
       "loss_simlar": {"state": False}}
 
 
-def run(name, g, n, reps, dev):
+def run(name, g, n, reps, dev, tune=()):
     from ptyrad_amd import synthetic as syn
     from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
     N, P, O, Nz = g["N"], g["P"], g["O"], g["Nz"]
@@ -69,7 +69,7 @@ def run(name, g, n, reps, dev):
     ms = e0.elapsed_time(e1) / reps
     ks = {k: round(v[1] / reps, 3) for k, v in plan.profile_end().items()}
     ok = bool(torch.isfinite(terms).all())
-    print(json.dumps({"geometry": name, **g, "patterns": n, "object": [Ny, Nx], "ms_per_call": round(ms, 3),
+    print(json.dumps({"geometry": name, **g, "tune": list(tune), "patterns": n, "object": [Ny, Nx], "ms_per_call": round(ms, 3),
                       "patterns_per_s": round(n / ms * 1e3, 1), "finite": ok, "kernels_ms": ks}), flush=True)
 
 
@@ -78,10 +78,15 @@ def main():
     ap.add_argument("names", nargs="*", default=list(GEOMS))
     ap.add_argument("--patterns", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--tune", action="append", default=[], help="key=value for ptyx_set_tuning (A/B runs)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    from ptyrad_amd import _lib
+    for kv in a.tune:
+        k, v = kv.split("=")
+        _lib.set_tuning(k, int(v))
     for name in a.names:
-        run(name, GEOMS[name], a.patterns, a.reps, dev)
+        run(name, GEOMS[name], a.patterns, a.reps, dev, tune=a.tune)
         torch.cuda.empty_cache()
 
 
