@@ -13,11 +13,13 @@
 //               ×H between slices (forward.py:50-63, image_proc.py:531-532); far field
 //               v = F(ψ_out) stored K-packed (Ψ = v/N, forward.py:79)
 //   k_fmm_loss  pattern b: I = Σ_p occ|v_p|²/N² + 1e-10, dp_out, the loss partial sums and
-//               u = ∂ℓ/∂I per unit mini-batch coefficient (K-packed; losses.py:36-75)
+//               u = ∂ℓ/∂I per unit mini-batch coefficient, one plane per data term (K-packed;
+//               losses.py:36-75)
 //   k_finalize  c_m per mini-batch
-//   k_fmm_adj   job (b, p): g = F⁻¹(v_p·2 occ u/N)/N; for n = Nz−1 … 0: slot (b, n, p) =
-//               g·conj(ψⁿ) (unit coefficient: k_obj_gather applies c_m and sums the P planes),
-//               g ← g·conj(O_n), ×conj(H) between slices; then c_m·g → probe-gradient spectrum
+//   k_fmm_adj   job (b, p): g = F⁻¹(v_p·2 occ (c1 u1 + c2 u2)/N)/N (the coefficients applied here:
+//               this kernel runs after k_finalize, so both data terms fit one field); for
+//               n = Nz−1 … 0: slot (b, n, p) = g·conj(ψⁿ) (k_obj_gather sums the P planes), g ←
+//               g·conj(O_n), ×conj(H) between slices; then g → probe-gradient spectrum
 //               (per-workgroup segment of one mode) and the position sums, as k_fused3ms
 //
 // 4·Nz FFTs per job, 4·Nz·P per pattern, no recomputed forward.  Slots and far fields live in the
@@ -37,9 +39,11 @@ struct FmArgs {
   F3Args f;             // fpk: P planes (K-packed F(P_p), or the probes R-packed without shifts)
   int P;
   long long pstride;    // float2 planes per pattern in f.slots: P·(Nz + 1)
-  float* ubuf;          // (patterns, N²) f32 K-packed: ∂ℓ/∂I per unit coefficient
+  float* ubuf;          // (patterns, N²) f32 K-packed: ∂ℓ_single/∂I (or ∂ℓ_poissn/∂I) per unit coefficient
+  float* ubuf2;         // both data terms: ∂ℓ_poissn/∂I per unit coefficient (else unused)
+  float q1, q2;         // dp_pow of loss_single / loss_poissn (f.eps2: the poissn eps)
   const float* coef;    // k_finalize's per-mini-batch coefficients
-  int ci;               // data-term coefficient index (0 single, 1 poissn)
+  int ci;               // one data term: its coefficient index (0 single, 1 poissn)
 };
 
 __device__ __forceinline__ float ld1(Rsrc r, int voff, int off) {
@@ -219,12 +223,14 @@ __global__ __launch_bounds__(256, 2) void k_fmm_fwd(FmArgs m) {
 // ------------------------------------------------------------------ loss: pattern → u, sums
 // One workgroup per pattern: the DP streams HBM → LDS (k_fused3's swizzled image) while the P
 // far fields are read K-packed and their intensities summed in mode order.
-template <int QM, bool SINGLE>
+// TERMS: 1 loss_single, 2 loss_poissn, 3 both (QM: loss_single's dp_pow form; loss_poissn
+// always takes the general form)
+template <int QM, int TERMS>
 __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
   using namespace rf;
   const F3Args& a = m.f;
   __shared__ float2 buf[kLdsElems];
-  __shared__ float s_red[4 * 2];
+  __shared__ float s_red[4 * 4];
   const Coord cd = coord(threadIdx.x);
   const int pat = blockIdx.x;
   const PatInfo pi = pat_info<false>(a, pat);
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  float S = 0.f, Ms = 0.f;
+  float S1 = 0.f, Ms1 = 0.f, S2 = 0.f, Ms2 = 0.f;
   {
     const int r = (fx + 64) & 127;   // fftshifted DP row of ky
     const int b = 1 - l0;            // fftshifted column half of kx = k + 64 l0
@@ -275,6 +281,7 @@ __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
     const Rsrc r_dp = rsrc(a.dp_out ? a.dp_out + (size_t)pat * kN2 : a.psums, a.dp_out ? kN2 * 4 : 0);
     const int vdp = 4 * (r * kN + 64 * b);
     const Rsrc r_u = rsrc(m.ubuf + (size_t)pat * kN2, kN2 * 4);
+    const Rsrc r_u2 = rsrc(TERMS == 3 ? m.ubuf2 + (size_t)pat * kN2 : m.ubuf, TERMS == 3 ? kN2 * 4 : 0);
     const int vu = 4 * tid;
 #pragma unroll
     for (int kq = 0; kq < 16; ++kq) {
@@ -285,27 +292,29 @@ __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
       for (int e = 0; e < 4; ++e) {
         const int k = 4 * kq + e;
         Iv[e] = acc[k] + kDpEps;
-        st1(loss_point<QM, SINGLE>(Iv[e], Mv[e], a.q, a.eps2, S, Ms), r_u, vu, 1024 * k);
+        if constexpr (TERMS & 1) st1(loss_point<QM, true>(Iv[e], Mv[e], m.q1, a.eps2, S1, Ms1), r_u, vu, 1024 * k);
+        if constexpr (TERMS == 2) st1(loss_point<2, false>(Iv[e], Mv[e], m.q2, a.eps2, S2, Ms2), r_u, vu, 1024 * k);
+        if constexpr (TERMS == 3) st1(loss_point<2, false>(Iv[e], Mv[e], m.q2, a.eps2, S2, Ms2), r_u2, vu, 1024 * k);
       }
       const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, i4),
                                              r_dp, vdp + 16 * kq, 0, 0);
     }
   }
-  float v2[2] = {S, Ms};
-  block_sum4<2>(v2, s_red);
+  float v4[4] = {S1, Ms1, S2, Ms2};
+  block_sum4<4>(v4, s_red);
   if (threadIdx.x == 0) {
     float* ps = a.psums + (size_t)pat * kNSum;
-    const int base = SINGLE ? 0 : 2;
-    ps[base] = v2[0];
-    ps[base + 1] = v2[1];
-    ps[2 - base] = 0.f;
-    ps[3 - base] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ps[i] = v4[i];
   }
 }
 
 // ------------------------------------------------------------------ adjoint: job → slots, slab
-template <bool SHIFT>
+// BOTH: loss_single and loss_poissn; the data coefficients c_m (k_finalize, which runs before this
+// kernel) are applied to g_Ψ itself, so the slots, the probe spectrum and the position sums all
+// carry them (k_obj_gather then takes data coefficient 1: FinArgs ci = 2)
+template <bool SHIFT, bool BOTH>
 __global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
   using namespace rf;
   const F3Args& a = m.f;
@@ -373,10 +382,14 @@ __global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
         rf::sfor<0, 8>([&](auto Q) { issue3(Q, sp, so, vpo, voo); });
       }
     };
-    // g_Ψ·N = v_p·(2 occ u/N) per unit coefficient (as k_fused3's loss epilogue)
+    // g_Ψ·N = v_p·(2 occ ∂ℓ/∂I/N), ∂ℓ/∂I = c1·u1 (+ c2·u2): the mini-batch's coefficients applied here
     {
+      const float* cf = m.coef + (size_t)pi.m * kNCoef;
+      const float c1 = occ2_n * (BOTH ? cf[0] : cf[m.ci]);
+      const float c2 = BOTH ? occ2_n * cf[1] : 0.f;
       const Rsrc r_far = rsrc(a.slots + fmm_far(m, pat, p), kN2 * 8);
       const Rsrc r_u = rsrc(m.ubuf + (size_t)pat * kN2, kN2 * 4);
+      const Rsrc r_u2 = rsrc(BOTH ? m.ubuf2 + (size_t)pat * kN2 : m.ubuf, BOTH ? kN2 * 4 : 0);
       const int vpk = 8 * tid, vu = 4 * tid;
       pipeline<16>(
           [&](auto C) {
@@ -385,13 +398,14 @@ __global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
             for (int r = 0; r < 4; ++r) {
               t.x[r] = ld2(r_far, vpk, 2048 * (4 * C + r));
               t.u[r] = ld1(r_u, vu, 1024 * (4 * C + r));
+              if constexpr (BOTH) t.u[r] = fmaf(c2, ld1(r_u2, vu, 1024 * (4 * C + r)), c1 * t.u[r]);
             }
             return t;
           },
           [&](auto C, const Ch4u& t) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              v[4 * C + r] = pscale(t.x[r], occ2_n * t.u[r]);
+              v[4 * C + r] = pscale(t.x[r], BOTH ? t.u[r] : c1 * t.u[r]);
               pin(v[4 * C + r]);
             }
           });
@@ -467,9 +481,6 @@ __global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
     const Rsrc r_slab_ld = rsrc(segs, first ? 0u : (unsigned)(kN2 * 8));
     const Rsrc r_slab_st = rsrc(segs, kN2 * 8);
     if (first && threadIdx.x == 0) a.segbid[seg] = p;
-    const float cm = m.coef[(size_t)pi.m * kNCoef + m.ci];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) v[k] = pscale(v[k], cm);
     const Rsrc r_fpk = rsrc(a.fpk + (size_t)p * kN2, kN2 * 8);
     if constexpr (SHIFT) {
       fft_fwd(v, buf, lc, cd.wsign);   // G = F(h), K layout

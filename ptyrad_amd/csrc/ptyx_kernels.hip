@@ -542,7 +542,7 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
       for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
   }
   if (f.pcoef) {   // the coefficients of lane 0, written for every pattern of the mini-batch
-    const float c = __shfl(f.ci == 0 ? cf[0] : cf[1], 0, 64);
+    const float c = __shfl(f.ci == 0 ? cf[0] : f.ci == 1 ? cf[1] : 1.f, 0, 64);   // (ci 2: already applied)
 #pragma unroll
     for (int o = 0; o < kMaxModesO; ++o) {
       if (o >= f.pcoef_O) break;
@@ -959,6 +959,7 @@ struct ptyx_plan {
   float* psums = nullptr;
   float* coef = nullptr;
   float* Ibuf = nullptr;
+  float* Ibuf2 = nullptr;     // mixed-state register engine with both data terms: ∂ℓ_poissn/∂I planes
   float* Imodes = nullptr;    // probe-mode split: P mode-intensity planes per pattern (≤ kModeSplitCap)
   float2* slab = nullptr;
   float2* Gsum = nullptr;
@@ -1299,7 +1300,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     // per-pattern memory of its own and takes the same call sizes; jobs are (pattern, probe mode)
     int occ3 = 0, o2 = 0;
     bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fmm_fwd<true>, 256, 0) == hipSuccess && occ3 > 0;
-    for (auto kf : {f3::k_fmm_fwd<false>, f3::k_fmm_adj<true>, f3::k_fmm_adj<false>})
+    for (auto kf : {f3::k_fmm_fwd<false>, f3::k_fmm_adj<true, false>, f3::k_fmm_adj<false, false>,
+                    f3::k_fmm_adj<true, true>, f3::k_fmm_adj<false, true>})
       if (ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
     if (ok && occ3 > 0) {
       pl->nwg3 = (int)std::min<long long>((long long)cu * occ3, std::max<long long>(1, (long long)d.max_patterns * d.P));
@@ -1312,7 +1314,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->preftot, (size_t)d.Nz * ((d.Ny + f3::kPrefChunk - 1) / f3::kPrefChunk) * (d.Nx + 1))) ||
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) || (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * d.P * 2)) ||
-          (rc = dalloc(pl, &pl->segpart, (size_t)d.P * f3::kSegSplit * N2)) || (rc = alloc_bins(pl))) {
+          (rc = dalloc(pl, &pl->segpart, (size_t)d.P * f3::kSegSplit * N2)) || (rc = alloc_bins(pl)) ||
+          (rc = dalloc(pl, &pl->Ibuf2, (size_t)pl->ffc_cap * N2))) {
         free_plan(pl);
         return rc;
       }
@@ -1808,12 +1811,16 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   const int nj = a.n_idx * P;
   const int G = std::max(1, std::min(pl->nwg3, nj));
   const int nseg = P + G;
+  const bool both = cfg->single_on && cfg->poissn_on;
   f3::FmArgs m{};
   m.f = register_args(pl, in, a, cfg, gz);
   m.f.slots = pl->ffc;
   m.P = P;
   m.pstride = (long long)P * (Nz + 1);
   m.ubuf = pl->Ibuf;
+  m.ubuf2 = both ? pl->Ibuf2 : nullptr;
+  m.q1 = cfg->single_q;
+  m.q2 = cfg->poissn_q;
   m.coef = pl->coef;
   m.ci = ci;
   int rc = PTYX_OK;
@@ -1827,9 +1834,12 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     {
       ProfScope ps(pl, kKForward, st);
       const dim3 gr(a.n_idx), bl(256);
-      if (single && m.f.q == 0.5f) hipLaunchKernelGGL((f3::k_fmm_loss<0, true>), gr, bl, 0, st, m);
-      else if (single) hipLaunchKernelGGL((f3::k_fmm_loss<2, true>), gr, bl, 0, st, m);
-      else hipLaunchKernelGGL((f3::k_fmm_loss<2, false>), gr, bl, 0, st, m);
+      const bool half = cfg->single_q == 0.5f;
+      if (both && half) hipLaunchKernelGGL((f3::k_fmm_loss<0, 3>), gr, bl, 0, st, m);
+      else if (both) hipLaunchKernelGGL((f3::k_fmm_loss<2, 3>), gr, bl, 0, st, m);
+      else if (single && half) hipLaunchKernelGGL((f3::k_fmm_loss<0, 1>), gr, bl, 0, st, m);
+      else if (single) hipLaunchKernelGGL((f3::k_fmm_loss<2, 1>), gr, bl, 0, st, m);
+      else hipLaunchKernelGGL((f3::k_fmm_loss<2, 2>), gr, bl, 0, st, m);
     }
     if ((rc = launch_status("k_fmm forward launch"))) return rc;
   }
@@ -1841,7 +1851,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
   if (gz.d_obja || gz.d_objp) {
     fa.pcoef = pl->pcoef;
-    fa.ci = ci;
+    fa.ci = 2;   // the slots already carry the data coefficients (k_fmm_adj): the gather's is 1
   }
   fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
   fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
@@ -1854,8 +1864,10 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   if (!any_grad) return PTYX_OK;
   {
     ProfScope ps(pl, kKAdjoint, st);
-    if (a.shift) hipLaunchKernelGGL(f3::k_fmm_adj<true>, dim3(G), dim3(256), 0, st, m);
-    else hipLaunchKernelGGL(f3::k_fmm_adj<false>, dim3(G), dim3(256), 0, st, m);
+    if (a.shift && both) hipLaunchKernelGGL((f3::k_fmm_adj<true, true>), dim3(G), dim3(256), 0, st, m);
+    else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_adj<true, false>), dim3(G), dim3(256), 0, st, m);
+    else if (both) hipLaunchKernelGGL((f3::k_fmm_adj<false, true>), dim3(G), dim3(256), 0, st, m);
+    else hipLaunchKernelGGL((f3::k_fmm_adj<false, false>), dim3(G), dim3(256), 0, st, m);
   }
   if ((rc = launch_status("k_fmm_adj launch"))) return rc;
   const bool bins = a.n_idx > f3::kSmallCall;
@@ -2298,7 +2310,7 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && one_term;
   // mixed-state register engine (N = 128, P > 1, O = 1): one data term, f32 DPs, the call within
   // the far-field cache its slots live in
-  const bool fmm = any_grad && !want_H && pl->fmm && !a.meas_f16 && one_term && n_idx <= pl->ffc_cap;
+  const bool fmm = any_grad && !want_H && pl->fmm && !a.meas_f16 && n_idx <= pl->ffc_cap;   // (either or both terms)
 #ifdef PTYX_ONLY_N
   *engine = (fused3 || fused3ms) && PTYX_ONLY_N == 128 ? kEngFused3 : fmm && PTYX_ONLY_N == 128 ? kEngFmm
           : stripe && PTYX_ONLY_N == 256 ? kEngStripe : kEngTwoPass;

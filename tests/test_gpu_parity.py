@@ -223,13 +223,13 @@ def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     _general_engine_case(256, P, O, Nz, shift, both)
 
 
-@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, True), (1, 2, 2, False, False),
+@pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 2, 3, True, True), (1, 2, 2, False, False),
                                                (3, 2, 1, True, False), (1, 1, 1, True, True)])
 def test_n128_general_engine_vs_oracle(P, O, Nz, shift, both):
     """N = 128 through the general engine's LDS FFT — mixed-state multislice with both data terms
-    (one object mode and one term takes the mixed-state register engine), several object modes with
-    the far-field cache and the probe-mode split, broadcast probes, and the single-mode two-term
-    path (k_forward1 / k_adjoint1): vs the oracle as above."""
+    and two object modes (one object mode takes the mixed-state register engine), several object
+    modes with the far-field cache and the probe-mode split, broadcast probes, and the single-mode
+    two-term path (k_forward1 / k_adjoint1): vs the oracle as above."""
     _general_engine_case(128, P, O, Nz, shift, both)
 
 
@@ -485,14 +485,19 @@ def _mixed_state(P, Nz, shift, seed, ns=6, nf=7):
 
 
 @pytest.mark.parametrize("P,Nz,shift,q", [(2, 1, True, 0.5), (3, 2, True, 0.5), (6, 6, True, 0.5), (2, 3, False, 0.5),
-                                          (4, 1, False, 1.0), (2, 2, True, 0.7)])
+                                          (4, 1, False, 1.0), (2, 2, True, 0.7), (3, 2, True, "both"),
+                                          (2, 1, False, "both")])
 def test_mixed_state_register_engine_vs_oracle(P, Nz, shift, q):
     """N = 128, P probe modes, Nz slices through the mixed-state register engine (k_fmm_fwd →
     k_fmm_loss → k_fmm_adj, ptyx_fmm.hpp): ragged mini-batches vs the oracle — the tBL_WSe2 demo's
-    6 × 6 geometry, single slice, broadcast probes, and the general dp_pow form."""
+    6 × 6 geometry, single slice, broadcast probes, the general dp_pow form, and loss_single +
+    loss_poissn together (both coefficients applied in k_fmm_adj)."""
     device = dev()
     d = _mixed_state(P, Nz, shift, seed=50 + 7 * P + Nz)
-    d["loss_params"]["loss_single"]["dp_pow"] = q
+    if q == "both":
+        d["loss_params"]["loss_poissn"]["state"] = True
+    else:
+        d["loss_params"]["loss_single"]["dp_pow"] = q
     S = d["shifts"].shape[0]
     perm = np.random.default_rng(P + Nz).permutation(S)
     cuts = [0, 9, 10, 30, S]

@@ -1,6 +1,6 @@
 """Time the caller contract (recon_step, reconstruction.py:658-781) end to end on one GPU.
 
-    python tools/bench_recon.py [--scan 256] [--ga 1 16 2048] [--iters 1]
+    python tools/bench_recon.py [--scan 256] [--ga 1 16 2048] [--iters 1] [--rccl split|whole]
 
 PtychoHIP + CombinedLoss.fused_into + torch Adam at the c2 geometry (N = 128, P = O = Nz = 1, the
 scan² raster, mini-batches of 32, make_batches 'random', seeded uniform DPs): one iteration =
@@ -33,7 +33,20 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="ptyx_set_tuning key=value (A/B runs)")
     ap.add_argument("--graphs", choices=["auto", "on", "off"], default="auto",
                     help="recon_step(graphs=...): hipGraph-replayed optimizer steps")
+    ap.add_argument("--rccl", choices=["off", "split", "whole"], default="off",
+                    help="init_process_group('nccl') at world size 1 with every collective of the data-parallel "
+                         "step executed (DistContext(always_reduce=True)): mini-batches split over the ranks "
+                         "(the default cadence on several GPUs) or dealt whole")
     a = ap.parse_args()
+    ctx = None
+    if a.rccl != "off":
+        import torch.distributed as dist
+        from ptyrad_amd.reconstruction import DistContext
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        ctx = DistContext(split_batches=a.rccl == "split", always_reduce=True)
     from ptyrad_amd import _lib
     from ptyrad_amd import synthetic as syn
     for kv in a.tune:
@@ -75,16 +88,17 @@ def main():
         loss_fn = CombinedLoss(lp, device=dev)
         batches = make_batches(np.arange(n), scan.crop_pos, 32, mode="random", rng=np.random.default_rng(3))
         graphs = {"auto": None, "on": True, "off": False}[a.graphs]
-        recon_step(batches, ga, model, opt, loss_fn, None, 1, verbose=False, graphs=graphs)   # warm-up iteration
+        recon_step(batches, ga, model, opt, loss_fn, None, 1, verbose=False, graphs=graphs,
+                   dist_ctx=ctx)   # warm-up iteration
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for it in range(a.iters):
-            recon_step(batches, ga, model, opt, loss_fn, None, 2 + it, verbose=False, graphs=graphs)
+            recon_step(batches, ga, model, opt, loss_fn, None, 2 + it, verbose=False, graphs=graphs, dist_ctx=ctx)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
         sg = getattr(model, "_step_graphs", None)
-        print(json.dumps({"ga": ga, "P": P, "Nz": Nz, "graphs": a.graphs, "tune": a.tune, "replays": sg.replays if sg else 0,
+        print(json.dumps({"ga": ga, "P": P, "Nz": Nz, "graphs": a.graphs, "rccl": a.rccl, "tune": a.tune, "replays": sg.replays if sg else 0,
                           "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
@@ -95,3 +109,5 @@ def main():
 
 if __name__ == "__main__":
     main()
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
