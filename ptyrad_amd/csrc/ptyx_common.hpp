@@ -24,6 +24,11 @@ template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr b
 template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
 template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
 template <> struct Geo<256> { static constexpr int NT = kG256Threads; static constexpr bool kLds = false; static constexpr int kWaves = 4; };
+// mixed-radix N (general engine only): 96² fits LDS (78 KiB, two workgroups a CU); 160² and 192²
+// do not, so they transform in the per-workgroup global scratch pair (four Stockham passes a 2-D FFT)
+template <> struct Geo<96>  { static constexpr int NT = 768;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
+template <> struct Geo<160> { static constexpr int NT = 1024; static constexpr bool kLds = false; static constexpr int kWaves = 1; };
+template <> struct Geo<192> { static constexpr int NT = 1024; static constexpr bool kLds = false; static constexpr int kWaves = 1; };
 
 struct KArgs {
   int P, O, Nz, Ny, Nx, n_scans;

@@ -70,10 +70,64 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// In-register DFT of size R ∈ {2,4,8,16}, natural order in and out, radix-2 DIT recursion.
+// compile-time sin / cos of 2πk/M (argument reduced to (-π, π], Taylor series, error < 1e-15)
+constexpr double ct_sin2pi(int k, int M) {
+  k = ((k % M) + M) % M;
+  if (2 * k > M) k -= M;
+  const double x = 2.0 * 3.14159265358979323846264338327950288 * (double)k / (double)M;
+  double t = x, s = x;
+  for (int i = 1; i < 30; ++i) {
+    t *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+    s += t;
+  }
+  return s;
+}
+constexpr double ct_cos2pi(int k, int M) {
+  k = ((k % M) + M) % M;
+  if (2 * k > M) k -= M;
+  const double x = 2.0 * 3.14159265358979323846264338327950288 * (double)k / (double)M;
+  double t = 1.0, s = 1.0;
+  for (int i = 1; i < 30; ++i) {
+    t *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+    s += t;
+  }
+  return s;
+}
+
+// Direct DFT of a size R that is not a power of two (mixed-radix N: radix 3, 5, 6, 10, 12 …):
+// X[k] = Σ_n v[n] exp(DIR·2πi nk/R), compile-time twiddles, R² complex multiply-adds.
+template <int R, int DIR>
+__device__ __forceinline__ void dft_direct(float2 (&v)[R]) {
+  float2 out[R];
+  static_for<0, R>([&](auto KK) {
+    constexpr int k = decltype(KK)::value;
+    float2 acc = v[0];
+    static_for<1, R>([&](auto NN) {
+      constexpr int n = decltype(NN)::value;
+      constexpr int e = (n * k) % R;
+      constexpr float c = (float)ct_cos2pi(e, R), s = (float)((double)DIR * ct_sin2pi(e, R));
+      acc.x = fmaf(v[n].x, c, fmaf(-v[n].y, s, acc.x));
+      acc.y = fmaf(v[n].x, s, fmaf(v[n].y, c, acc.y));
+    });
+    out[k] = acc;
+  });
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+// In-register DFT of size R, natural order in and out: radix-2 DIT recursion for R ∈ {2,4,8,16},
+// the direct form for the other radices of mixed-radix N.
 template <int R, int DIR>
 struct DFT {
   __device__ __forceinline__ static void run(float2 (&v)[R]) {
+    if constexpr ((R & (R - 1)) != 0) {
+      dft_direct<R, DIR>(v);
+      return;
+    } else {
+      run_pow2(v);
+    }
+  }
+  __device__ __forceinline__ static void run_pow2(float2 (&v)[R]) {
     float2 e[R / 2], o[R / 2];
 #pragma unroll
     for (int i = 0; i < R / 2; ++i) {
@@ -118,6 +172,10 @@ template <> struct Plan1D<32>  { static constexpr int R1 = 8,  R2 = 4; };
 template <> struct Plan1D<64>  { static constexpr int R1 = 8,  R2 = 8; };
 template <> struct Plan1D<128> { static constexpr int R1 = 16, R2 = 8; };
 template <> struct Plan1D<256> { static constexpr int R1 = 16, R2 = 16; };
+// mixed-radix sizes (general engine only): 96 in LDS, 160 / 192 in the global scratch pair
+template <> struct Plan1D<96>  { static constexpr int R1 = 16, R2 = 6; };
+template <> struct Plan1D<160> { static constexpr int R1 = 16, R2 = 10; };
+template <> struct Plan1D<192> { static constexpr int R1 = 16, R2 = 12; };
 
 // ---------------------------------------------------------------- array views
 // LDS view, in place.  Row stride N + N/16 and one pad point per 16 spreads the

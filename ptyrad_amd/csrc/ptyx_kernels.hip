@@ -1077,14 +1077,18 @@ struct ProfScope {
   }
 };
 
-static bool is_supported_n(int n) { return n == 32 || n == 64 || n == 128 || n == 256; }
+// powers of two (every engine) and the mixed-radix sizes of the general engine (Plan1D)
+static bool is_supported_n(int n) { return n == 32 || n == 64 || n == 96 || n == 128 || n == 160 || n == 192 || n == 256; }
 
 static int blocks_per_cu(int N) {
   // LDS-limited residency (160 KiB per CU) of the workgroup-resident FFT kernels
   switch (N) {
     case 32: return 8;
     case 64: return 4;
+    case 96: return 2;
     case 128: return 1;
+    case 160:
+    case 192: return 2;
     default: return 160 * 1024 / (int)(sizeof(float2) * (kG256Elems + 5 * 256) + 256);   // N = 256: 2
   }
 }
@@ -1098,7 +1102,10 @@ static int blocks_per_cu(int N) {
   switch (N_) {                                          \
     case 32: FN<32>(__VA_ARGS__); break;                 \
     case 64: FN<64>(__VA_ARGS__); break;                 \
+    case 96: FN<96>(__VA_ARGS__); break;                 \
     case 128: FN<128>(__VA_ARGS__); break;               \
+    case 160: FN<160>(__VA_ARGS__); break;               \
+    case 192: FN<192>(__VA_ARGS__); break;               \
     case 256: FN<256>(__VA_ARGS__); break;               \
   }
 #endif
@@ -1188,7 +1195,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     return fail(PTYX_EINVAL, "ptyx_dims.abi_version " + std::to_string(d.abi_version) + " != " +
                                  std::to_string(PTYX_ABI_VERSION) +
                                  ": the binding's structs follow another revision of include/ptyx.h");
-  if (!is_supported_n(d.N)) return fail(PTYX_EUNSUPPORTED, "N must be one of 32, 64, 128, 256");
+  if (!is_supported_n(d.N)) return fail(PTYX_EUNSUPPORTED, "N must be one of 32, 64, 96, 128, 160, 192, 256");
   if (d.P < 1 || d.O < 1 || d.Nz < 1 || d.n_scans < 1 || d.max_patterns < 1)
     return fail(PTYX_EINVAL, "P, O, Nz, n_scans, max_patterns must be >= 1");
   if (d.O > kMaxModesO) return fail(PTYX_EUNSUPPORTED, "at most 8 object modes");

@@ -343,6 +343,15 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--constrained-only":
         constrained_trajectory()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--mixed-radix":
+        # N with factors 3 and 5 (meas_crop / meas_resample / meas_pad output, init_params.py:53, 340,
+        # 361): the general engine's mixed-radix Stockham passes, in LDS (96) and in global scratch
+        run_case("n96_p2o1z2_mixed", 96, 2, 1, 2, 3, 3, 6, seed=101)
+        run_case("n96_p1o1z1_single", 96, 1, 1, 1, 3, 3, 5, seed=102)
+        run_case("n160_p1o1z1_mixed", 160, 1, 1, 1, 3, 3, 4, seed=103, big=True)
+        run_case("n192_p2o2z1_mixed", 192, 2, 2, 1, 3, 3, 4, seed=104, big=True)
+        run_trajectory("traj_n96_p2_ga1", 96, 2, 1, 1, 3, 3, 3, 3, 1, seed=105)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--large":
         # the (N, P, O, Nz) of BASELINE configs[2..4] and of both demos, so the engines that only
         # run at these sizes (N = 256 stripe / general stages, mixed-state multislice, Nz = 16)

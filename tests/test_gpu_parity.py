@@ -233,6 +233,27 @@ def test_n128_general_engine_vs_oracle(P, O, Nz, shift, both):
     _general_engine_case(128, P, O, Nz, shift, both)
 
 
+@pytest.mark.parametrize("N,P,O,Nz,shift,both", [(96, 2, 1, 2, True, False), (96, 1, 1, 1, True, True),
+                                                 (160, 1, 2, 1, True, False), (192, 2, 1, 2, False, False)])
+def test_mixed_radix_general_engine_vs_oracle(N, P, O, Nz, shift, both):
+    """N with factors 3 / 5 (the reference takes whatever meas_crop /
+    meas_resample / meas_pad produce, init_params.py:53, 340, 361): the general engine's mixed-radix
+    Stockham passes (16 × 6 in LDS at N = 96, 16 × 10 and 16 × 12 in global scratch at 160 / 192)
+    vs the oracle, as above."""
+    _general_engine_case(N, P, O, Nz, shift, both)
+
+
+def test_unsupported_n_is_refused():
+    """N with a prime factor other than 2, 3, 5 in the supported set (e.g. 100 = 4·25 is not one of
+    the planned sizes) is refused with PTYX_EUNSUPPORTED at plan creation, not run."""
+    dev()
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import Plan
+    with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
+        Plan(100, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0))
+    Plan(96, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0)).close()
+
+
 def _general_engine_case(N, P, O, Nz, shift, both):
     device = dev()
     from ptyrad_amd import synthetic as syn
