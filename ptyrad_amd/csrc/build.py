@@ -28,8 +28,29 @@ OUT = os.path.join(PKG, "lib", "libptyx.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_constraints.hip"),
            os.path.join(HERE, "ptyx_ingest.hip"), os.path.join(HERE, "ptyx_optim.hip")]
+GEN_SOURCE = os.path.join(HERE, "ptyx_gen.hip")
+
+
+def smooth_sizes(lo: int = 32, hi: int = 256):
+    """Every 2·3·5-smooth N in [lo, hi]: the general engine's supported sizes."""
+    out = []
+    for n in range(lo, hi + 1):
+        m = n
+        for f in (2, 3, 5):
+            while m % f == 0:
+                m //= f
+        if m == 1:
+            out.append(n)
+    return out
+
+
+GEN_SIZES = smooth_sizes()
+# size groups of the general engine, one ptyx_gen.hip object each (compiled in parallel): dealt
+# round-robin over the sizes in descending order so every group gets a similar mix
+N_GEN_GROUPS = 10
+GEN_GROUPS = [sorted(GEN_SIZES[::-1][g::N_GEN_GROUPS]) for g in range(N_GEN_GROUPS)]
 HEADERS = glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
-DEPS = SOURCES + HEADERS
+DEPS = SOURCES + [GEN_SOURCE] + HEADERS
 ARCH = os.environ.get("PTYX_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC"]
 
@@ -70,6 +91,12 @@ def _headers_of(src: str):
     if os.path.basename(src) == "ptyx_constraints.hip":
         return [os.path.join(HERE, "ptyx_constraints.hpp"), os.path.join(HERE, "ptyx_abi.hpp"),
                 os.path.join(ROOT, "include", "ptyx.h")]
+    gen = [os.path.join(HERE, h) for h in ("ptyx_general.hpp", "ptyx_single.hpp")]
+    if os.path.basename(src) == "ptyx_gen.hip":
+        return gen + [os.path.join(HERE, h) for h in ("ptyx_common.hpp", "ptyx_fft.hpp", "ptyx_genops.hpp")] + \
+            [os.path.join(ROOT, "include", "ptyx.h")]
+    if os.path.basename(src) == "ptyx_kernels.hip":
+        return [h for h in HEADERS if h not in gen]
     if os.path.basename(src) == "ptyx_ingest.hip":
         return [os.path.join(HERE, "ptyx_abi.hpp"), os.path.join(ROOT, "include", "ptyx.h")]
     return HEADERS
@@ -92,19 +119,29 @@ def build(force: bool = False, only_n: int | None = None, out: str = OUT, extra=
     os.makedirs(odir, exist_ok=True)
     cc = hipcc()
 
-    def compile_one(src):
-        obj = os.path.join(odir, os.path.basename(src) + ".o")
+    groups = [[only_n]] if only_n else GEN_GROUPS
+    units = [(src, os.path.basename(src), []) for src in SOURCES]
+    units += [(GEN_SOURCE, f"ptyx_gen_{'_'.join(map(str, g))}.hip",
+               [f"-DPTYX_GEN_SIZES={','.join(map(str, g))}"]) for g in groups]
+
+    def compile_one(unit):
+        src, name, udefs = unit
+        obj = os.path.join(odir, name + ".o")
         if force or _stale(obj, src):
-            cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, *defs, "-I", os.path.join(ROOT, "include"), "-c", src,
-                   "-o", obj + ".tmp"]
+            cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, *defs, *udefs, "-I", os.path.join(ROOT, "include"), "-c",
+                   src, "-o", obj + ".tmp"]
             if verbose:
                 print("[ptyx build]", " ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
             os.replace(obj + ".tmp", obj)
         return obj
 
-    with ThreadPoolExecutor(len(SOURCES)) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
+    jobs = int(os.environ.get("PTYX_BUILD_JOBS", "0")) or min(len(units), os.cpu_count() or 4, 16)
+    # the two slowest units first, so they do not start last
+    order = sorted(range(len(units)), key=lambda i: 0 if units[i][1] == "ptyx_kernels.hip" else 1)
+    with ThreadPoolExecutor(jobs) as ex:
+        done = dict(zip(order, ex.map(compile_one, [units[i] for i in order])))
+    objs = [done[i] for i in range(len(units))]
     # build id: the content hash of the sources this library is made of
     bid = source_hash(defs)
     bsrc = os.path.join(odir, "ptyx_build_id.cpp")

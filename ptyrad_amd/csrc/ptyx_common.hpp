@@ -17,18 +17,22 @@ constexpr int kNBatchSum = 5 + kMaxModesO;     // per mini-batch: [count, S1, Σ
 static_assert(kNBatchSum == PTYX_BATCH_SUMS, "include/ptyx.h PTYX_BATCH_SUMS");
 constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
 
-template <int N> struct Geo;
-// kWaves: minimum waves per SIMD the general-engine kernels are compiled for (≤ 512 / kWaves
-// VGPRs); N = 256 runs two 512-thread workgroups per CU (LDS ≈ 78 KiB each)
-template <> struct Geo<32>  { static constexpr int NT = 256;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
-template <> struct Geo<64>  { static constexpr int NT = 512;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
-template <> struct Geo<128> { static constexpr int NT = 1024; static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
-template <> struct Geo<256> { static constexpr int NT = kG256Threads; static constexpr bool kLds = false; static constexpr int kWaves = 4; };
-// mixed-radix N (general engine only): 96² fits LDS (78 KiB, two workgroups a CU); 160² and 192²
-// do not, so they transform in the per-workgroup global scratch pair (four Stockham passes a 2-D FFT)
-template <> struct Geo<96>  { static constexpr int NT = 768;  static constexpr bool kLds = true;  static constexpr int kWaves = 1; };
-template <> struct Geo<160> { static constexpr int NT = 1024; static constexpr bool kLds = false; static constexpr int kWaves = 1; };
-template <> struct Geo<192> { static constexpr int NT = 1024; static constexpr bool kLds = false; static constexpr int kWaves = 1; };
+// Launch geometry of the general engine's workgroup-resident FFT kernels.
+//  N ≤ 128: the N×N wave in LDS (in place, ≤ 136 KiB), NT = 8·N threads (≤ 1024).
+//  N > 128: the per-workgroup global scratch pair (four Stockham passes a 2-D FFT), 1024 threads.
+//  512 threads whenever a radix above 16 holds up to 27 points a thread (125, 162, 200, 216,
+//  243, 250: 256 VGPRs, no spills); N = 256 has its own two-stage
+//  path with two 512-thread workgroups a CU (LDS ≈ 78 KiB each).
+// kWaves: minimum waves per SIMD the kernels are compiled for (≤ 512 / kWaves VGPRs).
+template <int N>
+struct Geo {
+  static constexpr bool kLds = N <= 128;
+  static constexpr int NT = N == 256 ? kG256Threads
+                          : Plan1D<N>::R1 > 16 ? 512
+                          : kLds ? ((8 * N + 63) / 64 * 64 > 1024 ? 1024 : (8 * N + 63) / 64 * 64)
+                          : 1024;
+  static constexpr int kWaves = N == 256 ? 4 : 1;
+};
 
 struct KArgs {
   int P, O, Nz, Ny, Nx, n_scans;

@@ -94,8 +94,32 @@ constexpr double ct_cos2pi(int k, int M) {
   return s;
 }
 
-// Direct DFT of a size R that is not a power of two (mixed-radix N: radix 3, 5, 6, 10, 12 …):
-// X[k] = Σ_n v[n] exp(DIR·2πi nk/R), compile-time twiddles, R² complex multiply-adds.
+// v · exp(DIR·2πi·E/R) with compile-time constants; the quarter-turn rotations without multiplies.
+template <int R, int E, int DIR>
+__device__ __forceinline__ float2 ctwmul(float2 v) {
+  constexpr int e = E % R;
+  if constexpr (e == 0) {
+    return v;
+  } else if constexpr (4 * e == R) {   // DIR·i
+    return DIR < 0 ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+  } else if constexpr (2 * e == R) {
+    return make_float2(-v.x, -v.y);
+  } else if constexpr (4 * e == 3 * R) {
+    return DIR < 0 ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+  } else {
+    constexpr float c = (float)ct_cos2pi(e, R), s = (float)((double)DIR * ct_sin2pi(e, R));
+    return make_float2(fmaf(v.x, c, -v.y * s), fmaf(v.x, s, v.y * c));
+  }
+}
+
+constexpr int ct_smallest_factor(int R) {
+  for (int f = 2; f * f <= R; ++f)
+    if (R % f == 0) return f;
+  return R;
+}
+
+// Direct DFT of a prime size (radix 3, 5 of mixed-radix N): X[k] = Σ_n v[n] exp(DIR·2πi nk/R),
+// compile-time twiddles, (R-1)² complex multiply-adds.
 template <int R, int DIR>
 __device__ __forceinline__ void dft_direct(float2 (&v)[R]) {
   float2 out[R];
@@ -104,10 +128,7 @@ __device__ __forceinline__ void dft_direct(float2 (&v)[R]) {
     float2 acc = v[0];
     static_for<1, R>([&](auto NN) {
       constexpr int n = decltype(NN)::value;
-      constexpr int e = (n * k) % R;
-      constexpr float c = (float)ct_cos2pi(e, R), s = (float)((double)DIR * ct_sin2pi(e, R));
-      acc.x = fmaf(v[n].x, c, fmaf(-v[n].y, s, acc.x));
-      acc.y = fmaf(v[n].x, s, fmaf(v[n].y, c, acc.y));
+      acc = cadd(acc, ctwmul<R, n * k, DIR>(v[n]));
     });
     out[k] = acc;
   });
@@ -115,16 +136,41 @@ __device__ __forceinline__ void dft_direct(float2 (&v)[R]) {
   for (int k = 0; k < R; ++k) v[k] = out[k];
 }
 
-// In-register DFT of size R, natural order in and out: radix-2 DIT recursion for R ∈ {2,4,8,16},
-// the direct form for the other radices of mixed-radix N.
+// In-register DFT of size R, natural order in and out.  Powers of two: radix-2 DIT recursion;
+// composite R = F·M (F its smallest prime factor): decimation in time, F sub-DFTs of size M over
+// n ≡ n1 (mod F), twiddles W_R^{n1·k1}, then M DFTs of size F (X[k1 + M·k2]); prime R: direct.
 template <int R, int DIR>
 struct DFT {
   __device__ __forceinline__ static void run(float2 (&v)[R]) {
-    if constexpr ((R & (R - 1)) != 0) {
-      dft_direct<R, DIR>(v);
-      return;
-    } else {
+    constexpr int F = ct_smallest_factor(R);
+    if constexpr ((R & (R - 1)) == 0) {
       run_pow2(v);
+    } else if constexpr (F == R) {
+      dft_direct<R, DIR>(v);
+    } else {
+      constexpr int M = R / F;
+      float2 sub[F][M];
+#pragma unroll
+      for (int n1 = 0; n1 < F; ++n1)
+#pragma unroll
+        for (int n2 = 0; n2 < M; ++n2) sub[n1][n2] = v[n1 + F * n2];
+      static_for<0, F>([&](auto N1) {
+        constexpr int n1 = decltype(N1)::value;
+        DFT<M, DIR>::run(sub[n1]);
+        static_for<1, M>([&](auto K1) {
+          constexpr int k1 = decltype(K1)::value;
+          sub[n1][k1] = ctwmul<R, n1 * k1, DIR>(sub[n1][k1]);
+        });
+      });
+#pragma unroll
+      for (int k1 = 0; k1 < M; ++k1) {
+        float2 t[F];
+#pragma unroll
+        for (int n1 = 0; n1 < F; ++n1) t[n1] = sub[n1][k1];
+        DFT<F, DIR>::run(t);
+#pragma unroll
+        for (int k2 = 0; k2 < F; ++k2) v[k1 + M * k2] = t[k2];
+      }
     }
   }
   __device__ __forceinline__ static void run_pow2(float2 (&v)[R]) {
@@ -165,17 +211,35 @@ struct DFT<4, DIR> {
 };
 
 // ---------------------------------------------------------------- radix plans
-// Per-dimension Stockham radices: N = R1·R2 (R2 = 1 ⇒ one pass per dimension).
-template <int N> struct Plan1D;
-template <> struct Plan1D<16>  { static constexpr int R1 = 16, R2 = 1; };
-template <> struct Plan1D<32>  { static constexpr int R1 = 8,  R2 = 4; };
-template <> struct Plan1D<64>  { static constexpr int R1 = 8,  R2 = 8; };
-template <> struct Plan1D<128> { static constexpr int R1 = 16, R2 = 8; };
-template <> struct Plan1D<256> { static constexpr int R1 = 16, R2 = 16; };
-// mixed-radix sizes (general engine only): 96 in LDS, 160 / 192 in the global scratch pair
-template <> struct Plan1D<96>  { static constexpr int R1 = 16, R2 = 6; };
-template <> struct Plan1D<160> { static constexpr int R1 = 16, R2 = 10; };
-template <> struct Plan1D<192> { static constexpr int R1 = 16, R2 = 12; };
+// Per-dimension Stockham radices: N = R1·R2 (R2 = 1 ⇒ one pass per dimension).  Powers of two
+// keep their measured plans; every other 2·3·5-smooth N takes the largest R1 ≤ 16 with
+// N / R1 ≤ 16, else the smallest R1 ≤ 27 with N / R1 ≤ 16 (125, 162, 200, 216, 243, 250).
+constexpr bool is_smooth235(int n) {
+  if (n < 1) return false;
+  for (int f : {2, 3, 5})
+    while (n % f == 0) n /= f;
+  return n == 1;
+}
+constexpr int plan_r1(int N) {
+  switch (N) {
+    case 16: return 16;
+    case 32: return 8;
+    case 64: return 8;
+    case 128: return 16;
+    case 256: return 16;
+    default: break;
+  }
+  for (int r = 16; r >= 2; --r)
+    if (N % r == 0 && N / r <= 16) return r;
+  for (int r = 17; r <= 27; ++r)
+    if (N % r == 0 && N / r <= 16) return r;
+  return 0;
+}
+template <int N>
+struct Plan1D {
+  static_assert(is_smooth235(N) && plan_r1(N) > 0, "N must be 2·3·5-smooth with a two-pass plan");
+  static constexpr int R1 = plan_r1(N), R2 = N / plan_r1(N);
+};
 
 // ---------------------------------------------------------------- array views
 // LDS view, in place.  Row stride N + N/16 and one pad point per 16 spreads the

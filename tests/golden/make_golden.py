@@ -352,6 +352,16 @@ if __name__ == "__main__":
         run_case("n192_p2o2z1_mixed", 192, 2, 2, 1, 3, 3, 4, seed=104, big=True)
         run_trajectory("traj_n96_p2_ga1", 96, 2, 1, 1, 3, 3, 3, 3, 1, seed=105)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--smooth":
+        # every 2·3·5-smooth N in [32, 256] runs the general engine: odd N (45, 125), a radix-15
+        # LDS plan (120), and the radix > 16 plans on 512-thread workgroups (125 = 25·5 in LDS,
+        # 216 = 18·12 and 250 = 25·10 in global scratch)
+        run_case("n45_p1o1z2_odd", 45, 1, 1, 2, 3, 3, 5, seed=111)
+        run_case("n120_p2o1z1_r15", 120, 2, 1, 1, 3, 3, 5, seed=112)
+        run_case("n125_p1o1z1_odd", 125, 1, 1, 1, 3, 3, 4, seed=113, big=True)
+        run_case("n216_p2o1z2_r18", 216, 2, 1, 2, 3, 3, 4, seed=114, big=True)
+        run_case("n250_p1o2z1_r25", 250, 1, 2, 1, 3, 3, 4, seed=115, big=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--large":
         # the (N, P, O, Nz) of BASELINE configs[2..4] and of both demos, so the engines that only
         # run at these sizes (N = 256 stripe / general stages, mixed-state multislice, Nz = 16)

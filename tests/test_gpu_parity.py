@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from oracle import ptyx_oracle as orc
+from ptyrad_amd.csrc.build import GEN_SIZES
 from tests.test_oracle_golden import CASES as ALL_CASES, load_case, rel
 
 # raw C-ABI cases: the optional-stage (blur) and optimised-propagator fixtures run through
@@ -243,15 +244,32 @@ def test_mixed_radix_general_engine_vs_oracle(N, P, O, Nz, shift, both):
     _general_engine_case(N, P, O, Nz, shift, both)
 
 
+# every 2·3·5-smooth N in [32, 256] (the sizes ptyx_gen.hip registers), cycling through mode /
+# slice / shift / loss-term configurations; 128 and 256 run the register / stripe engines for some
+# of these and have their own cases
+_SMOOTH_CFGS = [(1, 1, 1, True, False), (2, 1, 2, True, False), (1, 2, 1, True, True), (2, 1, 1, False, False),
+                (1, 1, 3, True, False)]
+_SMOOTH_N = [n for n in GEN_SIZES if n not in (128, 256)]
+
+
+@pytest.mark.parametrize("N", _SMOOTH_N)
+def test_every_smooth_n_vs_oracle(N):
+    """Radix plans 2-27 (ptyx_fft.hpp plan_r1): odd N, radix 9 / 15 / 25 / 27 in-register DFTs, the
+    LDS (N ≤ 128) and global-scratch layouts, 512-thread workgroups for radices above 16."""
+    P, O, Nz, shift, both = _SMOOTH_CFGS[_SMOOTH_N.index(N) % len(_SMOOTH_CFGS)]
+    _general_engine_case(N, P, O, Nz, shift, both)
+
+
 def test_unsupported_n_is_refused():
-    """N with a prime factor other than 2, 3, 5 in the supported set (e.g. 100 = 4·25 is not one of
-    the planned sizes) is refused with PTYX_EUNSUPPORTED at plan creation, not run."""
+    """N with a prime factor other than 2, 3, 5 (98 = 2·7², 112 = 16·7), or outside [32, 256], is
+    refused with PTYX_EUNSUPPORTED at plan creation, not run."""
     dev()
     from ptyrad_amd import _lib
     from ptyrad_amd.engine import Plan
-    with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
-        Plan(100, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0))
-    Plan(96, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0)).close()
+    for n in (98, 112, 16, 270):
+        with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
+            Plan(n, 1, 1, 1, 300, 300, 4, 4, device=torch.device("cuda", 0))
+    Plan(100, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0)).close()
 
 
 def _general_engine_case(N, P, O, Nz, shift, both):
