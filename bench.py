@@ -57,8 +57,9 @@ def parse():
                     help="patterns for the CPU baseline (0: about 20 s of the host's cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loss", default="single", choices=["single", "poissn", "both"],
-                    help="data term(s) beside loss_sparse (both: the stripe / register engines cannot take two "
-                         "data terms in one pass, so the call runs the general engine)")
+                    help="data term(s) beside loss_sparse (both: the stripe engine runs k_s3 twice around "
+                         "k_finalize, the N = 128 mixed-state engine applies both coefficients in k_fmm_adj; "
+                         "k_fused3 / k_fused3ms calls run the general engine)")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "band"],
                     help="N > 1: object gradients by one flat all-reduce, or by row band (ObjectBands: halo "
                          "rows to their owners, Adam on the owned band, bands all-gathered)")

@@ -1159,10 +1159,11 @@ static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_los
   s.mrows = a.mrows;
   s.Fp = pl->Fp; s.oc = pl->oc; s.obja = a.obja; s.objp = a.objp; s.meas = a.meas; s.occu = a.occu;
   s.q = single ? cfg->single_q : cfg->poissn_q;
+  s.q2 = cfg->poissn_q;
   s.eps2 = cfg->poissn_eps;
   s.sparse_on = cfg->sparse_on; s.sparse_n = cfg->sparse_n;
   s.t14 = pl->st14; s.psi0 = pl->spsi0; s.t23 = pl->st23; s.psum_s = pl->spsum; s.dp_out = a.dp_out;
-  s.coef = pl->coef; s.ci = single ? 0 : 1;
+  s.coef = pl->coef; s.ci = (single && cfg->poissn_on) ? 2 : single ? 0 : 1;
   s.d_obja = gz.d_obja; s.d_objp = gz.d_objp;
   const bool sgather = pl->sgather && (gz.d_obja || gz.d_objp);
   s.oslot = sgather ? pl->st23 : nullptr;
@@ -1176,6 +1177,42 @@ static sp::SArgs stripe_args(const ptyx_plan* pl, const KArgs& a, const ptyx_los
   s.slabpart = pl->sslab; s.dsp = pl->sdsp;
   s.twg = pl->twg;
   return s;
+}
+
+// k_s3.  ph 0: one data term (unit-coefficient g_Ψ);  both terms: ph 1 the partial sums before
+// k_finalize, ph 2 the coefficient-weighted g_Ψ after it.
+static void launch_s3(const ptyx_plan* pl, const sp::SArgs& s, const ptyx_loss_cfg* cfg, int ph, hipStream_t st) {
+  using namespace sp;
+  ProfScope ps(pl, kKS3, st);
+  const dim3 gr(s.n, kStripes), bl(256);
+  const int P = s.P, O = s.O;
+  const bool single = cfg->single_on != 0;
+  const bool half = single && s.q == 0.5f;
+  if (ph == 1) {
+    if (half) hipLaunchKernelGGL((k_s3<true, 0, 0, 1>), gr, bl, 0, st, s);
+    else hipLaunchKernelGGL((k_s3<true, 2, 0, 1>), gr, bl, 0, st, s);
+    return;
+  }
+  // Ψ of the first min(P·O, hold) modes stays in registers between k_s3's two sweeps, the other
+  // modes' column FFTs are redone.  Default (profiles/r02/ab/r02n_*): 2 of P·O ≤ 4 (c5: three
+  // workgroups per CU beat the saved re-reads), 4 above (c3)
+  const int hold_max = g_tuning[kTuneHold] >= 0 ? std::min<int>(4, (int)g_tuning[kTuneHold]) : (P * O <= 4 ? 2 : 4);
+  const int H = std::min(P * O, hold_max);
+#define PTYX_S3(SG, QM, PH)                                                                              \
+  switch (H) {                                                                                         \
+    case 1: hipLaunchKernelGGL((k_s3<SG, QM, 1, PH>), gr, bl, 0, st, s); break;                         \
+    case 2: hipLaunchKernelGGL((k_s3<SG, QM, 2, PH>), gr, bl, 0, st, s); break;                         \
+    case 3: hipLaunchKernelGGL((k_s3<SG, QM, 3, PH>), gr, bl, 0, st, s); break;                         \
+    case 4: hipLaunchKernelGGL((k_s3<SG, QM, 4, PH>), gr, bl, 0, st, s); break;                         \
+    default: hipLaunchKernelGGL((k_s3<SG, QM, 0, PH>), gr, bl, 0, st, s); break;                        \
+  }
+  if (ph == 2) {
+    if (half) { PTYX_S3(true, 0, 2) }
+    else { PTYX_S3(true, 2, 2) }
+  } else if (half) { PTYX_S3(true, 0, 0) }
+  else if (single) { PTYX_S3(true, 2, 0) }
+  else { PTYX_S3(false, 2, 0) }
+#undef PTYX_S3
 }
 
 // Stripe engine before k_finalize: preparation, pattern table, k_s1..k_s3, per-pattern sums.
@@ -1213,28 +1250,7 @@ static int stripe_pass(ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg, 
     if (O == 1) hipLaunchKernelGGL(k_s2<1>, dim3(n, kStripes), bl, 0, st, s);
     else hipLaunchKernelGGL(k_s2<2>, dim3(n, kStripes), bl, 0, st, s);
   }
-  {
-    ProfScope ps(pl, kKS3, st);
-    const dim3 gr(n, kStripes);
-    // Ψ of the first min(P·O, hold) modes stays in registers between k_s3's two sweeps, the other
-    // modes' column FFTs are redone.  Default (profiles/r02/ab/r02n_*): 2 of P·O ≤ 4 (c5: three
-    // workgroups per CU beat the saved re-reads), 4 above (c3)
-    const int hold_max = g_tuning[kTuneHold] >= 0 ? std::min<int>(4, (int)g_tuning[kTuneHold]) : (P * O <= 4 ? 2 : 4);
-    const int H = std::min(P * O, hold_max);
-    const bool half = single && s.q == 0.5f;
-#define PTYX_S3(SG, QM)                                                                                  \
-  switch (H) {                                                                                         \
-    case 1: hipLaunchKernelGGL((k_s3<SG, QM, 1>), gr, bl, 0, st, s); break;                             \
-    case 2: hipLaunchKernelGGL((k_s3<SG, QM, 2>), gr, bl, 0, st, s); break;                             \
-    case 3: hipLaunchKernelGGL((k_s3<SG, QM, 3>), gr, bl, 0, st, s); break;                             \
-    case 4: hipLaunchKernelGGL((k_s3<SG, QM, 4>), gr, bl, 0, st, s); break;                             \
-    default: hipLaunchKernelGGL((k_s3<SG, QM, 0>), gr, bl, 0, st, s); break;                            \
-  }
-    if (half) { PTYX_S3(true, 0) }
-    else if (single) { PTYX_S3(true, 2) }
-    else { PTYX_S3(false, 2) }
-#undef PTYX_S3
-  }
+  launch_s3(pl, s, cfg, s.ci == 2 ? 1 : 0, st);
   int rc = launch_status("stripe forward launch");
   if (rc) return rc;
   {
@@ -1282,6 +1298,10 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
   if (!any_grad) return PTYX_OK;
+  if (s.ci == 2) {   // both data terms: g_Ψ with the mini-batch coefficients, now known
+    launch_s3(pl, s, cfg, 2, st);
+    if ((rc = launch_status("k_s3 launch"))) return rc;
+  }
   {
     ProfScope ps(pl, kKS4, st);
     SArgs s4 = s;
@@ -1528,8 +1548,10 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   // co-residency or max_batch condition: they never wait)
   const bool fused3 = any_grad && single_mode && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 && slots_fit && one_term;
   const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit && one_term;
-  // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): one data term, call within capacity
-  const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && one_term;
+  // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): either or both data terms (both: k_s3
+  // twice, around k_finalize), call within capacity
+  const bool both_terms = cfg->single_on && cfg->poissn_on;
+  const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && (one_term || both_terms);
   // mixed-state register engine (N = 128, P > 1, O = 1): one data term, f32 DPs, the call within
   // the far-field cache its slots live in
   const bool fmm = any_grad && !want_H && pl->fmm && !a.meas_f16 && n_idx <= pl->ffc_cap;   // (either or both terms)

@@ -72,6 +72,7 @@ struct SArgs {
   const void* meas;
   const float* occu;
   float q, eps2;
+  float q2;              // loss_poissn's dp_pow when both data terms are on (k_s3 PH 1 / 2)
   int sparse_on, sparse_n;
   float2* t14;           // (n, P, N²)   T1, later T4
   float2* t4;            // = t14 when P4 writes T4 (probe / position gradients wanted), else NULL
@@ -80,7 +81,7 @@ struct SArgs {
   float* psum_s;         // (n, kStripes, kNSum) per-stripe loss partial sums
   float* dp_out;         // (n, N, N) or NULL
   const float* coef;     // (batches, kNCoef) from k_finalize
-  int ci;                // data-term coefficient index (0 single, 1 poissn)
+  int ci;                // data-term coefficient index (0 single, 1 poissn; 2: both, applied in k_s3)
   float* d_obja;
   float* d_objp;
   float2* oslot;         // non-NULL: P4 stores the object-gradient waves (unit c_m) as slots over
@@ -346,11 +347,16 @@ __global__ __launch_bounds__(256, kPassWG) void k_s2(SArgs a) {
 // grid (n, kStripes): columns kx of every mode: column FFT → Ψ, intensity, loss, g_Ψ → column IFFT.
 // The first HOLD modes keep Ψ in registers between the two sweeps; the column FFTs of the others
 // (P·O − HOLD of them) are redone in the second sweep.
-template <bool SINGLE, int QM, int HOLD>
+//
+// PH (loss_single + loss_poissn together, whose two mini-batch coefficients cannot be factored out
+// of one unit-coefficient field): 1 = the loss partial sums of both terms (and dp_out) only, no
+// stores to T3;  2 = after k_finalize, g_Ψ with ∂ℓ/∂I = c_single u_single + c_poissn u_poissn of the
+// pattern's mini-batch (the later passes then take coefficient 1: SArgs.ci = 2).  0 = one term.
+template <bool SINGLE, int QM, int HOLD, int PH = 0>
 __global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
   __shared__ float2 xb[kXElems];
   __shared__ float2 tw[kN];
-  __shared__ float red[8];
+  __shared__ float red[16];   // 4 waves × up to 4 sums (PH 1)
   load_tw(tw, a.twg);
   __syncthreads();
   const int j = blockIdx.x, s = blockIdx.y;
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) I[k] = fmaf(occ, cabs2(v[k]), I[k]);
   }
-  // loss at every point of the stripe (fftshifted DP index), unit-coefficient ∂ℓ/∂I
+  // loss at every point of the stripe (fftshifted DP index), unit-coefficient ∂ℓ/∂I (PH 2: scaled)
   const int sidx = scan_of(a, j);
   const size_t mi = (size_t)meas_row(a.mrow, a.mrows, sidx);
   const int col = (kx + kN / 2) & (kN - 1);
@@ -398,6 +404,36 @@ __global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
   }
   fence_sched();
   float S = 0.f, Ms = 0.f, u[16];
+  if constexpr (PH == 1) {   // both terms' partial sums, no ∂ℓ/∂I
+    float S2 = 0.f, Ms2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int ky = m.slot + 16 * k;
+      const int e = ((ky + kN / 2) & (kN - 1)) * kN + col;
+      const float Iv = I[k] + kDpEps;
+      if (a.dp_out) a.dp_out[(size_t)j * kN2 + e] = Iv;
+      (void)f3::loss_point<QM, true>(Iv, Mv[k], a.q, a.eps2, S, Ms);
+      (void)f3::loss_point<2, false>(Iv, Mv[k], a.q2, a.eps2, S2, Ms2);
+    }
+    float v4[4] = {S, Ms, S2, Ms2};
+    bsum<4>(v4, red);
+    if (threadIdx.x == 0) {
+      float* ps = a.psum_s + ((size_t)j * kStripes + s) * kNSum;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ps[i] = v4[i];
+    }
+    return;
+  } else if constexpr (PH == 2) {
+    const int mb = a.bid[j];
+    const float c1 = a.coef[(size_t)mb * kNCoef + 0], c2 = a.coef[(size_t)mb * kNCoef + 1];
+    float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float Iv = I[k] + kDpEps;
+      u[k] = fmaf(c1, f3::loss_point<QM, true>(Iv, Mv[k], a.q, a.eps2, d0, d1),
+                  c2 * f3::loss_point<2, false>(Iv, Mv[k], a.q2, a.eps2, d0, d1));
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int ky = m.slot + 16 * k;
@@ -418,6 +454,7 @@ __global__ __launch_bounds__(256, kPassWG) void k_s3(SArgs a) {
       ps[2 - b0] = 0.f;
       ps[3 - b0] = 0.f;
     }
+  }
   }
   // g_Ψ = 2 occ Ψ u → column IFFT, in place over T2
   auto back = [&](int q, float2 (&v)[16]) {
@@ -546,7 +583,7 @@ __global__ __launch_bounds__(256, kPassWG) void k_s4(SArgs a) {
   // object gradient.  The slot accumulators are re-mapped through the (now free) exchange buffer
   // so that each wave owns 4 whole rows: every atomic / object load is 256 contiguous bytes per
   // wave instruction (the full-rate shape of global float atomics) instead of 4 × 64 B.
-  const float c = a.coef[(size_t)mb * kNCoef + a.ci];
+  const float c = a.ci == 2 ? 1.f : a.coef[(size_t)mb * kNCoef + a.ci];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int o = 0; o < O_; ++o) {
@@ -623,7 +660,7 @@ __global__ __launch_bounds__(256, kPassWG) void k_s5(SArgs a) {
   int bid_n = gi < a.n ? a.bid[gi] : 0;
   for (int j = gi, it = 0; j < a.n; j += a.groups, ++it) {
     const float sy = sh_n.x, sx = sh_n.y;
-    const float c = a.coef[(size_t)bid_n * kNCoef + a.ci];
+    const float c = a.ci == 2 ? 1.f : a.coef[(size_t)bid_n * kNCoef + a.ci];
     if (j + a.groups < a.n) {
       sh_n = a.sxy[j + a.groups];
       bid_n = a.bid[j + a.groups];

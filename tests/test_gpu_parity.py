@@ -214,14 +214,40 @@ def test_n256_mixed_state_vs_oracle():
 
 @pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 1, 3, True, False), (1, 1, 3, True, False),
                                                (1, 2, 2, False, False), (2, 2, 2, True, False),
-                                               (1, 3, 1, True, False), (2, 2, 1, True, True)])
+                                               (1, 3, 1, True, False), (2, 2, 2, True, True)])
 def test_n256_general_engine_vs_oracle(P, O, Nz, shift, both):
     """N = 256 through the general two-pass engine (multislice, more object modes than the
-    stripe engine takes, or both data terms on a stripe plan) — the fused g256_fstage chains, with
+    stripe engine takes, or broadcast probes) — the fused g256_fstage chains, with
     and without the far-field cache (P·O > 1 vs P·O = 1), ψ⁰ parking (O > 1) and broadcast
     probes: ragged mini-batches vs the oracle, plus ptyx_forward's DPs and the external-dL/dI
     adjoint."""
     _general_engine_case(256, P, O, Nz, shift, both)
+
+
+@pytest.mark.parametrize("P,O,q1", [(2, 1, 0.5), (2, 2, 0.5), (3, 2, 1.0), (1, 1, 0.7)])
+def test_stripe_engine_both_terms_vs_oracle(P, O, q1):
+    """N = 256 stripe engine with loss_single + loss_poissn (+ loss_sparse): k_s3 takes both terms'
+    partial sums, k_finalize both coefficients, a second k_s3 the weighted ∂ℓ/∂I; ragged
+    mini-batches vs the oracle (losses.py:36-75)."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(256, 3, 3, P=P, O=O, Nz=1, seed=60 + 3 * P + O)
+    lp = orc_default_loss()
+    lp["loss_poissn"]["state"] = True
+    lp["loss_single"]["dp_pow"] = q1
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=lp)
+    batches = [np.array([4, 0, 7, 2]), np.array([8]), np.array([1, 5, 3, 6])]
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
+    assert "k_s3" in ks and ks["k_s3"][0] == 2 and "k_adjoint" not in ks, ks     # k_s3 around k_finalize
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, lp, grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
 
 
 @pytest.mark.parametrize("P,O,Nz,shift,both", [(2, 2, 3, True, True), (1, 2, 2, False, False),

@@ -34,7 +34,7 @@ def one(N, P, O, Nz, shift, device):
     errs = [rel(dp, np.concatenate(odps)), float(np.max(np.abs(terms - oterms)))]
     errs += [rel(g[k], og[k]) for k in ("obja", "objp", "probe")]
     plan.close()
-    eng = "k_adjoint1" if "k_adjoint1" in ks else "k_adjoint" if "k_adjoint" in ks else sorted(ks)
+    eng = "k_adjoint1" if "k_adjoint1" in ks else "k_adjoint" if "k_adjoint" in ks else "+".join(sorted(ks))[:24]
     print(f"N={N:3d} P{P} O{O} Nz{Nz} shift={int(shift)} {eng:10s} dp {errs[0]:.1e} terms {errs[1]:.1e} "
           f"obja {errs[2]:.1e} objp {errs[3]:.1e} probe {errs[4]:.1e}", flush=True)
 
