@@ -39,6 +39,8 @@ def summarize(d):
             m["wait_any_frac"] = m.get("SQ_WAIT_ANY", 0) / m["SQ_WAVE_CYCLES"]
         if m.get("SQ_LDS_IDX_ACTIVE"):
             m["lds_bank_conflict_frac"] = m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_LDS_IDX_ACTIVE"]
+        if m.get("TCC_HIT_sum", 0) + m.get("TCC_MISS_sum", 0) > 0:   # L2 (per XCD) hit rate
+            m["l2_hit_rate"] = m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
         if "TCC_EA0_ATOMIC_sum" in m:
             m["atomic_bytes"] = 64 * m["TCC_EA0_ATOMIC_sum"]
         out[k] = m

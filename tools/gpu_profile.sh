@@ -3,7 +3,8 @@
 # bench run, and the FETCH_SIZE / WRITE_SIZE PMC passes (separate runs, MI355X_MICROARCH.md
 # "rocprofv3 PMC slots") summarised per kernel by profiles/summarize_pmc.py.
 #   tools/gpu_profile.sh <tag> [config ...]        (outputs under gpurun_out/<tag>/)
-#   PROF_TESTS=1 also runs the -m gpu suite first; PROF_PMC=0 skips the PMC passes.
+#   PROF_TESTS=1 also runs the -m gpu suite first; PROF_PMC=0 skips the PMC passes;
+#   PROF_EXTRA_PASSES="TCC_HIT_sum+TCC_MISS_sum" adds PMC passes (L2 hit rate per kernel).
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 TAG=${1:-prof}
@@ -28,8 +29,9 @@ for c in $CONFIGS; do
   cp "$(find "$OUT/prof_$c" -name '*kernel_stats.csv' | head -1)" "$OUT/${c}_kernel_stats.csv"
   echo "rocprof $c ok"
   if [ "${PROF_PMC:-1}" = "1" ]; then
-    for pass in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 -s KILL 400 rocprofv3 --pmc $pass --output-format csv -d "$OUT/pmc_$c/pass_$pass" -o pmc -- \
+    # PROF_EXTRA_PASSES: more passes, counters of one pass joined by '+' (e.g. TCC_HIT_sum+TCC_MISS_sum)
+    for pass in FETCH_SIZE WRITE_SIZE ${PROF_EXTRA_PASSES:-}; do
+      timeout -k 10 -s KILL 400 rocprofv3 --pmc ${pass//+/ } --output-format csv -d "$OUT/pmc_$c/pass_$pass" -o pmc -- \
         python3 "$R/bench.py" --config "$c" --steps 1 --warmup 0 --no-cpu-baseline \
         > "$OUT/pmc_${c}_$pass.json" 2> "$OUT/pmc_${c}_$pass.err"
     done
