@@ -568,5 +568,40 @@ __global__ void k_shift_apply_modes(const int* idx, int n, int n_scans, int P, c
   atomicAdd(d_shifts + 2 * s + 1, dx * k);
 }
 
+// Small calls: k_segslab_reduce_modes + k_segslab_final (every mode: blockIdx.y = p) and
+// k_shift_apply_modes in ONE launch, the segment sums in exactly their order (bit-identical).
+template <bool KL>
+__global__ __launch_bounds__(256) void k_small_tail_modes(const float2* segslab, const int* segbid, int nseg,
+                                                          float2* out, const int* idx, int n, int n_scans, int P,
+                                                          const float* dsu, float* d_shifts) {
+  constexpr int kSlabBlocks = kN2 / 256;
+  if (blockIdx.x >= kSlabBlocks) {
+    const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
+    if (blockIdx.y != 0 || !d_shifts || j >= n) return;
+    const int s = min(max(idx[j], 0), n_scans - 1);
+    float dy = 0.f, dx = 0.f;
+    for (int p = 0; p < P; ++p) {
+      dy += dsu[2 * ((size_t)p * n + j)];
+      dx += dsu[2 * ((size_t)p * n + j) + 1];
+    }
+    constexpr float k = 6.283185307179586f / kN2;
+    atomicAdd(d_shifts + 2 * s, dy * k);
+    atomicAdd(d_shifts + 2 * s + 1, dx * k);
+    return;
+  }
+  if (!out) return;
+  const int e = blockIdx.x * 256 + threadIdx.x, p = blockIdx.y;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int y = 0; y < kSegSplit; ++y) {
+    float2 part = make_float2(0.f, 0.f);
+    for (int g = y; g < nseg; g += kSegSplit) {
+      if (segbid[g] != p) continue;
+      part = cadd(part, segslab[(size_t)g * kN2 + e]);
+    }
+    acc = cadd(acc, part);
+  }
+  out[(size_t)p * kN2 + packed_rc<KL>(e & 255, e >> 8)] = acc;
+}
+
 }  // namespace f3
 }  // namespace ptyx

@@ -131,6 +131,42 @@ __global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid
   atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
 }
 
+// Small calls (one mini-batch per optimizer step, ≤ kSmallCall patterns): k_segslab_reduce +
+// k_segslab_final + k_shift_apply in ONE launch.  Blocks [0, N²/256) sum the segments in exactly
+// the two kernels' order (partial y = Σ_{g ≡ y mod kSegSplit} c·u, then the partials in order:
+// bit-identical results); the blocks after them apply the position gradient.
+template <bool KL>
+__global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const int* segbid, int nseg,
+                                                    const float* coef, int ci, float2* out, const int* idx, int n,
+                                                    int n_scans, const int* bid, const float* dsu, float* d_shifts) {
+  constexpr int kSlabBlocks = kN2 / 256;
+  if (blockIdx.x >= kSlabBlocks) {
+    const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
+    if (!d_shifts || j >= n) return;
+    const int s = min(max(idx[j], 0), n_scans - 1);
+    const float k = 6.283185307179586f * coef[(size_t)bid[j] * kNCoef + ci] * (1.0f / kN2);
+    atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
+    atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
+    return;
+  }
+  if (!out) return;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int y = 0; y < kSegSplit; ++y) {
+    float2 part = make_float2(0.f, 0.f);
+    for (int g = y; g < nseg; g += kSegSplit) {
+      const int m = segbid[g];
+      if (m < 0) continue;
+      const float c = coef[(size_t)m * kNCoef + ci];
+      const float2 u = segslab[(size_t)g * kN2 + e];
+      part.x = fmaf(c, u.x, part.x);
+      part.y = fmaf(c, u.y, part.y);
+    }
+    acc = cadd(acc, part);
+  }
+  out[packed_rc<KL>(e & 255, e >> 8)] = acc;
+}
+
 // Per call: complex object O = A e^{iφ} (the fused kernel then needs no transcendental per
 // object point), and — for loss_sparse — per-row fp64 prefix sums of |φ|^n:
 // pref[y][x] = Σ_{x' < x} |φ(y, x')|^n, x = 0..Nx.  One workgroup per object row.
@@ -275,8 +311,8 @@ __global__ __launch_bounds__(256) void k_bbox(const int* idx, int n, const int* 
 // reference's default grad_accumulation = 1): the bounding box in ONE workgroup (no init launch,
 // no atomics), which also clears the call's segment table (no memset launch).
 constexpr int kSmallCall = 256;
-__global__ __launch_bounds__(256) void k_bbox_small(const int* idx, int n, const int* crop, int n_scans, int Ny,
-                                                    int Nx, int* bbox, int win, int* segbid, int nseg) {
+__device__ __forceinline__ void k_bbox_small_body(const int* idx, int n, const int* crop, int n_scans, int Ny,
+                                                  int Nx, int* bbox, int win, int* segbid, int nseg) {
   __shared__ int red[4][4];
   int a = 0x7fffffff, b = -0x7fffffff, c = 0x7fffffff, d = -0x7fffffff;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
@@ -315,6 +351,10 @@ __global__ __launch_bounds__(256) void k_bbox_small(const int* idx, int n, const
     bbox[2] = c;
     bbox[3] = d;
   }
+}
+__global__ __launch_bounds__(256) void k_bbox_small(const int* idx, int n, const int* crop, int n_scans, int Ny,
+                                                    int Nx, int* bbox, int win, int* segbid, int nseg) {
+  k_bbox_small_body(idx, n, crop, n_scans, Ny, Nx, bbox, win, segbid, nseg);
 }
 
 // pattern → (mini-batch, clamped window origin) and, with pref (the summed-area table of
@@ -367,26 +407,31 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
 // One workgroup per pattern: wave w sums rows w, w + 4, … of every slice, a lane two columns, 8
 // rows per round (16 loads in flight); fp64 lane sums, fixed-order wave reduction, waves added in
 // order through LDS (deterministic).
-__global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, int n, const int* boff, int n_batches,
-                                                              const int* crop, int n_scans, int Ny, int Nx, int* bid,
-                                                              int2* geo, const float* objp, int sparse_n, float* psums,
-                                                              int Nz, TableCheck tc) {
+// one pattern's table entry (mini-batch by binary search over boff, clamped window origin) and
+// its input validation
+__device__ __forceinline__ void table_entry(int j, const int* idx, const int* boff, int n_batches, const int* crop,
+                                            int n_scans, int Ny, int Nx, int* bid, int2* geo, TableCheck tc) {
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
+  check_pattern(tc.err, idx[j], n_scans, crop, Ny, Nx, kN, tc.mrow, tc.mrows);
+  int lo = 0, hi = n_batches;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (boff[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  bid[j] = lo;
+  geo[j] = make_int2(cy, cx);
+}
+__device__ __forceinline__ void k_pattern_table_direct_body(int j, const int* idx, int n, const int* boff,
+                                                            int n_batches, const int* crop, int n_scans, int Ny,
+                                                            int Nx, int* bid, int2* geo, const float* objp,
+                                                            int sparse_n, float* psums, int Nz, TableCheck tc) {
   __shared__ double s_w[4];
-  const int j = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = min(max(idx[j], 0), n_scans - 1);
   const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
-  if (threadIdx.x == 0) {
-    check_pattern(tc.err, idx[j], n_scans, crop, Ny, Nx, kN, tc.mrow, tc.mrows);
-    int lo = 0, hi = n_batches;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (boff[mid] <= j) lo = mid;
-      else hi = mid;
-    }
-    bid[j] = lo;
-    geo[j] = make_int2(cy, cx);
-  }
+  if (threadIdx.x == 0) table_entry(j, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
   double acc = 0;
   for (int z = 0; z < Nz; ++z) {
     const float* ph = objp + ((size_t)z * Ny + cy) * Nx + cx + lane;
@@ -409,6 +454,59 @@ __global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, in
   if (lane == 0) s_w[wave] = acc;
   __syncthreads();
   if (threadIdx.x == 0) psums[(size_t)j * kNSum + kSumBase] = (float)(((s_w[0] + s_w[1]) + s_w[2]) + s_w[3]);
+}
+__global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, int n, const int* boff, int n_batches,
+                                                              const int* crop, int n_scans, int Ny, int Nx, int* bid,
+                                                              int2* geo, const float* objp, int sparse_n, float* psums,
+                                                              int Nz, TableCheck tc) {
+  k_pattern_table_direct_body(blockIdx.x, idx, n, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, objp, sparse_n,
+                              psums, Nz, tc);
+}
+
+// Small calls with PTYX_PREP_CALL (one mini-batch per optimizer step): k_pattern_table_direct,
+// k_obj_prep and k_bbox_small as ONE launch of independent block roles —
+//   blocks [0, n)            the pattern table (+ the loss_sparse window sums when SPARSE);
+//   blocks [n, n + Nz·Ny)    O = A e^{iφ} for object row y of slice z, if any window of the call
+//                            covers it (decided from the ≤ 256 windows directly, not the bbox);
+//   block n + Nz·Ny          the bounding box (k_obj_gather) and the segment-table clear.
+// Same outputs as the three kernels (the rows no window touches are never read under PREP_CALL).
+template <bool SPARSE>
+__global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const int* boff, int n_batches,
+                                                    const int* crop, int n_scans, int Ny, int Nx, int* bid, int2* geo,
+                                                    const float* obja, const float* objp, int sparse_n, float* psums,
+                                                    int Nz, TableCheck tc, float2* oc, int* bbox, int* segbid,
+                                                    int nseg) {
+  const int b = blockIdx.x;
+  if (b < n) {
+    if constexpr (SPARSE) {
+      k_pattern_table_direct_body(b, idx, n, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, objp, sparse_n, psums,
+                                  Nz, tc);
+    } else if (threadIdx.x == 0) {
+      table_entry(b, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
+    }
+    return;
+  }
+  if (b == n + Nz * Ny) {
+    k_bbox_small_body(idx, n, crop, n_scans, Ny, Nx, bbox, kN, segbid, nseg);
+    return;
+  }
+  const int y = b - n;
+  const int r = y % Ny;
+  int hit = 0;
+  if ((int)threadIdx.x < n) {
+    const int s = min(max(idx[threadIdx.x], 0), n_scans - 1);
+    const int cy = min(max(crop[2 * s], 0), Ny - kN);
+    hit = r >= cy && r < cy + kN;
+  }
+  if (!__syncthreads_or(hit)) return;
+  const float* ar = obja + (size_t)y * Nx;
+  const float* pr = objp + (size_t)y * Nx;
+  float2* orow = oc + (size_t)y * Nx;
+  for (int x = threadIdx.x; x < Nx; x += blockDim.x) {
+    float sn, cs;
+    phase_sincos(pr[x], &sn, &cs);
+    orow[x] = make_float2(ar[x] * cs, ar[x] * sn);
+  }
 }
 
 // Far-field loss at one point, branch-free.  Returns u = ∂ℓ/∂I per unit mini-batch coefficient

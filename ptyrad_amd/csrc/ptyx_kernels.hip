@@ -393,7 +393,9 @@ template <int N, bool ROWPERM, bool MP>
 static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg, bool sparse_tiles, hipStream_t st) {
   const int parts = tiles * nzg;
   int S = 1;
-  if (parts < 1024 && pl->gpart) S = std::max(1, std::min({8, (2048 + parts - 1) / parts, kGatherPartCap / parts}));
+  // (not for small calls: a tile's few candidates are not worth the extra partial-sum launch)
+  if (parts < 1024 && pl->gpart && g.n > f3::kSmallCall)
+    S = std::max(1, std::min({8, (2048 + parts - 1) / parts, kGatherPartCap / parts}));
   if (g_tuning[kTuneGatherSplit] >= 1 && pl->gpart)
     S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], kGatherPartCap / parts));
   g.part = pl->gpart;
@@ -838,6 +840,20 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
   // segment table, and direct loss_sparse window sums instead of the summed-area table
   const bool small = a.n_idx <= f3::kSmallCall && pl->bbox;
   const bool direct_sums = sparse && small && cfg->prep == PTYX_PREP_CALL;
+  if (small && cfg->prep == PTYX_PREP_CALL) {   // table, object rows, bbox: one launch (k_small_prep)
+    ProfScope ps(pl, kKTable, st);
+    const dim3 gr(a.n_idx + Nz * d.Ny + 1), bl(256);
+    const f3::TableCheck tc{a.err, a.mrow, a.mrows};
+    if (sparse)
+      hipLaunchKernelGGL(f3::k_small_prep<true>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop, a.n_scans,
+                         d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc, pl->oc,
+                         pl->bbox, pl->segbid, nseg);
+    else
+      hipLaunchKernelGGL(f3::k_small_prep<false>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop, a.n_scans,
+                         d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc, pl->oc,
+                         pl->bbox, pl->segbid, nseg);
+    return launch_status("register engine preparation (small call)");
+  }
   if (small) {
     ProfScope ps(pl, kKTable, st);
     hipLaunchKernelGGL(f3::k_bbox_small, dim3(1), dim3(256), 0, st, a.idx, a.n_idx, a.crop, a.n_scans, d.Ny, d.Nx,
@@ -1003,7 +1019,23 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  if (a.shift && gz.d_shifts) {
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)
+        hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts);
+    }
+    if (gz.d_probe) launch_probe_fin(pl, a, st, gz.d_probe, 1);
+    return launch_status("probe finalize launch");
+  }
+  if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.n_scans,
                        pl->bid, pl->coef, ci, pl->dsu, gz.d_shifts);
@@ -1124,7 +1156,23 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  if (a.shift && gz.d_shifts) {
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)
+        hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts);
+    }
+    if (gz.d_probe) launch_probe_fin(pl, a, st, gz.d_probe, P);
+    return launch_status("k_fmm probe / position reduction launch");
+  }
+  if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply_modes, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx,
                        a.n_scans, P, pl->dsu, gz.d_shifts);

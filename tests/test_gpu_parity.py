@@ -411,7 +411,9 @@ def test_register_engine_ragged_batches_vs_oracle(shift):
 
 
 def test_register_engine_is_the_path_taken():
-    """The c2-shaped call runs k_fused3 (its prep kernels show up in the per-kernel timing)."""
+    """The c2-shaped call runs k_fused3 (its prep kernels show up in the per-kernel timing; a
+    small call's table, object rows and bounding box are one k_small_prep launch, timed as
+    k_pattern_table)."""
     device = dev()
     from ptyrad_amd.engine import LossConfig, batch_offsets
     d = _c2_like(8, 8, seed=2)
@@ -424,7 +426,7 @@ def test_register_engine_is_the_path_taken():
                            LossConfig.from_loss_params(d["loss_params"]), grads)
     torch.cuda.synchronize()
     stats = plan.profile_end()
-    assert "k_obj_prep" in stats and "k_fused" in stats, stats
+    assert "k_pattern_table" in stats and "k_fused" in stats and "k_obj_prep" not in stats, stats
 
 
 @pytest.mark.parametrize("nz,shift", [(3, True), (2, False), (16, True)])
@@ -460,7 +462,7 @@ def test_multislice_register_engine_vs_oracle(nz, shift):
                            LossConfig.from_loss_params(d["loss_params"]), grads)
     torch.cuda.synchronize()
     stats = plan.profile_end()
-    assert "k_obj_prep" in stats and "k_fused" in stats and "k_adjoint" not in stats, stats
+    assert "k_pattern_table" in stats and "k_fused" in stats and "k_adjoint" not in stats, stats
 
 
 def test_multislice_call_split_at_batch_boundaries(monkeypatch):
