@@ -365,8 +365,10 @@ int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
  * slots + gather instead of f32 atomics), "s_defer_groups" (0: the stripe engine ignores
  * PTYX_PREP_DEFER_PROBE; n > 0: k_s5 partial groups of deferring calls), "gather_split" (n >= 1:
  * the object-gradient gather splits every tile's candidates over n workgroups; the default splits
- * only grids too small to fill the GPU); value -1 restores the measured default.  Process-wide,
- * read by ptyx_plan_create (s_psi0, s_gather) and by each call (s3_hold).  Every variant computes
+ * only grids too small to fill the GPU), "gen_wg_per_cu" (n >= 1: the general engine's persistent
+ * workgroups per CU instead of its LDS / thread residency); value -1 restores the measured
+ * default.  Process-wide, read by ptyx_plan_create (s_psi0, s_gather, gen_wg_per_cu) and by each
+ * call (s3_hold).  Every variant computes
  * the same results.  ptyx_get_tuning returns the current value (-1 default, -2 unknown key). */
 int ptyx_set_tuning(const char *key, int64_t value);
 int64_t ptyx_get_tuning(const char *key);

@@ -203,7 +203,7 @@ def set_tuning(key: str, value: int) -> None:
     check(load().ptyx_set_tuning(key.encode(), int(value)))
 
 
-TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split")   # ptyx_set_tuning's keys
+TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu")   # ptyx_set_tuning's keys
 
 
 def get_tuning(key: str) -> int:

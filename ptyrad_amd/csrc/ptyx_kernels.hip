@@ -205,10 +205,11 @@ struct DeviceGuard {
 };
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
-enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneCount };
-const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1};
+enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneCount };
+const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
+                                            "gen_wg_per_cu"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -463,7 +464,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->device = device;
   pl->n_cu = cu;
   pl->gen = gen;
-  pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * gen->blocks_per_cu));
+  const int wg_cu = g_tuning[kTuneGenWg] >= 1 ? (int)g_tuning[kTuneGenWg] : gen->blocks_per_cu;
+  pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * wg_cu));
   const size_t N2 = (size_t)d.N * d.N;
   const bool lds = gen->lds;
   const bool prop_grad = (d.flags & PTYX_PROP_GRAD) && d.Nz > 1;
