@@ -565,6 +565,104 @@ __device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float
   g256_fstage<DIR, 0, LAST, FIRST, PRELOAD, true, LAST>(src, dst, lds, tw, pre, nm, post);
 }
 
+// ---------------------------------------------------------------- 128 < N < 256: line blocks
+// A field that does not fit LDS (and is not 256², which has its own stages above) transforms in
+// TWO global round trips: stage 1 takes blocks of kLines rows through LDS (pre hook on the loads,
+// both Stockham passes of the row DFT in LDS, stored to the pair's b), stage 2 blocks of kLines
+// columns (128-B row segments in, both passes, post hook on the way out to a).
+template <int N>
+struct LineTile {
+  static constexpr int kLines = 32;
+  static constexpr int kStride = N + N / 16;                 // one pad point per 16 (LdsArray's rule)
+  static constexpr int kElems = kLines * kStride;
+  __device__ __forceinline__ static int off(int line, int x) { return line * kStride + x + (x >> 4); }
+};
+
+// One in-place Stockham pass of radix R (span NS) along `lines` lines of a LineTile.
+template <int N, int NT, int R, int NS, int DIR>
+__device__ __forceinline__ void line_pass(float2* tile, const float2* tw, int lines) {
+  using LT = LineTile<N>;
+  constexpr int L = N / R;                 // butterflies per line
+  constexpr int TWS = N / (NS * R);        // twiddle table stride
+  constexpr int KB = (LT::kLines * L + NT - 1) / NT;
+  const int NB = lines * L;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  float2 v[KB][R];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int bf = tid + kb * NT;
+    if (bf < NB) {
+      const int line = bf / L, j = bf % L, k = j % NS;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float2 val = tile[LT::off(line, j + r * L)];
+        if constexpr (NS > 1) {
+          if (r > 0) val = cmul(val, twiddle<DIR>(tw, k * r * TWS));
+        }
+        v[kb][r] = val;
+      }
+      DFT<R, DIR>::run(v[kb]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int bf = tid + kb * NT;
+    if (bf < NB) {
+      const int line = bf / L, j = bf % L, k = j % NS;
+      const int d0 = (j / NS) * NS * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) tile[LT::off(line, d0 + r * NS)] = v[kb][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int N, int NT, int DIR, bool PRELOAD, class Pre, class Post>
+__device__ __forceinline__ void fft2d_lines(const GlobalPair<N>& arr, const float2* tw, Pre& pre, Post& post) {
+  using LT = LineTile<N>;
+  using P1 = Plan1D<N>;
+  constexpr int B = LT::kLines;
+  float2* T = arr.lds;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  for (int l0 = 0; l0 < N; l0 += B) {          // rows of a → b
+    const int nl = N - l0 < B ? N - l0 : B;
+    for (int e = tid; e < nl * N; e += NT) {
+      const int r = e / N, x = e % N, y = l0 + r;
+      float2 val;
+      if constexpr (PRELOAD) val = call_pre(pre, y, x, arr.a[y * N + x], 0);
+      else val = call_pre(pre, y, x, make_float2(0.f, 0.f), 0);
+      T[LT::off(r, x)] = val;
+    }
+    __syncthreads();
+    line_pass<N, NT, P1::R1, 1, DIR>(T, tw, nl);
+    line_pass<N, NT, P1::R2, P1::R1, DIR>(T, tw, nl);
+    for (int e = tid; e < nl * N; e += NT) {
+      const int r = e / N, x = e % N;
+      arr.b[(l0 + r) * N + x] = T[LT::off(r, x)];
+    }
+    __syncthreads();
+  }
+  for (int c0 = 0; c0 < N; c0 += B) {          // columns of b → a
+    const int nc = N - c0 < B ? N - c0 : B;
+    for (int e = tid; e < nc * N; e += NT) {
+      const int y = e / nc, c = e % nc;
+      T[LT::off(c, y)] = arr.b[y * N + c0 + c];
+    }
+    __syncthreads();
+    line_pass<N, NT, P1::R1, 1, DIR>(T, tw, nc);
+    line_pass<N, NT, P1::R2, P1::R1, DIR>(T, tw, nc);
+    for (int e = tid; e < nc * N; e += NT) {
+      const int y = e / nc, c = e % nc, x = c0 + c;
+      float2 val = T[LT::off(c, y)];
+      if (call_post(post, y, x, val, 0)) arr.a[y * N + x] = val;
+    }
+    __syncthreads();
+  }
+}
+
 template <int DIR, bool PRELOAD, class Pre, class Post>
 __device__ __forceinline__ void fft2d_g256(const GlobalPair<256>& arr, const float2* tw, Pre& pre, Post& post) {
   g256_stage<DIR, true, false, PRELOAD>(arr.a, arr.b, arr.lds, tw, pre, post);
@@ -591,15 +689,16 @@ __device__ __forceinline__ void fft2d(const Arr& arr, const float2* tw, Pre&& pr
     static_assert(R2 != 1, "global ping-pong needs two passes per dimension");
     if constexpr (N == 256 && NT == kG256Threads) {
       fft2d_g256<DIR, PRELOAD>(arr, tw, pre, post);
-      return;
+    } else {
+      fft2d_lines<N, NT, DIR, PRELOAD>(arr, tw, pre, post);
     }
-    const GlobalView<N> A{arr.a}, B{arr.b};
-    stockham_pass<N, NT, R1, 1, true, DIR, kFirst, PRELOAD, false>(A, B, tw, pre, post);
-    stockham_pass<N, NT, R2, R1, true, DIR, kMid, false, false>(B, A, tw, pre, post);
-    stockham_pass<N, NT, R1, 1, false, DIR, kMid, false, false>(A, B, tw, pre, post);
-    stockham_pass<N, NT, R2, R1, false, DIR, kLast, false, false>(B, A, tw, pre, post);
   }
 }
 
+
+// LDS (float2) a general-engine kernel declares for its N×N transforms: the whole field (N ≤ 128),
+// N = 256's stage tile, or the line-block tile (128 < N < 256)
+template <int N, bool LDS>
+constexpr int kFieldLds = LDS ? LdsArray<N>::kElems : N == 256 ? kG256Elems : LineTile<N>::kElems;
 
 }  // namespace ptyx

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_spectrum(K
   constexpr int NT = Geo<N>::NT;
   constexpr bool LDS = Geo<N>::kLds;
   __shared__ float2 s_tw[N];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
+  __shared__ float2 s_buf[kFieldLds<N, LDS>];
   const int p = blockIdx.x;
   if constexpr (N == 256) {
     if (p == a.P) {   // the extra workgroup of a Nz > 1 call: HT = Hᵀ for the fused chains
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_forward(KArgs a)
   constexpr float inv_n = 1.0f / (float)N;
   __shared__ float2 s_tw[N], s_wy[N], s_wx[N], s_ty[N], s_tx[N];
   __shared__ float s_red[(NT / 64) * 4];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
+  __shared__ float2 s_buf[kFieldLds<N, LDS>];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   typename ArrayFor<N, LDS>::type arr;
   if constexpr (LDS) arr.p = s_buf;
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint(KArgs a)
   constexpr float inv_n2 = 1.0f / (float)N2;
   __shared__ float2 s_tw[N], s_wy[N], s_wx[N], s_ty[N], s_tx[N];
   __shared__ float s_red[(NT / 64) * 2];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
+  __shared__ float2 s_buf[kFieldLds<N, LDS>];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   typename ArrayFor<N, LDS>::type arr;
   if constexpr (LDS) arr.p = s_buf;
@@ -741,7 +741,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_finalize(K
   constexpr int N2 = N * N;
   constexpr float inv_n2 = 1.0f / (float)N2;
   __shared__ float2 s_tw[N];
-  __shared__ float2 s_buf[LDS ? LdsArray<N>::kElems : (N == 256 ? kG256Elems : 1)];
+  __shared__ float2 s_buf[kFieldLds<N, LDS>];
   for (int i = threadIdx.x; i < N; i += NT) s_tw[i] = a.twg[i];
   __syncthreads();
   const int p = blockIdx.x;
@@ -814,7 +814,7 @@ struct GenLaunch {
   }
   // LDS-limited residency (160 KiB per CU, 2048 threads) of the workgroup-resident FFT kernels
   static constexpr int blocks_per_cu() {
-    constexpr int lds = (int)sizeof(float2) * (5 * N + (Geo<N>::kLds ? LdsArray<N>::kElems : N == 256 ? kG256Elems : 1)) + 256;
+    constexpr int lds = (int)sizeof(float2) * (5 * N + kFieldLds<N, Geo<N>::kLds>) + 256;
     constexpr int by_lds = 160 * 1024 / lds, by_threads = 2048 / NT;
     return by_lds < by_threads ? by_lds : by_threads;
   }

@@ -7,6 +7,7 @@ reference's own demo parameter files, next to the BASELINE configs' engines:
   plus single-mode / single-slice neighbours of tbl for comparison.
 
     python tools/bench_modes.py [name ...] [--patterns 4096] [--reps 3] [--tune key=value ...]
+    (name: a GEOMS key or n<N>_p<P>_o<O>_z<Nz>)
 
 Synthetic raster (2.871 px step), seeded uniform DPs, random mini-batches of 32, loss_single
 (q 0.5) + loss_sparse, all gradients on.  One JSON line per geometry with the per-kernel times.
@@ -86,7 +87,11 @@ def main():
         k, v = kv.split("=")
         _lib.set_tuning(k, int(v))
     for name in a.names:
-        run(name, GEOMS[name], a.patterns, a.reps, dev, tune=a.tune)
+        g = GEOMS.get(name)
+        if g is None:   # any geometry as n<N>_p<P>_o<O>_z<Nz>, e.g. n192_p1_o1_z1
+            N, P, O, Nz = (int(x[1:]) for x in name.split("_"))
+            g = dict(N=N, P=P, O=O, Nz=Nz)
+        run(name, g, a.patterns, a.reps, dev, tune=a.tune)
         torch.cuda.empty_cache()
 
 
