@@ -66,6 +66,10 @@ struct F3Args {
   // at slots + (pat·Nz + n)·N²), oc is (Nz, Ny, Nx)
   int Nz;
   const float2* hpk;
+  // both data terms (k_fused3 MODE 1 / 2): loss_poissn's dp_pow, and the per-mini-batch
+  // coefficients [c_single, c_poissn] (k_finalize) MODE 2 weights ∂ℓ/∂I with
+  float q2 = 1.f;
+  const float* coef = nullptr;
 };
 
 // Packed layouts (thread t = 0..255, register i = 0..63):
@@ -102,7 +106,7 @@ __global__ void k_segslab_reduce(const float2* segslab, const int* segbid, int n
   for (int g = y; g < nseg; g += kSegSplit) {
     const int m = segbid[g];
     if (m < 0) continue;
-    const float c = coef[(size_t)m * kNCoef + ci];
+    const float c = ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci];   // (ci 2: applied by the kernel)
     const float2 u = segslab[(size_t)g * kN2 + e];
     acc.x = fmaf(c, u.x, acc.x);
     acc.y = fmaf(c, u.y, acc.y);
@@ -126,7 +130,7 @@ __global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const int s = min(max(idx[j], 0), n_scans - 1);
-  const float k = 6.283185307179586f * coef[(size_t)bid[j] * kNCoef + ci] * (1.0f / kN2);
+  const float k = 6.283185307179586f * (ci >= 2 ? 1.f : coef[(size_t)bid[j] * kNCoef + ci]) * (1.0f / kN2);
   atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
   atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
 }
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
     const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
     if (!d_shifts || j >= n) return;
     const int s = min(max(idx[j], 0), n_scans - 1);
-    const float k = 6.283185307179586f * coef[(size_t)bid[j] * kNCoef + ci] * (1.0f / kN2);
+    const float k = 6.283185307179586f * (ci >= 2 ? 1.f : coef[(size_t)bid[j] * kNCoef + ci]) * (1.0f / kN2);
     atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
     atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
     return;
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
     for (int g = y; g < nseg; g += kSegSplit) {
       const int m = segbid[g];
       if (m < 0) continue;
-      const float c = coef[(size_t)m * kNCoef + ci];
+      const float c = ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci];
       const float2 u = segslab[(size_t)g * kN2 + e];
       part.x = fmaf(c, u.x, part.x);
       part.y = fmaf(c, u.y, part.y);
@@ -849,7 +853,12 @@ struct Ramp {
 // Two workgroups per CU (≤ 256 VGPRs).  Holding ψ⁰ and the segment slab in AGPRs at one workgroup
 // per CU instead of the park and the slab read-modify-write measured the same time
 // (profiles/r02/ab/r02l_c2hold: 12.29 vs 12.16 ms), so the kernel parks them.
-template <bool SHIFT, bool SINGLE, int QM>
+// MODE (loss_single + loss_poissn, whose mini-batch coefficients are known only after
+// k_finalize): 1 = forward and both terms' loss partial sums only (no park, no adjoint; the next
+// pattern's v formed right after the sums), 2 = the full pass with ∂ℓ/∂I = c_single u_single +
+// c_poissn u_poissn of the pattern's mini-batch (slots / slabs / position sums then carry the
+// coefficients; no partial sums written).  0 = one data term, unit coefficient (the c2 kernel).
+template <bool SHIFT, bool SINGLE, int QM, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
@@ -952,7 +961,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
           const float2 O = sl[rb * 64 + io];
-          st2(v[j], r_park, vpark, 2048 * j);
+          if constexpr (MODE != 1) st2(v[j], r_park, vpark, 2048 * j);
           v[j] = pcm(v[j], O);
           pin(v[j]);
         }
@@ -973,7 +982,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const int j = 8 * C + r;
-              st2(v[j], r_slot, vslot, 2048 * j);
+              if constexpr (MODE != 1) st2(v[j], r_slot, vslot, 2048 * j);
               v[j] = cmul(v[j], t.x[r]);
               pin(v[j]);
             }
@@ -998,8 +1007,10 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    float S = 0.f, Ms = 0.f;
+    float S = 0.f, Ms = 0.f, S2 = 0.f, Ms2 = 0.f;
     const float occ_n2 = occ * inv_n2, occ2_n = 2.0f * occ * inv_n;
+    float2 cc = make_float2(0.f, 0.f);   // MODE 2: (c_single, c_poissn) of the pattern's mini-batch
+    if constexpr (MODE == 2) cc = s_ldf2(a.coef + (size_t)p.m * kNCoef);
     {
       const int r = (fx + 64) & 127;               // fftshifted DP row of ky
       const int b = 1 - l0;                        // fftshifted column half of kx = k + 64 l0
@@ -1018,9 +1029,19 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
           const int k = 4 * kq + e;
           // Ψ = v/N with N a power of two: |Ψ|² occ = |v|² (occ/N²) and g_Ψ = v (2 occ u / N) exactly
           Iv[e] = fmaf(occ_n2, cabs2(v[k]), kDpEps);
-          const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
-          v[k] = pscale(v[k], occ2_n * u);
-          pin(v[k]);
+          if constexpr (MODE == 1) {
+            (void)loss_point<QM, true>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+            (void)loss_point<2, false>(Iv[e], Mv[e], a.q2, a.eps2, S2, Ms2);
+          } else if constexpr (MODE == 2) {
+            const float u = fmaf(cc.x, loss_point<QM, true>(Iv[e], Mv[e], q, a.eps2, S, Ms),
+                                 cc.y * loss_point<2, false>(Iv[e], Mv[e], a.q2, a.eps2, S2, Ms2));
+            v[k] = pscale(v[k], occ2_n * u);
+            pin(v[k]);
+          } else {
+            const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+            v[k] = pscale(v[k], occ2_n * u);
+            pin(v[k]);
+          }
         }
         {
           const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
@@ -1030,11 +1051,42 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
         if (kq & 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    {
+    if constexpr (MODE == 1) {
+      // both terms' sums, then the next pattern's v (the prologue's arithmetic) and no adjoint
+      float v4[4] = {S, Ms, S2, Ms2};
+      block_sum4<4>(v4, s_red);
+      if (threadIdx.x == 0) {
+        float* ps = a.psums + (size_t)pat * kNSum;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ps[i] = v4[i];
+      }
+      const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
+      p_nxt = pn;
+      const int vpk = rf::opaque(8 * tid);
+      Ramp rp;
+      rp.init(pn.sy, pn.sx, gy, rf::opaque(tid) & 1);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = rp.a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (kRing) v[4 * C + r] = pcm(t.x[r], pcm(A, rp.B[r]));
+              else v[4 * C + r] = SHIFT ? cmul(t.x[r], cmul(A, rp.B[r])) : t.x[r];
+              pin(v[4 * C + r]);
+            }
+          });
+      continue;
+    } else {
       // (block_sum4's first barrier also retires every wave's DP reads before the next exchange)
       float v2[2] = {S, Ms};
       block_sum4<2>(v2, s_red);
-      if (threadIdx.x == 0) {
+      if (MODE == 0 && threadIdx.x == 0) {
         float* ps = a.psums + (size_t)pat * kNSum;
         const int base = SINGLE ? 0 : 2;
         ps[base] = v2[0];

@@ -917,7 +917,26 @@ static f3::F3Args register_args(const ptyx_plan* pl, const ptyx_inputs* in, cons
   f.dp_out = a.dp_out;
   f.Nz = d.Nz;
   f.hpk = pl->hpk;
+  f.q2 = cfg->poissn_q;
+  f.coef = pl->coef;
   return f;
+}
+
+// k_fused3 with both data terms: MODE 1 (forward + both terms' sums) before k_finalize, MODE 2
+// (the full pass with the mini-batch coefficients) after it
+static void launch_fused3_both(const ptyx_plan* pl, const f3::F3Args& f, bool shift, int mode, int G, hipStream_t st) {
+  ProfScope ps(pl, kKFused, st);
+  const dim3 gr(G), bl(256);
+  const bool half = f.q == 0.5f;
+#define PTYX_F3B(SH, QM, MD) hipLaunchKernelGGL((f3::k_fused3<SH, true, QM, MD>), gr, bl, 0, st, f)
+  if (mode == 1) {
+    if (shift) { if (half) PTYX_F3B(true, 0, 1); else PTYX_F3B(true, 2, 1); }
+    else { if (half) PTYX_F3B(false, 0, 1); else PTYX_F3B(false, 2, 1); }
+  } else {
+    if (shift) { if (half) PTYX_F3B(true, 0, 2); else PTYX_F3B(true, 2, 2); }
+    else { if (half) PTYX_F3B(false, 0, 2); else PTYX_F3B(false, 2, 2); }
+  }
+#undef PTYX_F3B
 }
 
 // Preparation, pattern table and the k_fused3 / k_fused3ms pass (everything before k_finalize).
@@ -943,6 +962,8 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
       else if (single) hipLaunchKernelGGL((f3::k_fused3ms<false, true, 2>), gr, bl, 0, st, f);
       else hipLaunchKernelGGL((f3::k_fused3ms<false, false, 2>), gr, bl, 0, st, f);
     }
+  } else if (cfg->single_on && cfg->poissn_on) {
+    launch_fused3_both(pl, f, a.shift, 1, G, st);
   } else {
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
@@ -967,7 +988,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const bool sparse = cfg->sparse_on != 0;
   const int Nz = d.Nz;
   const bool single = cfg->single_on != 0;
-  const int ci = single ? 0 : 1;
+  const bool both = single && cfg->poissn_on && Nz == 1;   // k_fused3 MODE 1 / 2
+  const int ci = both ? 2 : single ? 0 : 1;                // (2: the kernel applies the coefficients)
   const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
   const int nseg = a.n_batches + G;
   int rc = PTYX_OK;
@@ -989,6 +1011,12 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
   }
   if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
+  if (both) {   // the adjoint pass, now that the coefficients are known (dp_out written by MODE 1)
+    f3::F3Args f = register_args(pl, in, a, cfg, gz);
+    f.dp_out = nullptr;
+    launch_fused3_both(pl, f, a.shift, 2, G, st);
+    if ((rc = launch_status("k_fused3 (both terms) launch"))) return rc;
+  }
   // small calls: every tile scans the call's few patterns directly (no binning launches)
   const bool bins = a.n_idx > f3::kSmallCall;
   if ((gz.d_obja || gz.d_objp) && bins) {
@@ -1596,11 +1624,13 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   // register-resident engines: k_fused3 (N = 128, single mode) and k_fused3ms (N = 128, P = O = 1,
   // Nz ≥ 2); f32 DPs, one data term, slots and segment slabs large enough for the call (no
   // co-residency or max_batch condition: they never wait)
-  const bool fused3 = any_grad && single_mode && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 && slots_fit && one_term;
+  const bool both_terms = cfg->single_on && cfg->poissn_on;
+  // (k_fused3 takes both data terms as two passes around k_finalize; k_fused3ms one term)
+  const bool fused3 = any_grad && single_mode && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 && slots_fit &&
+                      (one_term || both_terms);
   const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit && one_term;
   // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): either or both data terms (both: k_s3
   // twice, around k_finalize), call within capacity
-  const bool both_terms = cfg->single_on && cfg->poissn_on;
   const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && (one_term || both_terms);
   // mixed-state register engine (N = 128, P > 1, O = 1): one data term, f32 DPs, the call within
   // the far-field cache its slots live in

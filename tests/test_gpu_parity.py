@@ -410,6 +410,35 @@ def test_register_engine_ragged_batches_vs_oracle(shift):
         assert rel(g["shifts"], og["shifts"]) < TOL_SH
 
 
+@pytest.mark.parametrize("shift,q1,n", [(True, 0.5, 144), (False, 0.5, 144), (True, 1.0, 144), (True, 0.5, 300)])
+def test_register_engine_both_terms_vs_oracle(shift, q1, n):
+    """loss_single + loss_poissn on k_fused3: a forward pass taking both terms' sums (MODE 1),
+    k_finalize, then the full pass with c_single u_single + c_poissn u_poissn (MODE 2; the gather,
+    probe and position sums then take coefficient 1).  Ragged mini-batches vs the oracle; n 300
+    takes the binned (non-small-call) gather and tail."""
+    device = dev()
+    d = _c2_like(12 if n == 144 else 18, 12 if n == 144 else 17, seed=12)
+    d["shift_probes"] = shift
+    d["loss_params"]["loss_poissn"]["state"] = True
+    d["loss_params"]["loss_single"]["dp_pow"] = q1
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(5).permutation(S)[:n]
+    cuts = sorted({0, 5, 37, 38, 70, 101, n})
+    batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+    ks = {}
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.25, kernels=ks)
+    assert ks["k_fused"][0] == 2 and "k_adjoint" not in ks, ks          # MODE 1 + MODE 2
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"],
+                                             shift_probes=shift, grad_scale=0.25)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    if shift:
+        assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
 def test_register_engine_is_the_path_taken():
     """The c2-shaped call runs k_fused3 (its prep kernels show up in the per-kernel timing; a
     small call's table, object rows and bounding box are one k_small_prep launch, timed as

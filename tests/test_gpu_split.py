@@ -55,14 +55,15 @@ def to_np(g):
 
 # geometry -> engine that serves it: k_fused3, k_fused3ms, the mixed-state register engine, the N = 256
 # stripe engine, the two-pass engine
-# (*_both: loss_single + loss_poissn, whose coefficients the stripe engine applies in a second k_s3
-# and the mixed-state engine in k_fmm_adj, both after k_finalize — i.e. in _end of a split call)
+# (*_both: loss_single + loss_poissn, whose coefficients the stripe engine applies in a second k_s3,
+# the mixed-state engine in k_fmm_adj and k_fused3 in its MODE 2 pass, all after k_finalize — i.e.
+# in _end of a split call)
 GEOMS = {"fused3": (128, 1, 1, 1), "fused3ms": (128, 1, 1, 3), "fmm": (128, 3, 1, 2), "stripe": (256, 2, 1, 1),
          "stripe_o2": (256, 2, 2, 1), "two_pass": (64, 2, 2, 2), "stripe_both": (256, 2, 1, 1),
-         "stripe_o2_both": (256, 2, 2, 1), "fmm_both": (128, 3, 1, 2)}
+         "stripe_o2_both": (256, 2, 2, 1), "fmm_both": (128, 3, 1, 2), "fused3_both": (128, 1, 1, 1)}
 ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "fmm": "k_fused", "stripe": "k_s3",
                  "stripe_o2": "k_obj_gather", "two_pass": "k_forward", "stripe_both": "k_s3",
-                 "stripe_o2_both": "k_obj_gather", "fmm_both": "k_fused"}
+                 "stripe_o2_both": "k_obj_gather", "fmm_both": "k_fused", "fused3_both": "k_fused"}
 
 
 @pytest.mark.parametrize("world", [2, 3])
