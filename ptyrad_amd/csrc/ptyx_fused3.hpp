@@ -1321,7 +1321,9 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
 // per-slice point-wise passes stream their operands through k_fused3's LDS-DMA ring: slice n's
 // object window (forward; ψⁿ parked in the ring's park layout) or its park + object window
 // (backward) are issued during the preceding inverse FFT, D register pairs ahead of their use.
-template <bool SHIFT, bool SINGLE, int QM>
+// MODE: as k_fused3 (1: forward through every slice + both terms' sums, no parks, no adjoint;
+// 2: the full pass with both mini-batch coefficients applied; 0: one term, unit coefficient).
+template <bool SHIFT, bool SINGLE, int QM, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
@@ -1451,7 +1453,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
           for (int rb = 0; rb < 2; ++rb) {
             const int j = 2 * q + rb;
             const float2 O = sl[rb * 64 + io];
-            st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
+            if constexpr (MODE != 1) st2_stream(v[j], r_slot, vpark, 2048 * j);   // ψⁿ park (ring layout: read back by pre3)
             v[j] = pcm(v[j], O);
             pin(v[j]);
           }
@@ -1474,7 +1476,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) {
                 const int j = 8 * C + r;
-                st2(v[j], r_slot, vslot, 2048 * j);
+                if constexpr (MODE != 1) st2(v[j], r_slot, vslot, 2048 * j);
                 v[j] = pcm(v[j], t.x[r]);
                 pin(v[j]);
               }
@@ -1504,8 +1506,10 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    float S = 0.f, Ms = 0.f;
+    float S = 0.f, Ms = 0.f, S2 = 0.f, Ms2 = 0.f;
     const float occ_n2 = occ * inv_n2, occ2_n = 2.0f * occ * inv_n;
+    float2 cc = make_float2(0.f, 0.f);   // MODE 2: (c_single, c_poissn) of the pattern's mini-batch
+    if constexpr (MODE == 2) cc = s_ldf2(a.coef + (size_t)p.m * kNCoef);
     {
       const int r = (fx + 64) & 127;
       const int b = 1 - l0;
@@ -1522,9 +1526,19 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
           const int k = 4 * kq + e;
           // Ψ = v/N with N a power of two: occ|Ψ|² = |v|²·(occ/N²) and g_Ψ = v·(2 occ u/N), exactly
           Iv[e] = fmaf(occ_n2, cabs2(v[k]), kDpEps);
-          const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
-          v[k] = pscale(v[k], occ2_n * u);
-          pin(v[k]);
+          if constexpr (MODE == 1) {
+            (void)loss_point<QM, true>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+            (void)loss_point<2, false>(Iv[e], Mv[e], a.q2, a.eps2, S2, Ms2);
+          } else if constexpr (MODE == 2) {
+            const float u = fmaf(cc.x, loss_point<QM, true>(Iv[e], Mv[e], q, a.eps2, S, Ms),
+                                 cc.y * loss_point<2, false>(Iv[e], Mv[e], a.q2, a.eps2, S2, Ms2));
+            v[k] = pscale(v[k], occ2_n * u);
+            pin(v[k]);
+          } else {
+            const float u = loss_point<QM, SINGLE>(Iv[e], Mv[e], q, a.eps2, S, Ms);
+            v[k] = pscale(v[k], occ2_n * u);
+            pin(v[k]);
+          }
         }
         {
           const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
@@ -1534,10 +1548,40 @@ __global__ __launch_bounds__(256, 2) void k_fused3ms(F3Args a) {
         if (kq & 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    {
+    if constexpr (MODE == 1) {
+      // both terms' sums, then the next pattern's v (the prologue's arithmetic) and no adjoint
+      float v4[4] = {S, Ms, S2, Ms2};
+      block_sum4<4>(v4, s_red);
+      if (threadIdx.x == 0) {
+        float* ps = a.psums + (size_t)pat * kNSum;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ps[i] = v4[i];
+      }
+      const PatInfo pn = pat_info<SHIFT>(a, min(pat + 1, p1 - 1));
+      p_nxt = pn;
+      const int vpk = rf::opaque(8 * tid);
+      Ramp rp;
+      rp.init(pn.sy, pn.sx, gy, rf::opaque(tid) & 1);
+      pipeline<16>(
+          [&](auto C) {
+            Ch4x2 t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_fpk, vpk, 2048 * (4 * C + r));
+            return t;
+          },
+          [&](auto C, const Ch4x2& t) {
+            const float2 A = rp.a(C);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[4 * C + r] = SHIFT ? pcm(t.x[r], pcm(A, rp.B[r])) : t.x[r];
+              pin(v[4 * C + r]);
+            }
+          });
+      continue;
+    } else {
       float v2[2] = {S, Ms};
       block_sum4<2>(v2, s_red);
-      if (threadIdx.x == 0) {
+      if (MODE == 0 && threadIdx.x == 0) {
         float* ps = a.psums + (size_t)pat * kNSum;
         const int base = SINGLE ? 0 : 2;
         ps[base] = v2[0];

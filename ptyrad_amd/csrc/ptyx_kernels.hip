@@ -928,7 +928,12 @@ static void launch_fused3_both(const ptyx_plan* pl, const f3::F3Args& f, bool sh
   ProfScope ps(pl, kKFused, st);
   const dim3 gr(G), bl(256);
   const bool half = f.q == 0.5f;
-#define PTYX_F3B(SH, QM, MD) hipLaunchKernelGGL((f3::k_fused3<SH, true, QM, MD>), gr, bl, 0, st, f)
+  const bool ms = f.Nz > 1;   // k_fused3ms
+#define PTYX_F3B(SH, QM, MD)                                                               \
+  do {                                                                                     \
+    if (ms) hipLaunchKernelGGL((f3::k_fused3ms<SH, true, QM, MD>), gr, bl, 0, st, f);     \
+    else hipLaunchKernelGGL((f3::k_fused3<SH, true, QM, MD>), gr, bl, 0, st, f);          \
+  } while (0)
   if (mode == 1) {
     if (shift) { if (half) PTYX_F3B(true, 0, 1); else PTYX_F3B(true, 2, 1); }
     else { if (half) PTYX_F3B(false, 0, 1); else PTYX_F3B(false, 2, 1); }
@@ -949,7 +954,9 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   if (rc) return rc;
   const bool single = cfg->single_on != 0;
   const f3::F3Args f = register_args(pl, in, a, cfg, gz);
-  if (Nz > 1) {
+  if (cfg->single_on && cfg->poissn_on) {
+    launch_fused3_both(pl, f, a.shift, 1, G, st);
+  } else if (Nz > 1) {
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;
@@ -962,8 +969,6 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
       else if (single) hipLaunchKernelGGL((f3::k_fused3ms<false, true, 2>), gr, bl, 0, st, f);
       else hipLaunchKernelGGL((f3::k_fused3ms<false, false, 2>), gr, bl, 0, st, f);
     }
-  } else if (cfg->single_on && cfg->poissn_on) {
-    launch_fused3_both(pl, f, a.shift, 1, G, st);
   } else {
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
@@ -988,7 +993,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const bool sparse = cfg->sparse_on != 0;
   const int Nz = d.Nz;
   const bool single = cfg->single_on != 0;
-  const bool both = single && cfg->poissn_on && Nz == 1;   // k_fused3 MODE 1 / 2
+  const bool both = single && cfg->poissn_on;               // k_fused3 / k_fused3ms MODE 1 / 2
   const int ci = both ? 2 : single ? 0 : 1;                // (2: the kernel applies the coefficients)
   const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
   const int nseg = a.n_batches + G;
@@ -1625,10 +1630,11 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   // Nz ≥ 2); f32 DPs, one data term, slots and segment slabs large enough for the call (no
   // co-residency or max_batch condition: they never wait)
   const bool both_terms = cfg->single_on && cfg->poissn_on;
-  // (k_fused3 takes both data terms as two passes around k_finalize; k_fused3ms one term)
+  // (both data terms: two passes around k_finalize, MODE 1 / 2)
   const bool fused3 = any_grad && single_mode && pl->nwg3 > 0 && pl->d.N == 128 && !a.meas_f16 && slots_fit &&
                       (one_term || both_terms);
-  const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit && one_term;
+  const bool fused3ms = any_grad && !want_H && pl->ms3 && pl->nwg3 > 0 && !a.meas_f16 && slots_fit &&
+                        (one_term || both_terms);
   // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): either or both data terms (both: k_s3
   // twice, around k_finalize), call within capacity
   const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && (one_term || both_terms);
