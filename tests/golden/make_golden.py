@@ -352,6 +352,16 @@ if __name__ == "__main__":
         run_case("n192_p2o2z1_mixed", 192, 2, 2, 1, 3, 3, 4, seed=104, big=True)
         run_trajectory("traj_n96_p2_ga1", 96, 2, 1, 1, 3, 3, 3, 3, 1, seed=105)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--both-terms":
+        # loss_single + loss_poissn (+ loss_sparse) at the shapes of every engine that takes both
+        # terms in two passes around k_finalize: k_fused3, k_fused3ms, the mixed-state engine, stripe
+        both = json.loads(json.dumps(DEFAULT_LOSS))
+        both["loss_poissn"].update(state=True, weight=0.5, dp_pow=1.0, eps=1e-6)
+        run_case("n128_p1o1z1_both", 128, 1, 1, 1, 3, 3, 8, seed=121, loss_params=both)
+        run_case("n128_p1o1z3_both", 128, 1, 1, 3, 3, 3, 8, seed=122, loss_params=both)
+        run_case("n128_p3o1z2_both", 128, 3, 1, 2, 3, 3, 8, seed=123, loss_params=both)
+        run_case("n256_p2o2z1_both", 256, 2, 2, 1, 3, 3, 6, seed=124, loss_params=both, big=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--smooth":
         # every 2·3·5-smooth N in [32, 256] runs the general engine: odd N (45, 125), a radix-15
         # LDS plan (120), and the radix > 16 plans on 512-thread workgroups (125 = 25·5 in LDS,
