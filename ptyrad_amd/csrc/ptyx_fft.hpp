@@ -570,18 +570,18 @@ __device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float
 // TWO global round trips: stage 1 takes blocks of kLines rows through LDS (pre hook on the loads,
 // both Stockham passes of the row DFT in LDS, stored to the pair's b), stage 2 blocks of kLines
 // columns (128-B row segments in, both passes, post hook on the way out to a).
-template <int N>
+template <int N, int L = 32>
 struct LineTile {
-  static constexpr int kLines = 32;
+  static constexpr int kLines = L;
   static constexpr int kStride = N + N / 16;                 // one pad point per 16 (LdsArray's rule)
   static constexpr int kElems = kLines * kStride;
   __device__ __forceinline__ static int off(int line, int x) { return line * kStride + x + (x >> 4); }
 };
 
-// One in-place Stockham pass of radix R (span NS) along `lines` lines of a LineTile.
-template <int N, int NT, int R, int NS, int DIR>
+// One in-place Stockham pass of radix R (span NS) along `lines` lines of a LineTile<N, L>.
+template <int N, int NT, int R, int NS, int DIR, int LINES = 32>
 __device__ __forceinline__ void line_pass(float2* tile, const float2* tw, int lines) {
-  using LT = LineTile<N>;
+  using LT = LineTile<N, LINES>;
   constexpr int L = N / R;                 // butterflies per line
   constexpr int TWS = N / (NS * R);        // twiddle table stride
   constexpr int KB = (LT::kLines * L + NT - 1) / NT;

@@ -767,6 +767,69 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_probe_finalize(K
       });
 }
 
+// ------------------------------------------------------------ multi-workgroup probe transforms
+// The per-call probe spectrum F(P_p) and the probe-gradient inverse F⁻¹(G_p) as two launches of
+// N/kSpecLines workgroups per mode (rows, then columns, kSpecLines lines each through LDS) instead
+// of one workgroup per mode: a lone N² transform on one CU is latency-bound, and at the reference's
+// default cadence (one 32-pattern call per optimizer step) both sit on every step's critical path.
+constexpr int kSpecLines = 8;
+constexpr int kSpecThreads = 256;
+
+// rows of src (plane p at src + p·N²) → tmp, DIR transform, natural order
+template <int N, int DIR>
+__global__ __launch_bounds__(kSpecThreads) void k_lines_rows(const float2* src, float2* tmp, const float2* twg) {
+  using LT = LineTile<N, kSpecLines>;
+  using P1 = Plan1D<N>;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 T[LT::kElems];
+  const int l0 = blockIdx.x * kSpecLines, p = blockIdx.y;
+  const float2* s = src + (size_t)p * N * N;
+  float2* d = tmp + (size_t)p * N * N;
+  for (int i = threadIdx.x; i < N; i += kSpecThreads) s_tw[i] = twg[i];
+  const int nl = min(kSpecLines, N - l0);
+  for (int e = threadIdx.x; e < nl * N; e += kSpecThreads) T[LT::off(e / N, e % N)] = s[(size_t)(l0 + e / N) * N + e % N];
+  __syncthreads();
+  line_pass<N, kSpecThreads, P1::R1, 1, DIR, kSpecLines>(T, s_tw, nl);
+  line_pass<N, kSpecThreads, P1::R2, P1::R1, DIR, kSpecLines>(T, s_tw, nl);
+  for (int e = threadIdx.x; e < nl * N; e += kSpecThreads) d[(size_t)(l0 + e / N) * N + e % N] = T[LT::off(e / N, e % N)];
+}
+
+// columns of tmp, DIR transform; KIND 0: the probe spectrum — Fp natural, plus the K-packed copy
+// of the register engines at N = 128 (k_probe_spectrum's fpk layout); KIND 1: d_probe += v / N²
+template <int N, int DIR, int KIND>
+__global__ __launch_bounds__(kSpecThreads) void k_lines_cols(const float2* tmp, float2* out, float2* fpk,
+                                                             const float2* twg) {
+  using LT = LineTile<N, kSpecLines>;
+  using P1 = Plan1D<N>;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 T[LT::kElems];
+  const int c0 = blockIdx.x * kSpecLines, p = blockIdx.y;
+  const float2* s = tmp + (size_t)p * N * N;
+  for (int i = threadIdx.x; i < N; i += kSpecThreads) s_tw[i] = twg[i];
+  const int nc = min(kSpecLines, N - c0);
+  for (int e = threadIdx.x; e < nc * N; e += kSpecThreads) {
+    const int y = e / nc, c = e % nc;
+    T[LT::off(c, y)] = s[(size_t)y * N + c0 + c];
+  }
+  __syncthreads();
+  line_pass<N, kSpecThreads, P1::R1, 1, DIR, kSpecLines>(T, s_tw, nc);
+  line_pass<N, kSpecThreads, P1::R2, P1::R1, DIR, kSpecLines>(T, s_tw, nc);
+  constexpr float inv_n2 = 1.0f / (float)(N * N);
+  for (int e = threadIdx.x; e < nc * N; e += kSpecThreads) {
+    const int y = e / nc, c = e % nc, x = c0 + c;
+    const float2 v = T[LT::off(c, y)];
+    if constexpr (KIND == 0) {
+      out[(size_t)p * N * N + y * N + x] = v;
+      if constexpr (N == 128) {
+        if (fpk) fpk[(size_t)p * N * N + (x & 63) * 256 + ((x >> 6) | ((y & 31) << 1) | ((y >> 5) << 6))] = v;
+      }
+    } else {
+      float2* dp = out + (size_t)p * N * N + y * N + x;
+      *dp = cadd(*dp, cscale(v, inv_n2));
+    }
+  }
+}
+
 #include "ptyx_single.hpp"
 
 // ------------------------------------------------------------------- per-N launchers
@@ -812,6 +875,19 @@ struct GenLaunch {
   static void probe_finalize(const KArgs& a, int nblk, const float2* G, float2* d_probe, hipStream_t st) {
     hipLaunchKernelGGL(k_probe_finalize<N>, dim3(nblk), dim3(NT), 0, st, a, G, d_probe);
   }
+  // the two-launch forms (k_lines_rows / k_lines_cols), tmp: P·N² float2 of scratch
+  static void spectrum_lines(const float2* probe, int P, float2* Fp, float2* fpk, float2* tmp, const float2* twg,
+                             hipStream_t st) {
+    const dim3 gr((N + kSpecLines - 1) / kSpecLines, P), bl(kSpecThreads);
+    hipLaunchKernelGGL((k_lines_rows<N, -1>), gr, bl, 0, st, probe, tmp, twg);
+    hipLaunchKernelGGL((k_lines_cols<N, -1, 0>), gr, bl, 0, st, tmp, Fp, fpk, twg);
+  }
+  static void probe_finalize_lines(const float2* G, int P, float2* d_probe, float2* tmp, const float2* twg,
+                                   hipStream_t st) {
+    const dim3 gr((N + kSpecLines - 1) / kSpecLines, P), bl(kSpecThreads);
+    hipLaunchKernelGGL((k_lines_rows<N, +1>), gr, bl, 0, st, G, tmp, twg);
+    hipLaunchKernelGGL((k_lines_cols<N, +1, 1>), gr, bl, 0, st, tmp, d_probe, nullptr, twg);
+  }
   // LDS-limited residency (160 KiB per CU, 2048 threads) of the workgroup-resident FFT kernels
   static constexpr int blocks_per_cu() {
     constexpr int lds = (int)sizeof(float2) * (5 * N + kFieldLds<N, Geo<N>::kLds>) + 256;
@@ -819,7 +895,8 @@ struct GenLaunch {
     return by_lds < by_threads ? by_lds : by_threads;
   }
   static const GenOps* ops() {
-    static const GenOps o{N, NT, Geo<N>::kLds, blocks_per_cu(), &spectrum, &forward, &modesum, &adjoint, &probe_finalize};
+    static const GenOps o{N, NT, Geo<N>::kLds, blocks_per_cu(), &spectrum, &forward, &modesum, &adjoint, &probe_finalize,
+                          &spectrum_lines, &probe_finalize_lines};
     return &o;
   }
 };

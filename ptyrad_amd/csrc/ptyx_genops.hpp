@@ -23,6 +23,12 @@ struct GenOps {
   void (*modesum)(const KArgs& a, hipStream_t st);
   void (*adjoint)(const KArgs& a, int grid, bool one_mode, bool single, bool ext, hipStream_t st);
   void (*probe_finalize)(const KArgs& a, int nblk, const float2* G, float2* d_probe, hipStream_t st);
+  // two-launch row / column forms (N/8 workgroups a mode each; tmp: P·N² float2 of scratch):
+  // F(P) → Fp (+ the N = 128 K-packed fpk), and d_probe += F⁻¹(G)/N² (no probe shift: not used)
+  void (*spectrum_lines)(const float2* probe, int P, float2* Fp, float2* fpk, float2* tmp, const float2* twg,
+                         hipStream_t st);
+  void (*probe_finalize_lines)(const float2* G, int P, float2* d_probe, float2* tmp, const float2* twg,
+                               hipStream_t st);
 };
 
 // registry (ptyx_kernels.hip): gen_register is called from the size groups' static initialisers

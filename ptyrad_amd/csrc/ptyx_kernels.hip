@@ -781,6 +781,16 @@ static void launch_probe_fin(const ptyx_plan* pl, const KArgs& a, hipStream_t st
   ProfScope ps(pl, kKProbeFinalize, st);
   pl->gen->probe_finalize(a, np, pl->Gsum, reinterpret_cast<float2*>(d_probe), st);
 }
+// The register engines' form: with shifted probes the inverse transform as two multi-workgroup
+// launches (k_lines_rows / k_lines_cols; the general engine's slab as scratch, unused by them)
+static void launch_probe_fin_reg(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe, int np) {
+  if (!a.shift) {
+    launch_probe_fin(pl, a, st, d_probe, np);
+    return;
+  }
+  ProfScope ps(pl, kKProbeFinalize, st);
+  pl->gen->probe_finalize_lines(pl->Gsum, np, reinterpret_cast<float2*>(d_probe), pl->slab, pl->twg, st);
+}
 static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream_t st, float* d_probe,
                                   int n_slabs) {
   const long long per = (long long)pl->d.P * pl->d.N * pl->d.N;
@@ -825,10 +835,9 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
   const int Nz = d.Nz;
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
   if (reuse) {
-  } else if (a.shift) {
-    KArgs b = a;
-    b.fpk = pl->fpk;   // F(P_p) packed by the spectrum kernel itself
-    launch_spectrum(pl, b, st);
+  } else if (a.shift) {   // F(P_p), natural and K-packed: rows then columns, N/8 workgroups a mode each
+    ProfScope ps(pl, kKSpectrum, st);
+    pl->gen->spectrum_lines(a.probe, d.P, pl->Fp, pl->fpk, pl->Gsum, pl->twg, st);
   } else {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256, d.P), dim3(256), 0, st,
@@ -1067,7 +1076,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
         hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
                            out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts);
     }
-    if (gz.d_probe) launch_probe_fin(pl, a, st, gz.d_probe, 1);
+    if (gz.d_probe) launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
     return launch_status("probe finalize launch");
   }
   if (d_shifts) {
@@ -1085,7 +1094,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
       else
         hipLaunchKernelGGL(f3::k_segslab_final<false>, dim3(N2 / 256), dim3(256), 0, st, pl->segpart, pl->Gsum);
     }
-    launch_probe_fin(pl, a, st, gz.d_probe, 1);
+    launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
   }
   if ((rc = launch_status("probe finalize launch"))) return rc;
   return PTYX_OK;
@@ -1204,7 +1213,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
         hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
                            a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts);
     }
-    if (gz.d_probe) launch_probe_fin(pl, a, st, gz.d_probe, P);
+    if (gz.d_probe) launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
     return launch_status("k_fmm probe / position reduction launch");
   }
   if (d_shifts) {
@@ -1222,7 +1231,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
       else
         hipLaunchKernelGGL(f3::k_segslab_final<false>, dim3(N2 / 256, P), dim3(256), 0, st, pl->segpart, pl->Gsum);
     }
-    launch_probe_fin(pl, a, st, gz.d_probe, P);
+    launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
   }
   return launch_status("k_fmm probe / position reduction launch");
 }
