@@ -124,12 +124,11 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
     acc[r] = make_float2(0.f, 0.f);
     cnt[r] = 0.f;
   }
-  // scan: wave w of split s takes the 64-pattern chunks s + S·(w + GW·k); bins: candidate
-  // i = s + S·(w + GW·(lane + 64·k)) (a tile's few candidates spread over all its waves and splits)
-  const bool bins = ga.boff != nullptr;
-  const int first = bins ? s + S * wave : (s + S * wave) * 64;
+  // scan: candidate i = s + S·(w + GW·(lane + 64·k)) of the bins' list (or of the call's patterns,
+  // small calls): a tile's candidates spread over all its waves and splits
+  const int first = s + S * wave;
   for (int base = first; base < total; base += 64 * GW * S) {
-    const int i = bins ? base + S * GW * lane : base + lane;
+    const int i = base + S * GW * lane;
     int j = i;
     int2 o = make_int2(-(1 << 29), -(1 << 29));
     float2 cj = make_float2(0.f, 0.f);
