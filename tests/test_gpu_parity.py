@@ -304,6 +304,40 @@ def test_general_engine_maximum_modes_vs_oracle(N, P, O, Nz, shift, both):
     _general_engine_case(N, P, O, Nz, shift, both)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_random_configuration_vs_oracle(seed, monkeypatch):
+    """Seeded random (N, P, O, Nz, shifted probes, one or both data terms, far-field cache on /
+    off, ragged mini-batches) through whichever engine the plan picks, vs the oracle — the
+    combinations no hand-written case lists (tools/check_sweep.py runs the long form)."""
+    device = dev()
+    from ptyrad_amd import synthetic as syn
+    rng = np.random.default_rng(1000 + seed)
+    N = int(rng.choice([32, 48, 64, 96, 128, 160, 256]))
+    P, O = int(rng.integers(1, 4)), int(rng.integers(1, 3))
+    Nz = int(rng.integers(1, 4)) if N <= 128 else int(rng.integers(1, 3))
+    shift, both, cache = (bool(rng.integers(0, 2)) for _ in range(3))
+    if not cache:
+        monkeypatch.setenv("PTYX_FFC_MB", "0")
+    pr = syn.random_problem(N, 3, 3, P=P, O=O, Nz=Nz, seed=int(rng.integers(0, 1 << 30)))
+    lp = orc_default_loss()
+    lp["loss_poissn"]["state"] = both
+    d = dict(obja=pr.obja, objp=(pr.objp / Nz).astype(np.float32), probe=pr.probe * np.float32(30.0),
+             shifts=pr.shifts, crop_pos=pr.crop_pos, H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=shift,
+             loss_params=lp)
+    perm = rng.permutation(9)
+    cut = sorted(set([0, 9] + [int(c) for c in rng.integers(1, 9, 2)]))
+    batches = [perm[a:b] for a, b in zip(cut[:-1], cut[1:])]
+    terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5)
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, lp, shift_probes=shift, grad_scale=0.5)
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-6)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < (TOL_G_BOTH if both and k == "probe" else TOL_G), k
+    if shift:
+        assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
 def test_unsupported_n_is_refused():
     """N with a prime factor other than 2, 3, 5 (98 = 2·7², 112 = 16·7), or outside [32, 256], is
     refused with PTYX_EUNSUPPORTED at plan creation, not run."""
