@@ -287,7 +287,7 @@ __global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_forward(KArgs a)
     // split: this job's mode intensity Σ_o occ|Ψ_{p,o}|² in its own plane (k_forward_modesum adds)
     float* Ip = SINGLE ? nullptr : (PS > 1 ? a.Imodes + ((size_t)pat * PS + pbeg) * N2 : a.Ibuf + (size_t)pat * N2);
     float2* psi0 = scratch_psi<N>(a);   // this workgroup's ψ⁰ park (multi-object-mode calls)
-    float2* cache = (!SINGLE && a.ffc) ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
+    float2* cache = a.ffc ? a.ffc + (size_t)pat * a.ffc_per : nullptr;
     for (int p = pbeg; p < pend; ++p) {
       for (int o = 0; o < a.O; ++o) {
         const bool sparse = want_sums && a.sparse_on && p == 0;

@@ -247,7 +247,7 @@ struct ptyx_plan {
   float2* slab = nullptr;
   float2* Gsum = nullptr;
   float2* hslab = nullptr;    // PTYX_PROP_GRAD: per-workgroup dL/dH slabs
-  float2* ffc = nullptr;      // far-field cache (general engine, P·O > 1)
+  float2* ffc = nullptr;      // far-field cache (general engine: P·O > 1, N > 128 or Nz > 1)
   long long ffc_per = 0, ffc_cap = 0;
   float2* scratch = nullptr;
   // register engines (k_fused3 / k_fused3ms): per-pattern object-gradient slots
@@ -531,7 +531,11 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       }
     }
   }
-  if (d.P * d.O > 1) {
+  // (one probe and object mode: the global-scratch general engine (N > 128) and the multislice one
+  // (Nz > 1) cache too, so k_adjoint reads the far field and the ψⁿ instead of recomputing the
+  // forward; N = 128 single-mode calls run on the register engines)
+  const bool ffc_single = d.P * d.O == 1 && d.N != 128 && (d.N > 128 || d.Nz > 1);
+  if (d.P * d.O > 1 || ffc_single) {
     // far-field cache: per pattern of a call the P·O far fields plus ψ⁰ of every probe mode (Nz = 1)
     // or every slice's ψⁿ of every (p, o) (Nz > 1) — (P·O + P)·N² or P·O·(1 + Nz)·N² float2 —
     // within PTYX_FFC_MB (default the smaller of 64 GiB and a third of the free HBM); calls beyond
