@@ -82,7 +82,7 @@ def test_generic_autograd_path_matches_reference():
     dp = model(d["batch"])
     total, terms = loss_fn(dp, model.get_measurements(d["batch"]), model._current_object_patches, model.omode_occu)
     total.backward()
-    np.testing.assert_allclose([float(t) for t in terms], d["loss_terms"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose([float(t.detach()) if torch.is_tensor(t) else float(t) for t in terms], d["loss_terms"], rtol=2e-5, atol=1e-7)
     assert rel(model.opt_obja.grad.cpu().numpy(), d["g_obja"]) < 5e-5
     assert rel(model.opt_objp.grad.cpu().numpy(), d["g_objp"]) < 5e-5
     gp = model.opt_probe.grad.cpu().numpy()
