@@ -19,11 +19,15 @@ constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
 
 // Launch geometry of the general engine's workgroup-resident FFT kernels.
 //  N ≤ 128: the N×N wave in LDS (in place, ≤ 136 KiB), NT = 8·N threads (≤ 1024).
-//  N > 128: the per-workgroup global scratch pair (four Stockham passes a 2-D FFT), 1024 threads.
-//  512 threads whenever a radix above 16 holds up to 27 points a thread (125, 162, 200, 216,
-//  243, 250: 256 VGPRs, no spills); N = 256 has its own two-stage
-//  path with two 512-thread workgroups a CU (LDS ≈ 78 KiB each).
-// kWaves: minimum waves per SIMD the kernels are compiled for (≤ 512 / kWaves VGPRs).
+//  N > 128: the per-workgroup global scratch pair (two line-block round trips a 2-D FFT), 1024
+//  threads.  512 threads whenever a radix above 16 holds up to 27 points a thread (125, 162, 200,
+//  216, 243, 250: 256 VGPRs, no spills); N = 256 has its own two-stage path with two 512-thread
+//  workgroups a CU (LDS ≈ 78 KiB each).
+// kWaves: minimum waves per SIMD the kernels are compiled for (≤ 512 / kWaves VGPRs): enough for
+// every workgroup LDS and threads allow on a CU to be resident at once (capped at 8 = 64 VGPRs).
+// Measured (profiles/r04/occ/): N 135-240 +12-21 %, 45 / 60 / 75 / 81 / 90 +11-32 %, no size
+// slower by more than 1.5 %; the floor of waves / 4 instead of rounding a workgroup's waves up per
+// SIMD made N 80 16 % slower (two workgroups still did not fit, so the cap only added spills).
 template <int N>
 struct Geo {
   static constexpr bool kLds = N <= 128;
@@ -31,7 +35,11 @@ struct Geo {
                           : Plan1D<N>::R1 > 16 ? 512
                           : kLds ? ((8 * N + 63) / 64 * 64 > 1024 ? 1024 : (8 * N + 63) / 64 * 64)
                           : 1024;
-  static constexpr int kWaves = N == 256 ? 4 : 1;
+  // workgroups a CU holds by LDS and threads (as GenLaunch::blocks_per_cu)
+  static constexpr int kLdsBytes = (int)sizeof(float2) * (5 * N + kFieldLds<N, kLds>) + 256;
+  static constexpr int kResident = (160 * 1024 / kLdsBytes) < (2048 / NT) ? (160 * 1024 / kLdsBytes) : (2048 / NT);
+  static constexpr int kWavesRes = kResident * ((NT + 255) / 256);   // a workgroup's waves round up per SIMD
+  static constexpr int kWaves = N == 256 ? 4 : Plan1D<N>::R1 > 16 ? 1 : kWavesRes > 8 ? 8 : kWavesRes;
 };
 
 struct KArgs {

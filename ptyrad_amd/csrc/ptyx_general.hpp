@@ -889,11 +889,7 @@ struct GenLaunch {
     hipLaunchKernelGGL((k_lines_cols<N, +1, 1>), gr, bl, 0, st, tmp, d_probe, nullptr, twg);
   }
   // LDS-limited residency (160 KiB per CU, 2048 threads) of the workgroup-resident FFT kernels
-  static constexpr int blocks_per_cu() {
-    constexpr int lds = (int)sizeof(float2) * (5 * N + kFieldLds<N, Geo<N>::kLds>) + 256;
-    constexpr int by_lds = 160 * 1024 / lds, by_threads = 2048 / NT;
-    return by_lds < by_threads ? by_lds : by_threads;
-  }
+  static constexpr int blocks_per_cu() { return Geo<N>::kResident; }
   static const GenOps* ops() {
     static const GenOps o{N, NT, Geo<N>::kLds, blocks_per_cu(), &spectrum, &forward, &modesum, &adjoint, &probe_finalize,
                           &spectrum_lines, &probe_finalize_lines};
