@@ -94,7 +94,7 @@ __device__ __forceinline__ void prefetch_spectrum(const KArgs& a, int tid,
 
 // Forward + per-pattern loss partial sums (SUMS) and/or dp_out.
 template <int N, bool SHIFT, bool SUMS>
-__global__ __launch_bounds__(Geo<N>::NT) void k_forward1(KArgs a) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_forward1(KArgs a) {
   constexpr int NT = Geo<N>::NT;
   constexpr int N2 = N * N;
   using PM = PassMap<N, NT>;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(Geo<N>::NT) void k_forward1(KArgs a) {
 
 // Adjoint (EXT: dL/dI from the caller).
 template <int N, bool SHIFT, bool EXT>
-__global__ __launch_bounds__(Geo<N>::NT) void k_adjoint1(KArgs a) {
+__global__ __launch_bounds__(Geo<N>::NT, Geo<N>::kWaves) void k_adjoint1(KArgs a) {
   constexpr int NT = Geo<N>::NT;
   constexpr int N2 = N * N;
   using PM = PassMap<N, NT>;
