@@ -98,7 +98,7 @@ def test_generic_path_with_stages_matches_reference(path):
     assert rel(dp.detach().cpu().numpy(), d["dp"]) < 1e-5
     total, terms = loss_fn(dp, model.get_measurements(d["batch"]), model._current_object_patches, model.omode_occu)
     total.backward()
-    np.testing.assert_allclose([float(t) for t in terms], d["loss_terms"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose([float(t.detach()) if torch.is_tensor(t) else float(t) for t in terms], d["loss_terms"], rtol=2e-5, atol=1e-7)
     _check_grads(model, d)
 
 
