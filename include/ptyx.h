@@ -353,10 +353,11 @@ int ptyx_adam_step(void *stream, int32_t n, float *const *params, const float *c
                    float *const *exp_avg_sqs, const float *const *steps, const int64_t *numels, const double *lrs,
                    double beta1, double beta2, double eps, double weight_decay, int32_t flags);
 
-/* Patterns one ptyx_forward_loss_grad call may hold and still run on the register-resident
- * engines (k_fused3 / k_fused3ms: slot capacity); larger calls take the general engine.
- * 0 when the plan's geometry has no register engine.  Callers with host-side batch offsets
- * split larger calls at mini-batch boundaries (gradients accumulate). */
+/* Patterns one ptyx_forward_loss_grad call may hold and still run on the plan's fast engine:
+ * the register-resident engines' slot capacity (k_fused3 / k_fused3ms / mixed-state), the stripe
+ * engine's call size, else the general engine's far-field cache capacity (calls beyond it
+ * recompute the forward in k_adjoint).  0 when the plan keeps none of these.  Callers with
+ * host-side batch offsets split larger calls at mini-batch boundaries (gradients accumulate). */
 int64_t ptyx_plan_register_capacity(const ptyx_plan *plan);
 
 /* Engine-variant selection for tests and A/B measurements (no environment variable changes an
