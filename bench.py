@@ -21,6 +21,9 @@ Other workloads (--config; all one process per GPU, same step structure):
   c5         N=256, P=4, fp16 DP storage: a resident sub-stripe (--patterns positions) of each
              rank's shard of the 4096² scan (the full shard is 275 GB of DPs per GPU)
 
+  --cadence reference  recon_step at grad_accumulation = 1 (the reference's default cadence), c2 scan,
+             mini-batches split over the ranks, graph-replayed steps with captured RCCL collectives
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
        torchrun --nproc-per-node N bench.py --gpus N ...   (driver, one rank per GPU, RCCL)
 """
@@ -60,9 +63,13 @@ def parse():
                     help="data term(s) beside loss_sparse (both: the stripe engine runs k_s3 twice around "
                          "k_finalize, the N = 128 mixed-state engine applies both coefficients in k_fmm_adj; "
                          "k_fused3 / k_fused3ms calls run the general engine)")
-    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "band"],
+    ap.add_argument("--exchange", default="auto", choices=["auto", "allreduce", "band"],
                     help="N > 1: object gradients by one flat all-reduce, or by row band (ObjectBands: halo "
-                         "rows to their owners, Adam on the owned band, bands all-gathered)")
+                         "rows to their owners, Adam on the owned band, updated halo rows back to their "
+                         "readers; no all-gather); auto (default) = band when the ranks' touched object rows "
+                         "line up by rank within a window (every weak-scaling config), as recon_step's "
+                         "DistContext decides.  With --geom-world W the band bytes of rank --geom-rank are "
+                         "computed from the W ranks' geometry (no collective)")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--geom-world", type=int, default=0,
                     help="diagnostic (c2): build rank --geom-rank's shard of a W-GPU weak-scaling geometry on one GPU "
@@ -70,6 +77,14 @@ def parse():
     ap.add_argument("--geom-rank", type=int, default=0)
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="engine variant for A/B runs (ptyx_set_tuning, include/ptyx.h); recorded in the output")
+    ap.add_argument("--cadence", default="iteration", choices=["iteration", "reference"],
+                    help="iteration: one optimizer step per pass over the shard (default, the headline); "
+                         "reference: recon_step at grad_accumulation = 1 (the reference's default cadence) on "
+                         "the c2 scan, every mini-batch split over the ranks, graph-replayed steps with their "
+                         "RCCL collectives captured; one bench step = one recon_step iteration")
+    ap.add_argument("--always-reduce", action="store_true",
+                    help="--cadence reference at one GPU: init RCCL anyway and run every collective of the "
+                         "multi-rank step (split mini-batches), as an 8-GPU job would")
     return ap.parse_args()
 
 
@@ -160,6 +175,121 @@ def gt_object(shape, dev, seed=1):
     return torch.ones_like(phase), phase
 
 
+def reference_cadence(a, world, rank, local, cpu):
+    """--cadence reference: what a PtyRAD user's multi-GPU job runs.  recon_step
+    (reconstruction.py:658-781) at the reference's default grad_accumulation = 1
+    (params/recon_params.py:17) on the c2 geometry: the 256x256 scan, make_batches 'random' with 32
+    positions a mini-batch (identical on every rank), every mini-batch split over the ranks
+    (accelerate's split_batches, utils/common.py:63 — the global mini-batch stays 32, so this is
+    strong scaling), each rank holding only its parts' DPs, hipGraph-replayed optimizer steps with
+    the loss-sum and gradient RCCL all-reduces captured inside them, the HIP Adam.  One bench step
+    = one recon_step iteration = 2,048 optimizer steps over all 65,536 positions."""
+    import torch
+    import torch.distributed as dist
+    from ptyrad_amd import synthetic as syn
+    from ptyrad_amd.engine import Plan
+    from ptyrad_amd.losses import CombinedLoss
+    from ptyrad_amd.models import PtychoHIP
+    from ptyrad_amd.reconstruction import DistContext, create_optimizer, make_batches, recon_step
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1 or a.always_reduce:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    ctx = DistContext(split_batches=True if a.always_reduce else None, always_reduce=a.always_reduce)
+    N = 128
+    crop_pos, shifts, (Ny, Nx), _, _ = syn.bench_geometry("c2", 1, 0, scan=a.scan)
+    n = crop_pos.shape[0]
+    lrs = {"obja": 5e-4, "objp": 5e-4, "obj_tilts": 0.0, "slice_thickness": 0.0, "probe": 1e-4,
+           "probe_pos_shifts": 1e-4}
+    lp = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+          "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+          "loss_pacbed": {"state": False, "weight": 0.5, "dp_pow": 0.2},
+          "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1}, "loss_simlar": {"state": False}}
+    probe = syn.stem_probe(N) * np.float32(60.0)
+    H = syn.fresnel_propagator(N, syn.DX_ANG, 2.0)
+    # DPs: the engine's forward model of the ground-truth object (as the default cadence)
+    plan = Plan(N, 1, 1, 1, Ny, Nx, n, n, shift_probes=True, device=dev)
+    gta, gtp = gt_object((1, 1, Ny, Nx), dev)
+    t = {"obja": gta, "objp": gtp, "probe": torch.view_as_real(torch.tensor(probe[None], device=dev)).contiguous(),
+         "shifts": torch.tensor(shifts, device=dev), "H": torch.tensor(H, device=dev),
+         "occu": torch.ones(1, device=dev), "crop_pos": torch.tensor(crop_pos, device=dev)}
+    meas = torch.empty((n, N, N), dtype=torch.float32, device=dev)
+    plan.forward(t, np.arange(n, dtype=np.int32), dp_out=meas)
+    del gta, gtp, t, plan
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    iv = {"obja": np.ones((1, 1, Ny, Nx), np.float32),
+          "objp": (1e-8 * torch.rand((1, 1, Ny, Nx), generator=g, device=dev)).cpu().numpy(), "obj": None,
+          "probe": probe[None], "probe_pos_shifts": shifts, "omode_occu": np.ones(1, np.float32), "H": H,
+          "crop_pos": crop_pos, "N_scan_slow": int(round(math.sqrt(n))), "N_scan_fast": int(round(math.sqrt(n))),
+          "slice_thickness": 2.0, "dx": syn.DX_ANG, "dk": 1.0 / (N * syn.DX_ANG),
+          "lambd": syn.electron_wavelength(syn.KV), "obj_tilts": np.zeros((1, 2), np.float32)}
+    mp_ = {"detector_blur_std": None, "obj_preblur_std": None,
+           "update_params": {k: {"start_iter": 1 if v else None, "lr": v} for k, v in lrs.items()},
+           "optimizer_params": {"name": "Adam", "configs": {}, "load_state": None}}
+    batches = make_batches(np.arange(n), crop_pos, a.batch, mode="random", verbose=False,
+                           rng=np.random.default_rng(3))
+    loss_fn = CombinedLoss(lp, device=dev)
+    mi = ctx.local_indices(batches, 1, loss_fn=loss_fn, model_params=mp_, init_variables=iv)
+    iv["measurements"] = meas[torch.as_tensor(mi, device=dev)].contiguous()
+    iv["measurements_index"] = mi
+    del meas
+    model = PtychoHIP(iv, mp_, device=dev, verbose=False)
+    opt = create_optimizer(model.optimizer_params, model.optimizable_params)
+    it = 0
+    for _ in range(a.warmup):
+        it += 1
+        recon_step(batches, 1, model, opt, loss_fn, None, it, verbose=False, dist_ctx=ctx)
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        it += 1
+        recon_step(batches, 1, model, opt, loss_fn, None, it, verbose=False, dist_ctx=ctx)
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    sg = getattr(model, "_step_graphs", None)
+    n_steps = len(batches)
+    last = float(model.loss_iters[-1][1])
+    assert math.isfinite(last), "non-finite loss"
+    out = {
+        "metric": "diffraction-patterns/sec/iter (fwd+bwd), 256x256 probe positions, 128x128 DP",
+        "value": round(n * a.steps / elapsed, 1), "unit": "patterns/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: DPs = engine forward model of a ground-truth atom-lattice object; recon init exp(1e-8 iU)",
+        "config": {"workload": f"c2 scan {int(round(math.sqrt(n)))}^2 at the reference's default cadence: recon_step, "
+                               f"grad_accumulation = 1, mini-batches of {a.batch} ('random') split over the ranks, "
+                               "loss_single(q=0.5)+loss_sparse(L1), HIP Adam; one bench step = one iteration",
+                   "cadence": "reference", "N": N, "P": 1, "O": 1, "Nz": 1, "mini_batch": a.batch,
+                   "optimizer_steps_per_iteration": n_steps, "object": [Ny, Nx],
+                   "parallelism": f"dp{world} (split mini-batches; RCCL loss-sum + gradient all-reduce per "
+                                  f"optimizer step{', forced at world size 1' if a.always_reduce and world == 1 else ''})"},
+        "ms_per_optimizer_step": round(1e3 * elapsed / a.steps / n_steps, 4),
+        "graphs": {"captures": sg.captures, "replays": sg.replays, "eager": sg.eager} if sg else None,
+        "loss_last_iteration": last,
+        "roofline": None,
+        "roofline_note": "32-pattern optimizer steps are launch / latency bound; the kernel roofline is the "
+                         "default (--cadence iteration) line's",
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     cfg = CONFIGS[a.config]
@@ -172,6 +302,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(128, a.batch, a.cpu_sample)          # before the GPU is touched
+    if a.cadence == "reference":
+        if a.config != "c2":
+            raise SystemExit("--cadence reference runs the c2 geometry")
+        return reference_cadence(a, world, rank, local, cpu)
 
     import torch
     import torch.distributed as dist
@@ -258,18 +392,42 @@ def main():
     opt = create_optimizer({"name": "Adam", "configs": {}}, [{"params": [t[k]], "lr": lr} for k, lr in lrs.items()])
     bands = None
     n_obj = t["obja"].numel() + t["objp"].numel()
-    if world > 1 and a.exchange == "band":
+    row_b = t["obja"].shape[0] * t["obja"].shape[1] * Nx * 4 * 2      # one object row, amplitude + phase
+    exchange = a.exchange
+    if world > 1 and exchange != "allreduce":
+        from ptyrad_amd.reconstruction import ObjectBands, exchange_ranges
+        rows = exchange_ranges(ctx, int(crop_pos[:, 0].min()), int(crop_pos[:, 0].max()) + N, dev)
+        if exchange == "band" or ObjectBands.disjoint(rows, Ny, world, N):
+            exchange = "band"
+            bands = ObjectBands(ctx, Ny, dev, rows)
+            objs = [t["obja"], t["objp"]]
+        else:
+            exchange = "allreduce"
+    # bytes each rank sends per step in the exchange (ring all-reduce: 2(W-1)/W of the buffer; band:
+    # its touched rows outside its band to their owners + its band rows others read back to them,
+    # + the ring all-reduce of the probe part)
+    W_x = gw if a.geom_world else world
+    xb = bands
+    if a.geom_world and W_x > 1 and exchange != "allreduce":
+        # --geom-world: the W ranks' touched rows from the geometry alone
         from ptyrad_amd.reconstruction import ObjectBands
-        bands = ObjectBands(ctx, Ny, dev)
-        bands.set_rows(int(crop_pos[:, 0].min()), int(crop_pos[:, 0].max()) + N)
-        objs = [t["obja"], t["objp"]]
-    # bytes each rank sends per step in the exchange (ring all-reduce / all-gather: (W-1)/W per pass)
-    if bands is None:
-        xbytes = 2 * (world - 1) / world * flat.numel() * 4 if world > 1 else 0
+
+        class _Ctx:
+            rank, world, group = gr, gw, None
+        rows = []
+        for r_ in range(gw):
+            cp_ = syn.bench_geometry(a.config, gw, r_, a.patterns, a.scan)[0]
+            rows.append((int(cp_[:, 0].min()), int(cp_[:, 0].max()) + N))
+        if exchange == "band" or ObjectBands.disjoint(rows, Ny, gw, N):
+            exchange = "band"
+            xb = ObjectBands(_Ctx(), Ny, "cpu", rows)
+        else:
+            exchange = "allreduce"
+    if xb is not None:
+        xbytes = ((xb.sent_rows() + xb.halo_rows()) * row_b +
+                  2 * (W_x - 1) / W_x * (flat.numel() - n_obj) * 4)
     else:
-        row_b = t["obja"].shape[0] * t["obja"].shape[1] * Nx * 4
-        xbytes = (2 * bands.sent_rows() * row_b + (world - 1) / world * n_obj * 4 +
-                  2 * (world - 1) / world * (flat.numel() - n_obj) * 4)
+        xbytes = 2 * (W_x - 1) / W_x * flat.numel() * 4 if W_x > 1 else 0
 
     def step(timed=False):
         flat.zero_()
@@ -300,7 +458,7 @@ def main():
             if timed:
                 e2 = torch.cuda.Event(enable_timing=True)
                 e2.record(stream)
-            bands.gather(objs)
+            bands.halo(objs)                                  # updated rows back to their readers
             if timed:
                 e3 = torch.cuda.Event(enable_timing=True)
                 e3.record(stream)
@@ -408,7 +566,8 @@ def main():
                    **({"geometry_only": f"rank {gr} of a {gw}-GPU scan, no collective"} if a.geom_world else {})},
         "roofline": roof,
         "per_rank_ms": {"engine": round(engine_max, 3), "allreduce": round(ar_max, 3),
-                        "allreduce_bytes": int(flat.numel() * 4), "exchange": a.exchange if world > 1 else None,
+                        "allreduce_bytes": int(flat.numel() * 4),
+                        "exchange": exchange if (world > 1 or a.geom_world) else None,
                         "exchange_bytes_sent_per_rank": int(xbytes)},
         "fft_tflops": round(value / world * f_alg / 1e12, 2) if cfg["mode"] != "strong" else
         round(value * f_alg / 1e12 / world, 2),

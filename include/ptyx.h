@@ -328,6 +328,40 @@ int ptyx_meas_stats(void *stream, const float *raw, int64_t n, int32_t H, int32_
 int ptyx_meas_finish(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
                      const double *stats, void *ws, void *dst, int32_t dst_f16);
 
+/* The mean diffraction pattern of the processed (normalised) stack, mean (Ho,Wo) f64, from the
+ * complete stats alone (no pass over the frames): the meas.mean(0) that _meas_pad fits its
+ * background to (initialization.py:987).  ws as for ptyx_meas_finish. */
+int ptyx_meas_mean(void *stream, int32_t H, int32_t W, const ptyx_meas_proc *p, const double *stats, void *ws,
+                   double *mean);
+
+/* The reference's f32 mean pattern of the stack after the negative-value rule (normalized = 0),
+ * or after normalisation by p's constant (normalized = 1): numpy's meas.mean(0), i.e. a
+ * sequential f32 sum over the frames in order, then / n, bit for bit.  mean (Ho,Wo) f32.  The
+ * single-rank ingest takes the normalisation constant (max / mean / sum of the first) and
+ * meas_pad's fit input (the second) from it; stats as for ptyx_meas_finish (the min). */
+int ptyx_meas_mean_seq(void *stream, const float *raw, int64_t n, int32_t H, int32_t W, const ptyx_meas_proc *p,
+                       const double *stats, void *ws, int32_t normalized, float *mean);
+
+/* meas_pad's padded background (initialization.py:986-1025), bg (Hp,Wp) f64: the amplitude
+ * amp = sqrt(mean) of the (Hm,Wm) mean pattern placed at (h1, w1) and padded by pad_type
+ *   0 constant (amp = value), 1 edge, 2 linear_ramp (to value at the canvas border; numpy.pad's
+ *   axis order), all three in f32 like the reference's f32 amp_avg;
+ *   3 exp  a·exp(-b·r), 4 power  a·r^-b  (f64), r = distance to (Hm/2 + h1, Wm/2 + w1) + 1e-10,
+ *   with (a, b) the host's curve_fit of the thresholded mean (image_proc.py:458-492);
+ * then squared back to intensity and zeroed under the frame [h1, h1+Hm) × [w1, w1+Wm). */
+int ptyx_meas_pad_background(void *stream, const double *mean, int32_t Hm, int32_t Wm, int32_t pad_type, double a,
+                             double b, double value, int32_t Hp, int32_t Wp, int32_t h1, int32_t w1, double *bg);
+
+/* meas_pad / meas_resample 'precompute' (initialization.py:1030-1034, 1083-1086) fused into one
+ * pass: frame k of the canvas is bg (Hp,Wp) f64 with src frame k (Hm,Wm; f32, or f16 when
+ * src_f16) pasted at (h1, w1) — bg NULL = no padding (Hp,Wp = Hm,Wm, h1 = w1 = 0) — and dst
+ * (n,Ho,Wo) is that canvas resampled as scipy.ndimage.zoom(order=1, grid_mode=False) does
+ * (output pixel o reads input coordinate o·(Hp-1)/(Ho-1)), f64 arithmetic, stored f32 (or f16
+ * with dst_f16).  Ho,Wo = Hp,Wp copies the canvas (padding only). */
+int ptyx_meas_pad_resample(void *stream, const void *src, int32_t src_f16, int64_t n, int32_t Hm, int32_t Wm,
+                           const double *bg, int32_t Hp, int32_t Wp, int32_t h1, int32_t w1, int32_t Ho, int32_t Wo,
+                           void *dst, int32_t dst_f16);
+
 /* ---------------------------------------------------------------------------------------------
  * Optimizer-step bookkeeping for graph-replayed recon_step (reconstruction.py:658-781 at
  * grad_accumulation = 1: one step per mini-batch).  A captured step reads its mini-batch through

@@ -33,6 +33,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
+           "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
            "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_plan_check")
 
 
@@ -162,6 +163,11 @@ def load(path: str | None = None):
     lib.ptyx_meas_ws_bytes.restype = ctypes.c_size_t
     lib.ptyx_meas_stats.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp]
     lib.ptyx_meas_finish.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp, vp, i32]
+    lib.ptyx_meas_mean.argtypes = [vp, i32, i32, ctypes.POINTER(MeasProc), vp, vp, vp]
+    lib.ptyx_meas_mean_seq.argtypes = [vp, vp, i64, i32, i32, ctypes.POINTER(MeasProc), vp, vp, i32, vp]
+    lib.ptyx_meas_pad_background.argtypes = [vp, vp, i32, i32, i32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                             i32, i32, i32, i32, vp]
+    lib.ptyx_meas_pad_resample.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp, i32]
     lib.ptyx_step_select.argtypes = [vp, vp, vp, vp, i32, vp, vp, i64]
     lib.ptyx_step_store.argtypes = [vp, vp, i32, vp, vp, vp]
     d64 = ctypes.c_double
@@ -170,7 +176,8 @@ def load(path: str | None = None):
                  "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
-                 "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish"):
+                 "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish",
+                 "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample"):
         getattr(lib, name).restype = ctypes.c_int
     _check_abi(lib)
     _lib = lib

@@ -45,6 +45,9 @@ def _portable(v):
 
 def make_save_dict(output_path, model, params, optimizer, niter, indices, batch_losses):
     """save.py:85-137: the dict PtyRAD saves per checkpoint, same keys and meanings."""
+    if getattr(model, "_stale_object", False):
+        raise RuntimeError("the band exchange left object rows out of date on this rank: call "
+                           "DistContext.sync_object(model) on every rank before saving")
     avg_losses = {name: float(np.mean(values)) for name, values in batch_losses.items() if len(values)}
     avg_iter_t = float(np.mean(model.iter_times)) if len(model.iter_times) else float("nan")
     optimizable_tensors = {}

@@ -30,6 +30,23 @@ def _on(cp, name, niter):
     return f is not None and niter % f == 0
 
 
+def object_footprint(cp, niter):
+    """What iteration ``niter``'s object constraints read (constraints.py:83-208): 'global' for the
+    Fourier filters (kr / kz), the lateral blur and objp_postiv's subtract_min (the global
+    minimum); 'pointwise' when only per-pixel ones run (obj_zblur acts along z at one (y, x),
+    complex_ratio, mirrored_amp, obja_thresh, objp_postiv clip_neg); else 'none'.  The band
+    exchange refreshes the whole object before a 'global' iteration only."""
+    blur = cp.get("obj_rblur") or {}
+    pos = cp.get("objp_postiv") or {}
+    if _on(cp, "kr_filter", niter) or _on(cp, "kz_filter", niter) or \
+            (_on(cp, "obj_rblur", niter) and blur.get("std", 0) != 0) or \
+            (_on(cp, "objp_postiv", niter) and pos.get("mode", "clip_neg") == "subtract_min"):
+        return "global"
+    if any(_on(cp, k, niter) for k in ("obj_zblur", "complex_ratio", "mirrored_amp", "obja_thresh", "objp_postiv")):
+        return "pointwise"
+    return "none"
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
@@ -240,6 +257,11 @@ class CombinedConstraint(torch.nn.Module):
             return
         t = model.opt_obj_tilts.data.reshape(model.N_scan_slow, model.N_scan_fast, 2).permute(2, 0, 1).contiguous()
         model.opt_obj_tilts.data = self._rblur(t, 5, c["std"]).permute(1, 2, 0).reshape(-1, 2).contiguous()
+
+    def object_footprint(self, niter):
+        """'none' / 'pointwise' / 'global': what this iteration's object constraints read (the
+        band exchange keeps only a rank's own rows current; recon_step syncs before 'global')."""
+        return object_footprint(self.constraint_params, niter)
 
     def forward(self, model, niter):
         """constraints.py:227-246."""

@@ -243,6 +243,248 @@ extern "C" int ptyx_meas_finish(void* stream, const float* raw, int64_t n, int32
   return abi::launch_status("meas_finish launch");
 }
 
+// ---------------------------------------------------------------------------------------------
+// meas_pad / meas_resample (initialization.py:956-1102).  The mean pattern comes from the stats
+// (the same per-pixel sums the normalisation used, so a sharded ingest fits the global mean);
+// the 2-parameter background fit runs on the host (ptyrad_amd/ingest.py); the background and the
+// fused paste + bilinear zoom run here.
+namespace {
+__global__ __launch_bounds__(256) void k_meas_mean(const double* __restrict__ stats, int P, NegRule r,
+                                                   const float* __restrict__ cst, double* __restrict__ mean) {
+  const double mn = stats[0], n = stats[1];
+  const bool applied = cst[0] != 0.f;
+  const double c = (double)cst[1];
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    double s = stats[2 + p];
+    if (applied) s = r.mode == 1 ? s - n * mn : stats[2 + P + p];
+    mean[p] = s / n / c;
+  }
+}
+
+// The reference's own f32 mean pattern (numpy's meas.mean(0) on a float32 stack: frame by frame
+// in f32, then / n in f32 — a sequential sum, bit for bit): one thread per output pixel, frames in
+// order, of the value after the negative-value rule (normalized = 0), or of that value divided by
+// the normalisation constant as ptyx_meas_finish stores it (normalized = 1).  Not decomposable
+// over ranks or chunks (the f64 stats are); the single-rank ingest uses it so that the
+// normalisation constant and meas_pad's background fit see exactly the reference's values.
+__global__ __launch_bounds__(256) void k_meas_mean_seq(const float* __restrict__ raw, long long n, Geom g, NegRule r,
+                                                       const float* __restrict__ cst, int normalized,
+                                                       float* __restrict__ mean) {
+  const int P = g.Ho * g.Wo;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const bool applied = cst[0] != 0.f;
+  const float c = cst[1], mn = cst[2];
+  const long long fs = (long long)g.H * g.W;
+  const float* src = raw + src_of(g, p / g.Wo, p % g.Wo);
+  float acc = 0.f;
+  long long f = 0;
+  for (; f + 8 <= n; f += 8) {
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = src[(f + i) * fs];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = applied ? neg_apply(x[i], r, mn) : x[i];
+      if (normalized) v = fmaxf(v / c, 0.f);
+      acc = __fadd_rn(acc, v);
+    }
+  }
+  for (; f < n; ++f) {
+    float v = applied ? neg_apply(src[f * fs], r, mn) : src[f * fs];
+    if (normalized) v = fmaxf(v / c, 0.f);
+    acc = __fadd_rn(acc, v);
+  }
+  mean[p] = acc / (float)n;
+}
+
+struct PadGeom {
+  int Hm, Wm, Hp, Wp, h1, w1, type;
+  double a, b, value;
+};
+
+// numpy.linspace(end, edge, w, endpoint=False)[k] = k·((edge - end)/w) + end, cast to f32
+__device__ __forceinline__ float ramp_at(float edge, double end, int w, int k) {
+  return (float)((double)k * (((double)edge - end) / (double)w) + end);
+}
+__device__ __forceinline__ float amp_of(const double* __restrict__ mean, const PadGeom& g, int y, int x) {
+  return sqrtf((float)mean[(size_t)y * g.Wm + x]);
+}
+// numpy.pad(linear_ramp) pads axis 0 over the frame's columns first, then axis 1 over all rows
+__device__ float ramp_col(const double* __restrict__ mean, const PadGeom& g, int i, int jj) {
+  const int ii = i - g.h1;
+  if (ii < 0) return ramp_at(amp_of(mean, g, 0, jj), g.value, g.h1, i);
+  if (ii >= g.Hm) {
+    const int w = g.Hp - g.h1 - g.Hm;
+    return ramp_at(amp_of(mean, g, g.Hm - 1, jj), g.value, w, w - 1 - (ii - g.Hm));
+  }
+  return amp_of(mean, g, ii, jj);
+}
+
+__global__ __launch_bounds__(256) void k_pad_background(const double* __restrict__ mean, PadGeom g,
+                                                        double* __restrict__ bg) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.Hp * g.Wp) return;
+  const int y = e / g.Wp, x = e - y * g.Wp;
+  const int yy = y - g.h1, xx = x - g.w1;
+  if (yy >= 0 && yy < g.Hm && xx >= 0 && xx < g.Wm) {
+    bg[e] = 0.0;
+    return;
+  }
+  double v;
+  if (g.type <= 2) {
+    float amp;
+    if (g.type == 0) {
+      amp = (float)g.value;
+    } else if (g.type == 1) {
+      amp = amp_of(mean, g, min(max(yy, 0), g.Hm - 1), min(max(xx, 0), g.Wm - 1));
+    } else if (xx < 0) {
+      amp = ramp_at(ramp_col(mean, g, y, 0), g.value, g.w1, x);
+    } else if (xx >= g.Wm) {
+      const int w = g.Wp - g.w1 - g.Wm;
+      amp = ramp_at(ramp_col(mean, g, y, g.Wm - 1), g.value, w, w - 1 - (xx - g.Wm));
+    } else {
+      amp = ramp_col(mean, g, y, xx);
+    }
+    v = (double)(amp * amp);   // np.square of the f32 amplitude
+  } else {
+    const double dy = (double)y - (double)(g.Hm / 2 + g.h1), dx = (double)x - (double)(g.Wm / 2 + g.w1);
+    const double r = sqrt(dy * dy + dx * dx) + 1e-10;
+    const double amp = g.type == 3 ? g.a * exp(-g.b * r) : g.a * pow(r, -g.b);
+    v = amp * amp;
+  }
+  bg[e] = v;
+}
+
+struct ZoomGeom {
+  int Hm, Wm, Hp, Wp, h1, w1, Ho, Wo, src_f16, dst_f16, zoom;
+  double ry, rx;   // (Hp-1)/(Ho-1), (Wp-1)/(Wo-1); 1 when the output axis has one pixel
+};
+
+__device__ __forceinline__ double canvas_at(const void* __restrict__ src, size_t base, const double* __restrict__ bg,
+                                            const ZoomGeom& g, int r, int c) {
+  const int rr = r - g.h1, cc = c - g.w1;
+  if (rr >= 0 && rr < g.Hm && cc >= 0 && cc < g.Wm) {
+    const size_t off = base + (size_t)rr * g.Wm + cc;
+    return g.src_f16 ? (double)__half2float(reinterpret_cast<const __half*>(src)[off])
+                     : (double)reinterpret_cast<const float*>(src)[off];
+  }
+  return bg ? bg[(size_t)r * g.Wp + c] : 0.0;
+}
+
+// order-1 spline weights at coordinate c on an axis of n points: (i0, i1, t); false when c lies
+// past the last pixel — scipy's mode 'constant' then returns cval = 0 for the whole output pixel,
+// even when only the rounding of o·(n-1)/(no-1) put it there (32 px zoomed by 0.5: 31.000000000000004)
+__device__ __forceinline__ bool zoom_src(int o, double ratio, int n, int& i0, int& i1, double& t) {
+  const double c = (double)o * ratio;
+  i0 = min((int)floor(c), n - 1);
+  t = c - (double)i0;
+  if (t < 0.0) t = 0.0;
+  i1 = i0 + 1 < n ? i0 + 1 : i0;
+  return c <= (double)(n - 1);
+}
+
+__global__ __launch_bounds__(256) void k_pad_resample(const void* __restrict__ src, long long n,
+                                                      const double* __restrict__ bg, ZoomGeom g,
+                                                      void* __restrict__ dst) {
+  const long long per = (long long)g.Ho * g.Wo, total = n * per;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long f = i / per;
+    const int e = (int)(i - f * per);
+    const int y = e / g.Wo, x = e - y * g.Wo;
+    const size_t base = (size_t)f * g.Hm * g.Wm;
+    double v;
+    if (!g.zoom) {
+      v = canvas_at(src, base, bg, g, y, x);
+    } else {
+      int y0, y1, x0, x1;
+      double ty, tx;
+      const bool iny = zoom_src(y, g.ry, g.Hp, y0, y1, ty);
+      const bool inx = zoom_src(x, g.rx, g.Wp, x0, x1, tx);
+      const double wy = 1.0 - ty, wx = 1.0 - tx;
+      v = canvas_at(src, base, bg, g, y0, x0) * wy * wx;
+      v += canvas_at(src, base, bg, g, y0, x1) * wy * tx;
+      v += canvas_at(src, base, bg, g, y1, x0) * ty * wx;
+      v += canvas_at(src, base, bg, g, y1, x1) * ty * tx;
+      if (!(iny && inx)) v = 0.0;
+    }
+    if (g.dst_f16) reinterpret_cast<__half*>(dst)[i] = __float2half((float)v);
+    else reinterpret_cast<float*>(dst)[i] = (float)v;
+  }
+}
+}  // namespace
+
+extern "C" int ptyx_meas_mean(void* stream, int32_t H, int32_t W, const ptyx_meas_proc* p, const double* stats,
+                              void* ws, double* mean) {
+  abi::clear_error();
+  Geom g;
+  NegRule r;
+  int rc = make_geom(p, H, W, g, r);
+  if (rc) return rc;
+  if (!stats || !ws || !mean) return abi::fail(PTYX_EINVAL, "meas_mean: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int P = g.Ho * g.Wo;
+  float* cst = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_meas_const, dim3(1), dim3(256), 0, st, stats, P, r, p->norm_mode, p->norm_value, cst);
+  hipLaunchKernelGGL(k_meas_mean, dim3((P + 255) / 256), dim3(256), 0, st, stats, P, r, cst, mean);
+  return abi::launch_status("meas_mean launch");
+}
+
+extern "C" int ptyx_meas_mean_seq(void* stream, const float* raw, int64_t n, int32_t H, int32_t W,
+                                  const ptyx_meas_proc* p, const double* stats, void* ws, int32_t normalized,
+                                  float* mean) {
+  abi::clear_error();
+  Geom g;
+  NegRule r;
+  int rc = make_geom(p, H, W, g, r);
+  if (rc) return rc;
+  if (n <= 0) return abi::fail(PTYX_EINVAL, "meas_mean_seq: n must be > 0");
+  if (!raw || !stats || !ws || !mean) return abi::fail(PTYX_EINVAL, "meas_mean_seq: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int P = g.Ho * g.Wo;
+  float* cst = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_meas_const, dim3(1), dim3(256), 0, st, stats, P, r, p->norm_mode, p->norm_value, cst);
+  hipLaunchKernelGGL(k_meas_mean_seq, dim3((P + 255) / 256), dim3(256), 0, st, raw, (long long)n, g, r, cst,
+                     normalized ? 1 : 0, mean);
+  return abi::launch_status("meas_mean_seq launch");
+}
+
+extern "C" int ptyx_meas_pad_background(void* stream, const double* mean, int32_t Hm, int32_t Wm, int32_t pad_type,
+                                        double a, double b, double value, int32_t Hp, int32_t Wp, int32_t h1,
+                                        int32_t w1, double* bg) {
+  abi::clear_error();
+  if (Hm <= 0 || Wm <= 0 || Hp <= 0 || Wp <= 0) return abi::fail(PTYX_EINVAL, "meas_pad_background: bad shape");
+  if (pad_type < 0 || pad_type > 4) return abi::fail(PTYX_EINVAL, "meas_pad_background: pad_type must be 0..4");
+  if (h1 < 0 || w1 < 0 || h1 + Hm > Hp || w1 + Wm > Wp)
+    return abi::fail(PTYX_EINVAL, "meas_pad_background: the frame does not fit the canvas");
+  if (!bg || (pad_type >= 1 && pad_type <= 2 && !mean)) return abi::fail(PTYX_EINVAL, "meas_pad_background: null pointer");
+  PadGeom g{Hm, Wm, Hp, Wp, h1, w1, pad_type, a, b, value};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_pad_background, dim3((Hp * Wp + 255) / 256), dim3(256), 0, st, mean, g, bg);
+  return abi::launch_status("meas_pad_background launch");
+}
+
+extern "C" int ptyx_meas_pad_resample(void* stream, const void* src, int32_t src_f16, int64_t n, int32_t Hm,
+                                      int32_t Wm, const double* bg, int32_t Hp, int32_t Wp, int32_t h1, int32_t w1,
+                                      int32_t Ho, int32_t Wo, void* dst, int32_t dst_f16) {
+  abi::clear_error();
+  if (Hm <= 0 || Wm <= 0 || Ho <= 0 || Wo <= 0 || n < 0) return abi::fail(PTYX_EINVAL, "meas_pad_resample: bad shape");
+  if (!bg && (Hp != Hm || Wp != Wm || h1 != 0 || w1 != 0))
+    return abi::fail(PTYX_EINVAL, "meas_pad_resample: without a background Hp, Wp must equal Hm, Wm and h1 = w1 = 0");
+  if (h1 < 0 || w1 < 0 || h1 + Hm > Hp || w1 + Wm > Wp)
+    return abi::fail(PTYX_EINVAL, "meas_pad_resample: the frame does not fit the canvas");
+  if (n == 0) return PTYX_OK;
+  if (!src || !dst) return abi::fail(PTYX_EINVAL, "meas_pad_resample: null pointer");
+  const bool zoom = Ho != Hp || Wo != Wp;
+  ZoomGeom g{Hm, Wm, Hp, Wp, h1, w1, Ho, Wo, src_f16 ? 1 : 0, dst_f16 ? 1 : 0, zoom ? 1 : 0,
+             Ho > 1 ? (double)(Hp - 1) / (double)(Ho - 1) : 1.0, Wo > 1 ? (double)(Wp - 1) / (double)(Wo - 1) : 1.0};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long long total = n * (long long)Ho * Wo;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_pad_resample, dim3(grid), dim3(256), 0, st, src, (long long)n, bg, g, dst);
+  return abi::launch_status("meas_pad_resample launch");
+}
+
 extern "C" int ptyx_raw_read(void* stream, const char* path, int64_t offset, int32_t H, int32_t W, int32_t gap,
                              int64_t file_frames, int64_t first, int64_t count, float* dst) {
   abi::clear_error();

@@ -273,6 +273,7 @@ struct ptyx_plan {
   int* blist = nullptr;       // (max_patterns) patterns by bin
   float2* gpart = nullptr;    // split gather: tile partials (kGatherPartCap × 64·16)
   float* gpcnt = nullptr;
+  int gpart_cap = 0;          // partial tiles gpart / gpcnt hold
   float* dsu = nullptr;       // per-pattern unit position-gradient sums
   float2* segpart = nullptr;  // k_segslab_reduce partials (kSegSplit × N²)
   float2* hpk = nullptr;      // k_fused3ms: K-packed propagator / N²
@@ -333,14 +334,15 @@ static int busy(const ptyx_plan* pl) {
 
 enum KernelKind {
   kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather,
-  kKObjPrep, kKPack, kKS1, kKS2, kKS3, kKS4, kKS5, kKCount
+  kKObjPrep, kKPack, kKS1, kKS2, kKS3, kKS4, kKS5, kKFmmFwd, kKFmmLoss, kKFmmAdj, kKCount
 };
 static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize",
                                                   "k_adjoint",        "k_slab_reduce",    "k_probe_finalize",
                                                   "k_fused",          "k_pattern_table",  "k_obj_gather",
                                                   "k_obj_prep",       "k_pack",           "k_s1",
                                                   "k_s2",             "k_s3",             "k_s4",
-                                                  "k_s5"};
+                                                  "k_s5",             "k_fmm_fwd",        "k_fmm_loss",
+                                                  "k_fmm_adj"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -380,9 +382,15 @@ static int alloc_bins(ptyx_plan* pl) {
   int rc;
   if ((rc = dalloc(pl, &pl->bcnt, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->boff, (size_t)pl->nbins + 1)) ||
       (rc = dalloc(pl, &pl->bcur, (size_t)pl->nbins)) || (rc = dalloc(pl, &pl->bkey, (size_t)d.max_patterns)) ||
-      (rc = dalloc(pl, &pl->blist, (size_t)d.max_patterns)) ||
-      (rc = dalloc(pl, &pl->gpart, (size_t)kGatherPartCap * kGTY * kGTX)) ||
-      (rc = dalloc(pl, &pl->gpcnt, (size_t)kGatherPartCap * kGTY * kGTX)))
+      (rc = dalloc(pl, &pl->blist, (size_t)d.max_patterns)))
+    return rc;
+  // split-gather partials: the default rule (launch_gather) splits only below 1,024 tile planes and
+  // then uses at most parts·min(8, ⌈2048/parts⌉) < 3,072 partial tiles; a plan whose single slice
+  // already has 1,024 tiles never splits (no buffer) unless the gather_split tuning key was set
+  // when it was created (then the whole kGatherPartCap)
+  pl->gpart_cap = g_tuning[kTuneGatherSplit] >= 1 ? kGatherPartCap : pl->nbins >= 1024 ? 0 : 3072;
+  if ((rc = dalloc(pl, &pl->gpart, (size_t)pl->gpart_cap * kGTY * kGTX)) ||
+      (rc = dalloc(pl, &pl->gpcnt, (size_t)pl->gpart_cap * kGTY * kGTX)))
     return rc;
   return PTYX_OK;
 }
@@ -396,9 +404,9 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
   int S = 1;
   // (not for small calls: a tile's few candidates are not worth the extra partial-sum launch)
   if (parts < 1024 && pl->gpart && g.n > f3::kSmallCall)
-    S = std::max(1, std::min({8, (2048 + parts - 1) / parts, kGatherPartCap / parts}));
+    S = std::max(1, std::min({8, (2048 + parts - 1) / parts, pl->gpart_cap / parts}));
   if (g_tuning[kTuneGatherSplit] >= 1 && pl->gpart)
-    S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], kGatherPartCap / parts));
+    S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], pl->gpart_cap / parts));
   g.part = pl->gpart;
   g.pcnt = pl->gpcnt;
   if (S == 1) {
@@ -1133,12 +1141,12 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   if (ph != kPhaseEnd) {
     if ((rc = register_prep(pl, in, a, cfg, st, nseg))) return rc;
     {
-      ProfScope ps(pl, kKFused, st);
+      ProfScope ps(pl, kKFmmFwd, st);
       if (a.shift) hipLaunchKernelGGL(f3::k_fmm_fwd<true>, dim3(G), dim3(256), 0, st, m);
       else hipLaunchKernelGGL(f3::k_fmm_fwd<false>, dim3(G), dim3(256), 0, st, m);
     }
     {
-      ProfScope ps(pl, kKForward, st);
+      ProfScope ps(pl, kKFmmLoss, st);
       const dim3 gr(a.n_idx), bl(256);
       const bool half = cfg->single_q == 0.5f;
       if (both && half) hipLaunchKernelGGL((f3::k_fmm_loss<0, 3>), gr, bl, 0, st, m);
@@ -1169,7 +1177,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   const bool any_grad = gz.d_obja || gz.d_objp || gz.d_probe || gz.d_shifts;
   if (!any_grad) return PTYX_OK;
   {
-    ProfScope ps(pl, kKAdjoint, st);
+    ProfScope ps(pl, kKFmmAdj, st);
     if (a.shift && both) hipLaunchKernelGGL((f3::k_fmm_adj<true, true>), dim3(G), dim3(256), 0, st, m);
     else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_adj<true, false>), dim3(G), dim3(256), 0, st, m);
     else if (both) hipLaunchKernelGGL((f3::k_fmm_adj<false, true>), dim3(G), dim3(256), 0, st, m);
@@ -1651,8 +1659,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   // stripe engine (N = 256, Nz = 1, O ≤ 2, shifted probes): either or both data terms (both: k_s3
   // twice, around k_finalize), call within capacity
   const bool stripe = pl->stripe_cap > 0 && n_idx <= pl->stripe_cap && !want_H && a.shift && (one_term || both_terms);
-  // mixed-state register engine (N = 128, P > 1, O = 1): one data term, f32 DPs, the call within
-  // the far-field cache its slots live in
+  // mixed-state register engine (N = 128, P > 1, O = 1): either or both data terms (both applied
+  // in k_fmm_adj), f32 DPs, the call within the far-field cache its slots live in
   const bool fmm = any_grad && !want_H && pl->fmm && !a.meas_f16 && n_idx <= pl->ffc_cap;   // (either or both terms)
 #ifdef PTYX_ONLY_N
   *engine = (fused3 || fused3ms) && PTYX_ONLY_N == 128 ? kEngFused3 : fmm && PTYX_ONLY_N == 128 ? kEngFmm

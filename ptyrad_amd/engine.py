@@ -179,7 +179,7 @@ class Plan:
 
     def profile_end(self) -> dict:
         """{kernel name: (launches, total_ms)} from HIP events recorded on the launch stream."""
-        cap = 16
+        cap = 32
         arr = (_lib.KernelStat * cap)()
         n = ctypes.c_int32(0)
         _lib.check(self.lib.ptyx_profile_end(self._h, arr, cap, ctypes.byref(n)))

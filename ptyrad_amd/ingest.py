@@ -11,23 +11,43 @@ ptyx_meas_finish) and returns the (N', Npix_y, Npix_x) stack the model consumes,
 its contiguous block of scan rows; the normalisation statistics are all-reduced (one MIN and
 one SUM) so every rank divides by the global constant, exactly like a single-rank run.
 
+A single rank holding the whole stack takes the normalisation constant from the reference's own
+f32 mean pattern (ptyx_meas_mean_seq: numpy's sequential f32 meas.mean(0), bit for bit), so the
+stored stack is the reference's meas / const exactly; sharded ingest uses the f64 statistics
+(summable over ranks, ≈ 1e-6).
+
+meas_pad (initialization.py:956-1048: constant / edge / linear_ramp / exp / power backgrounds,
+'precompute' or 'on_the_fly') and meas_resample (:1050-1102: 'precompute' bilinear zoom, or
+'on_the_fly' scale factors) follow the normalisation: the mean pattern is again the reference's
+f32 one (single rank) or comes from the statistics (ptyx_meas_mean, global across ranks), the
+2-parameter background fit of
+image_proc.py:458-492 runs on the host (scipy.optimize.curve_fit, the reference's own solver,
+on Ho·Wo values), the background is built on the device (ptyx_meas_pad_background) and a
+precomputed pad and / or resample is ONE fused paste + zoom pass (ptyx_meas_pad_resample).
+On-the-fly options return the model's init_variables (on_the_fly_meas_padded, _idx,
+on_the_fly_meas_scale_factors), which PtychoHIP consumes through ptyx_meas_gather.
+
 Not supported here (NotImplementedError, run the reference's host path for them): meas_permute,
-meas_reshape, meas_pad, meas_resample and the simulation options meas_add_source_size /
-meas_add_detector_blur / meas_add_poisson_noise.  There is no CPU fallback.
+meas_reshape and the simulation options meas_add_source_size / meas_add_detector_blur /
+meas_add_poisson_noise (each when enabled; None, and 0 for the two blurs, are off as in the
+reference).  There is no CPU fallback.
 """
 from __future__ import annotations
 
 import ctypes
 import math
 
+import numpy as np
 import torch
 
 from . import _lib
 
 _NEG = {"clip_neg": 0, "subtract_min": 1, "clip_value": 2, "subtract_value": 3}
 _NORM = {"max_at_one": 0, "mean_at_one": 1, "sum_to_one": 2, "divide_const": 3}
-_UNSUPPORTED = ("meas_permute", "meas_reshape", "meas_pad", "meas_resample", "meas_add_source_size",
-                "meas_add_detector_blur", "meas_add_poisson_noise")
+_UNSUPPORTED = ("meas_permute", "meas_reshape", "meas_add_source_size", "meas_add_detector_blur",
+                "meas_add_poisson_noise")
+_PAD_TYPES = {"constant": 0, "edge": 1, "linear_ramp": 2, "exp": 3, "power": 4}
+_MODES = ("on_the_fly", "precompute")
 
 
 def _stream(dev):
@@ -41,7 +61,8 @@ def _p(t):
 def proc_from_params(init_params: dict, H: int, W: int) -> _lib.MeasProc:
     """The ptyx_meas_proc of init_params (flipT, ky/kx crop, negative values, normalisation)."""
     for k in _UNSUPPORTED:
-        if init_params.get(k) is not None:
+        v = init_params.get(k)
+        if v is not None and not (k in ("meas_add_source_size", "meas_add_detector_blur") and v == 0):
             raise NotImplementedError(f"{k} is not supported by the device ingest path")
     p = _lib.MeasProc()
     f = init_params.get("meas_flipT")
@@ -146,22 +167,209 @@ def _ws(lib, Ho, Wo, dev):
     return torch.empty((int(lib.ptyx_meas_ws_bytes(Ho, Wo)) + 7) // 8, dtype=torch.float64, device=dev)
 
 
-def process_meas(raw: torch.Tensor, init_params: dict, out_f16=False, reduce_across_ranks=False, chunk_frames=None):
+def pad_config(init_params: dict):
+    """meas_pad (initialization.py:973-982, 1041-1042): None, or a dict whose 'mode' is None, is off."""
+    cfg = init_params.get("meas_pad")
+    if cfg is None or cfg.get("mode") is None:
+        return None
+    mode, ptype = cfg["mode"], cfg["padding_type"]
+    if ptype not in _PAD_TYPES:
+        raise ValueError(f"Unsupported padding_type = '{ptype}'")
+    if mode not in _MODES:
+        raise ValueError(f"meas_pad does not support mode = '{mode}', please choose from 'on_the_fly', 'precompute', or null")
+    return {"mode": mode, "type": ptype, "target": int(cfg["target_Npix"]), "value": cfg.get("value", 10),
+            "threshold": cfg.get("threshold", 70)}
+
+
+def resample_config(init_params: dict, otf_pad: bool):
+    """meas_resample (initialization.py:1055-1095): off for None / mode None; unequal scale factors
+    become their minimum; an on-the-fly pad forces an on-the-fly resample."""
+    cfg = init_params.get("meas_resample")
+    if cfg is None or cfg.get("mode") is None:
+        return None
+    if "scale_factors" not in cfg:
+        raise KeyError("Missing required configuration field: 'scale_factors'")
+    sf = cfg["scale_factors"]
+    if len(sf) != 2:
+        raise ValueError("scale_factors for resample must be a list or tuple of two elements.")
+    s = min(sf) if sf[0] != sf[1] else sf[0]
+    mode = "on_the_fly" if otf_pad else cfg["mode"]
+    if mode not in _MODES:
+        raise ValueError(f"meas_resample does not support mode = '{mode}', please choose from 'on_the_fly', 'precompute', or null")
+    return {"mode": mode, "scale": s}
+
+
+def pad_geometry(Ho, Wo, pad):
+    """Canvas (Hp, Wp) and frame origin (h1, w1) of meas_pad (initialization.py:990-998): the
+    frame centred with the odd pixel after it; exp / power evaluate on target_Npix²."""
+    T = pad["target"]
+    py, px = max(0, T - Ho), max(0, T - Wo)
+    if pad["type"] in ("exp", "power"):
+        if Ho > T or Wo > T:
+            raise ValueError(f"meas_pad: target_Npix {T} is smaller than the measurement ({Ho}, {Wo})")
+        Hp = Wp = T
+    else:
+        Hp, Wp = Ho + py, Wo + px
+    return Hp, Wp, py // 2, px // 2
+
+
+def fit_background(amp: np.ndarray, percentile, fit_type):
+    """(a, b) of the radial background of image_proc.py:458-492: pixels at or below the given
+    percentile of the amplitude, fitted by a·exp(-b·r) or a·r^-b with r measured from the
+    (H//2, W//2) centre, a, b ≥ 0, by scipy.optimize.curve_fit (the reference's solver: TRF under
+    bounds, maxfev 10000, started at (max, 0.1) / (max, 1))."""
+    from scipy.optimize import curve_fit
+    keep = amp <= np.percentile(amp, percentile)
+    yy, xx = np.indices(amp.shape)
+    cy, cx = amp.shape[0] // 2, amp.shape[1] // 2
+    r = np.sqrt((xx - cx) ** 2 + (yy - cy) ** 2) + 1e-10
+    rr, vv = r[keep], amp[keep]
+    if fit_type == "exp":
+        def model(x, a, b):
+            return a * np.exp(-b * x)
+        start = [np.max(vv), 0.1]
+    else:
+        def model(x, a, b):
+            return a * x ** -b
+        start = [np.max(vv), 1]
+    popt, _ = curve_fit(model, rr, vv, p0=start, bounds=([0, 0], [np.inf, np.inf]), maxfev=10000)
+    return float(popt[0]), float(popt[1])
+
+
+def meas_mean(p, stats: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """ptyx_meas_mean: the (Ho, Wo) f64 mean of the processed stack, from its statistics."""
+    lib = _lib.load()
+    Ho, Wo = _out_shape(p, H, W)
+    dev = stats.device
+    mean = torch.empty((Ho, Wo), dtype=torch.float64, device=dev)
+    _lib.check(lib.ptyx_meas_mean(_stream(dev), H, W, ctypes.byref(p), _p(stats), _p(_ws(lib, Ho, Wo, dev)),
+                                  _p(mean)))
+    return mean
+
+
+def meas_mean_seq(raw: torch.Tensor, p, stats: torch.Tensor, normalized: bool) -> torch.Tensor:
+    """ptyx_meas_mean_seq: numpy's f32 meas.mean(0) of the stack after the negative-value rule
+    (normalized False) or after normalisation by p's constant (True), bit for bit: (Ho, Wo) f32."""
+    lib = _lib.load()
+    n, H, W = raw.shape
+    Ho, Wo = _out_shape(p, H, W)
+    mean = torch.empty((Ho, Wo), dtype=torch.float32, device=raw.device)
+    _lib.check(lib.ptyx_meas_mean_seq(_stream(raw.device), _p(raw), n, H, W, ctypes.byref(p), _p(stats),
+                                      _p(_ws(lib, Ho, Wo, raw.device)), int(bool(normalized)), _p(mean)))
+    return mean
+
+
+def reference_normalization(raw: torch.Tensor, p, stats: torch.Tensor):
+    """The proc with the reference's own f32 normalisation constant (initialization.py:928-944:
+    max / mean / sum of the f32 mean pattern, computed by numpy on exactly that pattern), as a
+    divide_const: the stored stack is then bit-identical to the reference's meas / const."""
+    if p.norm_mode == _NORM["divide_const"]:
+        return p
+    m = meas_mean_seq(raw, p, stats, False).cpu().numpy()
+    const = {0: m.max(), 1: m.mean(), 2: m.sum()}[p.norm_mode]
+    q = _lib.MeasProc()
+    ctypes.memmove(ctypes.byref(q), ctypes.byref(p), ctypes.sizeof(p))
+    q.norm_mode, q.norm_value = _NORM["divide_const"], float(const)
+    return q
+
+
+def pad_background(mean: torch.Tensor, pad: dict):
+    """The padded background canvas (initialization.py:986-1025) on the device from the mean
+    pattern (f32: the reference's own, or f64 from the statistics): (bg (Hp, Wp) f64,
+    (Hp, Wp, h1, w1), (a, b))."""
+    lib = _lib.load()
+    Ho, Wo = mean.shape
+    Hp, Wp, h1, w1 = pad_geometry(Ho, Wo, pad)
+    a = b = 0.0
+    if pad["type"] in ("exp", "power"):
+        amp = np.sqrt(mean.cpu().numpy().astype(np.float32))   # the reference's f32 amp_avg
+        a, b = fit_background(amp, pad["threshold"], pad["type"])
+    mean = mean.double()
+    value = float(pad["value"]) if pad["type"] in ("constant", "linear_ramp") else 0.0
+    bg = torch.empty((Hp, Wp), dtype=torch.float64, device=mean.device)
+    _lib.check(lib.ptyx_meas_pad_background(_stream(mean.device), _p(mean), Ho, Wo, _PAD_TYPES[pad["type"]], a, b,
+                                            value, Hp, Wp, h1, w1, _p(bg)))
+    return bg, (Hp, Wp, h1, w1), (a, b)
+
+
+def pad_resample(meas: torch.Tensor, bg, geom, out_hw, out_f16=False) -> torch.Tensor:
+    """ptyx_meas_pad_resample: paste every frame of meas (n, Hm, Wm) into the background canvas
+    (bg None = no padding) and zoom it to out_hw (order-1 spline, scipy's grid), in one pass."""
+    lib = _lib.load()
+    n, Hm, Wm = meas.shape
+    Hp, Wp, h1, w1 = geom if bg is not None else (Hm, Wm, 0, 0)
+    Ho, Wo = out_hw
+    out = torch.empty((n, Ho, Wo), dtype=torch.float16 if out_f16 else torch.float32, device=meas.device)
+    _lib.check(lib.ptyx_meas_pad_resample(_stream(meas.device), _p(meas), int(meas.dtype == torch.float16), n, Hm, Wm,
+                                          None if bg is None else _p(bg), Hp, Wp, h1, w1, Ho, Wo, _p(out),
+                                          int(bool(out_f16))))
+    return out
+
+
+def process_meas_ex(raw: torch.Tensor, init_params: dict, out_f16=False, reduce_across_ranks=False,
+                    chunk_frames=None):
     """_process_meas (initialization.py:709-752) on a device-resident (n, H, W) f32 stack: flipT,
-    ky/kx crop, negative values, normalisation, final clip.  With reduce_across_ranks the
-    statistics are all-reduced so every rank uses the global constants."""
-    p = proc_from_params(init_params, raw.shape[1], raw.shape[2])
+    ky/kx crop, negative values, normalisation, meas_pad, meas_resample, final clip.  Returns
+    (meas, extras); extras holds what the reference leaves in init_variables / init_params:
+    on_the_fly_meas_padded ((1, Hp, Wp) f64 device tensor or None), on_the_fly_meas_padded_idx,
+    on_the_fly_meas_scale_factors, meas_Npix, and pad_int_sum (the on-the-fly background's
+    intensity that init_measurements adds to meas_avg_sum, :107-112)."""
+    n, H, W = raw.shape
+    p = proc_from_params(init_params, H, W)
+    pad = pad_config(init_params)
+    rs = resample_config(init_params, otf_pad=pad is not None and pad["mode"] == "on_the_fly")
     stats = meas_stats(raw, p, chunk_frames)
     if reduce_across_ranks:
         allreduce_stats(stats)
-    return meas_finish(raw, p, stats, out_f16)
+    # one rank holding the whole stack: the reference's f32 normalisation constant and mean
+    # pattern exactly (a sequential f32 pass); sharded / chunked: the f64 statistics (≈ 1e-6)
+    exact = not reduce_across_ranks and n > 0
+    if exact:
+        p = reference_normalization(raw, p, stats)
+    Ho, Wo = _out_shape(p, H, W)
+    extras = {"on_the_fly_meas_padded": None, "on_the_fly_meas_padded_idx": None,
+              "on_the_fly_meas_scale_factors": None, "meas_Npix": Wo, "pad_int_sum": 0.0, "pad_fit": None}
+    bg, geom, cur = None, None, (Ho, Wo)
+    if pad is not None:
+        mean = meas_mean_seq(raw, p, stats, True) if exact else meas_mean(p, stats, H, W)
+        bg, geom, extras["pad_fit"] = pad_background(mean, pad)
+        extras["meas_Npix"] = geom[1]
+        if pad["mode"] == "on_the_fly":
+            Hp, Wp, h1, w1 = geom
+            extras["on_the_fly_meas_padded"] = bg[None]
+            extras["on_the_fly_meas_padded_idx"] = [h1, h1 + Ho, w1, w1 + Wo]
+            extras["pad_int_sum"] = float(bg.sum())
+        else:
+            cur = geom[:2]
+    out_hw = cur
+    if rs is not None:
+        s = rs["scale"]
+        if rs["mode"] == "precompute":
+            out_hw = (int(round(cur[0] * float(s))), int(round(cur[1] * float(s))))   # scipy.ndimage.zoom's shape
+            extras["meas_Npix"] = out_hw[1]
+        else:
+            extras["meas_Npix"] = math.floor(extras["meas_Npix"] * s)
+            extras["on_the_fly_meas_scale_factors"] = [s, s]
+    precompute_pad = pad is not None and pad["mode"] == "precompute"
+    if not precompute_pad and out_hw == (Ho, Wo):
+        return meas_finish(raw, p, stats, out_f16), extras
+    m32 = meas_finish(raw, p, stats, False)
+    meas = pad_resample(m32, bg if precompute_pad else None, geom, out_hw, out_f16)
+    del m32
+    return meas, extras
+
+
+def process_meas(raw: torch.Tensor, init_params: dict, out_f16=False, reduce_across_ranks=False, chunk_frames=None):
+    """process_meas_ex without the extras: the processed stack only."""
+    return process_meas_ex(raw, init_params, out_f16, reduce_across_ranks, chunk_frames)[0]
 
 
 def ingest_raw(file_path, init_params: dict, device="cuda", file_shape=None, offset=0, gap=1024, out_f16=False,
                rank=0, world=1):
     """load_raw + _process_meas for this rank's share of the scan; returns (meas, info) where info
     holds the updated (pos_N_scan_slow, pos_N_scan_fast, meas_Npix, rows) like the reference's
-    init_params after meas_crop."""
+    init_params after meas_crop / meas_pad / meas_resample, plus process_meas_ex's extras (the
+    on-the-fly init_variables)."""
     N_slow, N_fast = int(init_params["pos_N_scan_slow"]), int(init_params["pos_N_scan_fast"])
     N, H, W = file_shape if file_shape is not None else (N_slow * N_fast, init_params["meas_Npix"],
                                                          init_params["meas_Npix"])
@@ -179,10 +387,9 @@ def ingest_raw(file_path, init_params: dict, device="cuda", file_shape=None, off
         dst = raw[i * (f1 - f0):(i + 1) * (f1 - f0)]
         _lib.check(lib.ptyx_raw_read(_stream(dev), str(file_path).encode(), int(offset), H, W, int(gap), N,
                                      r * N_fast + f0, f1 - f0, _p(dst)))
-    meas = process_meas(raw, init_params, out_f16=out_f16, reduce_across_ranks=world > 1)
+    meas, extras = process_meas_ex(raw, init_params, out_f16=out_f16, reduce_across_ranks=world > 1)
     del raw
-    p = proc_from_params(init_params, H, W)
-    Ho, Wo = _out_shape(p, H, W)
     info = {"pos_N_scan_slow": s1 - s0, "pos_N_scan_fast": f1 - f0, "pos_N_scans": (s1 - s0) * (f1 - f0),
-            "meas_Npix": Wo, "meas_shape": (Ho, Wo), "rows": (mine[0], mine[-1] + 1) if mine else (s0, s0)}
+            "meas_shape": tuple(meas.shape[-2:]), "rows": (mine[0], mine[-1] + 1) if mine else (s0, s0)}
+    info.update(extras)
     return meas, info

@@ -106,8 +106,9 @@ class PtychoHIP(nn.Module):
             self._stack_plans = {}
             # on-the-fly measurement padding / resampling (models.py:81-86, :384-412)
             pad = init_variables.get("on_the_fly_meas_padded")
-            self.meas_padded = None if pad is None else torch.tensor(np.asarray(pad), dtype=torch.float32,
-                                                                     device=device).contiguous()
+            if pad is not None and not torch.is_tensor(pad):     # numpy (reference init) or a device
+                pad = torch.tensor(np.asarray(pad))              # tensor (ptyrad_amd.ingest)
+            self.meas_padded = None if pad is None else pad.to(device=device, dtype=torch.float32).contiguous()
             self.meas_padded_idx = None if pad is None else \
                 torch.tensor(np.asarray(init_variables["on_the_fly_meas_padded_idx"]), dtype=torch.int32)
             sf = init_variables.get("on_the_fly_meas_scale_factors")

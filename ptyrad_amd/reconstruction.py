@@ -30,7 +30,9 @@ Multi-GPU (replaces the accelerate/DDP wrapper, utils/common.py:58-90): ``DistCo
 """
 from __future__ import annotations
 
+import hashlib
 import time
+import zlib
 
 import numpy as np
 import torch
@@ -139,20 +141,24 @@ def loss_logger(batch_losses, niter, iter_t, verbose=True):
 class DistContext:
     """Rank/world of a torch.distributed job (backend 'nccl' = RCCL on ROCm, or 'gloo' on CPU)."""
 
-    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=False):
+    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=None):
         """split_batches: None = split a group's mini-batches over the ranks only when the group has
         fewer mini-batches than ranks; True = always (accelerate's split_batches=True,
         utils/common.py:63); False = never (whole mini-batches round-robin).
         always_reduce: run the collectives even with one rank (tests that exercise RCCL on one GPU).
         band_exchange: object gradients by row band (ObjectBands): each rank sends only the rows
         its windows touched to their owners, owners run the optimizer on their band (ZeRO-1),
-        then the updated bands are all-gathered; the rest of the gradient is all-reduced."""
+        then send the updated rows back to the ranks that read them; the rest of the gradient is
+        all-reduced.  None (default) = auto: by band when the ranks' touched rows line up by rank
+        within a window of their bands (a row-sharded scan), else one flat all-reduce; True /
+        False force it.  With the band exchange, call ``sync_object(model)`` on every rank before
+        reading the object outside recon_step."""
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.split_batches = split_batches
         self.always_reduce = bool(always_reduce) and dist.is_initialized()
-        self.band_exchange = bool(band_exchange)
+        self.band_exchange = None if band_exchange is None else bool(band_exchange)
         self.bands = None
         self.block_split = None   # the split decision local_indices built a measurement block for
 
@@ -255,6 +261,47 @@ class DistContext:
             off += p.numel()
         return flat
 
+    def sync_object(self, model):
+        """Make the whole object current on every rank.  Call it on EVERY rank (it is a
+        collective) before reading the object outside recon_step — a checkpoint, a plot — when the
+        band exchange is in use: it leaves rows a rank neither owns nor reads out of date."""
+        if self.bands is not None and self.bands.stale:
+            self.bands.sync([model.opt_obja, model.opt_objp])
+        model._stale_object = False
+
+    def agree(self, *items, device=None):
+        """For each ``items`` tuple (plain values): whether every rank holds the same one.  ONE
+        all-reduce(MAX) of (h, -h) per tuple, h a 62-bit hash of its repr; every rank gets the
+        same answers, so every rank takes the same branch afterwards."""
+        if not self._collective():
+            return [True] * len(items)
+        hs = [int.from_bytes(hashlib.blake2b(repr(it).encode(), digest_size=8).digest(), "little") >> 2
+              for it in items]
+        on_dev = dist.get_backend(self.group) == "nccl" and device is not None
+        t = torch.tensor([v for h in hs for v in (h, -h)], dtype=torch.int64,
+                         device=device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        t = t.cpu().tolist()
+        return [t[2 * i] == h and -t[2 * i + 1] == h for i, h in enumerate(hs)]
+
+    def step_plan(self, batches, ga, split_ok, band, n_flat, cap):
+        """What this iteration's collectives depend on, as plain values: the mini-batches (sizes
+        and a CRC of their indices: every rank must iterate the same global batching), the
+        grad_accumulation, the split decision of every optimizer step and its engine-call ranges
+        (one loss-sum all-reduce each), the exchange and the flat gradient size.  Ranks that
+        disagree on any of these would pair mismatched RCCL collectives (a hang)."""
+        crc, sizes = 0, []
+        for b in batches:
+            a = np.ascontiguousarray(np.asarray(b).reshape(-1), dtype=np.int64)
+            crc = zlib.crc32(a.tobytes(), crc)
+            sizes.append(int(a.size))
+        steps = []
+        for g0 in range(0, len(batches), ga):
+            group = batches[g0:g0 + ga]
+            sp = bool(split_ok) and self.splits(group)
+            steps.append((sp, len(group), tuple(self.split_ranges(group, cap)) if sp else None))
+        return (self.world, int(ga), bool(split_ok), bool(band), int(n_flat), tuple(sizes), crc, tuple(steps))
+
     def allreduce(self, flat):
         """ONE all-reduce(sum) of the gradient buffer (in place)."""
         if self._collective() and flat is not None and flat.numel():
@@ -280,18 +327,23 @@ class ObjectBands:
     """Row-band ownership of the object for the band-sized gradient exchange (the
     ZeRO-1 option; replaces the object part of DDP's bucketed all-reduce, reconstruction.py:753).
 
-    Rank j owns rows [j·R, (j+1)·R) of every (O, Nz, Ny, Nx) object tensor, R = ⌈Ny / W⌉.  A rank's
-    windows touch rows [lo, hi) only (its shard of the scan), so its object gradient is zero
-    elsewhere:
+    Rank j owns rows [e_j, e_{j+1}) of every (O, Nz, Ny, Nx) object tensor.  The edges follow the
+    ranks' touched rows (a row-sharded scan: each edge is the middle of two neighbours' overlap,
+    so a band is the rank's own rows less half a window at each inner edge), or are uniform when
+    the touched ranges do not line up by rank.  A rank's windows touch rows [lo, hi) only, so its
+    object gradient is zero elsewhere.  Per optimizer step:
       reduce   each rank sends the rows of [lo, hi) that other ranks own to their owners (P2P); an
                owner adds what it receives to its own rows, in rank order;
       step     the caller's optimizer class, with the same hyperparameters, steps views of the
                owned rows (optimizer state for 1/W of the object per rank);
-      gather   the updated bands are all-gathered, so every rank again holds the whole object
-               (the constraints and the next forward read any row).
-    Gradient bytes sent per rank: the touched rows outside the own band (the halo of a row-sharded
-    scan) instead of a full-object all-reduce; the all-gather moves (W − 1) / W of the object.  A
-    pixel that at most two ranks touch gets the same sum as the all-reduce bit for bit (a + b);
+      halo     each owner sends its updated rows that other ranks touch back to them (P2P): every
+               rank again holds current values of the rows its windows read.
+    Bytes per rank and step: twice the touched rows outside the own band (the halo of a
+    row-sharded scan), instead of a full-object all-reduce (2·(W−1)/W of the object).  Rows a rank
+    neither owns nor touches go stale; ``sync`` (one all-gather of the bands) refreshes the whole
+    object when a consumer needs it: a constraint with a global footprint (recon_step checks
+    CombinedConstraint.object_footprint), a checkpoint or a plot (``DistContext.sync_object``).
+    A pixel that at most two ranks touch gets the same sum as the all-reduce bit for bit (a + b);
     with more contributors only the fp32 summation order differs.
 
     Optimizer state: the objects' moments live in this rank's band optimizer (``ObjectBands.opt``),
@@ -299,65 +351,107 @@ class ObjectBands:
     does not hold them: a run resumed from such a checkpoint restarts the object moments.  The
     band optimizer's hyperparameters (lr, betas, …) are copied from the caller's groups every step."""
 
-    def __init__(self, ctx, Ny, device):
+    def __init__(self, ctx, Ny, device, ranges=None):
         self.ctx, self.Ny, self.device = ctx, int(Ny), device
         W = ctx.world
-        self.R = -(-self.Ny // W)
-        self.b0 = min(self.Ny, ctx.rank * self.R)
-        self.b1 = min(self.Ny, (ctx.rank + 1) * self.R)
-        self.ranges = [(0, self.Ny)] * W
+        self.ranges = list(ranges) if ranges is not None else [(0, self.Ny)] * W
+        self.edges = self.band_edges(self.ranges, self.Ny, W)
+        self.b0, self.b1 = self.edges[ctx.rank], self.edges[ctx.rank + 1]
+        self.stale = False        # rows outside [b0, b1) ∪ [lo, hi) may be out of date
         self.opt = None
         self._src_groups = []   # the caller's param group behind each band-optimizer group
         self.views = {}
 
+    @staticmethod
+    def band_edges(ranges, Ny, W):
+        """W + 1 edges: the middles of neighbouring ranks' touched ranges when those are ordered by
+        rank (lo and hi increasing), else the uniform split ⌈Ny / W⌉."""
+        lo = [r[0] for r in ranges]
+        hi = [r[1] for r in ranges]
+        if W > 1 and all(lo[j] < lo[j + 1] and hi[j] < hi[j + 1] for j in range(W - 1)) and \
+                all(h > l for l, h in ranges):
+            e = [0]
+            for j in range(1, W):
+                e.append(min(Ny, max(e[-1], (hi[j - 1] + lo[j]) // 2)))
+            return e + [Ny]
+        R = -(-Ny // W)
+        return [min(Ny, j * R) for j in range(W)] + [Ny]
+
+    @classmethod
+    def disjoint(cls, ranges, Ny, W, halo):
+        """The ranks' touched rows line up by rank and each reaches at most ``halo`` rows past its
+        band: the band exchange then moves halos instead of whole objects (the auto default)."""
+        e = cls.band_edges(ranges, Ny, W)
+        ordered = all(ranges[j][0] < ranges[j + 1][0] and ranges[j][1] < ranges[j + 1][1] for j in range(W - 1))
+        return W > 1 and ordered and all(h > l and l >= e[j] - halo and h <= e[j + 1] + halo
+                                         for j, (l, h) in enumerate(ranges))
+
     def set_rows(self, lo, hi):
         """Every rank's touched rows [lo, hi), exchanged (one small all-gather; every rank calls it)."""
-        W = self.ctx.world
-        rng_ = torch.tensor([int(lo), int(hi)], dtype=torch.int64, device=self.device)
-        allr = [torch.zeros_like(rng_) for _ in range(W)]
-        if W > 1:
-            dist.all_gather(allr, rng_, group=self.ctx.group)
-        else:
-            allr = [rng_]
-        self.ranges = [(int(r[0]), int(r[1])) for r in allr]
+        self.ranges = exchange_ranges(self.ctx, lo, hi, self.device)
 
     def band(self, j):
-        return min(self.Ny, j * self.R), min(self.Ny, (j + 1) * self.R)
+        return self.edges[j], self.edges[j + 1]
 
     def _peer(self, r):
         return dist.get_global_rank(self.ctx.group, r) if self.ctx.group is not None else r
 
     def sent_rows(self):
-        """Rows this rank sends in reduce() (the all-reduce would move 2·(W−1)/W of Ny)."""
+        """Rows this rank sends in reduce() — and receives back in halo() (the all-reduce would
+        move 2·(W−1)/W of Ny)."""
         lo, hi = self.ranges[self.ctx.rank]
         return sum(max(0, min(hi, self.band(j)[1]) - max(lo, self.band(j)[0]))
                    for j in range(self.ctx.world) if j != self.ctx.rank)
 
+    def halo_rows(self):
+        """Rows of this rank's band that other ranks touch (sent in halo())."""
+        return sum(max(0, min(h, self.b1) - max(l, self.b0))
+                   for i, (l, h) in enumerate(self.ranges) if i != self.ctx.rank)
+
+    def _exchange(self, t, sends, recvs):
+        """One batched P2P group: sends [(peer, a, b)] rows of t, receives [(peer, a, b)] rows into
+        fresh buffers; returns [(a, b, buf)] in peer order."""
+        ops, bufs = [], []
+        for j, a, b in sends:
+            ops.append(dist.P2POp(dist.isend, t[:, :, a:b].contiguous(), self._peer(j), self.ctx.group))
+        for i, a, b in recvs:
+            buf = torch.empty(t[:, :, a:b].shape, dtype=t.dtype, device=t.device)
+            ops.append(dist.P2POp(dist.irecv, buf, self._peer(i), self.ctx.group))
+            bufs.append((a, b, buf))
+        # one batched group: RCCL pairs every send with its receive without ordering deadlocks
+        for req in (dist.batch_isend_irecv(ops) if ops else []):
+            req.wait()
+        return bufs
+
+    def _pairs(self, mine_rows):
+        """(peer, a, b) row blocks: mine_rows=True → my touched rows in peer j's band (reduce
+        sends, halo receives); False → peer i's touched rows in my band (reduce receives, halo
+        sends)."""
+        me, W = self.ctx.rank, self.ctx.world
+        out = []
+        for j in range(W):
+            if j == me:
+                continue
+            if mine_rows:
+                a, b = max(self.ranges[me][0], self.band(j)[0]), min(self.ranges[me][1], self.band(j)[1])
+            else:
+                a, b = max(self.ranges[j][0], self.b0), min(self.ranges[j][1], self.b1)
+            if a < b:
+                out.append((j, a, b))
+        return out
+
     def reduce(self, grads):
         """grads: (O, Nz, Ny, Nx) object-gradient tensors, in place: the owner's rows get the sum."""
-        me, W = self.ctx.rank, self.ctx.world
-        lo, hi = self.ranges[me]
         for g in grads:
-            ops, bufs = [], []
-            for j in range(W):                     # send my touched rows of band j to its owner
-                if j == me:
-                    continue
-                a, b = max(lo, self.band(j)[0]), min(hi, self.band(j)[1])
-                if a < b:
-                    ops.append(dist.P2POp(dist.isend, g[:, :, a:b].contiguous(), self._peer(j), self.ctx.group))
-            for i in range(W):                     # receive rank i's rows of my band
-                if i == me:
-                    continue
-                a, b = max(self.ranges[i][0], self.b0), min(self.ranges[i][1], self.b1)
-                if a < b:
-                    buf = torch.empty(g[:, :, a:b].shape, dtype=g.dtype, device=g.device)
-                    ops.append(dist.P2POp(dist.irecv, buf, self._peer(i), self.ctx.group))
-                    bufs.append((a, b, buf))
-            # one batched group: RCCL pairs every send with its receive without ordering deadlocks
-            for req in (dist.batch_isend_irecv(ops) if ops else []):
-                req.wait()
-            for a, b, buf in bufs:                 # in rank order
+            for a, b, buf in self._exchange(g, self._pairs(True), self._pairs(False)):   # in rank order
                 g[:, :, a:b] += buf
+
+    def halo(self, params):
+        """The owners' current rows back to every rank whose windows read them."""
+        for p in params:
+            for a, b, buf in self._exchange(p.data, self._pairs(False), self._pairs(True)):
+                p.data[:, :, a:b] = buf
+        self.stale = self.ctx.world > 1
 
     def step(self, optimizer, params, candidates=None):
         """Step `optimizer`'s class on the owned rows of the object params (their .grad holds the
@@ -373,7 +467,7 @@ class ObjectBands:
                     views = []
                     for p in mine:
                         v = torch.nn.Parameter(p.data[:, :, self.b0:self.b1])   # shares p's storage
-                        self.views[id(p)] = v
+                        self.views[id(p)] = (p, v)
                         views.append(v)
                     groups.append({**{k: v for k, v in gr.items() if k != "params"}, "params": views})
                     self._src_groups.append(gr)
@@ -383,23 +477,27 @@ class ObjectBands:
                 for k, v in gr.items():
                     if k != "params":
                         bg[k] = v
-        for v in self.views.values():
+        for p, v in self.views.values():
             v.grad = None
+            band = p.data[:, :, self.b0:self.b1]
+            if v.data.data_ptr() != band.data_ptr():   # a constraint replaced the tensor's storage
+                v.data = band
         for p in params:
-            v = self.views.get(id(p))
-            if v is not None:
-                v.grad = p.grad[:, :, self.b0:self.b1] if p.grad is not None else None
+            pv = self.views.get(id(p))
+            if pv is not None:
+                pv[1].grad = p.grad[:, :, self.b0:self.b1] if p.grad is not None else None
         if self.opt is not None:
             self.opt.step()
-            for v in self.views.values():
+            for _, v in self.views.values():
                 v.grad = None
 
-    def gather(self, params):
-        """Every rank receives every owner's updated rows."""
+    def sync(self, params):
+        """Every rank receives every owner's rows: the whole object is current again."""
         W = self.ctx.world
+        Rm = max(self.edges[j + 1] - self.edges[j] for j in range(W))
         for p in params:
             O, Nz, _, Nx = p.shape
-            mine = torch.zeros((O, Nz, self.R, Nx), dtype=p.dtype, device=p.device)
+            mine = torch.zeros((O, Nz, Rm, Nx), dtype=p.dtype, device=p.device)
             mine[:, :, :self.b1 - self.b0] = p.data[:, :, self.b0:self.b1]
             out = torch.empty(W * mine.numel(), dtype=p.dtype, device=p.device)
             if W > 1:
@@ -411,6 +509,22 @@ class ObjectBands:
                 a, b = self.band(j)
                 if a < b and j != self.ctx.rank:
                     p.data[:, :, a:b] = out[j, :, :, :b - a]
+        self.stale = False
+
+    gather = sync
+
+
+def exchange_ranges(ctx, lo, hi, device):
+    """Every rank's (lo, hi) (one small all-gather; every rank calls it)."""
+    W = ctx.world
+    rng_ = torch.tensor([int(lo), int(hi)], dtype=torch.int64,
+                        device=device if dist.is_initialized() and dist.get_backend(ctx.group) == "nccl" else "cpu")
+    allr = [torch.zeros_like(rng_) for _ in range(W)]
+    if W > 1:
+        dist.all_gather(allr, rng_, group=ctx.group)
+    else:
+        allr = [rng_]
+    return [(int(r[0]), int(r[1])) for r in allr]
 
 
 def touched_rows(model, batches, N):
@@ -465,16 +579,23 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
                          "split mini-batches: build it with local_indices(..., loss_fn=loss_fn, model_params=..., "
                          "init_variables=...)")
     objs = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in live)]
-    band = ctx.band_exchange and ctx._collective() and bool(objs)
-    if band:
-        if ctx.bands is None:
-            ctx.bands = ObjectBands(ctx, model.opt_obja.shape[2], dev)
-        # the rows this rank's windows reach this iteration (recomputed: the batches may change)
-        lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok),
-                              int(model.opt_probe.shape[1]))
-        ctx.bands.set_rows(lo, hi)
-        obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
-        live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
+    band = False
+    obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
+    if ctx.band_exchange is not False and ctx._collective() and objs:
+        # the rows each rank's windows reach this iteration (recomputed: the batches may change);
+        # band_exchange None = auto: by band when the ranks' rows line up (a row-sharded scan)
+        N = int(model.opt_probe.shape[1])
+        lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok), N)
+        ranges = exchange_ranges(ctx, lo, hi, dev)
+        Ny = int(model.opt_obja.shape[2])
+        if ctx.bands is None and (ctx.band_exchange or ObjectBands.disjoint(ranges, Ny, ctx.world, N)):
+            ctx.bands = ObjectBands(ctx, Ny, dev, ranges)
+        if ctx.bands is not None:
+            band = True
+            ctx.bands.ranges = ranges
+            if ctx.bands.stale:
+                ctx.bands.halo(obj_all)      # rows this iteration reads, current from their owners
+            live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
     rows = []
     use_graphs = False
     if graphs is not False and not band:
@@ -485,6 +606,24 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         use_graphs = why is None and (graphs or -(-len(batches) // ga) >= GRAPH_MIN_STEPS) and bool(live)
     # with collectives, the step's loss terms ride in the gradient all-reduce (5·ga extra floats)
     extra = 5 * ga if ctx._collective() else 0
+    if ctx._collective():
+        # before any step collective: every rank must plan the same collective sequence (else
+        # refuse on every rank instead of hanging in RCCL), and take the same graph decision
+        # (else every rank runs the eager steps)
+        cap = model.plan.call_capacity if hasattr(model, "plan") else None
+        plan_fp = ctx.step_plan(batches, ga, split_ok, band, sum(p.numel() for p in live) + extra, cap)
+        same_plan, same_mode = ctx.agree(plan_fp, ("graphs", bool(use_graphs)), device=dev)
+        if not same_plan:
+            raise RuntimeError(f"recon_step iteration {niter} (rank {ctx.rank}): the ranks disagree on the "
+                               "iteration's mini-batches, grad_accumulation, split decision or parameter set, so "
+                               "their collectives would not pair up; every rank must pass the same global batches")
+        if not same_mode:
+            if not getattr(ctx, "_warned_graphs", False):
+                print(f"[ptyrad_amd] rank {ctx.rank}: ranks disagree on graph-replay eligibility "
+                      f"(this rank: {'eligible' if use_graphs else 'not eligible'}); every rank runs eager steps",
+                      flush=True)
+                ctx._warned_graphs = True
+            use_graphs = False
     if use_graphs:
         sg = getattr(model, "_step_graphs", None)
         if sg is None:
@@ -532,7 +671,7 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             for p, g in zip(objs, saved):
                 p.grad = g
             ctx.bands.step(optimizer, objs, obj_all)
-            ctx.bands.gather(objs)
+            ctx.bands.halo(objs)                       # updated rows back to the ranks that read them
         else:
             ctx.allreduce(flat)
             optimizer.step()
@@ -544,8 +683,12 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         for name, v in zip(LOSS_TERM_NAMES, row):
             if name in batch_losses:
                 batch_losses[name].append(v)
+    check_plans(model, niter)
     if constraint_fn is not None:
+        if band and ctx.bands.stale and object_footprint(constraint_fn, niter) == "global":
+            ctx.bands.sync(obj_all)              # (a Fourier filter / blur / global min reads every row)
         constraint_fn(model, niter)
+    model._stale_object = bool(band and ctx.bands.stale)
     iter_t = time_sync() - t0
     model.loss_iters.append((niter, loss_logger(batch_losses, niter, iter_t, verbose=verbose)))
     model.iter_times.append(iter_t)
@@ -554,12 +697,38 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     return batch_losses
 
 
+def object_footprint(constraint_fn, niter):
+    """What the constraints of this iteration read of the object: 'none', 'pointwise' (every pixel
+    from its own value: a rank's current rows stay exact) or 'global' (anything else, and any
+    constraint function that does not say)."""
+    f = getattr(constraint_fn, "object_footprint", None)
+    return f(niter) if f is not None else "global"
+
+
+def check_plans(model, niter):
+    """Raise the input errors (scan index, window, measurement row out of range) that the device
+    flagged during this iteration's engine calls, right after the iteration's one host sync.
+    Graph-replayed steps never pass through Plan's per-call check, so without this a bad index
+    would surface only at some later eager call (ptyx_plan_check: a host read, no sync)."""
+    plans = [getattr(model, "_plan", None)] + list(getattr(model, "_stack_plans", {}).values())
+    for pl in plans:
+        if pl is None:
+            continue
+        try:
+            pl._prev_errors()
+        except IndexError as e:
+            raise IndexError(f"recon_step iteration {niter}: {e}") from None
+
+
 def recon_loop(model, optimizer, loss_fn, constraint_fn, batches, NITER, grad_accumulation=1, verbose=True,
                dist_ctx=None):
-    """Minimal recon_loop (reconstruction.py:589-656) without saving/plotting."""
+    """Minimal recon_loop (reconstruction.py:589-656) without saving/plotting; the whole object is
+    current on every rank when it returns."""
     for niter in range(1, NITER + 1):
         recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint_fn, niter, verbose=verbose,
                    dist_ctx=dist_ctx)
+    if dist_ctx is not None:
+        dist_ctx.sync_object(model)
     return model.loss_iters
 
 

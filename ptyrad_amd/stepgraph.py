@@ -43,7 +43,7 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
     the same path."""
     if not torch.cuda.is_available() or model.opt_obja.device.type != "cuda":
         return "no HIP device"
-    if ctx is not None and ctx.band_exchange:
+    if ctx is not None and (ctx.band_exchange or ctx.bands is not None):
         return "band exchange (point-to-point collectives per step)"
     if not (hasattr(loss_fn, "_special") and hasattr(loss_fn, "supports_batch_split")):
         return "loss_fn is not ptyrad_amd.losses.CombinedLoss"

@@ -146,6 +146,7 @@ def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band
     cfn = None
     if "constraint_params" in z.files and json.loads(str(z["constraint_params"])) is not None:
         cp, pis = json.loads(str(z["constraint_params"])), float(z["probe_int_sum"])
+        from ptyrad_amd.constraints import object_footprint
 
         def cfn(m, it):   # the constraints oracle on the replica's parameters (every rank alike)
             from tests.test_oracle_golden import apply_constraint_oracle
@@ -156,8 +157,10 @@ def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band
                 m.opt_obja.copy_(torch.from_numpy(prm["obja"]))
                 m.opt_objp.copy_(torch.from_numpy(prm["objp"]))
                 m.opt_probe.copy_(torch.from_numpy(prm["probe"]))
+        cfn.object_footprint = lambda it: object_footprint(cp, it)   # as CombinedConstraint reports it
     for it in range(1, (niter or int(z["niter"])) + 1):
         recon_step(batches, int(z["grad_accumulation"]), model, opt, loss, cfn, it, verbose=False, dist_ctx=ctx)
+    ctx.sync_object(model)
     model._band_ctx = ctx
     return {k: v.detach().numpy().copy() for k, v in (("obja", model.opt_obja), ("objp", model.opt_objp),
                                                        ("probe", model.opt_probe),
@@ -228,5 +231,110 @@ def gpu_dist_worker(rank, world, port, path, out_path):
         np.savez(out_path.replace(".npz", f"_r{rank}.npz"), obja=model.opt_obja.detach().cpu().numpy(),
                  objp=model.opt_objp.detach().cpu().numpy(), probe=model.opt_probe.detach().cpu().numpy(),
                  held=np.array(model.measurements.shape[0]))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+class _NpzDict(dict):
+    """An editable copy of an np.load result (keeps its ``.files``)."""
+    def __init__(self, z):
+        super().__init__({k: z[k] for k in z.files})
+
+    @property
+    def files(self):
+        return list(self.keys())
+
+
+def mismatch_worker(rank, world, port, path, out_path, mode):
+    """One gloo rank of a deliberately inconsistent job.  mode 'batches': rank 1 iterates another
+    batching (its collectives would not pair up) -> every rank must refuse with RuntimeError
+    instead of hanging.  mode 'graphs': only rank 0 believes its steps can be graph-replayed ->
+    every rank must fall back to eager steps and finish the same trajectory."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        z = np.load(path, allow_pickle=False)
+        if mode == "batches" and rank == 1:
+            sizes = z["batch_sizes"]
+            rev = np.concatenate(np.split(z["batches"], np.cumsum(sizes)[:-1])[::-1])
+            z = _NpzDict(z)
+            z["batches"], z["batch_sizes"] = rev, sizes[::-1].copy()
+        if mode == "graphs" and rank == 0:
+            import ptyrad_amd.reconstruction as rec
+            import ptyrad_amd.stepgraph as sg
+            sg.ineligible_reason = lambda *a, **k: None
+            rec.GRAPH_MIN_STEPS = 1
+        try:
+            params, model = run_recon(z, niter=2)
+            res = {"ok": np.array(1), **params}
+        except RuntimeError as e:
+            res = {"ok": np.array(0), "msg": np.array(str(e))}
+        np.savez(out_path.replace(".npz", f"_r{rank}.npz"), **res)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def row_sharded_problem(W, seed=0, N=32, rows_per_rank=2, n_fast=3, step_px=18.0, niter=3):
+    """A trajectory-fixture-shaped problem whose scan is sharded by rows over W ranks: rank r's
+    mini-batches hold only scan rows [r·rows_per_rank, (r+1)·rows_per_rank) (grad_accumulation =
+    W, whole mini-batches dealt round-robin), and the scan step is large enough that every object
+    pixel is reached by at most two ranks.  Pointwise object constraints every iteration and a
+    Fourier filter (a global footprint) in the last one."""
+    from ptyrad_amd import synthetic as syn
+    rng = np.random.default_rng(seed)
+    sc = syn.raster_scan(W * rows_per_rank, n_fast, N, step_px=step_px, seed=seed)
+    S = sc.crop_pos.shape[0]
+    Ny, Nx = sc.obj_shape
+    z = _NpzDict.__new__(_NpzDict)
+    dict.__init__(z)
+    z["init_obja"] = (1.0 + 0.02 * rng.standard_normal((1, 1, Ny, Nx))).astype(np.float32)
+    z["init_objp"] = (0.05 * rng.standard_normal((1, 1, Ny, Nx))).astype(np.float32)
+    z["init_probe"] = (syn.stem_probe(N) * np.float32(20.0))[None].astype(np.complex64)
+    z["init_shifts"] = sc.shifts.astype(np.float32)
+    z["crop_pos"] = sc.crop_pos.astype(np.int32)
+    z["H"] = syn.fresnel_propagator(N, syn.DX_ANG, 2.0)
+    z["occu"] = np.ones(1, np.float32)
+    z["meas"] = rng.random((S, N, N)).astype(np.float32)
+    z["lrs"] = np.array(json.dumps({"obja": 1e-3, "objp": 1e-3, "obj_tilts": 0, "slice_thickness": 0,
+                                    "probe": 1e-4, "probe_pos_shifts": 1e-3}))
+    z["loss_params"] = np.array(json.dumps({
+        "loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
+        "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
+        "loss_pacbed": {"state": False, "weight": 0.5, "dp_pow": 0.2},
+        "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1}, "loss_simlar": {"state": False}}))
+    per_rank = rows_per_rank * n_fast
+    batches = []
+    for half in range(2):                       # two optimizer steps per iteration
+        for r in range(W):
+            own = np.arange(r * per_rank, (r + 1) * per_rank)
+            batches.append(np.array_split(own, 2)[half])
+    z["batches"] = np.concatenate(batches).astype(np.int64)
+    z["batch_sizes"] = np.array([len(b) for b in batches])
+    z["grad_accumulation"] = np.array(W)
+    z["niter"] = np.array(niter)
+    z["constraint_params"] = np.array(json.dumps({
+        "mirrored_amp": {"freq": 1, "relax": 0.1, "scale": 0.03, "power": 4.0},
+        "obja_thresh": {"freq": 1, "relax": 0.0, "thresh": [0.98, 1.02]},
+        "objp_postiv": {"freq": 1, "relax": 0.0, "mode": "clip_neg"},
+        "kr_filter": {"freq": niter, "obj_type": "both", "radius": 0.15, "width": 0.05}}))
+    z["probe_int_sum"] = np.array(float(np.sum(np.abs(z["init_probe"]) ** 2)))
+    return z
+
+
+def band_worker(rank, world, port, out_path, band):
+    """One gloo rank of the row-sharded problem with band_exchange = band (None: auto)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        z = row_sharded_problem(world)
+        params, model = run_recon(z, band=band)
+        ctx = model._band_ctx
+        np.savez(out_path.replace(".npz", f"_r{rank}.npz"), **params,
+                 banded=np.array(ctx.bands is not None),
+                 sent_rows=np.array(ctx.bands.sent_rows() if ctx.bands is not None else -1),
+                 halo_rows=np.array(ctx.bands.halo_rows() if ctx.bands is not None else -1),
+                 ny=np.array(model.opt_obja.shape[2]))
     finally:
         torch.distributed.destroy_process_group()

@@ -227,3 +227,87 @@ def test_band_exchange_equals_flat_allreduce(tmp_path, name, start):
     for k in ("obja", "objp", "probe", "shifts"):
         assert np.array_equal(outs[True][0][k], outs[True][1][k]), f"band replicas diverged in {k}"
         assert np.array_equal(outs[True][0][k], outs[False][0][k]), f"band != all-reduce in {k}"
+
+
+def test_mismatched_ranks_refuse_instead_of_hanging(tmp_path):
+    """A rank iterating another batching would pair mismatched collectives: recon_step's
+    fingerprint all-reduce makes EVERY rank raise before the first step collective."""
+    from tests.dist_helpers import mismatch_worker
+    path = [p for p in TRAJ if "traj_n32_p2_ga2" in p][0]
+    out = str(tmp_path / "m.npz")
+    mp.start_processes(mismatch_worker, args=(2, free_port(), path, out, "batches"), nprocs=2, start_method="spawn")
+    for r in range(2):
+        z = np.load(out.replace(".npz", f"_r{r}.npz"))
+        assert int(z["ok"]) == 0 and "disagree" in str(z["msg"])
+
+
+def test_graph_decision_disagreement_falls_back_to_eager(tmp_path):
+    """Only rank 0 thinks its steps are graph-eligible: both ranks run eager steps (logged) and
+    finish the ordinary two-rank trajectory."""
+    from tests.dist_helpers import mismatch_worker
+    path = [p for p in TRAJ if "traj_n32_p2_ga2" in p][0]
+    z = np.load(path, allow_pickle=False)
+    single, _ = run_recon(z, niter=2)
+    out = str(tmp_path / "g.npz")
+    mp.start_processes(mismatch_worker, args=(2, free_port(), path, out, "graphs"), nprocs=2, start_method="spawn")
+    r0, r1 = (np.load(out.replace(".npz", f"_r{r}.npz")) for r in range(2))
+    assert int(r0["ok"]) == 1 and int(r1["ok"]) == 1
+    for k in ("obja", "objp", "probe", "shifts"):
+        assert np.array_equal(r0[k], r1[k])
+        np.testing.assert_allclose(r0[k], single[k], rtol=0, atol=2e-6)
+
+
+def test_agree_and_step_plan_single_process():
+    """Without collectives agree() is trivially true; step_plan changes with the batching."""
+    from ptyrad_amd.reconstruction import DistContext
+    ctx = DistContext()
+    assert ctx.agree((1, 2), ("x",)) == [True, True]
+    b = [np.arange(4), np.arange(4, 8)]
+    p1 = ctx.step_plan(b, 1, True, False, 100, None)
+    assert p1 == ctx.step_plan([x.copy() for x in b], 1, True, False, 100, None)
+    assert p1 != ctx.step_plan(b[::-1], 1, True, False, 100, None)
+    assert p1 != ctx.step_plan(b, 2, True, False, 100, None)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_band_exchange_row_sharded_auto_equals_flat(tmp_path, world):
+    """A row-sharded scan (each rank's mini-batches from its own scan rows, every pixel reached by
+    at most two ranks): the default DistContext picks the band exchange by itself (halo rows to
+    the owners, Adam on the owned band, updated rows back to their readers, no per-step
+    all-gather; the whole object is synced only before the Fourier-filter constraint of the last
+    iteration and at the end).  3 iterations with object constraints: every rank holds the same
+    parameters; at two ranks they equal the flat all-reduce bit for bit; at three and four the
+    probe / position gradients (which every rank contributes to) are all-reduced in a buffer of
+    another size than the flat one, so gloo sums their three or four terms in another order: equal
+    to fp32 summation order (2e-6), as is the one-rank run."""
+    from tests.dist_helpers import band_worker, row_sharded_problem
+    outs = {}
+    for band in (None, False):
+        out = str(tmp_path / f"b{band}.npz")
+        mp.start_processes(band_worker, args=(world, free_port(), out, band), nprocs=world, start_method="spawn")
+        outs[band] = [np.load(out.replace(".npz", f"_r{r}.npz")) for r in range(world)]
+    single, _ = run_recon(row_sharded_problem(world))
+    for r in range(world):
+        assert bool(outs[None][r]["banded"]) and not bool(outs[False][r]["banded"])
+        # halo traffic: a few window heights, far below the object's rows
+        assert 0 < int(outs[None][r]["sent_rows"]) + int(outs[None][r]["halo_rows"]) <= 4 * 32
+        for k in ("obja", "objp", "probe", "shifts"):
+            assert np.array_equal(outs[None][r][k], outs[None][0][k]), f"band replicas diverged in {k}"
+            if world == 2:
+                assert np.array_equal(outs[None][r][k], outs[False][0][k]), f"band != all-reduce in {k}"
+            else:
+                np.testing.assert_allclose(outs[None][r][k], outs[False][0][k], rtol=0, atol=2e-6)
+    for k in ("obja", "objp", "probe", "shifts"):
+        np.testing.assert_allclose(outs[None][0][k], single[k], rtol=0, atol=2e-6)
+
+
+def test_band_edges_and_auto_rule():
+    """Owner edges sit in the middle of neighbouring ranks' overlaps; the auto rule takes the band
+    exchange only for ranges ordered by rank that stay within a window of their bands."""
+    from ptyrad_amd.reconstruction import ObjectBands
+    rows = [(0, 300), (256, 556), (512, 812), (768, 1068)]          # 256-row shards, 44-row overlaps
+    assert ObjectBands.band_edges(rows, 1068, 4) == [0, 278, 534, 790, 1068]
+    assert ObjectBands.disjoint(rows, 1068, 4, 128)
+    assert not ObjectBands.disjoint([(0, 1068)] * 4, 1068, 4, 128)          # random batches: all rows
+    assert not ObjectBands.disjoint(rows[::-1], 1068, 4, 128)               # not ordered by rank
+    assert ObjectBands.band_edges([(0, 10)] * 3, 30, 3) == [0, 10, 20, 30]  # (uniform fallback)

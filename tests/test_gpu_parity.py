@@ -85,9 +85,9 @@ def run_fused(d, device, batches, grad_scale=1.0, meas_f16=False, want=("obja", 
 
 # the engine each BASELINE-config / demo-shaped fixture (make_golden.py --large) must run on
 ENGINE_OF = {"n256_p8o2z1_c3": "k_s1", "n256_p4o1z1_c5f16": "k_s1", "n128_p1o1z16_c4": "k_fused",
-             "n128_p6o1z6_tbl": "k_fused", "n256_p4o1z5_pso": "k_adjoint",
+             "n128_p6o1z6_tbl": "k_fmm_fwd", "n256_p4o1z5_pso": "k_adjoint",
              # loss_single + loss_poissn (make_golden.py --both-terms): the two-pass register / stripe paths
-             "n128_p1o1z1_both": "k_fused", "n128_p1o1z3_both": "k_fused", "n128_p3o1z2_both": "k_fused",
+             "n128_p1o1z1_both": "k_fused", "n128_p1o1z3_both": "k_fused", "n128_p3o1z2_both": "k_fmm_fwd",
              "n256_p2o2z1_both": "k_s3"}
 
 
@@ -681,7 +681,7 @@ def test_mixed_state_register_engine_vs_oracle(P, Nz, shift, q):
     batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
     ks = {}
     terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
-    assert "k_fused" in ks and "k_adjoint" in ks, ks
+    assert "k_fmm_fwd" in ks and "k_adjoint" in ks, ks
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"],
                                              shift_probes=shift, grad_scale=0.5)
@@ -705,7 +705,7 @@ def test_mixed_state_register_engine_poisson_and_binned_gather():
     batches = np.array_split(perm, 10)
     ks = {}
     terms, dp, g, _ = run_fused(d, device, batches, kernels=ks)
-    assert "k_fused" in ks and "k_obj_gather" in ks, ks
+    assert "k_fmm_fwd" in ks and "k_obj_gather" in ks, ks
     terms2, _, g2, _ = run_fused(d, device, batches)
     assert np.array_equal(terms, terms2) and np.array_equal(g["obja"], g2["obja"]) and np.array_equal(g["probe"], g2["probe"])
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
@@ -728,7 +728,7 @@ def test_mixed_state_call_split_at_batch_boundaries(monkeypatch):
     assert make_plan(d, device).register_capacity == 17
     ks = {}
     terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
-    assert ks["k_fused"][0] >= 3, ks
+    assert ks["k_fmm_fwd"][0] >= 3, ks
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"], grad_scale=0.5)
     assert rel(dp, np.concatenate(odps)) < TOL_DP

@@ -62,9 +62,9 @@ GEOMS = {"fused3": (128, 1, 1, 1), "fused3ms": (128, 1, 1, 3), "fmm": (128, 3, 1
          "stripe_o2": (256, 2, 2, 1), "two_pass": (64, 2, 2, 2), "stripe_both": (256, 2, 1, 1),
          "stripe_o2_both": (256, 2, 2, 1), "fmm_both": (128, 3, 1, 2), "fused3_both": (128, 1, 1, 1),
          "fused3ms_both": (128, 1, 1, 3)}
-ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "fmm": "k_fused", "stripe": "k_s3",
+ENGINE_KERNEL = {"fused3": "k_fused", "fused3ms": "k_fused", "fmm": "k_fmm_fwd", "stripe": "k_s3",
                  "stripe_o2": "k_obj_gather", "two_pass": "k_forward", "stripe_both": "k_s3",
-                 "stripe_o2_both": "k_obj_gather", "fmm_both": "k_fused", "fused3_both": "k_fused",
+                 "stripe_o2_both": "k_obj_gather", "fmm_both": "k_fmm_fwd", "fused3_both": "k_fused",
                  "fused3ms_both": "k_fused"}
 
 

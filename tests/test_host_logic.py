@@ -149,3 +149,32 @@ def test_stepgraph_tables_and_eligibility_on_cpu():
     class M:
         opt_obja = torch.zeros(1)
     assert ineligible_reason(M(), None, None, None, batches, 1) == "no HIP device"
+
+
+def test_check_plans_names_the_iteration():
+    """recon_step surfaces device-flagged input errors after the iteration's sync (graph-replayed
+    steps bypass Plan's per-call check), naming the iteration; plans without errors pass."""
+    import pytest
+    from ptyrad_amd.reconstruction import check_plans
+
+    class _Plan:
+        def __init__(self, bad):
+            self.bad, self.calls = bad, 0
+
+        def _prev_errors(self):
+            self.calls += 1
+            if self.bad:
+                raise IndexError("scan index 70000 out of range [0, 65536)")
+
+    class _Model:
+        pass
+    m = _Model()
+    m._plan, m._stack_plans = _Plan(False), {32: _Plan(False)}
+    check_plans(m, 3)
+    assert m._plan.calls == 1 and m._stack_plans[32].calls == 1
+    m._stack_plans[64] = _Plan(True)
+    with pytest.raises(IndexError, match=r"recon_step iteration 7: scan index 70000"):
+        check_plans(m, 7)
+    m2 = _Model()
+    m2._plan = None
+    check_plans(m2, 1)          # a pre-blur model without its main plan yet

@@ -56,7 +56,7 @@ def one(rng, device):
     tol = {"dp": TOL_DP, "terms": TOL_TERMS * 10, "obja": TOL_G, "objp": TOL_G,
            "probe": TOL_G_BOTH if both else TOL_G, "shifts": TOL_SH}
     bad = [k for k, v in e.items() if not v < tol[k]]
-    eng = "+".join(k for k in ("k_fused", "k_s1", "k_adjoint") if k in ks)
+    eng = "+".join(k for k in ("k_fused", "k_fmm_fwd", "k_s1", "k_adjoint") if k in ks)
     print(f"{'FAIL' if bad else 'ok  '} N={N:3d} P{P} O{O} Nz{Nz} shift={int(shift)} both={int(both)} cache={int(cache)} "
           f"batches={[len(b) for b in batches]} {eng:10s} " + " ".join(f"{k} {v:.1e}" for k, v in e.items()) +
           (f"  BAD {bad}" if bad else ""), flush=True)
