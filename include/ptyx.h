@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 204
+#define PTYX_ABI_VERSION 205
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -74,7 +74,7 @@ extern "C" {
 typedef struct ptyx_plan ptyx_plan;
 
 typedef struct ptyx_dims {
-  int32_t N;            /* probe / DP side: any 2^a 3^b 5^c in [32, 256] (else EUNSUPPORTED) */
+  int32_t N;            /* probe / DP side: any 2^a 3^b 5^c 7^d in [32, 256] but 245 (else EUNSUPPORTED) */
   int32_t P;            /* probe modes  (opt_probe.shape[0])                               */
   int32_t O;            /* object modes (opt_obja.shape[0])                                */
   int32_t Nz;           /* object slices (opt_obja.shape[1])                               */
@@ -170,11 +170,11 @@ int ptyx_forward_loss_grad(ptyx_plan *plan, void *stream, const ptyx_inputs *in,
  * single-device NRMSE normalisation losses.py:45-47 kept exact).
  *
  *   _begin runs the forward model and the loss partial sums of this rank's patterns and writes,
- *     per mini-batch of the call, PTYX_BATCH_SUMS doubles to batch_sums (n_batches, 13) f64 device:
+ *     per mini-batch of the call, PTYX_BATCH_SUMS doubles to batch_sums (n_batches, 37) f64 device:
  *     [pattern count, Σ(I^q-M^q)², ΣM^q (loss_single), Σ(M^q log(I^q+ε)-I^q), ΣM^q (loss_poissn),
- *      Σ|φ|^n per object mode (loss_sparse, 8 slots)].  Every quantity is additive over patterns.
+ *      Σ|φ|^n per object mode (loss_sparse, 32 slots)].  Every quantity is additive over patterns.
  *   the caller sums batch_sums over the ranks that hold parts of the same mini-batches (one
- *     all-reduce of n_batches·13 doubles), in place,
+ *     all-reduce of n_batches·37 doubles), in place,
  *   _end takes the summed batch_sums, writes loss_terms (n_batches,5) for the WHOLE mini-batches
  *     and accumulates this rank's share of the gradients; the ranks' gradients then sum (the
  *     caller's gradient all-reduce) to the single-device gradient of the whole mini-batches.
@@ -184,7 +184,7 @@ int ptyx_forward_loss_grad(ptyx_plan *plan, void *stream, const ptyx_inputs *in,
  * compute call may run on the plan in between (PTYX_EINVAL).  The call must fit the plan in one
  * piece (n_idx <= max_patterns and, for the register engines, <= ptyx_plan_register_capacity).
  * ptyx_forward_loss_grad is _begin + _end with the call's own sums (no collective). */
-#define PTYX_BATCH_SUMS 13
+#define PTYX_BATCH_SUMS 37
 int ptyx_forward_loss_grad_begin(ptyx_plan *plan, void *stream, const ptyx_inputs *in, const int32_t *idx,
                                  const int32_t *batch_offsets, int32_t n_batches, int32_t n_idx,
                                  const ptyx_loss_cfg *cfg, float *dp_out, const ptyx_grads *grads,
@@ -290,7 +290,7 @@ int ptyx_obj_constrain(void *stream, float *obja, float *objp, int32_t O, int32_
 int ptyx_probe_fix_int(void *stream, float *probe, int32_t P, int32_t N, const float *probe_int_sum, void *ws);
 
 /* ortho_pmode (constraints.py:34-41 → orthogonalize_modes_vec :255-291, sort=True): probe modes
- * (P,N,N,2), 1 ≤ P ≤ 16, replaced in place by V^H M sorted by descending power, V the
+ * (P,N,N,2), 1 ≤ P ≤ 64, replaced in place by V^H M sorted by descending power, V the
  * eigenvectors of M M^H (LAPACK geev normalisation).  Eigenvalues (P f64) land in
  * ws + ptyx_constraints_evals_offset(). */
 int ptyx_probe_ortho(void *stream, float *probe, int32_t P, int32_t N, void *ws);

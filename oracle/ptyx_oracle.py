@@ -392,7 +392,7 @@ def forward_loss_grad(obja, objp, probe, shifts, crop_pos, H, occu, meas, batche
     return np.array(all_terms), dps, grads
 
 
-N_BATCH_SUMS = 13   # include/ptyx.h PTYX_BATCH_SUMS
+N_BATCH_SUMS = 37   # include/ptyx.h PTYX_BATCH_SUMS
 
 
 def batch_sums(dp, meas, ph, lp):
@@ -445,7 +445,7 @@ def terms_from_sums(sums, n, Nz, occu, lp):
 def forward_loss_grad_parts(obja, objp, probe, shifts, crop_pos, H, occu, meas, parts, loss_params, reduce,
                             shift_probes=True, grad_scale=1.0, cdt=np.complex128):
     """Oracle of ptyx_forward_loss_grad_begin → all-reduce → _end for ONE rank: ``parts[m]`` is this
-    rank's share (possibly empty) of mini-batch m, ``reduce(sums)`` sums the (n_batches, 13) batch
+    rank's share (possibly empty) of mini-batch m, ``reduce(sums)`` sums the (n_batches, N_BATCH_SUMS) batch
     sums over the ranks in place.  Returns (terms of the whole mini-batches, grads of this rank's
     patterns); summed over the ranks the gradients equal forward_loss_grad over the whole batches."""
     if isinstance(loss_params, str):

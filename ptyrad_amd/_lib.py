@@ -14,10 +14,10 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 204     # include/ptyx.h
+PTYX_ABI_VERSION = 205     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_PREP_DEFER_PROBE = 4  # flag bit: the probe-gradient reduction may wait for a later piece
-PTYX_BATCH_SUMS = 13      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
+PTYX_BATCH_SUMS = 37      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
 PTYX_SHIFT_PROBES = 1
 PTYX_MEAS_F16 = 2

@@ -31,15 +31,27 @@ SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_cons
 GEN_SOURCE = os.path.join(HERE, "ptyx_gen.hip")
 
 
+def plan_r1(n: int) -> int:
+    """ptyx_fft.hpp plan_r1: the first-pass radix of the two-pass plan (0: none)."""
+    fixed = {16: 16, 32: 8, 64: 8, 128: 16, 256: 16}
+    if n in fixed:
+        return fixed[n]
+    for r in list(range(16, 1, -1)) + list(range(17, 28)):
+        if n % r == 0 and n // r <= 16:
+            return r
+    return 0
+
+
 def smooth_sizes(lo: int = 32, hi: int = 256):
-    """Every 2·3·5-smooth N in [lo, hi]: the general engine's supported sizes."""
+    """Every 2·3·5·7-smooth N in [lo, hi] with a two-pass plan (R1 ≤ 27, R2 ≤ 16): the general
+    engine's supported sizes (all but 245 = 5·7²)."""
     out = []
     for n in range(lo, hi + 1):
         m = n
-        for f in (2, 3, 5):
+        for f in (2, 3, 5, 7):
             while m % f == 0:
                 m //= f
-        if m == 1:
+        if m == 1 and plan_r1(n):
             out.append(n)
     return out
 

@@ -9,7 +9,7 @@
 
 namespace ptyx {
 
-constexpr int kMaxModesO = 8;
+constexpr int kMaxModesO = 32;                // object modes (loss_sparse sums / coefficients per mode)
 constexpr int kSumBase = 4;                    // [S_single, ΣM^q1, S_poissn, ΣM^q2] then O sparse sums
 constexpr int kNSum = kSumBase + kMaxModesO;
 constexpr int kNCoef = 2 + kMaxModesO;         // [c_single, c_poissn, c_sparse[o]...]

@@ -18,7 +18,7 @@ using cons::kMaxHalf;
 using cons::kMaxModes;
 using cons::kRedBlocks;
 constexpr int kGramChunks = 64;
-// workspace layout (doubles): stats[8] | partials[2·kRedBlocks] | gram[2·pairs·chunks] | evals[16]
+// workspace layout (doubles): stats[8] | partials[2·kRedBlocks] | gram[2·pairs·chunks] | evals[kMaxModes]
 // | U (kMaxModes² float2)
 constexpr size_t kWsStats = 0, kWsPart = 8, kWsGram = kWsPart + 2 * kRedBlocks,
                  kWsEvals = kWsGram + 2 * (kMaxModes * (kMaxModes + 1) / 2) * kGramChunks, kWsU = kWsEvals + kMaxModes;
@@ -70,9 +70,10 @@ void launch_column_h(int h, hipStream_t st, float* a, float* p, const cons::ObjC
     default: launch_column<7>(st, a, p, c, pw); break;
   }
 }
-template <int P>
-void launch_ortho_apply(hipStream_t st, float2* M, long long n2, const float2* U) {
-  hipLaunchKernelGGL(cons::k_ortho_apply<P>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, M, n2, U);
+template <int PM>
+void launch_ortho_apply(hipStream_t st, float2* M, long long n2, const float2* U, int P) {
+  constexpr int B = PM > 32 ? 128 : 256;
+  hipLaunchKernelGGL(cons::k_ortho_apply<PM>, dim3((unsigned)((n2 + B - 1) / B)), dim3(B), 0, st, M, n2, U, P);
 }
 }  // namespace
 
@@ -235,7 +236,7 @@ extern "C" int ptyx_probe_fix_int(void* stream, float* probe, int32_t P, int32_t
 extern "C" int ptyx_probe_ortho(void* stream, float* probe, int32_t P, int32_t N, void* ws) {
   abi::clear_error();
   if (P <= 0 || N <= 0) return abi::fail(PTYX_EINVAL, "ortho_pmode: bad shape");
-  if (P > kMaxModes) return abi::fail(PTYX_EUNSUPPORTED, "ortho_pmode: at most 16 probe modes");
+  if (P > kMaxModes) return abi::fail(PTYX_EUNSUPPORTED, "ortho_pmode: at most 64 probe modes");
   if (!probe || !ws) return abi::fail(PTYX_EINVAL, "ortho_pmode: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double* wsd = reinterpret_cast<double*>(ws);
@@ -244,24 +245,28 @@ extern "C" int ptyx_probe_ortho(void* stream, float* probe, int32_t P, int32_t N
   const int npair = P * (P + 1) / 2;
   float2* U = reinterpret_cast<float2*>(wsd + kWsU);
   hipLaunchKernelGGL(cons::k_gram, dim3(kGramChunks, npair), dim3(256), 0, st, M, P, n2, kGramChunks, wsd + kWsGram);
-  hipLaunchKernelGGL(cons::k_ortho_eig, dim3(1), dim3(256), 0, st, wsd + kWsGram, P, kGramChunks, U, wsd + kWsEvals);
+  hipLaunchKernelGGL(cons::k_ortho_eig, dim3(1), dim3(64), 0, st, wsd + kWsGram, P, kGramChunks, U, wsd + kWsEvals);
   switch (P) {
-    case 1: launch_ortho_apply<1>(st, M, n2, U); break;
-    case 2: launch_ortho_apply<2>(st, M, n2, U); break;
-    case 3: launch_ortho_apply<3>(st, M, n2, U); break;
-    case 4: launch_ortho_apply<4>(st, M, n2, U); break;
-    case 5: launch_ortho_apply<5>(st, M, n2, U); break;
-    case 6: launch_ortho_apply<6>(st, M, n2, U); break;
-    case 7: launch_ortho_apply<7>(st, M, n2, U); break;
-    case 8: launch_ortho_apply<8>(st, M, n2, U); break;
-    case 9: launch_ortho_apply<9>(st, M, n2, U); break;
-    case 10: launch_ortho_apply<10>(st, M, n2, U); break;
-    case 11: launch_ortho_apply<11>(st, M, n2, U); break;
-    case 12: launch_ortho_apply<12>(st, M, n2, U); break;
-    case 13: launch_ortho_apply<13>(st, M, n2, U); break;
-    case 14: launch_ortho_apply<14>(st, M, n2, U); break;
-    case 15: launch_ortho_apply<15>(st, M, n2, U); break;
-    default: launch_ortho_apply<16>(st, M, n2, U); break;
+    case 1: launch_ortho_apply<1>(st, M, n2, U, P); break;
+    case 2: launch_ortho_apply<2>(st, M, n2, U, P); break;
+    case 3: launch_ortho_apply<3>(st, M, n2, U, P); break;
+    case 4: launch_ortho_apply<4>(st, M, n2, U, P); break;
+    case 5: launch_ortho_apply<5>(st, M, n2, U, P); break;
+    case 6: launch_ortho_apply<6>(st, M, n2, U, P); break;
+    case 7: launch_ortho_apply<7>(st, M, n2, U, P); break;
+    case 8: launch_ortho_apply<8>(st, M, n2, U, P); break;
+    case 9: launch_ortho_apply<9>(st, M, n2, U, P); break;
+    case 10: launch_ortho_apply<10>(st, M, n2, U, P); break;
+    case 11: launch_ortho_apply<11>(st, M, n2, U, P); break;
+    case 12: launch_ortho_apply<12>(st, M, n2, U, P); break;
+    case 13: launch_ortho_apply<13>(st, M, n2, U, P); break;
+    case 14: launch_ortho_apply<14>(st, M, n2, U, P); break;
+    case 15: launch_ortho_apply<15>(st, M, n2, U, P); break;
+    case 16: launch_ortho_apply<16>(st, M, n2, U, P); break;
+    default:
+      if (P <= 32) launch_ortho_apply<32>(st, M, n2, U, P);
+      else launch_ortho_apply<64>(st, M, n2, U, P);
+      break;
   }
   return abi::launch_status("ortho_pmode launch");
 }

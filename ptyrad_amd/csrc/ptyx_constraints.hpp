@@ -15,13 +15,14 @@
 //   k_obj_reduce / k_reduce_final   the global scalars some options need (complex_ratio's Cbar,
 //                 objp_postiv 'subtract_min''s minimum): fp64 per-block partials summed in a
 //                 fixed order (deterministic), kept on the device — no host round trip.
-// Probe constraints (P ≤ 16 modes of N × N):
+// Probe constraints (P ≤ 64 modes of N × N):
 //   fix_probe_int (:70-81): k_sumsq partials → k_fix_int_final (scale) → k_cscale.
 //   ortho_pmode (:34-41, orthogonalize_modes_vec :255-291): k_gram (A = M M^H, one block column
-//   per mode pair, fp64) → k_ortho_eig (one workgroup: fixed-order partial sums, cyclic complex
-//   Jacobi in fp64, LAPACK geev eigenvector normalisation — unit norm, largest component real
-//   positive — and the descending-eigenvalue order that sort_by_mode_int produces) →
-//   k_ortho_apply (ortho = V^H M per pixel, in place).
+//   per mode pair, fp64) → k_ortho_eig (one wave: fixed-order partial sums, cyclic complex
+//   Jacobi in fp64 — the rotation by lane 0, its row / column updates one lane per k — LAPACK
+//   geev eigenvector normalisation — unit norm, largest component real positive — and the
+//   descending-eigenvalue order that sort_by_mode_int produces) → k_ortho_apply (ortho = V^H M
+//   per pixel, in place; P a template parameter up to 16, then padded to 32 / 64).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -30,7 +31,7 @@ namespace cons {
 
 constexpr int kMaxHalf = 7;        // kernel_size ≤ 15
 constexpr int kMaxTaps = 2 * kMaxHalf + 1;
-constexpr int kMaxModes = 16;
+constexpr int kMaxModes = 64;        // ortho_pmode probe modes (static LDS of k_ortho_eig: 2·64²·16 B)
 constexpr int kRedBlocks = 512;    // fixed reduction grid (deterministic partials)
 
 struct Taps {
@@ -392,12 +393,20 @@ __global__ __launch_bounds__(256) void k_gram(const float2* __restrict__ M, int 
   }
 }
 
-// one workgroup: Gram matrix from the partials (fixed order), Hermitian eigendecomposition by
-// cyclic complex Jacobi (fp64), geev normalisation, descending order; writes U (P × P, f32
-// complex, U[p][q] = conj(V[q][perm[p]]) so that ortho_p = Σ_q U[p][q] M_q).
-__global__ __launch_bounds__(256) void k_ortho_eig(const double* part, int P, int nchunk, float2* U, double* evals) {
+// one wave: Gram matrix from the partials (fixed order), Hermitian eigendecomposition by cyclic
+// complex Jacobi (fp64), geev normalisation, descending order; writes U (P × P, f32 complex,
+// U[p][q] = conj(V[q][perm[p]]) so that ortho_p = Σ_q U[p][q] M_q).  Lane 0 computes each
+// rotation and the convergence sum in the sequential order; the rotation's updates of row /
+// column element k run on lane k (the same arithmetic per element as a sequential loop).
+struct Rot {
+  Cd upp, upq, uqp, uqq;
+  int skip;
+};
+__global__ __launch_bounds__(64) void k_ortho_eig(const double* part, int P, int nchunk, float2* U, double* evals) {
   __shared__ Cd A[kMaxModes][kMaxModes];
   __shared__ Cd V[kMaxModes][kMaxModes];
+  __shared__ Rot rot;
+  __shared__ int done;
   const int npair = P * (P + 1) / 2;
   for (int pr = threadIdx.x; pr < npair; pr += blockDim.x) {
     int r = pr, i = 0;
@@ -415,30 +424,46 @@ __global__ __launch_bounds__(256) void k_ortho_eig(const double* part, int P, in
     A[j][i] = {sx, -sy};
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int i = 0; i < P; ++i) {
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
     A[i][i].y = 0;
     for (int j = 0; j < P; ++j) V[i][j] = {i == j ? 1.0 : 0.0, 0.0};
   }
+  __syncthreads();
   double scale = 0;
   for (int i = 0; i < P; ++i) scale += A[i][i].x;
   for (int sweep = 0; sweep < 40; ++sweep) {
-    double off = 0;
-    for (int i = 0; i < P; ++i)
-      for (int j = i + 1; j < P; ++j) off += A[i][j].x * A[i][j].x + A[i][j].y * A[i][j].y;
-    if (off <= 1e-30 * scale * scale) break;
+    if (threadIdx.x == 0) {
+      double off = 0;
+      for (int i = 0; i < P; ++i)
+        for (int j = i + 1; j < P; ++j) off += A[i][j].x * A[i][j].x + A[i][j].y * A[i][j].y;
+      done = off <= 1e-30 * scale * scale;
+    }
+    __syncthreads();
+    if (done) break;
     for (int p = 0; p < P; ++p)
       for (int q = p + 1; q < P; ++q) {
-        const double g = sqrt(A[p][q].x * A[p][q].x + A[p][q].y * A[p][q].y);
-        if (g <= 1e-300) continue;
-        const Cd e = {A[p][q].x / g, A[p][q].y / g};            // phase of A_pq
-        const double tau = (A[q][q].x - A[p][p].x) / (2 * g);
-        const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1 + tau * tau));
-        const double cs = 1 / sqrt(1 + t * t), sn = t * cs;
-        // U = diag(1, conj(e)) · [[c, s], [-s, c]] on (p, q)
-        const Cd upp = {cs, 0}, upq = {sn, 0};
-        const Cd uqp = cd_mul({-sn, 0}, cd_conj(e)), uqq = cd_mul({cs, 0}, cd_conj(e));
-        for (int k = 0; k < P; ++k) {   // A ← A U, V ← V U (columns p, q)
+        if (threadIdx.x == 0) {
+          const double g = sqrt(A[p][q].x * A[p][q].x + A[p][q].y * A[p][q].y);
+          rot.skip = g <= 1e-300;
+          if (!rot.skip) {
+            const Cd e = {A[p][q].x / g, A[p][q].y / g};            // phase of A_pq
+            const double tau = (A[q][q].x - A[p][p].x) / (2 * g);
+            const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1 + tau * tau));
+            const double cs = 1 / sqrt(1 + t * t), sn = t * cs;
+            // U = diag(1, conj(e)) · [[c, s], [-s, c]] on (p, q)
+            rot.upp = {cs, 0};
+            rot.upq = {sn, 0};
+            rot.uqp = cd_mul({-sn, 0}, cd_conj(e));
+            rot.uqq = cd_mul({cs, 0}, cd_conj(e));
+          }
+        }
+        __syncthreads();
+        if (rot.skip) {
+          __syncthreads();
+          continue;
+        }
+        const Cd upp = rot.upp, upq = rot.upq, uqp = rot.uqp, uqq = rot.uqq;
+        for (int k = threadIdx.x; k < P; k += blockDim.x) {   // A ← A U, V ← V U (columns p, q)
           const Cd akp = A[k][p], akq = A[k][q];
           A[k][p] = cd_add(cd_mul(akp, upp), cd_mul(akq, uqp));
           A[k][q] = cd_add(cd_mul(akp, upq), cd_mul(akq, uqq));
@@ -446,18 +471,24 @@ __global__ __launch_bounds__(256) void k_ortho_eig(const double* part, int P, in
           V[k][p] = cd_add(cd_mul(vkp, upp), cd_mul(vkq, uqp));
           V[k][q] = cd_add(cd_mul(vkp, upq), cd_mul(vkq, uqq));
         }
-        for (int k = 0; k < P; ++k) {   // A ← U^H A (rows p, q)
+        __syncthreads();
+        for (int k = threadIdx.x; k < P; k += blockDim.x) {   // A ← U^H A (rows p, q)
           const Cd apk = A[p][k], aqk = A[q][k];
           A[p][k] = cd_add(cd_mul(cd_conj(upp), apk), cd_mul(cd_conj(uqp), aqk));
           A[q][k] = cd_add(cd_mul(cd_conj(upq), apk), cd_mul(cd_conj(uqq), aqk));
         }
-        A[p][q] = {0, 0};
-        A[q][p] = {0, 0};
-        A[p][p].y = 0;
-        A[q][q].y = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          A[p][q] = {0, 0};
+          A[q][p] = {0, 0};
+          A[p][p].y = 0;
+          A[q][q].y = 0;
+        }
+        __syncthreads();
       }
   }
-  // geev normalisation: unit norm, largest-modulus component (first on ties) real positive
+  if (threadIdx.x != 0) return;
+// geev normalisation: unit norm, largest-modulus component (first on ties) real positive
   for (int j = 0; j < P; ++j) {
     double nrm = 0;
     for (int k = 0; k < P; ++k) nrm += V[k][j].x * V[k][j].x + V[k][j].y * V[k][j].y;
@@ -498,20 +529,23 @@ __global__ __launch_bounds__(256) void k_ortho_eig(const double* part, int P, in
   }
 }
 
-// ortho_p[n] = Σ_q U[p][q] M_q[n], one pixel per thread, in place (P a compile-time constant so
-// the P modes of a pixel stay in registers)
-template <int P>
-__global__ __launch_bounds__(256) void k_ortho_apply(float2* M, long long n2, const float2* U) {
+// ortho_p[n] = Σ_q U[p][q] M_q[n], one pixel per thread, in place.  PM (a compile-time constant
+// so the modes of a pixel stay in registers) = P up to 16, then 32 or 64 with the modes past P
+// masked (P runtime): the same fma chain for every P.
+template <int PM>
+__global__ __launch_bounds__(PM > 32 ? 128 : 256) void k_ortho_apply(float2* M, long long n2, const float2* U, int P) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n2) return;
-  float2 m[P];
+  float2 m[PM];
 #pragma unroll
-  for (int q = 0; q < P; ++q) m[q] = M[(size_t)q * n2 + k];
+  for (int q = 0; q < PM; ++q) m[q] = q < P ? M[(size_t)q * n2 + k] : make_float2(0.f, 0.f);
 #pragma unroll
-  for (int p = 0; p < P; ++p) {
+  for (int p = 0; p < PM; ++p) {
+    if (p >= P) break;
     float ax = 0.f, ay = 0.f;
 #pragma unroll
-    for (int q = 0; q < P; ++q) {
+    for (int q = 0; q < PM; ++q) {
+      if (q >= P) break;
       const float2 u = U[p * P + q];
       ax = fmaf(u.x, m[q].x, fmaf(-u.y, m[q].y, ax));
       ay = fmaf(u.x, m[q].y, fmaf(u.y, m[q].x, ay));

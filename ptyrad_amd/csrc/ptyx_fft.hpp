@@ -118,7 +118,7 @@ constexpr int ct_smallest_factor(int R) {
   return R;
 }
 
-// Direct DFT of a prime size (radix 3, 5 of mixed-radix N): X[k] = Σ_n v[n] exp(DIR·2πi nk/R),
+// Direct DFT of a prime size (radix 3, 5, 7 of mixed-radix N): X[k] = Σ_n v[n] exp(DIR·2πi nk/R),
 // compile-time twiddles, (R-1)² complex multiply-adds.
 template <int R, int DIR>
 __device__ __forceinline__ void dft_direct(float2 (&v)[R]) {
@@ -212,11 +212,13 @@ struct DFT<4, DIR> {
 
 // ---------------------------------------------------------------- radix plans
 // Per-dimension Stockham radices: N = R1·R2 (R2 = 1 ⇒ one pass per dimension).  Powers of two
-// keep their measured plans; every other 2·3·5-smooth N takes the largest R1 ≤ 16 with
-// N / R1 ≤ 16, else the smallest R1 ≤ 27 with N / R1 ≤ 16 (125, 162, 200, 216, 243, 250).
+// keep their measured plans; every other 2·3·5·7-smooth N takes the largest R1 ≤ 16 with
+// N / R1 ≤ 16, else the smallest R1 ≤ 27 with N / R1 ≤ 16 (125, 162, 175, 189, 200, 216, 243,
+// 250).  Radix 7 (and 14, 21) runs as a direct DFT (dft_direct) or by decimation in time inside
+// DFT<R>; N = 245 = 5·7² has no split with R1 ≤ 27 and R2 ≤ 16 and is not offered.
 constexpr bool is_smooth235(int n) {
   if (n < 1) return false;
-  for (int f : {2, 3, 5})
+  for (int f : {2, 3, 5, 7})
     while (n % f == 0) n /= f;
   return n == 1;
 }
@@ -237,7 +239,7 @@ constexpr int plan_r1(int N) {
 }
 template <int N>
 struct Plan1D {
-  static_assert(is_smooth235(N) && plan_r1(N) > 0, "N must be 2·3·5-smooth with a two-pass plan");
+  static_assert(is_smooth235(N) && plan_r1(N) > 0, "N must be 2·3·5·7-smooth with a two-pass plan");
   static constexpr int R1 = plan_r1(N), R2 = N / plan_r1(N);
 };
 

@@ -1,4 +1,4 @@
-// ptyx_general.hpp — the general engine's kernels (any P, O ≤ 8, Nz; every 2·3·5-smooth N in
+// ptyx_general.hpp — the general engine's kernels (any P, O ≤ 32, Nz; every 2·3·5-smooth N in
 // [32, 256]; f32 or f16 DPs).  One workgroup owns one pattern at a time and keeps the N×N wave in
 // LDS (N ≤ 128) or in a per-workgroup global scratch pair (N > 128); the grid is persistent and
 // walks the patterns with a grid stride.

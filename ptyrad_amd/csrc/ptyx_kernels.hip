@@ -81,7 +81,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
   if (f.bsums_in) {
     const double* bs = f.bsums_in + (size_t)m * kNBatchSum;
     B = bs[0]; S1 = bs[1]; M1 = bs[2]; S2 = bs[3]; M2 = bs[4];
-    for (int o = 0; o < f.O; ++o) sp[o] = bs[5 + o];
+#pragma unroll
+    for (int o = 0; o < kMaxModesO; ++o)
+      if (o < f.O) sp[o] = bs[5 + o];
   } else {
     for (int t = b0 + lane; t < b1; t += 64) {
       const float* ps = f.psums + (size_t)t * kNSum;
@@ -89,7 +91,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
       M1 += ps[1];
       S2 += ps[2];
       M2 += ps[3];
-      for (int o = 0; o < f.O; ++o) sp[o] += ps[kSumBase + o];
+#pragma unroll
+      for (int o = 0; o < kMaxModesO; ++o)
+        if (o < f.O) sp[o] += ps[kSumBase + o];
     }
 #pragma unroll
     for (int x = 32; x >= 1; x >>= 1) {
@@ -97,7 +101,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
       M1 += __shfl_xor(M1, x, 64);
       S2 += __shfl_xor(S2, x, 64);
       M2 += __shfl_xor(M2, x, 64);
-      for (int o = 0; o < f.O; ++o) sp[o] += __shfl_xor(sp[o], x, 64);
+#pragma unroll
+      for (int o = 0; o < kMaxModesO; ++o)
+        if (o < f.O) sp[o] += __shfl_xor(sp[o], x, 64);
     }
   }
   if (f.bsums_out) {
@@ -125,7 +131,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
     if (f.sparse_on && B > 0) {  // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
       const double cnt = B * f.Nz * f.N * f.N;
       double t = 0;
-      for (int o = 0; o < f.O; ++o) {
+#pragma unroll
+      for (int o = 0; o < kMaxModesO; ++o) {
+        if (o >= f.O) break;
         const double mo = sp[o] / cnt;
         const double inv = 1.0 / f.sparse_n;
         t += f.occu[o] * pow(mo, inv);
@@ -137,7 +145,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
     float* cfo = f.coef + (size_t)m * kNCoef;
     cfo[0] = cf[0];
     cfo[1] = cf[1];
-    for (int o = 0; o < f.O; ++o) cfo[2 + o] = cf[2 + o];
+#pragma unroll
+    for (int o = 0; o < kMaxModesO; ++o)
+      if (o < f.O) cfo[2 + o] = cf[2 + o];
     if (f.loss_terms)
       for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
   }
@@ -458,10 +468,11 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   const GenOps* gen = gen_ops(d.N);
   if (!gen)
     return fail(PTYX_EUNSUPPORTED, "N = " + std::to_string(d.N) +
-                                       ": N must be 2·3·5-smooth in [32, 256] (2^a 3^b 5^c: 32, 36, 40, 45, 48, ..., 250, 256)");
+                                       ": N must be 2·3·5·7-smooth in [32, 256] (2^a 3^b 5^c 7^d: 32, 35, 36, 40, 42, 45, ..., 252, 256; "
+                                       "not 245)");
   if (d.P < 1 || d.O < 1 || d.Nz < 1 || d.n_scans < 1 || d.max_patterns < 1)
     return fail(PTYX_EINVAL, "P, O, Nz, n_scans, max_patterns must be >= 1");
-  if (d.O > kMaxModesO) return fail(PTYX_EUNSUPPORTED, "at most 8 object modes");
+  if (d.O > kMaxModesO) return fail(PTYX_EUNSUPPORTED, "at most 32 object modes");
   if (d.Ny < d.N || d.Nx < d.N) return fail(PTYX_EINVAL, "object smaller than the probe window");
   DeviceGuard dg(device);
   int cu = 0;

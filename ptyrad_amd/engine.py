@@ -229,7 +229,7 @@ class Plan:
         boundaries; device offsets must fit in one call.
 
         batch_sums_reduce: the mini-batches are this rank's PARTS of mini-batches split over ranks
-        (ptyx_forward_loss_grad_begin / _end).  It is called with the (n_batches, 13) float64
+        (ptyx_forward_loss_grad_begin / _end).  It is called with the (n_batches, PTYX_BATCH_SUMS) float64
         device tensor of the parts' additive loss sums and must sum it over the ranks in place
         (one all-reduce); the loss terms and gradient coefficients then belong to the whole
         mini-batches.  Such a call is never split, so it must fit the plan's capacity.

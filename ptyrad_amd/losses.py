@@ -11,6 +11,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import _lib
 from .engine import LOSS_TERM_NAMES, LossConfig, batch_offsets
 
 
@@ -272,7 +273,7 @@ class CombinedLoss(torch.nn.Module):
         held = [m for m, b in enumerate(parts) if b.size]
         terms = torch.zeros((G, 5), dtype=torch.float32, device=dev)
         if not held:   # nothing here: still join the reduction of the group's sums
-            reduce(torch.zeros((G, 13), dtype=torch.float64, device=dev))
+            reduce(torch.zeros((G, _lib.PTYX_BATCH_SUMS), dtype=torch.float64, device=dev))
             return terms
         local = [parts[m] for m in held]
         flat = np.concatenate(local)
@@ -280,7 +281,7 @@ class CombinedLoss(torch.nn.Module):
         self._check_held(model, flat)
         sel = torch.as_tensor(held, dtype=torch.long, device=dev)
 
-        def group_reduce(sums):          # local rows -> the group's (G, 13) rows -> sum over ranks
+        def group_reduce(sums):          # local rows -> the group's (G, PTYX_BATCH_SUMS) rows -> sum over ranks
             full = torch.zeros((G, sums.shape[1]), dtype=torch.float64, device=dev)
             full.index_copy_(0, sel, sums)
             reduce(full)

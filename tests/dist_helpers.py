@@ -100,7 +100,7 @@ class OracleLoss:
             raise IndexError("a mini-batch position outside this rank's measurement block")
         probe = (model.opt_probe[..., 0] + 1j * model.opt_probe[..., 1]).detach().numpy()
 
-        def reduce_np(sums):            # the (n_batches, 13) float64 sums, summed over the ranks in place
+        def reduce_np(sums):            # the (n_batches, N_BATCH_SUMS) float64 sums, summed over the ranks in place
             reduce(torch.from_numpy(sums))
 
         return orc.forward_loss_grad_parts(

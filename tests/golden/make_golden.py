@@ -372,6 +372,14 @@ if __name__ == "__main__":
         run_case("n216_p2o1z2_r18", 216, 2, 1, 2, 3, 3, 4, seed=114, big=True)
         run_case("n250_p1o2z1_r25", 250, 1, 2, 1, 3, 3, 4, seed=115, big=True)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--radix7":
+        # 2·3·5·7-smooth N (round 5): radix 7 in LDS (112 = 16·7, 49 = 7·7 odd) and radix 14 / 21 in
+        # global scratch (196 = 14·14, 189 = 27·7 on 512-thread workgroups)
+        run_case("n112_p2o1z2_r7", 112, 2, 1, 2, 3, 3, 6, seed=131)
+        run_case("n49_p1o2z1_r7", 49, 1, 2, 1, 3, 3, 5, seed=132)
+        run_case("n196_p1o1z2_r14", 196, 1, 1, 2, 3, 3, 4, seed=133, big=True)
+        run_case("n189_p2o1z1_r27x7", 189, 2, 1, 1, 3, 3, 4, seed=134, big=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--large":
         # the (N, P, O, Nz) of BASELINE configs[2..4] and of both demos, so the engines that only
         # run at these sizes (N = 256 stripe / general stages, mixed-state multislice, Nz = 16)

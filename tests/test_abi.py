@@ -95,9 +95,9 @@ def test_integration_stub_matches_header_and_library(tmp_path, monkeypatch):
         assert py_layout(ns[py]) == (c[py][0], c[py][1]), py
     ns["check_abi"]()
 
-    class M:   # N = 98 (2·7²) is rejected by ptyx_plan_create before any HIP call
+    class M:   # N = 88 (8·11) is rejected by ptyx_plan_create before any HIP call
         opt_obja = __import__("torch").zeros((1, 1, 200, 200))
-        opt_probe = __import__("torch").zeros((1, 98, 98, 2))
+        opt_probe = __import__("torch").zeros((1, 88, 88, 2))
         crop_pos = __import__("torch").zeros((4, 2), dtype=__import__("torch").int32)
         shift_probes = True
     with pytest.raises(RuntimeError, match="N must be"):
@@ -115,14 +115,14 @@ def test_plan_create_rejects_stale_abi_version():
 def test_plan_create_rejects_bad_dims_without_gpu():
     lib = _lib.load()
     h = ctypes.c_void_p()
-    d = _lib.Dims(98, 1, 1, 1, 200, 200, 4, 4, 0)    # N=98 = 2·7² unsupported -> checked before any HIP call
+    d = _lib.Dims(88, 1, 1, 1, 200, 200, 4, 4, 0)    # N=88 = 8·11 unsupported -> checked before any HIP call
     rc = lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0)
     assert rc == _lib.PTYX_EUNSUPPORTED
     assert b"N must be" in lib.ptyx_last_error()
-    for n in (16, 112, 264, 512):    # below 32, a factor 7, above 256
+    for n in (16, 245, 121, 264, 512):    # below 32, 5·7² (no two-pass plan), 11², above 256
         d = _lib.Dims(n, 1, 1, 1, 600, 600, 4, 4, 0)
         assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EUNSUPPORTED, n
-    d = _lib.Dims(128, 1, 9, 1, 200, 200, 4, 4, 0)   # too many object modes
+    d = _lib.Dims(128, 1, 33, 1, 200, 200, 4, 4, 0)  # too many object modes (> 32)
     assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EUNSUPPORTED
     d = _lib.Dims(128, 1, 1, 1, 100, 200, 4, 4, 0)   # object smaller than the window
     assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EINVAL
@@ -136,7 +136,7 @@ def test_constraint_entry_points_validate_without_gpu():
     # argument checks happen before any HIP call
     assert lib.ptyx_obj_rblur(None, None, None, 1, 32, 32, 4, 1.0) == _lib.PTYX_EUNSUPPORTED   # even kernel
     assert lib.ptyx_obj_rblur(None, None, None, 1, 2, 32, 5, 1.0) == _lib.PTYX_EINVAL          # reflect pad
-    assert lib.ptyx_probe_ortho(None, None, 17, 32, None) == _lib.PTYX_EUNSUPPORTED             # > 16 modes
+    assert lib.ptyx_probe_ortho(None, None, 65, 32, None) == _lib.PTYX_EUNSUPPORTED             # > 64 modes
     c = _lib.ObjConstraints()
     c.zblur_a, c.zblur_ks, c.zblur_std = 1, 6, 1.0
     assert lib.ptyx_obj_constrain(None, ctypes.c_void_p(8), ctypes.c_void_p(8), 1, 2, 4, 4, ctypes.byref(c),

@@ -95,3 +95,27 @@ def test_ortho_eight_modes_orthonormal_and_deterministic(dev):
     d = np.real(np.diag(G))
     assert np.all(np.diff(d) <= 0)
     assert np.abs(G - np.diag(np.diag(G))).max() < 1e-5 * d.max()
+
+
+@pytest.mark.parametrize("P", [17, 24, 40, 64])
+def test_ortho_many_modes_vs_oracle(dev, P):
+    """ortho_pmode beyond 16 probe modes (the wave-parallel Jacobi and the padded apply kernels):
+    against the oracle's orthogonalize_modes (numpy eig), orthogonal, sorted, bitwise repeatable."""
+    from ptyrad_amd.constraints import CombinedConstraint
+    rng = np.random.default_rng(100 + P)
+    probe = (rng.standard_normal((P, 64, 64)) + 1j * rng.standard_normal((P, 64, 64))).astype(np.complex64)
+    probe *= (0.93 ** np.arange(P))[:, None, None].astype(np.float32)
+    cp = {"ortho_pmode": {"freq": 1}}
+    outs = []
+    for _ in range(2):
+        m = Model(np.ones((1, 1, 8, 8), np.float32), np.zeros((1, 1, 8, 8), np.float32), probe, 1.0, dev)
+        CombinedConstraint(cp, device=dev, verbose=False)(m, 1)
+        outs.append(torch.view_as_complex(m.opt_probe.detach()).cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    want = co.orthogonalize_modes(probe.astype(np.complex128))
+    assert rel(outs[0], want) < 5e-5
+    M = outs[0].reshape(P, -1).astype(np.complex128)
+    G = M @ M.conj().T
+    d = np.real(np.diag(G))
+    assert np.all(np.diff(d) <= 0)
+    assert np.abs(G - np.diag(np.diag(G))).max() < 2e-5 * d.max()

@@ -88,7 +88,10 @@ ENGINE_OF = {"n256_p8o2z1_c3": "k_s1", "n256_p4o1z1_c5f16": "k_s1", "n128_p1o1z1
              "n128_p6o1z6_tbl": "k_fmm_fwd", "n256_p4o1z5_pso": "k_adjoint",
              # loss_single + loss_poissn (make_golden.py --both-terms): the two-pass register / stripe paths
              "n128_p1o1z1_both": "k_fused", "n128_p1o1z3_both": "k_fused", "n128_p3o1z2_both": "k_fmm_fwd",
-             "n256_p2o2z1_both": "k_s3"}
+             "n256_p2o2z1_both": "k_s3",
+             # radix 7 / 14 / 21 (make_golden.py --radix7): the general engine
+             "n112_p2o1z2_r7": "k_adjoint", "n49_p1o2z1_r7": "k_adjoint", "n196_p1o1z2_r14": "k_adjoint",
+             "n189_p2o1z1_r27x7": "k_adjoint"}
 
 
 @pytest.mark.parametrize("path", CASES, ids=[p.split("/")[-1][:-4] for p in CASES])
@@ -280,7 +283,7 @@ def test_mixed_radix_general_engine_vs_oracle(N, P, O, Nz, shift, both):
     _general_engine_case(N, P, O, Nz, shift, both)
 
 
-# every 2·3·5-smooth N in [32, 256] (the sizes ptyx_gen.hip registers), cycling through mode /
+# every 2·3·5·7-smooth N in [32, 256] (the sizes ptyx_gen.hip registers), cycling through mode /
 # slice / shift / loss-term configurations; 128 and 256 run the register / stripe engines for some
 # of these and have their own cases
 _SMOOTH_CFGS = [(1, 1, 1, True, False), (2, 1, 2, True, False), (1, 2, 1, True, True), (2, 1, 1, False, False),
@@ -297,11 +300,20 @@ def test_every_smooth_n_vs_oracle(N):
 
 
 @pytest.mark.parametrize("N,P,O,Nz,shift,both", [(64, 2, 8, 1, True, False), (32, 3, 8, 2, True, True),
-                                                 (96, 8, 1, 2, False, False)])
+                                                 (96, 8, 1, 2, False, False), (32, 1, 12, 1, True, False),
+                                                 (48, 2, 20, 2, True, True), (32, 1, 32, 1, False, False)])
 def test_general_engine_maximum_modes_vs_oracle(N, P, O, Nz, shift, both):
-    """The plan's limits: 8 object modes (kMaxModesO, the loss_sparse sums per mode, the
+    """The plan's limits: up to 32 object modes (kMaxModesO, the loss_sparse sums per mode, the
     per-mode sparse coefficients) and 8 probe modes (the probe-mode split of small calls)."""
     _general_engine_case(N, P, O, Nz, shift, both)
+
+
+def test_object_modes_beyond_limit_are_refused():
+    dev()
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import Plan
+    with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
+        Plan(32, 1, 33, 1, 100, 100, 4, 4, device=torch.device("cuda", 0))
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -339,12 +351,12 @@ def test_random_configuration_vs_oracle(seed, monkeypatch):
 
 
 def test_unsupported_n_is_refused():
-    """N with a prime factor other than 2, 3, 5 (98 = 2·7², 112 = 16·7), or outside [32, 256], is
-    refused with PTYX_EUNSUPPORTED at plan creation, not run."""
+    """N with a prime factor above 7 (88 = 8·11, 143 = 11·13), 245 = 5·7² (no two-pass plan), or
+    outside [32, 256], is refused with PTYX_EUNSUPPORTED at plan creation, not run."""
     dev()
     from ptyrad_amd import _lib
     from ptyrad_amd.engine import Plan
-    for n in (98, 112, 16, 270):
+    for n in (88, 143, 245, 16, 270):
         with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
             Plan(n, 1, 1, 1, 300, 300, 4, 4, device=torch.device("cuda", 0))
     Plan(100, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0)).close()
@@ -681,7 +693,7 @@ def test_mixed_state_register_engine_vs_oracle(P, Nz, shift, q):
     batches = [perm[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
     ks = {}
     terms, dp, g, _ = run_fused(d, device, batches, grad_scale=0.5, kernels=ks)
-    assert "k_fmm_fwd" in ks and "k_adjoint" in ks, ks
+    assert "k_fmm_fwd" in ks and "k_fmm_adj" in ks, ks
     oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
                                              d["occu"], d["meas"], batches, d["loss_params"],
                                              shift_probes=shift, grad_scale=0.5)
