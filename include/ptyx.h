@@ -74,7 +74,7 @@ extern "C" {
 typedef struct ptyx_plan ptyx_plan;
 
 typedef struct ptyx_dims {
-  int32_t N;            /* probe / DP side: any 2^a 3^b 5^c 7^d in [32, 256] but 245 (else EUNSUPPORTED) */
+  int32_t N;            /* probe / DP side: any 2^a 3^b 5^c 7^d in [32, 512] (else EUNSUPPORTED)    */
   int32_t P;            /* probe modes  (opt_probe.shape[0])                               */
   int32_t O;            /* object modes (opt_obja.shape[0])                                */
   int32_t Nz;           /* object slices (opt_obja.shape[1])                               */

@@ -31,20 +31,26 @@ SOURCES = [os.path.join(HERE, "ptyx_kernels.hip"), os.path.join(HERE, "ptyx_cons
 GEN_SOURCE = os.path.join(HERE, "ptyx_gen.hip")
 
 
+MAX_RADIX = 49
+
+
 def plan_r1(n: int) -> int:
     """ptyx_fft.hpp plan_r1: the first-pass radix of the two-pass plan (0: none)."""
     fixed = {16: 16, 32: 8, 64: 8, 128: 16, 256: 16}
     if n in fixed:
         return fixed[n]
-    for r in list(range(16, 1, -1)) + list(range(17, 28)):
+    if n > 256:
+        r = next(r for r in range(2, n + 1) if n % r == 0 and r * r >= n)
+        return r if r <= MAX_RADIX else 0
+    for r in list(range(16, 1, -1)) + list(range(17, MAX_RADIX + 1)):
         if n % r == 0 and n // r <= 16:
             return r
     return 0
 
 
-def smooth_sizes(lo: int = 32, hi: int = 256):
-    """Every 2·3·5·7-smooth N in [lo, hi] with a two-pass plan (R1 ≤ 27, R2 ≤ 16): the general
-    engine's supported sizes (all but 245 = 5·7²)."""
+def smooth_sizes(lo: int = 32, hi: int = 512):
+    """Every 2·3·5·7-smooth N in [lo, hi] with a two-pass plan: the general engine's supported
+    sizes (all of them: the largest radix needed is 49, for 343 = 49·7)."""
     out = []
     for n in range(lo, hi + 1):
         m = n
@@ -59,7 +65,7 @@ def smooth_sizes(lo: int = 32, hi: int = 256):
 GEN_SIZES = smooth_sizes()
 # size groups of the general engine, one ptyx_gen.hip object each (compiled in parallel): dealt
 # round-robin over the sizes in descending order so every group gets a similar mix
-N_GEN_GROUPS = 10
+N_GEN_GROUPS = 16
 GEN_GROUPS = [sorted(GEN_SIZES[::-1][g::N_GEN_GROUPS]) for g in range(N_GEN_GROUPS)]
 HEADERS = glob.glob(os.path.join(HERE, "*.hpp")) + [os.path.join(ROOT, "include", "ptyx.h")]
 DEPS = SOURCES + [GEN_SOURCE] + HEADERS

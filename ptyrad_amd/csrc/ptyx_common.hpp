@@ -20,9 +20,9 @@ constexpr float kDpEps = 1e-10f;               // forward.py:20 eps
 // Launch geometry of the general engine's workgroup-resident FFT kernels.
 //  N ≤ 128: the N×N wave in LDS (in place, ≤ 136 KiB), NT = 8·N threads (≤ 1024).
 //  N > 128: the per-workgroup global scratch pair (two line-block round trips a 2-D FFT), 1024
-//  threads.  512 threads whenever a radix above 16 holds up to 27 points a thread (125, 162, 200,
-//  216, 243, 250: 256 VGPRs, no spills); N = 256 has its own two-stage path with two 512-thread
-//  workgroups a CU (LDS ≈ 78 KiB each).
+//  threads.  512 threads whenever a radix above 16 holds up to 49 points a thread (125, 162, 200,
+//  216, 243, 250 and most N > 256: one wave a SIMD, up to 512 registers); N = 256 has its own
+//  two-stage path with two 512-thread workgroups a CU (LDS ≈ 78 KiB each).
 // kWaves: minimum waves per SIMD the kernels are compiled for (≤ 512 / kWaves VGPRs): enough for
 // every workgroup LDS and threads allow on a CU to be resident at once (capped at 8 = 64 VGPRs).
 // Measured (profiles/r04/occ/): N 135-240 +12-21 %, 45 / 60 / 75 / 81 / 90 +11-32 %, no size

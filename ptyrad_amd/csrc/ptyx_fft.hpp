@@ -184,7 +184,10 @@ struct DFT {
     DFT<R / 2, DIR>::run(o);
     static_for<0, R / 2>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-      const float2 t = twmul<R, k, DIR>(o[k]);
+      // (the 16-entry table covers R ≤ 16; R = 32, the first pass of N = 512, takes ctwmul)
+      float2 t;
+      if constexpr (R <= 16) t = twmul<R, k, DIR>(o[k]);
+      else t = ctwmul<R, k, DIR>(o[k]);
       v[k] = cadd(e[k], t);
       v[k + R / 2] = csub(e[k], t);
     });
@@ -212,10 +215,12 @@ struct DFT<4, DIR> {
 
 // ---------------------------------------------------------------- radix plans
 // Per-dimension Stockham radices: N = R1·R2 (R2 = 1 ⇒ one pass per dimension).  Powers of two
-// keep their measured plans; every other 2·3·5·7-smooth N takes the largest R1 ≤ 16 with
-// N / R1 ≤ 16, else the smallest R1 ≤ 27 with N / R1 ≤ 16 (125, 162, 175, 189, 200, 216, 243,
-// 250).  Radix 7 (and 14, 21) runs as a direct DFT (dft_direct) or by decimation in time inside
-// DFT<R>; N = 245 = 5·7² has no split with R1 ≤ 27 and R2 ≤ 16 and is not offered.
+// keep their measured plans; every other 2·3·5·7-smooth N ≤ 256 takes the largest R1 ≤ 16 with
+// N / R1 ≤ 16, else the smallest R1 ≤ 49 with N / R1 ≤ 16 (125, 162, 175, 189, 200, 216, 243,
+// 245 = 35·7, 250); N in (256, 512] the smallest divisor R1 ≥ √N (512 = 32·16, 441 = 21·21,
+// 343 = 49·7).  Radix 7 (and 14, 21, 28, 35, 49) runs as a direct DFT (dft_direct) or by
+// decimation in time inside DFT<R>.
+constexpr int kMaxRadix = 49;   // largest Stockham radix (points a thread holds in one pass)
 constexpr bool is_smooth235(int n) {
   if (n < 1) return false;
   for (int f : {2, 3, 5, 7})
@@ -231,9 +236,16 @@ constexpr int plan_r1(int N) {
     case 256: return 16;
     default: break;
   }
+  if (N > 256) {   // the smallest divisor ≥ √N: the most balanced two-pass split (R1 ≤ 49: 343 = 49·7)
+    for (int r = 2; r <= N; ++r)
+      if (N % r == 0 && r * r >= N) return r <= kMaxRadix ? r : 0;
+    return 0;
+  }
   for (int r = 16; r >= 2; --r)
     if (N % r == 0 && N / r <= 16) return r;
   for (int r = 17; r <= 27; ++r)
+    if (N % r == 0 && N / r <= 16) return r;
+  for (int r = 28; r <= kMaxRadix; ++r)   // 245 = 35·7
     if (N % r == 0 && N / r <= 16) return r;
   return 0;
 }
@@ -567,12 +579,13 @@ __device__ __forceinline__ void g256_stage(const float2* __restrict__ src, float
   g256_fstage<DIR, 0, LAST, FIRST, PRELOAD, true, LAST>(src, dst, lds, tw, pre, nm, post);
 }
 
-// ---------------------------------------------------------------- 128 < N < 256: line blocks
+// ---------------------------------------------------------------- 128 < N ≤ 512: line blocks
 // A field that does not fit LDS (and is not 256², which has its own stages above) transforms in
 // TWO global round trips: stage 1 takes blocks of kLines rows through LDS (pre hook on the loads,
 // both Stockham passes of the row DFT in LDS, stored to the pair's b), stage 2 blocks of kLines
-// columns (128-B row segments in, both passes, post hook on the way out to a).
-template <int N, int L = 32>
+// columns (128-B row segments in, both passes, post hook on the way out to a).  32 lines a block
+// up to N = 256, 16 above (a 512-point line block is 70 KiB of LDS).
+template <int N, int L = (N > 256 ? 16 : 32)>
 struct LineTile {
   static constexpr int kLines = L;
   static constexpr int kStride = N + N / 16;                 // one pad point per 16 (LdsArray's rule)
@@ -581,7 +594,7 @@ struct LineTile {
 };
 
 // One in-place Stockham pass of radix R (span NS) along `lines` lines of a LineTile<N, L>.
-template <int N, int NT, int R, int NS, int DIR, int LINES = 32>
+template <int N, int NT, int R, int NS, int DIR, int LINES = LineTile<N>::kLines>
 __device__ __forceinline__ void line_pass(float2* tile, const float2* tw, int lines) {
   using LT = LineTile<N, LINES>;
   constexpr int L = N / R;                 // butterflies per line

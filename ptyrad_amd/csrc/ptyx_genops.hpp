@@ -4,9 +4,8 @@
 // translation units (ptyx_general.hpp's GenLaunch<N>), which register one GenOps each at load
 // time; ptyx_kernels.hip (plans, engine selection, the C ABI) looks the table up by N and never
 // instantiates those kernels itself.  Supported N = the sizes registered: every 2·3·5·7-smooth N
-// in [32, 256] with a two-pass plan, i.e. all but 245 (src/ptyrad/params/init_params.py:53, 340,
-// 361: meas_crop / meas_resample / meas_pad produce them; the reference transforms them with
-// torch's mixed-radix FFT).
+// in [32, 512] (src/ptyrad/params/init_params.py:53, 340, 361: meas_crop / meas_resample /
+// meas_pad produce them; the reference transforms them with torch's mixed-radix FFT).
 #pragma once
 #include <hip/hip_runtime.h>
 

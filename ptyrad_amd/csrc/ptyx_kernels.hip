@@ -468,8 +468,7 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   const GenOps* gen = gen_ops(d.N);
   if (!gen)
     return fail(PTYX_EUNSUPPORTED, "N = " + std::to_string(d.N) +
-                                       ": N must be 2·3·5·7-smooth in [32, 256] (2^a 3^b 5^c 7^d: 32, 35, 36, 40, 42, 45, ..., 252, 256; "
-                                       "not 245)");
+                                       ": N must be 2·3·5·7-smooth in [32, 512] (2^a 3^b 5^c 7^d: 32, 35, 36, 40, 42, 45, ..., 504, 512)");
   if (d.P < 1 || d.O < 1 || d.Nz < 1 || d.n_scans < 1 || d.max_patterns < 1)
     return fail(PTYX_EINVAL, "P, O, Nz, n_scans, max_patterns must be >= 1");
   if (d.O > kMaxModesO) return fail(PTYX_EUNSUPPORTED, "at most 32 object modes");

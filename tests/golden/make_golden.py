@@ -380,6 +380,13 @@ if __name__ == "__main__":
         run_case("n196_p1o1z2_r14", 196, 1, 1, 2, 3, 3, 4, seed=133, big=True)
         run_case("n189_p2o1z1_r27x7", 189, 2, 1, 1, 3, 3, 4, seed=134, big=True)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--big-n":
+        # N above 256 (round 5): the line-block two-pass plans with radices up to 49 on 512-thread
+        # workgroups — 384 = 24·16, 343 = 49·7 (odd, the largest radix), 512 = 32·16 with two modes
+        run_case("n384_p1o1z1_big", 384, 1, 1, 1, 3, 3, 4, seed=141, big=True)
+        run_case("n343_p1o1z2_r49", 343, 1, 1, 2, 3, 3, 3, seed=142, big=True)
+        run_case("n512_p2o1z1_big", 512, 2, 1, 1, 3, 3, 3, seed=143, big=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--large":
         # the (N, P, O, Nz) of BASELINE configs[2..4] and of both demos, so the engines that only
         # run at these sizes (N = 256 stripe / general stages, mixed-state multislice, Nz = 16)

@@ -119,7 +119,7 @@ def test_plan_create_rejects_bad_dims_without_gpu():
     rc = lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0)
     assert rc == _lib.PTYX_EUNSUPPORTED
     assert b"N must be" in lib.ptyx_last_error()
-    for n in (16, 245, 121, 264, 512):    # below 32, 5·7² (no two-pass plan), 11², above 256
+    for n in (16, 121, 264, 540, 1024):    # below 32, 11², 8·3·11, above 512
         d = _lib.Dims(n, 1, 1, 1, 600, 600, 4, 4, 0)
         assert lib.ptyx_plan_create(ctypes.byref(h), ctypes.byref(d), 0) == _lib.PTYX_EUNSUPPORTED, n
     d = _lib.Dims(128, 1, 33, 1, 200, 200, 4, 4, 0)  # too many object modes (> 32)

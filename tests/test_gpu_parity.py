@@ -91,7 +91,9 @@ ENGINE_OF = {"n256_p8o2z1_c3": "k_s1", "n256_p4o1z1_c5f16": "k_s1", "n128_p1o1z1
              "n256_p2o2z1_both": "k_s3",
              # radix 7 / 14 / 21 (make_golden.py --radix7): the general engine
              "n112_p2o1z2_r7": "k_adjoint", "n49_p1o2z1_r7": "k_adjoint", "n196_p1o1z2_r14": "k_adjoint",
-             "n189_p2o1z1_r27x7": "k_adjoint"}
+             "n189_p2o1z1_r27x7": "k_adjoint",
+             # N above 256 (make_golden.py --big-n): the general engine's line-block plans
+             "n384_p1o1z1_big": "k_adjoint", "n343_p1o1z2_r49": "k_adjoint", "n512_p2o1z1_big": "k_adjoint"}
 
 
 @pytest.mark.parametrize("path", CASES, ids=[p.split("/")[-1][:-4] for p in CASES])
@@ -283,7 +285,7 @@ def test_mixed_radix_general_engine_vs_oracle(N, P, O, Nz, shift, both):
     _general_engine_case(N, P, O, Nz, shift, both)
 
 
-# every 2·3·5·7-smooth N in [32, 256] (the sizes ptyx_gen.hip registers), cycling through mode /
+# every 2·3·5·7-smooth N in [32, 512] (the sizes ptyx_gen.hip registers), cycling through mode /
 # slice / shift / loss-term configurations; 128 and 256 run the register / stripe engines for some
 # of these and have their own cases
 _SMOOTH_CFGS = [(1, 1, 1, True, False), (2, 1, 2, True, False), (1, 2, 1, True, True), (2, 1, 1, False, False),
@@ -351,12 +353,12 @@ def test_random_configuration_vs_oracle(seed, monkeypatch):
 
 
 def test_unsupported_n_is_refused():
-    """N with a prime factor above 7 (88 = 8·11, 143 = 11·13), 245 = 5·7² (no two-pass plan), or
-    outside [32, 256], is refused with PTYX_EUNSUPPORTED at plan creation, not run."""
+    """N with a prime factor above 7 (88 = 8·11, 143 = 11·13), or outside [32, 512], is refused
+    with PTYX_EUNSUPPORTED at plan creation, not run."""
     dev()
     from ptyrad_amd import _lib
     from ptyrad_amd.engine import Plan
-    for n in (88, 143, 245, 16, 270):
+    for n in (88, 143, 16, 540, 1024):
         with pytest.raises(_lib.PtyxError, match="EUNSUPPORTED"):
             Plan(n, 1, 1, 1, 300, 300, 4, 4, device=torch.device("cuda", 0))
     Plan(100, 1, 1, 1, 200, 200, 4, 4, device=torch.device("cuda", 0)).close()
