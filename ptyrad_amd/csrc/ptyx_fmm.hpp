@@ -12,9 +12,9 @@
 //   k_fmm_fwd   job (b, p): ψ⁰ = F⁻¹(F(P_p)·W_b)/N²; for n: park ψⁿ (slot plane (b, n, p)), ×O_n,
 //               ×H between slices (forward.py:50-63, image_proc.py:531-532); far field
 //               v = F(ψ_out) stored K-packed (Ψ = v/N, forward.py:79)
-//   k_fmm_loss  pattern b: I = Σ_p occ|v_p|²/N² + 1e-10, dp_out, the loss partial sums and
-//               u = ∂ℓ/∂I per unit mini-batch coefficient, one plane per data term (K-packed;
-//               losses.py:36-75)
+//   k_fmm_loss  pattern b, in kLossParts parts of its K points: I = Σ_p occ|v_p|²/N² + 1e-10,
+//               dp_out, the loss partial sums and u = ∂ℓ/∂I per unit mini-batch coefficient, one
+//               plane per data term (K-packed; losses.py:36-75)
 //   k_finalize  c_m per mini-batch
 //   k_fmm_adj   job (b, p): g = F⁻¹(v_p·2 occ (c1 u1 + c2 u2)/N)/N (the coefficients applied here:
 //               this kernel runs after k_finalize, so both data terms fit one field); for
@@ -44,6 +44,7 @@ struct FmArgs {
   float q1, q2;         // dp_pow of loss_single / loss_poissn (f.eps2: the poissn eps)
   const float* coef;    // k_finalize's per-mini-batch coefficients
   int ci;               // one data term: its coefficient index (0 single, 1 poissn)
+  float* lparts;        // (patterns, kLossParts, 4) loss partial sums of k_fmm_loss
 };
 
 __device__ __forceinline__ float ld1(Rsrc r, int voff, int off) {
@@ -220,93 +221,79 @@ __global__ __launch_bounds__(256, 2) void k_fmm_fwd(FmArgs m) {
   }
 }
 
-// ------------------------------------------------------------------ loss: pattern → u, sums
-// One workgroup per pattern: the DP streams HBM → LDS (k_fused3's swizzled image) while the P
-// far fields are read K-packed and their intensities summed in mode order.
+// ------------------------------------------------------------------ loss: pattern part → u, sums
+// kLossParts workgroups per pattern, part s owning the K-packed registers k ∈ [s·KP, (s+1)·KP) of
+// every thread (KP = 64 / kLossParts): the P far fields are read in mode order and their
+// intensities summed, the DP values of those points are read directly (row (ky + 64) mod 128,
+// columns 4⌊k/4⌋ + 64(1 − l0) …: the fftshifted image), and the part's loss partial sums go to
+// lparts[pattern][part] (k_finalize adds the parts in order, fp64).  At the reference's default
+// cadence a call is one 32-pattern mini-batch: one workgroup per pattern would leave 224 CUs idle
+// behind a serial 6 × 128 KiB read; the same split at every call size keeps each pattern's sums
+// independent of how the call is cut.
 // TERMS: 1 loss_single, 2 loss_poissn, 3 both (QM: loss_single's dp_pow form; loss_poissn
 // always takes the general form)
+constexpr int kLossParts = 8;
 template <int QM, int TERMS>
 __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
-  using namespace rf;
+  constexpr int KP = 64 / kLossParts;
   const F3Args& a = m.f;
-  __shared__ float2 buf[kLdsElems];
   __shared__ float s_red[4 * 4];
-  const Coord cd = coord(threadIdx.x);
-  const int pat = blockIdx.x;
+  const int pat = blockIdx.x / kLossParts, part = blockIdx.x % kLossParts;
   const PatInfo pi = pat_info<false>(a, pat);
   const int tid = rf::opaque(threadIdx.x);
   const int fx = fixed_of(tid), l0 = tid & 1;
   constexpr float inv_n2 = 1.0f / kN2;
-  {
-    const float* dp = a.meas + (size_t)pi.mi * kN2;
-    const int lane = cd.lane;
-    const int wv = __builtin_amdgcn_readfirstlane(cd.wave);
+  const int k0 = part * KP;
+  // this part's DP values: KP / 4 float4 of row r, columns 4 kq + 64 b
+  const int r = (fx + 64) & 127;   // fftshifted DP row of ky
+  const int b = 1 - l0;            // fftshifted column half of kx = k + 64 l0
+  const float4* dp4 = reinterpret_cast<const float4*>(a.meas + (size_t)pi.mi * kN2 + r * kN + 64 * b) + k0 / 4;
+  float4 M4[KP / 4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int gi = wv * 16 + i;
-      const int r = 2 * gi + (lane >> 5);
-      const int sl = lane & 31;
-      const int c4 = sl ^ ((r & 7) | ((sl >> 4) << 3));
-      __builtin_amdgcn_global_load_lds(dp + r * kN + 4 * c4,
-                                       (__attribute__((address_space(3))) void*)((char*)buf + gi * 1024), 16, 0,
-                                       kNtAux);
-    }
-  }
+  for (int q = 0; q < KP / 4; ++q) M4[q] = dp4[q];
   const float occ_n2 = a.occp[0] * inv_n2;
-  float acc[64];
+  float acc[KP];
 #pragma unroll
-  for (int k = 0; k < 64; ++k) acc[k] = 0.f;
+  for (int k = 0; k < KP; ++k) acc[k] = 0.f;
   const int vpk = 8 * tid;
   for (int p = 0; p < m.P; ++p) {
     const Rsrc r_far = rsrc(a.slots + fmm_far(m, pat, p), kN2 * 8);
-    pipeline<16>(
-        [&](auto C) {
-          Ch4x2 t;
+    float2 t[KP];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) t.x[r] = ld2(r_far, vpk, 2048 * (4 * C + r));
-          return t;
-        },
-        [&](auto C, const Ch4x2& t) {
+    for (int k = 0; k < KP; ++k) t[k] = ld2(r_far, vpk, 2048 * (k0 + k));
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[4 * C + r] = fmaf(occ_n2, cabs2(t.x[r]), acc[4 * C + r]);
-        });
+    for (int k = 0; k < KP; ++k) acc[k] = fmaf(occ_n2, cabs2(t[k]), acc[k]);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   float S1 = 0.f, Ms1 = 0.f, S2 = 0.f, Ms2 = 0.f;
   {
-    const int r = (fx + 64) & 127;   // fftshifted DP row of ky
-    const int b = 1 - l0;            // fftshifted column half of kx = k + 64 l0
-    const float4* row4 = reinterpret_cast<const float4*>(buf) + r * 32;
     const Rsrc r_dp = rsrc(a.dp_out ? a.dp_out + (size_t)pat * kN2 : a.psums, a.dp_out ? kN2 * 4 : 0);
-    const int vdp = 4 * (r * kN + 64 * b);
+    const int vdp = 4 * (r * kN + 64 * b + k0);
     const Rsrc r_u = rsrc(m.ubuf + (size_t)pat * kN2, kN2 * 4);
     const Rsrc r_u2 = rsrc(TERMS == 3 ? m.ubuf2 + (size_t)pat * kN2 : m.ubuf, TERMS == 3 ? kN2 * 4 : 0);
     const int vu = 4 * tid;
 #pragma unroll
-    for (int kq = 0; kq < 16; ++kq) {
-      const float4 M4 = row4[(kq + 16 * b) ^ ((r & 7) | (b << 3))];
-      const float Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+    for (int q = 0; q < KP / 4; ++q) {
+      const float Mv[4] = {M4[q].x, M4[q].y, M4[q].z, M4[q].w};
       float Iv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = 4 * kq + e;
-        Iv[e] = acc[k] + kDpEps;
+        const int kk = 4 * q + e, k = k0 + kk;
+        Iv[e] = acc[kk] + kDpEps;
         if constexpr (TERMS & 1) st1(loss_point<QM, true>(Iv[e], Mv[e], m.q1, a.eps2, S1, Ms1), r_u, vu, 1024 * k);
         if constexpr (TERMS == 2) st1(loss_point<2, false>(Iv[e], Mv[e], m.q2, a.eps2, S2, Ms2), r_u, vu, 1024 * k);
         if constexpr (TERMS == 3) st1(loss_point<2, false>(Iv[e], Mv[e], m.q2, a.eps2, S2, Ms2), r_u2, vu, 1024 * k);
       }
       const __attribute__((ext_vector_type(4))) float i4 = {Iv[0], Iv[1], Iv[2], Iv[3]};
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, i4),
-                                             r_dp, vdp + 16 * kq, 0, 0);
+                                             r_dp, vdp + 16 * q, 0, 0);
     }
   }
   float v4[4] = {S1, Ms1, S2, Ms2};
   block_sum4<4>(v4, s_red);
   if (threadIdx.x == 0) {
-    float* ps = a.psums + (size_t)pat * kNSum;
+    float* lp = m.lparts + ((size_t)pat * kLossParts + part) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ps[i] = v4[i];
+    for (int i = 0; i < 4; ++i) lp[i] = v4[i];
   }
 }
 
@@ -570,6 +557,7 @@ __global__ void k_shift_apply_modes(const int* idx, int n, int n_scans, int P, c
 
 // Small calls: k_segslab_reduce_modes + k_segslab_final (every mode: blockIdx.y = p) and
 // k_shift_apply_modes in ONE launch, the segment sums in exactly their order (bit-identical).
+constexpr int kTailSegCap = 2048;   // segments (P + workgroups of k_fmm_adj) the LDS table holds
 template <bool KL>
 __global__ __launch_bounds__(256) void k_small_tail_modes(const float2* segslab, const int* segbid, int nseg,
                                                           float2* out, const int* idx, int n, int n_scans, int P,
@@ -590,16 +578,39 @@ __global__ __launch_bounds__(256) void k_small_tail_modes(const float2* segslab,
     return;
   }
   if (!out) return;
-  const int e = blockIdx.x * 256 + threadIdx.x, p = blockIdx.y;
-  float2 acc = make_float2(0.f, 0.f);
-  for (int y = 0; y < kSegSplit; ++y) {
-    float2 part = make_float2(0.f, 0.f);
-    for (int g = y; g < nseg; g += kSegSplit) {
-      if (segbid[g] != p) continue;
-      part = cadd(part, segslab[(size_t)g * kN2 + e]);
-    }
-    acc = cadd(acc, part);
+  // which segments are mode p's, as one bit each (ballots into LDS; read back into scalar
+  // registers, so the per-segment test is a scalar branch); the kSegSplit partial chains are
+  // independent, so each round issues the loads of all of them before adding: a missing segment
+  // adds +0, which leaves a partial (never −0: it starts at +0) unchanged — the same sums, in the
+  // same order, as k_segslab_reduce_modes + k_segslab_final
+  static_assert(kSegSplit == 32, "one 32-bit mask word a round");
+  __shared__ unsigned long long s_mask[kTailSegCap / 64];
+  const int p = blockIdx.y;
+  for (int g0 = 0; g0 < nseg; g0 += 256) {
+    const int g = g0 + (int)threadIdx.x;
+    const unsigned long long mk = __ballot(g < nseg && segbid[g] == p);
+    if ((threadIdx.x & 63) == 0) s_mask[g0 / 64 + (threadIdx.x >> 6)] = mk;
   }
+  __syncthreads();
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  float2 part[kSegSplit];
+#pragma unroll
+  for (int y = 0; y < kSegSplit; ++y) part[y] = make_float2(0.f, 0.f);
+  for (int g0 = 0; g0 < nseg; g0 += kSegSplit) {
+    const unsigned mw = __builtin_amdgcn_readfirstlane((unsigned)(s_mask[g0 / 64] >> (g0 & 32)));
+    if (!mw) continue;
+    float2 t[kSegSplit];
+#pragma unroll
+    for (int y = 0; y < kSegSplit; ++y) {
+      t[y] = make_float2(0.f, 0.f);
+      if (mw & (1u << y)) t[y] = segslab[(size_t)(g0 + y) * kN2 + e];
+    }
+#pragma unroll
+    for (int y = 0; y < kSegSplit; ++y) part[y] = cadd(part[y], t[y]);
+  }
+  float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[y]);
   out[(size_t)p * kN2 + packed_rc<KL>(e & 255, e >> 8)] = acc;
 }
 

@@ -154,20 +154,36 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
     return;
   }
   if (!out) return;
+  // the kSegSplit partial chains are independent: each round issues the loads of all of them, then
+  // adds (a missing segment adds 0·0 = +0 to a partial that is never −0: unchanged), so the sums
+  // and their order are k_segslab_reduce + k_segslab_final's
   const int e = blockIdx.x * 256 + threadIdx.x;
-  float2 acc = make_float2(0.f, 0.f);
-  for (int y = 0; y < kSegSplit; ++y) {
-    float2 part = make_float2(0.f, 0.f);
-    for (int g = y; g < nseg; g += kSegSplit) {
-      const int m = segbid[g];
-      if (m < 0) continue;
-      const float c = ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci];
-      const float2 u = segslab[(size_t)g * kN2 + e];
-      part.x = fmaf(c, u.x, part.x);
-      part.y = fmaf(c, u.y, part.y);
+  float2 part[kSegSplit];
+#pragma unroll
+  for (int y = 0; y < kSegSplit; ++y) part[y] = make_float2(0.f, 0.f);
+  for (int g0 = 0; g0 < nseg; g0 += kSegSplit) {
+    float2 u[kSegSplit];
+    float c[kSegSplit];
+#pragma unroll
+    for (int y = 0; y < kSegSplit; ++y) {
+      const int g = g0 + y;
+      const int m = g < nseg ? segbid[g] : -1;
+      u[y] = make_float2(0.f, 0.f);
+      c[y] = 0.f;
+      if (m >= 0) {
+        c[y] = ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci];
+        u[y] = segslab[(size_t)g * kN2 + e];
+      }
     }
-    acc = cadd(acc, part);
+#pragma unroll
+    for (int y = 0; y < kSegSplit; ++y) {
+      part[y].x = fmaf(c[y], u[y].x, part[y].x);
+      part[y].y = fmaf(c[y], u[y].y, part[y].y);
+    }
   }
+  float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[y]);
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
 }
 
@@ -408,9 +424,9 @@ __global__ void k_pattern_table3(const int* idx, int n, const int* boff, int n_b
 
 // Small calls (PTYX_PREP_CALL, ≤ kSmallCall patterns): k_pattern_table3's entries with the
 // loss_sparse window sum Σ_window |φ|^n read straight from objp — no summed-area table to build.
-// One workgroup per pattern: wave w sums rows w, w + 4, … of every slice, a lane two columns, 8
-// rows per round (16 loads in flight); fp64 lane sums, fixed-order wave reduction, waves added in
-// order through LDS (deterministic).
+// One workgroup per pattern: wave w sums rows w, w + 4, … of every slice, a lane two columns, a
+// slice's 32 rows per round (64 loads in flight: one round trip a slice); fp64 lane sums,
+// fixed-order wave reduction, waves added in order through LDS (deterministic).
 // one pattern's table entry (mini-batch by binary search over boff, clamped window origin) and
 // its input validation
 __device__ __forceinline__ void table_entry(int j, const int* idx, const int* boff, int n_batches, const int* crop,
@@ -438,19 +454,18 @@ __device__ __forceinline__ void k_pattern_table_direct_body(int j, const int* id
   if (threadIdx.x == 0) table_entry(j, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
   double acc = 0;
   for (int z = 0; z < Nz; ++z) {
-    const float* ph = objp + ((size_t)z * Ny + cy) * Nx + cx + lane;
-    for (int r0 = wave; r0 < kN; r0 += 32) {
-      float v[16];
+    // the wave's 32 rows of the slice in one round (64 loads in flight), summed in row order
+    const float* ph = objp + ((size_t)z * Ny + cy + wave) * Nx + cx + lane;
+    float v[64];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v[2 * k] = ph[(size_t)(r0 + 4 * k) * Nx];
-        v[2 * k + 1] = ph[(size_t)(r0 + 4 * k) * Nx + 64];
-      }
+    for (int k = 0; k < 32; ++k) {
+      v[2 * k] = ph[(size_t)(4 * k) * Nx];
+      v[2 * k + 1] = ph[(size_t)(4 * k) * Nx + 64];
+    }
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const float a = fabsf(v[k]);
-        acc += sparse_n == 1 ? (double)a : (double)powq(a, (float)sparse_n);
-      }
+    for (int k = 0; k < 64; ++k) {
+      const float a = fabsf(v[k]);
+      acc += sparse_n == 1 ? (double)a : (double)powq(a, (float)sparse_n);
     }
   }
 #pragma unroll
@@ -470,10 +485,15 @@ __global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, in
 // Small calls with PTYX_PREP_CALL (one mini-batch per optimizer step): k_pattern_table_direct,
 // k_obj_prep and k_bbox_small as ONE launch of independent block roles —
 //   blocks [0, n)            the pattern table (+ the loss_sparse window sums when SPARSE);
-//   blocks [n, n + Nz·Ny)    O = A e^{iφ} for object row y of slice z, if any window of the call
-//                            covers it (decided from the ≤ 256 windows directly, not the bbox);
-//   block n + Nz·Ny          the bounding box (k_obj_gather) and the segment-table clear.
+//   blocks [n, n + R)        O = A e^{iφ} for kPrepRows object rows (of the Nz·Ny) each, those any
+//                            window of the call covers (decided from the ≤ 256 windows directly,
+//                            not the bbox); R = ⌈Nz·Ny / kPrepRows⌉ (small_prep_blocks);
+//   block n + R              the bounding box (k_obj_gather) and the segment-table clear.
 // Same outputs as the three kernels (the rows no window touches are never read under PREP_CALL).
+constexpr int kPrepRows = 4;
+__host__ __device__ constexpr int small_prep_blocks(int n, int Nz, int Ny) {
+  return n + (Nz * Ny + kPrepRows - 1) / kPrepRows + 1;
+}
 template <bool SPARSE>
 __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const int* boff, int n_batches,
                                                     const int* crop, int n_scans, int Ny, int Nx, int* bid, int2* geo,
@@ -490,26 +510,41 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
     }
     return;
   }
-  if (b == n + Nz * Ny) {
+  const int nrb = (Nz * Ny + kPrepRows - 1) / kPrepRows;
+  if (b == n + nrb) {
     k_bbox_small_body(idx, n, crop, n_scans, Ny, Nx, bbox, kN, segbid, nseg);
     return;
   }
-  const int y = b - n;
-  const int r = y % Ny;
-  int hit = 0;
+  // kPrepRows consecutive object rows (flattened z·Ny + r): which of them any window covers, then
+  // their loads issued together
+  const int y0 = (b - n) * kPrepRows;
+  int cy = -(1 << 29);
   if ((int)threadIdx.x < n) {
     const int s = min(max(idx[threadIdx.x], 0), n_scans - 1);
-    const int cy = min(max(crop[2 * s], 0), Ny - kN);
-    hit = r >= cy && r < cy + kN;
+    cy = min(max(crop[2 * s], 0), Ny - kN);
   }
-  if (!__syncthreads_or(hit)) return;
-  const float* ar = obja + (size_t)y * Nx;
-  const float* pr = objp + (size_t)y * Nx;
-  float2* orow = oc + (size_t)y * Nx;
-  for (int x = threadIdx.x; x < Nx; x += blockDim.x) {
-    float sn, cs;
-    phase_sincos(pr[x], &sn, &cs);
-    orow[x] = make_float2(ar[x] * cs, ar[x] * sn);
+  bool hit[kPrepRows];
+#pragma unroll
+  for (int k = 0; k < kPrepRows; ++k) {
+    const int r = (y0 + k) % Ny;
+    hit[k] = __syncthreads_or(y0 + k < Nz * Ny && r >= cy && r < cy + kN) != 0;
+  }
+  for (int x0 = 0; x0 < Nx; x0 += 256) {
+    const int x = x0 + (int)threadIdx.x;
+    float av[kPrepRows], pv[kPrepRows];
+#pragma unroll
+    for (int k = 0; k < kPrepRows; ++k)
+      if (hit[k] && x < Nx) {
+        av[k] = obja[(size_t)(y0 + k) * Nx + x];
+        pv[k] = objp[(size_t)(y0 + k) * Nx + x];
+      }
+#pragma unroll
+    for (int k = 0; k < kPrepRows; ++k)
+      if (hit[k] && x < Nx) {
+        float sn, cs;
+        phase_sincos(pv[k], &sn, &cs);
+        oc[(size_t)(y0 + k) * Nx + x] = make_float2(av[k] * cs, av[k] * sn);
+      }
   }
 }
 

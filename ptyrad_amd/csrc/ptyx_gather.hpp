@@ -215,6 +215,143 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
   }
 }
 
+// Row-split variant (small calls of the mixed-state engine): the workgroup first lists the hits
+// of a chunk of 64·GW candidates in candidate order (ballot + prefix, LDS), then EVERY wave takes
+// all of them for its own kGTY / GW rows, HU hits' loads in flight at once.  k_obj_gather gives a
+// wave whole hits, 16 rows × np planes each, and at np = 6 the compiler issues them row by row (16
+// round trips a hit); here a hit costs one.  Each wave owns its rows to the end, so there is no
+// wave-partial reduction either.  Hits are summed in candidate order (deterministic).
+template <int N, bool ROWPERM, int GW, bool MP>
+__global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
+  constexpr int N2 = N * N;
+  constexpr int NB = BinReach<N>::n;
+  constexpr int RW = kGTY / GW;                          // rows per wave
+  constexpr int NPL = MP ? kGatherMaxNp : 1;             // planes per row and hit (≤; np at run time)
+  constexpr int HU = 32 / (RW * NPL) > 0 ? 32 / (RW * NPL) : 1;   // hits in flight per wave
+  static_assert(kGTY % GW == 0, "rows split evenly over the waves");
+  __shared__ int4 s_hit[64 * GW];     // (cy, cx, j, c) of the chunk's hits, candidate order
+  __shared__ float s_hcs[64 * GW];
+  __shared__ int s_wcnt[GW];
+  __shared__ int s_b0[NB], s_pre[NB + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
+  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;
+  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;
+  const int ty = tyi * kGTY, tx = txi * kGTX;
+  if (gather_tile_skip<N>(ga, ty, tx)) return;
+  int total = ga.n;
+  if (ga.boff) {
+    if (threadIdx.x < NB) {
+      const int by = tyi - (BinReach<N>::rows - 1) + (int)threadIdx.x / BinReach<N>::cols;
+      const int bx = txi - (BinReach<N>::cols - 1) + (int)threadIdx.x % BinReach<N>::cols;
+      int b0 = 0, len = 0;
+      if (by >= 0 && bx >= 0) {
+        const int b = by * ga.tiles_x + bx;
+        b0 = ga.boff[b];
+        len = ga.boff[b + 1] - b0;
+      }
+      s_b0[threadIdx.x] = b0;
+      s_pre[threadIdx.x + 1] = len;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_pre[0] = 0;
+      for (int k = 0; k < NB; ++k) s_pre[k + 1] += s_pre[k];
+    }
+    __syncthreads();
+    total = s_pre[NB];
+  }
+  const int x = tx + lane;
+  const int r0 = ty + wave * RW;   // this wave's first object row
+  float2 acc[RW];
+  float cnt[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    acc[r] = make_float2(0.f, 0.f);
+    cnt[r] = 0.f;
+  }
+  const int np = MP ? ga.np : 1;
+  for (int base = 0; base < total; base += 64 * GW) {
+    const int i = base + (int)threadIdx.x;
+    int j = i;
+    int2 o = make_int2(-(1 << 29), -(1 << 29));
+    float2 cj = make_float2(0.f, 0.f);
+    if (i < total) {
+      if (ga.boff) {
+        int k = 0;
+        while (k + 1 < NB && s_pre[k + 1] <= i) ++k;
+        j = ga.blist[s_b0[k] + (i - s_pre[k])];
+      }
+      o = ga.geo[j];
+      cj = ga.pcoef[j];
+    }
+    const bool hit = o.x > ty - N && o.x < ty + kGTY && o.y > tx - N && o.y < tx + kGTX;
+    const unsigned long long mk = __ballot(hit);
+    if (lane == 0) s_wcnt[wave] = __popcll(mk);
+    __syncthreads();
+    int off = 0, nh = 0;
+#pragma unroll
+    for (int w = 0; w < GW; ++w) {
+      const int c = s_wcnt[w];
+      off += w < wave ? c : 0;
+      nh += c;
+    }
+    if (hit) {
+      const int at = off + __popcll(mk & ((1ull << lane) - 1ull));
+      s_hit[at] = make_int4(o.x, o.y, j, __float_as_int(cj.x));
+      s_hcs[at] = cj.y;
+    }
+    __syncthreads();
+    for (int h0 = 0; h0 < nh; h0 += HU) {
+      float2 t[HU][RW][NPL];
+#pragma unroll
+      for (int hu = 0; hu < HU; ++hu) {
+        const int h = h0 + hu;
+        const int4 H = s_hit[h < nh ? h : 0];
+        const int col = x - H.y;
+        const bool colok = h < nh && col >= 0 && col < N;
+        const float2* src = MP ? ga.ogscr + ((size_t)H.z * ga.pstride + (size_t)zp * ga.np) * N2
+                               : ga.ogscr + ((size_t)H.z * ga.nz + zp) * N2;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const int row = r0 + r - H.x;
+          const int srow = ROWPERM ? 2 * (row & (N / 2 - 1)) + (row >> 6) : row;
+          const bool ok = colok && row >= 0 && row < N;
+#pragma unroll
+          for (int pp = 0; pp < NPL; ++pp)
+            t[hu][r][pp] = ok && pp < np ? src[(size_t)pp * N2 + srow * N + col] : make_float2(0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int hu = 0; hu < HU; ++hu) {
+        const int h = h0 + hu;
+        if (h >= nh) break;
+        const int4 H = s_hit[h];
+        const float c = __int_as_float(H.w), cs = s_hcs[h];
+        const int col = x - H.y;
+        const bool colok = col >= 0 && col < N;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          float2 v = t[hu][r][0];
+#pragma unroll
+          for (int pp = 1; pp < NPL; ++pp) v = cadd(v, t[hu][r][pp]);
+          acc[r].x = fmaf(c, v.x, acc[r].x);
+          acc[r].y = fmaf(c, v.y, acc[r].y);
+          const int row = r0 + r - H.x;
+          if (colok && row >= 0 && row < N) cnt[r] += cs;
+        }
+      }
+    }
+    __syncthreads();   // the next chunk rewrites the hit list
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int y = r0 + r;
+    if (y >= ga.Ny || x >= ga.Nx) continue;
+    gather_apply(ga, zoff + (size_t)y * ga.Nx + x, acc[r], cnt[r]);
+  }
+}
+
 // Split gather epilogue: tile (blockIdx.x, blockIdx.y) sums its S partials in split order.
 template <int N>
 __global__ __launch_bounds__(256) void k_obj_gather_fin(GatherArgs ga, int S) {

@@ -65,101 +65,123 @@ struct FinArgs {
   long long pcoef_stride = 0;  // patterns per plane
   double* bsums_out = nullptr;
   const double* bsums_in = nullptr;
+  const float* lparts = nullptr;   // the data-term sums [0, kSumBase) as nparts partials per pattern
+  int nparts = 0;                  // (k_fmm_loss, ≤ kFinMaxParts), added in part order
 };
+constexpr int kFinMaxParts = 8;
+static_assert(kSumBase == 4, "k_finalize reads the data-term sums as one float4");
 
 // One wave per mini-batch: lane l sums patterns b0 + l, b0 + l + 64, … (fp64), then a fixed
-// xor-tree over the lanes (deterministic, independent of how a call is split into pieces); lane 0
-// computes the terms and coefficients, every lane writes its share of the per-pattern coefficients.
+// xor-tree over the lanes (deterministic, independent of how a call is split into pieces).  After
+// the tree every lane holds the same sums, so every lane computes the (uniform) terms and
+// coefficients; lane 0 stores them, every lane writes its share of the per-pattern coefficients.
+// The object modes are a runtime loop with one accumulator at a time (no per-mode register arrays:
+// indexed by the runtime O they went to scratch).
 constexpr int kFinWaves = 2;   // mini-batches per 128-thread workgroup
 __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
   const int m = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (m >= f.n_batches) return;   // (wave-uniform)
   const int b0 = f.boff[m], b1 = f.boff[m + 1];
-  double B = (double)(b1 - b0);
-  double S1 = 0, M1 = 0, S2 = 0, M2 = 0, sp[kMaxModesO] = {0};
-  if (f.bsums_in) {
-    const double* bs = f.bsums_in + (size_t)m * kNBatchSum;
-    B = bs[0]; S1 = bs[1]; M1 = bs[2]; S2 = bs[3]; M2 = bs[4];
+  const double* bin = f.bsums_in ? f.bsums_in + (size_t)m * kNBatchSum : nullptr;
+  // additive sum k of the mini-batch (k < kSumBase: the data terms, kSumBase + o: sparse mode o)
+  auto wsum = [&](int k) -> double {
+    if (bin) return bin[1 + k];
+    double s = 0;
+    for (int t = b0 + lane; t < b1; t += 64) s += f.psums[(size_t)t * kNSum + k];
 #pragma unroll
-    for (int o = 0; o < kMaxModesO; ++o)
-      if (o < f.O) sp[o] = bs[5 + o];
+    for (int x = 32; x >= 1; x >>= 1) s += __shfl_xor(s, x, 64);
+    return s;
+  };
+  // the four data-term sums together (their loads in flight at once): from psums, or from the
+  // per-pattern part partials (lparts, parts in order)
+  double D[4] = {0, 0, 0, 0};
+  if (bin) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) D[k] = bin[1 + k];
   } else {
     for (int t = b0 + lane; t < b1; t += 64) {
-      const float* ps = f.psums + (size_t)t * kNSum;
-      S1 += ps[0];
-      M1 += ps[1];
-      S2 += ps[2];
-      M2 += ps[3];
+      if (f.lparts) {
+        const float4* lp = reinterpret_cast<const float4*>(f.lparts) + (size_t)t * f.nparts;
+        float4 q4[kFinMaxParts];
 #pragma unroll
-      for (int o = 0; o < kMaxModesO; ++o)
-        if (o < f.O) sp[o] += ps[kSumBase + o];
+        for (int q = 0; q < kFinMaxParts; ++q)
+          if (q < f.nparts) q4[q] = lp[q];
+#pragma unroll
+        for (int q = 0; q < kFinMaxParts; ++q)
+          if (q < f.nparts) {
+            D[0] += q4[q].x;
+            D[1] += q4[q].y;
+            D[2] += q4[q].z;
+            D[3] += q4[q].w;
+          }
+      } else {
+        const float4 v = *reinterpret_cast<const float4*>(f.psums + (size_t)t * kNSum);
+        D[0] += v.x;
+        D[1] += v.y;
+        D[2] += v.z;
+        D[3] += v.w;
+      }
     }
 #pragma unroll
-    for (int x = 32; x >= 1; x >>= 1) {
-      S1 += __shfl_xor(S1, x, 64);
-      M1 += __shfl_xor(M1, x, 64);
-      S2 += __shfl_xor(S2, x, 64);
-      M2 += __shfl_xor(M2, x, 64);
+    for (int x = 32; x >= 1; x >>= 1)
 #pragma unroll
-      for (int o = 0; o < kMaxModesO; ++o)
-        if (o < f.O) sp[o] += __shfl_xor(sp[o], x, 64);
-    }
+      for (int k = 0; k < 4; ++k) D[k] += __shfl_xor(D[k], x, 64);
   }
+  const double B = bin ? bin[0] : (double)(b1 - b0);
+  const double S1 = D[0], M1 = D[1], S2 = D[2], M2 = D[3];
   if (f.bsums_out) {
+    double* bs = f.bsums_out + (size_t)m * kNBatchSum;
     if (lane == 0) {
-      double* bs = f.bsums_out + (size_t)m * kNBatchSum;
       bs[0] = B; bs[1] = S1; bs[2] = M1; bs[3] = S2; bs[4] = M2;
-      for (int o = 0; o < kMaxModesO; ++o) bs[5 + o] = o < f.O ? sp[o] : 0.0;
+    }
+    for (int o = 0; o < kMaxModesO; ++o) {
+      const double so = o < f.O ? wsum(kSumBase + o) : 0.0;
+      if (lane == 0) bs[5 + o] = so;
     }
     return;
   }
-  float cf[2 + kMaxModesO] = {0};
-  if (lane == 0) {
-    const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
-    float terms[5] = {0, 0, 0, 0, 0};
-    if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
-      const double mu = M1 / K, rmse = sqrt(S1 / K);
-      terms[0] = (float)(f.w1 * rmse / mu);
-      cf[0] = rmse > 0 ? (float)(f.w1 / (mu * K * rmse) * f.grad_scale) : 0.f;
-    }
-    if (f.pois_on && B > 0) {  // -w·mean(M^q log(I^q+eps) - I^q) / mean(M^q)   losses.py:70-72
-      const double mu = M2 / K;
-      terms[1] = (float)(-f.w2 * (S2 / K) / mu);
-      cf[1] = (float)(-f.w2 / (mu * K) * f.grad_scale);
-    }
-    if (f.sparse_on && B > 0) {  // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
-      const double cnt = B * f.Nz * f.N * f.N;
-      double t = 0;
-#pragma unroll
-      for (int o = 0; o < kMaxModesO; ++o) {
-        if (o >= f.O) break;
-        const double mo = sp[o] / cnt;
-        const double inv = 1.0 / f.sparse_n;
-        t += f.occu[o] * pow(mo, inv);
-        const double dm = (f.sparse_n == 1) ? 1.0 : (mo > 0 ? pow(mo, inv - 1.0) : 0.0);
-        cf[2 + o] = (float)(f.ws * f.occu[o] * dm / cnt * f.grad_scale);
-      }
-      terms[3] = (float)(f.ws * t);
-    }
-    float* cfo = f.coef + (size_t)m * kNCoef;
-    cfo[0] = cf[0];
-    cfo[1] = cf[1];
-#pragma unroll
-    for (int o = 0; o < kMaxModesO; ++o)
-      if (o < f.O) cfo[2 + o] = cf[2 + o];
-    if (f.loss_terms)
-      for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
+  const double K = B * f.N * f.N;  // elements of the mini-batch DP stack
+  float terms[5] = {0, 0, 0, 0, 0};
+  float c_single = 0.f, c_pois = 0.f;
+  if (f.single_on && B > 0) {  // w·sqrt(mean((I^q-M^q)^2)) / mean(M^q)   losses.py:45-47
+    const double mu = M1 / K, rmse = sqrt(S1 / K);
+    terms[0] = (float)(f.w1 * rmse / mu);
+    c_single = rmse > 0 ? (float)(f.w1 / (mu * K * rmse) * f.grad_scale) : 0.f;
   }
-  if (f.pcoef) {   // the coefficients of lane 0, written for every pattern of the mini-batch
-    const float c = __shfl(f.ci == 0 ? cf[0] : f.ci == 1 ? cf[1] : 1.f, 0, 64);   // (ci 2: already applied)
-#pragma unroll
-    for (int o = 0; o < kMaxModesO; ++o) {
-      if (o >= f.pcoef_O) break;
-      const float2 pc = make_float2(c, __shfl(cf[2 + o], 0, 64));
+  if (f.pois_on && B > 0) {  // -w·mean(M^q log(I^q+eps) - I^q) / mean(M^q)   losses.py:70-72
+    const double mu = M2 / K;
+    terms[1] = (float)(-f.w2 * (S2 / K) / mu);
+    c_pois = (float)(-f.w2 / (mu * K) * f.grad_scale);
+  }
+  float* cfo = f.coef + (size_t)m * kNCoef;
+  if (lane == 0) {
+    cfo[0] = c_single;
+    cfo[1] = c_pois;
+  }
+  const float c = f.ci == 0 ? c_single : f.ci == 1 ? c_pois : 1.f;   // (ci 2: already applied)
+  const bool sparse = f.sparse_on && B > 0;
+  const int nO = f.pcoef ? max(f.O, f.pcoef_O) : f.O;
+  double t_sp = 0;
+  for (int o = 0; o < nO; ++o) {   // w·Σ_o occ_o (mean |φ|^n)^(1/n)   losses.py:101
+    float cs = 0.f;
+    if (o < f.O && sparse) {
+      const double cnt = B * f.Nz * f.N * f.N;
+      const double mo = wsum(kSumBase + o) / cnt;
+      const double inv = 1.0 / f.sparse_n;
+      t_sp += f.occu[o] * pow(mo, inv);
+      const double dm = (f.sparse_n == 1) ? 1.0 : (mo > 0 ? pow(mo, inv - 1.0) : 0.0);
+      cs = (float)(f.ws * f.occu[o] * dm / cnt * f.grad_scale);
+    }
+    if (o < f.O && lane == 0) cfo[2 + o] = cs;
+    if (f.pcoef && o < f.pcoef_O) {   // the mini-batch's coefficients, written for every pattern
+      const float2 pc = make_float2(c, cs);
       for (int t = b0 + lane; t < b1; t += 64) f.pcoef[o * f.pcoef_stride + t] = pc;
     }
   }
+  if (sparse) terms[3] = (float)(f.ws * t_sp);
+  if (lane == 0 && f.loss_terms)
+    for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
 }
 
 
@@ -253,6 +275,7 @@ struct ptyx_plan {
   float* coef = nullptr;
   float* Ibuf = nullptr;
   float* Ibuf2 = nullptr;     // mixed-state register engine with both data terms: ∂ℓ_poissn/∂I planes
+  float* lparts = nullptr;    // mixed-state register engine: k_fmm_loss partial sums (patterns, parts, 4)
   float* Imodes = nullptr;    // probe-mode split: P mode-intensity planes per pattern (≤ kModeSplitCap)
   float2* slab = nullptr;
   float2* Gsum = nullptr;
@@ -419,6 +442,13 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
     S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], pl->gpart_cap / parts));
   g.part = pl->gpart;
   g.pcnt = pl->gpcnt;
+  if constexpr (MP) {
+    if (S == 1 && g.n <= f3::kSmallCall) {   // mixed-state small calls: rows over waves
+      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
+      else hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
+      return;
+    }
+  }
   if (S == 1) {
     if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
     else hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
@@ -601,7 +631,8 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
           (rc = dalloc(pl, &pl->segslab, (size_t)pl->seg_cap * N2)) || (rc = dalloc(pl, &pl->segbid, (size_t)pl->seg_cap)) ||
           (rc = dalloc(pl, &pl->dsu, (size_t)d.max_patterns * d.P * 2)) ||
           (rc = dalloc(pl, &pl->segpart, (size_t)d.P * f3::kSegSplit * N2)) || (rc = alloc_bins(pl)) ||
-          (rc = dalloc(pl, &pl->Ibuf2, (size_t)pl->ffc_cap * N2))) {
+          (rc = dalloc(pl, &pl->Ibuf2, (size_t)pl->ffc_cap * N2)) ||
+          (rc = dalloc(pl, &pl->lparts, (size_t)d.max_patterns * f3::kLossParts * kSumBase))) {
         free_plan(pl);
         return rc;
       }
@@ -875,7 +906,7 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
   const bool direct_sums = sparse && small && cfg->prep == PTYX_PREP_CALL;
   if (small && cfg->prep == PTYX_PREP_CALL) {   // table, object rows, bbox: one launch (k_small_prep)
     ProfScope ps(pl, kKTable, st);
-    const dim3 gr(a.n_idx + Nz * d.Ny + 1), bl(256);
+    const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny)), bl(256);
     const f3::TableCheck tc{a.err, a.mrow, a.mrows};
     if (sparse)
       hipLaunchKernelGGL(f3::k_small_prep<true>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop, a.n_scans,
@@ -1147,6 +1178,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   m.q2 = cfg->poissn_q;
   m.coef = pl->coef;
   m.ci = ci;
+  m.lparts = pl->lparts;
   int rc = PTYX_OK;
   if (ph != kPhaseEnd) {
     if ((rc = register_prep(pl, in, a, cfg, st, nseg))) return rc;
@@ -1157,7 +1189,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     }
     {
       ProfScope ps(pl, kKFmmLoss, st);
-      const dim3 gr(a.n_idx), bl(256);
+      const dim3 gr(a.n_idx * f3::kLossParts), bl(256);
       const bool half = cfg->single_q == 0.5f;
       if (both && half) hipLaunchKernelGGL((f3::k_fmm_loss<0, 3>), gr, bl, 0, st, m);
       else if (both) hipLaunchKernelGGL((f3::k_fmm_loss<2, 3>), gr, bl, 0, st, m);
@@ -1173,6 +1205,8 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
   fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  static_assert(f3::kLossParts <= kFinMaxParts, "k_finalize's part loop");
+  fa.lparts = pl->lparts; fa.nparts = f3::kLossParts;
   if (gz.d_obja || gz.d_objp) {
     fa.pcoef = pl->pcoef;
     fa.ci = 2;   // the slots already carry the data coefficients (k_fmm_adj): the gather's is 1
@@ -1223,7 +1257,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
   float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+  if (!bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
     {
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);

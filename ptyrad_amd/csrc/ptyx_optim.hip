@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "ptyx.h"
 #include "ptyx_abi.hpp"
@@ -163,23 +164,47 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
   ptyx::abi::clear_error();
   if (n < 0 || (n && (!params || !grads || !exp_avgs || !exp_avg_sqs || !steps || !numels || !lrs)))
     return fail(PTYX_EINVAL, "ptyx_adam_step: null array or negative count");
-  for (int i0 = 0; i0 < n; i0 += opt::kMaxT) {
+  // Each tensor is one or two ranges: its first 4·⌊numel/4⌋ elements in float4 units when p, g,
+  // m, v are 16-B aligned, the (≤ 3) others as scalar units — a 591² × 6 object plane is not a
+  // multiple of 4 and would otherwise run at 4-byte accesses.  Ranges are grouped kMaxT a launch.
+  struct Range {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    const float* step;
+    double lr;
+    int64_t numel;
+    int vec;
+  };
+  std::vector<Range> rs;
+  rs.reserve(2 * (size_t)n);
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  for (int i = 0; i < n; ++i) {
+    if (numels[i] < 0 || (numels[i] && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i] || !steps[i])))
+      return fail(PTYX_EINVAL, "ptyx_adam_step: null tensor pointer or negative size");
+    if (!numels[i]) continue;
+    const bool aligned = al16(params[i]) && al16(grads[i]) && al16(exp_avgs[i]) && al16(exp_avg_sqs[i]);
+    const int64_t body = aligned ? numels[i] / 4 * 4 : 0;
+    if (body) rs.push_back({params[i], grads[i], exp_avgs[i], exp_avg_sqs[i], steps[i], lrs[i], body, 1});
+    if (numels[i] > body)
+      rs.push_back({params[i] + body, grads[i] + body, exp_avgs[i] + body, exp_avg_sqs[i] + body, steps[i], lrs[i],
+                    numels[i] - body, 0});
+  }
+  for (size_t i0 = 0; i0 < rs.size(); i0 += opt::kMaxT) {
     opt::AdamArgs a{};
-    a.nt = std::min(opt::kMaxT, n - i0);
+    a.nt = (int)std::min<size_t>(opt::kMaxT, rs.size() - i0);
     a.off[0] = 0;
     for (int k = 0; k < a.nt; ++k) {
-      const int i = i0 + k;
-      if (numels[i] < 0 || (numels[i] && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i] || !steps[i])))
-        return fail(PTYX_EINVAL, "ptyx_adam_step: null tensor pointer or negative size");
-      a.p[k] = params[i];
-      a.g[k] = grads[i];
-      a.m[k] = exp_avgs[i];
-      a.v[k] = exp_avg_sqs[i];
-      a.step[k] = steps[i];
-      a.lr[k] = lrs[i];
-      const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-      a.vec[k] = numels[i] % 4 == 0 && al16(params[i]) && al16(grads[i]) && al16(exp_avgs[i]) && al16(exp_avg_sqs[i]);
-      a.units[k] = a.vec[k] ? numels[i] / 4 : numels[i];
+      const Range& r = rs[i0 + k];
+      a.p[k] = r.p;
+      a.g[k] = r.g;
+      a.m[k] = r.m;
+      a.v[k] = r.v;
+      a.step[k] = r.step;
+      a.lr[k] = r.lr;
+      a.vec[k] = r.vec;
+      a.units[k] = r.vec ? r.numel / 4 : r.numel;
       a.off[k + 1] = a.off[k] + (a.units[k] + opt::kChunk - 1) / opt::kChunk * opt::kChunk;
     }
     for (int k = a.nt; k < opt::kMaxT; ++k) a.off[k + 1] = a.off[a.nt];
