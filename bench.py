@@ -151,6 +151,46 @@ def cpu_baseline(n, bsize, sample):
     return out
 
 
+def cpu_adam_ms(shapes, reps=5):
+    """One torch.optim.Adam step (single-tensor arithmetic, NumPy fp32) over tensors of the given
+    shapes on one host core: the per-optimizer-step cost a CPU run of the reference's default
+    cadence pays on top of the mini-batch's forward / loss / gradient."""
+    rng = np.random.default_rng(0)
+    ts = [(rng.random(s, dtype=np.float32), rng.random(s, dtype=np.float32) - np.float32(0.5),
+           np.zeros(s, np.float32), np.zeros(s, np.float32)) for s in shapes]
+    b1, b2, lr, eps = np.float32(0.9), np.float32(0.999), 5e-4, np.float32(1e-8)
+    best = float("inf")
+    for r in range(reps):
+        t = time.perf_counter()
+        step = r + 1
+        bc1, bc2s = 1.0 - 0.9 ** step, math.sqrt(1.0 - 0.999 ** step)
+        for p, g, m, v in ts:
+            m += (g - m) * (np.float32(1.0) - b1)
+            v *= b2
+            v += (np.float32(1.0) - b2) * g * g
+            p += np.float32(-lr / bc1) * m / (np.sqrt(v) / np.float32(bc2s) + eps)
+        best = min(best, time.perf_counter() - t)
+    return 1e3 * best
+
+
+def with_adam(cpu, shapes, bsize):
+    """cpu_baseline at the reference's default cadence: every mini-batch of `bsize` also pays one
+    Adam step over the full parameter set (each worker process its own, as independent replicas)."""
+    if not cpu:
+        return cpu
+    ms = cpu_adam_ms(shapes)
+    per_core = cpu["value"] / cpu["cores"]                  # patterns/s of one process
+    t_batch = bsize / per_core
+    out = dict(cpu)
+    out["value"] = round(cpu["cores"] * bsize / (t_batch + ms / 1e3), 1)
+    out["value_without_adam"] = cpu["value"]
+    out["adam_ms_per_optimizer_step"] = round(ms, 2)
+    out["sample"] = cpu["sample"] + (f"; plus one NumPy fp32 Adam step (torch single-tensor order) over the c2 "
+                                     f"parameters {[list(s) for s in shapes]} per mini-batch of {bsize}, "
+                                     f"{ms:.1f} ms on one core (grad_accumulation = 1, like for like)")
+    return out
+
+
 # ------------------------------------------------------------------ GPU workload
 def gt_object(shape, dev, seed=1):
     """Ground-truth object on the device: unit amplitude, Gaussian atoms (σ 1.5 px,
@@ -305,6 +345,10 @@ def main():
     if a.cadence == "reference":
         if a.config != "c2":
             raise SystemExit("--cadence reference runs the c2 geometry")
+        if cpu:
+            from ptyrad_amd import synthetic as syn
+            crop_pos, _, (Ny, Nx), _, _ = syn.bench_geometry("c2", 1, 0, scan=a.scan)
+            cpu = with_adam(cpu, [(1, 1, Ny, Nx), (1, 1, Ny, Nx), (1, 128, 128, 2), (crop_pos.shape[0], 2)], a.batch)
         return reference_cadence(a, world, rank, local, cpu)
 
     import torch
