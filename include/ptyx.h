@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 205
+#define PTYX_ABI_VERSION 206
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -257,6 +257,18 @@ int ptyx_patch_gather(void *stream, const float *obj, int32_t O, int32_t Nz, int
  * are summed in arrival order).  Same shapes and limits. */
 int ptyx_patch_scatter_add(void *stream, const float *gpatches, int32_t O, int32_t Nz, int32_t Ny, int32_t Nx,
                            const int32_t *crop_pos, const int32_t *idx, int32_t n_idx, int32_t N, float *gobj);
+
+/* loss_simlar's core (CombinedLoss.get_loss_simlar, src/ptyrad/losses.py:106-141):
+ * x (O, n_planes, n_pix) f32 — the (blurred / resampled) patches of one type, modes outermost —,
+ * occ (O) f32.  sums[q] = Σ_pix std_o(occ_o·x[o,q,pix]), the unbiased (correction 1) std over the
+ * modes as torch.std(1); per plane a fixed-order reduction (deterministic).  O = 1 gives NaN, as
+ * torch does.  n_planes ≤ 2^31 − 1. */
+int ptyx_simlar_std(void *stream, const float *x, int32_t O, int64_t n_planes, int32_t n_pix, const float *occ,
+                    float *sums);
+/* Its backward: gx[o,q,pix] = gsum[q]·occ_o·(w_o − mean_o w)/((O − 1)·std), w = occ·x (torch's
+ * std backward; 0/0 where the std is 0, as torch). */
+int ptyx_simlar_std_grad(void *stream, const float *x, int32_t O, int64_t n_planes, int32_t n_pix, const float *occ,
+                         const float *gsum, float *gx);
 
 /* loss_pacbed (src/ptyrad/losses.py:77-89) per mini-batch, on model intensities dp (n_idx,N,N)
  * (e.g. the dp_out of ptyx_forward_loss_grad): loss_terms[m*5 + 2] = w·sqrt(mse(mean_b dp^q…)) /

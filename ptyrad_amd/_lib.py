@@ -14,7 +14,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 205     # include/ptyx.h
+PTYX_ABI_VERSION = 206     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_PREP_DEFER_PROBE = 4  # flag bit: the probe-gradient reduction may wait for a later piece
 PTYX_BATCH_SUMS = 37      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
@@ -30,7 +30,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning", "ptyx_get_tuning",
            "ptyx_adjoint_dldi", "ptyx_profile_begin", "ptyx_profile_end", "ptyx_plan_workspace_bytes",
            "ptyx_last_error", "ptyx_version", "ptyx_constraints_ws_bytes", "ptyx_constraints_evals_offset",
-           "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add",
+           "ptyx_meas_gather", "ptyx_pacbed_ws_bytes", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather", "ptyx_patch_scatter_add", "ptyx_simlar_std", "ptyx_simlar_std_grad",
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
            "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
@@ -169,6 +169,8 @@ def load(path: str | None = None):
                                              i32, i32, i32, i32, vp]
     lib.ptyx_meas_pad_resample.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp, i32]
     lib.ptyx_step_select.argtypes = [vp, vp, vp, vp, i32, vp, vp, i64]
+    lib.ptyx_simlar_std.argtypes = [vp, vp, i32, i64, i32, vp, vp]
+    lib.ptyx_simlar_std_grad.argtypes = [vp, vp, i32, i64, i32, vp, vp, vp]
     lib.ptyx_step_store.argtypes = [vp, vp, i32, vp, vp, vp]
     d64 = ctypes.c_double
     lib.ptyx_adam_step.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32]
@@ -177,7 +179,8 @@ def load(path: str | None = None):
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
                  "ptyx_probe_ortho", "ptyx_raw_read", "ptyx_meas_stats", "ptyx_meas_finish",
-                 "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample"):
+                 "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
+                 "ptyx_simlar_std", "ptyx_simlar_std_grad"):
         getattr(lib, name).restype = ctypes.c_int
     _check_abi(lib)
     _lib = lib

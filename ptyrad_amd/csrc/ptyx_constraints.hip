@@ -52,6 +52,28 @@ cons::Taps torchvision_taps(int ks, float sigma) {
   return t;
 }
 
+// the separable blur (or its transpose) with H = kernel_size / 2 at compile time
+template <bool ADJ, int H>
+void launch_blur(hipStream_t st, const float* in, float* out, int n_planes, int Ny, int Nx, const cons::Taps& t) {
+  const dim3 gr((Nx + cons::kTX - 1) / cons::kTX, (Ny + cons::kBTY - 1) / cons::kBTY, n_planes);
+  if constexpr (ADJ) hipLaunchKernelGGL(cons::k_rblur_adj<H>, gr, dim3(256), 0, st, in, out, Ny, Nx, t);
+  else hipLaunchKernelGGL(cons::k_rblur<H>, gr, dim3(256), 0, st, in, out, Ny, Nx, t);
+}
+template <bool ADJ>
+void launch_blur_h(int h, hipStream_t st, const float* in, float* out, int n_planes, int Ny, int Nx,
+                   const cons::Taps& t) {
+  switch (h) {
+    case 0: launch_blur<ADJ, 0>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 1: launch_blur<ADJ, 1>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 2: launch_blur<ADJ, 2>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 3: launch_blur<ADJ, 3>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 4: launch_blur<ADJ, 4>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 5: launch_blur<ADJ, 5>(st, in, out, n_planes, Ny, Nx, t); break;
+    case 6: launch_blur<ADJ, 6>(st, in, out, n_planes, Ny, Nx, t); break;
+    default: launch_blur<ADJ, 7>(st, in, out, n_planes, Ny, Nx, t); break;
+  }
+}
+
 template <int H>
 void launch_column(hipStream_t st, float* a, float* p, const cons::ObjCfg& c, int pointwise_on) {
   const long long cols = (long long)c.O * c.Ny * c.Nx;
@@ -93,8 +115,7 @@ extern "C" int ptyx_obj_rblur(void* stream, const float* in, float* out, int32_t
   if (!in || !out || in == out) return abi::fail(PTYX_EINVAL, "obj_rblur: in / out null or aliased");
   const cons::Taps t = torchvision_taps(kernel_size, sigma);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(cons::k_rblur, dim3((Nx + cons::kTX - 1) / cons::kTX, (Ny + cons::kTY - 1) / cons::kTY, n_planes),
-                     dim3(256), 0, st, in, out, Ny, Nx, t);
+  launch_blur_h<false>(t.half, st, in, out, n_planes, Ny, Nx, t);
   return abi::launch_status("k_rblur launch");
 }
 
@@ -112,9 +133,48 @@ extern "C" int ptyx_blur_adjoint(void* stream, const float* in, float* out, int3
   if (n_planes > 65535) return abi::fail(PTYX_EUNSUPPORTED, "blur_adjoint: at most 65535 planes per call");
   const cons::Taps t = torchvision_taps(kernel_size, sigma);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(cons::k_rblur_adj, dim3((Nx + 63) / 64, (Ny + 3) / 4, n_planes), dim3(256), 0, st, in, out, Ny,
-                     Nx, t);
+  launch_blur_h<true>(t.half, st, in, out, n_planes, Ny, Nx, t);
   return abi::launch_status("k_rblur_adj launch");
+}
+
+extern "C" int ptyx_simlar_std(void* stream, const float* x, int32_t O, int64_t n_planes, int32_t n_pix,
+                               const float* occ, float* sums) {
+  abi::clear_error();
+  if (O < 1 || n_planes < 0 || n_pix < 0) return abi::fail(PTYX_EINVAL, "simlar_std: bad shape");
+  if (O > cons::kSimlarMaxO) return abi::fail(PTYX_EUNSUPPORTED, "simlar_std: at most 32 object modes");
+  if (n_planes > 2147483647LL) return abi::fail(PTYX_EUNSUPPORTED, "simlar_std: at most 2^31 - 1 planes");
+  if (n_planes == 0) return PTYX_OK;
+  if (!x || !occ || !sums) return abi::fail(PTYX_EINVAL, "simlar_std: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 gr((unsigned)n_planes), bl(256);
+  const bool v4 = n_pix % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (v4 && O == 2) hipLaunchKernelGGL(cons::k_simlar_std<2>, gr, bl, 0, st, x, O, (long long)n_planes, n_pix, occ, sums);
+  else if (v4 && O == 3) hipLaunchKernelGGL(cons::k_simlar_std<3>, gr, bl, 0, st, x, O, (long long)n_planes, n_pix, occ, sums);
+  else if (v4 && O == 4) hipLaunchKernelGGL(cons::k_simlar_std<4>, gr, bl, 0, st, x, O, (long long)n_planes, n_pix, occ, sums);
+  else hipLaunchKernelGGL(cons::k_simlar_std<0>, gr, bl, 0, st, x, O, (long long)n_planes, n_pix, occ, sums);
+  return abi::launch_status("k_simlar_std launch");
+}
+
+extern "C" int ptyx_simlar_std_grad(void* stream, const float* x, int32_t O, int64_t n_planes, int32_t n_pix,
+                                    const float* occ, const float* gsum, float* gx) {
+  abi::clear_error();
+  if (O < 1 || n_planes < 0 || n_pix < 0) return abi::fail(PTYX_EINVAL, "simlar_std_grad: bad shape");
+  if (O > cons::kSimlarMaxO) return abi::fail(PTYX_EUNSUPPORTED, "simlar_std_grad: at most 32 object modes");
+  const long long total = (long long)n_planes * n_pix;
+  if (total == 0) return PTYX_OK;
+  if (!x || !occ || !gsum || !gx || x == gx) return abi::fail(PTYX_EINVAL, "simlar_std_grad: null or aliased pointer");
+  const bool v4 = n_pix % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(gx) & 15) == 0 &&
+                  O >= 2 && O <= 4;
+  const long long blocks = (total / (v4 ? 4 : 1) + 255) / 256;
+  if (blocks > 2147483647LL) return abi::fail(PTYX_EUNSUPPORTED, "simlar_std_grad: too many elements");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 gr((unsigned)blocks), bl(256);
+  const long long np = n_planes;
+  if (v4 && O == 2) hipLaunchKernelGGL(cons::k_simlar_std_grad<2>, gr, bl, 0, st, x, O, np, n_pix, occ, gsum, gx);
+  else if (v4 && O == 3) hipLaunchKernelGGL(cons::k_simlar_std_grad<3>, gr, bl, 0, st, x, O, np, n_pix, occ, gsum, gx);
+  else if (v4 && O == 4) hipLaunchKernelGGL(cons::k_simlar_std_grad<4>, gr, bl, 0, st, x, O, np, n_pix, occ, gsum, gx);
+  else hipLaunchKernelGGL(cons::k_simlar_std_grad<0>, gr, bl, 0, st, x, O, np, n_pix, occ, gsum, gx);
+  return abi::launch_status("k_simlar_std_grad launch");
 }
 
 namespace {

@@ -45,35 +45,39 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   i = i < 0 ? -i : i;
   return i >= n ? 2 * (n - 1) - i : i;
 }
-// grid (ceil(Nx/64), ceil(Ny/16), planes); block 256
+// grid (ceil(Nx/kTX), ceil(Ny/kBTY), planes); block 256.  H = kernel_size / 2 at compile time
+// (unrolled taps, constant tile geometry); the taps in the same order as before (j = 0 … 2H).
+constexpr int kBTY = 32;   // rows of a blur tile (halo overhead (32 + 2H) / 32)
+template <int H>
 __global__ __launch_bounds__(256) void k_rblur(const float* __restrict__ in, float* __restrict__ out, int Ny, int Nx,
                                                Taps t) {
-  __shared__ float s_in[kTY + 2 * kMaxHalf][kTX + 2 * kMaxHalf + 1];
-  __shared__ float s_mid[kTY + 2 * kMaxHalf][kTX + 1];
-  const int h = t.half;
+  constexpr int rows = kBTY + 2 * H, cols = kTX + 2 * H;
+  __shared__ float s_in[rows][cols + 1];
+  __shared__ float s_mid[rows][kTX + 1];
   const size_t plane = (size_t)blockIdx.z * Ny * Nx;
-  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
-  const int rows = kTY + 2 * h, cols = kTX + 2 * h;
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kBTY;
   for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
     const int r = e / cols, c = e - r * cols;
-    const int gy = reflect_idx(min(y0 + r - h, Ny - 1 + h), Ny);
-    const int gx = reflect_idx(min(x0 + c - h, Nx - 1 + h), Nx);
+    const int gy = reflect_idx(min(y0 + r - H, Ny - 1 + H), Ny);
+    const int gx = reflect_idx(min(x0 + c - H, Nx - 1 + H), Nx);
     s_in[r][c] = in[plane + (size_t)gy * Nx + gx];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < rows * kTX; e += blockDim.x) {
     const int r = e / kTX, c = e - r * kTX;
     float acc = 0.f;
-    for (int j = 0; j <= 2 * h; ++j) acc = fmaf(t.w[j], s_in[r][c + j], acc);
+#pragma unroll
+    for (int j = 0; j <= 2 * H; ++j) acc = fmaf(t.w[j], s_in[r][c + j], acc);
     s_mid[r][c] = acc;
   }
   __syncthreads();
   const int c = threadIdx.x & (kTX - 1);
-  for (int r = threadIdx.x >> 6; r < kTY; r += blockDim.x >> 6) {
+  for (int r = threadIdx.x >> 6; r < kBTY; r += blockDim.x >> 6) {
     const int gy = y0 + r, gx = x0 + c;
     if (gy >= Ny || gx >= Nx) continue;
     float acc = 0.f;
-    for (int i = 0; i <= 2 * h; ++i) acc = fmaf(t.w[i], s_mid[r + i][c], acc);
+#pragma unroll
+    for (int i = 0; i <= 2 * H; ++i) acc = fmaf(t.w[i], s_mid[r + i][c], acc);
     out[plane + (size_t)gy * Nx + gx] = acc;
   }
 }
@@ -85,7 +89,7 @@ __global__ __launch_bounds__(256) void k_rblur(const float* __restrict__ in, flo
 //               gaussian_blur.  Output pixel u collects the input pixels s whose padded
 //               neighbourhood reads u at tap t: s = u - t + h (interior), s = -u - t + h (top /
 //               left reflection, u > 0) and s = 2(n-1) - u - t + h (bottom / right, u < n-1).
-//               Gather form, fixed order (deterministic, no atomics); one thread per output.
+//               Gather form, fixed order (deterministic, no atomics), LDS-tiled and separable.
 // k_patch_gather   (O,Nz,Ny,Nx) plane → (O,Nz,B,N,N) patch stack at crop_pos[idx[b]]
 //               (get_obj_ROI, models.py:251-265); lanes along x, one 256-B row segment per wave.
 // k_patch_scatter  the transpose: gobj[crop + (y, x)] += gpatch, f32 atomics (overlapping
@@ -105,38 +109,184 @@ __device__ __forceinline__ int blur_sources(int u, int t, int h, int n, int* s) 
   return k;
 }
 
-// grid (ceil(Nx/64), ceil(Ny/4), planes); block 256 = 64 x 4
+// grid (ceil(Nx/kTX), ceil(Ny/kBTY), planes); block 256.  The transpose of k_rblur's (horizontal,
+// then vertical) pass is the vertical transpose, then the horizontal one, tiled like k_rblur.  A
+// 1-D transpose is the transposed convolution onto the reflect-padded line, folded back: output
+// u takes the padded sample u + H (Σ_t w_t g[u + H − t], branch-free: the LDS tile is zero
+// outside the plane) plus, within H of an edge, the padded sample its reflection came from (top
+// u ∈ [1, H]: H − u; bottom u ∈ [n−1−H, n−2]: 2(n−1) − u + H).  Every source lies within H of the
+// tile, so the (kBTY + 2H) × (kTX + 2H) input tile is read once, each output written once.
+template <int H>
+__device__ __forceinline__ float blur_adj_line(const float* col, int stride, int r, int u, int n, int base,
+                                               const Taps& t) {
+  // col[k·stride] = g[base + k] (0 outside [0, n)); r = u − base − H
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j <= 2 * H; ++j) acc = fmaf(t.w[j], col[(r + 2 * H - j) * stride], acc);
+  if (H > 0 && u >= 1 && u <= H) {   // the top reflection of u: padded H − u → g[H − u − j]
+#pragma unroll
+    for (int j = 0; j <= 2 * H; ++j) {
+      const int sidx = H - u - j;
+      if (sidx >= 0) acc = fmaf(t.w[j], col[(sidx - base) * stride], acc);
+    }
+  }
+  if (H > 0 && u >= n - 1 - H && u <= n - 2) {   // the bottom reflection: padded 2(n−1) − u + H
+#pragma unroll
+    for (int j = 0; j <= 2 * H; ++j) {
+      const int sidx = 2 * (n - 1) - u + H - j;
+      if (sidx < n) acc = fmaf(t.w[j], col[(sidx - base) * stride], acc);
+    }
+  }
+  return acc;
+}
+template <int H>
 __global__ __launch_bounds__(256) void k_rblur_adj(const float* __restrict__ g, float* __restrict__ out, int Ny,
                                                    int Nx, Taps t) {
-  const int v = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int u = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (u >= Ny || v >= Nx) return;
+  constexpr int rows = kBTY + 2 * H, cols = kTX + 2 * H;
+  __shared__ float s_g[rows][cols + 1];
+  __shared__ float s_mid[kBTY][cols + 1];
   const size_t plane = (size_t)blockIdx.z * Ny * Nx;
-  const int h = t.half;
-  int xs[3 * kMaxTaps];
-  float xw[3 * kMaxTaps];
-  int nx = 0;
-  for (int j = 0; j <= 2 * h; ++j) {
-    int s[3];
-    const int k = blur_sources(v, j, h, Nx, s);
-    for (int q = 0; q < k; ++q) {
-      xs[nx] = s[q];
-      xw[nx] = t.w[j];
-      ++nx;
-    }
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kBTY;
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int r = e / cols, c = e - r * cols;
+    const int gy = y0 + r - H, gx = x0 + c - H;
+    s_g[r][c] = gy >= 0 && gy < Ny && gx >= 0 && gx < Nx ? g[plane + (size_t)gy * Nx + gx] : 0.f;
   }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kBTY * cols; e += blockDim.x) {   // vertical transpose, rows u of the tile
+    const int r = e / cols, c = e - r * cols;
+    const int u = y0 + r;
+    s_mid[r][c] = u < Ny ? blur_adj_line<H>(&s_g[0][c], cols + 1, r, u, Ny, y0 - H, t) : 0.f;
+  }
+  __syncthreads();
+  const int c = threadIdx.x & (kTX - 1);
+  const int v = x0 + c;
+  for (int r = threadIdx.x >> 6; r < kBTY; r += blockDim.x >> 6) {   // horizontal transpose
+    const int u = y0 + r;
+    if (u >= Ny || v >= Nx) continue;
+    out[plane + (size_t)u * Nx + v] = blur_adj_line<H>(&s_mid[r][0], 1, c, v, Nx, x0 - H, t);
+  }
+}
+
+// ------------------------------------------------------------------ loss_simlar
+// k_simlar_std: one workgroup per plane q: per pixel the unbiased std over the O modes of
+// occ_o·x[o,q,pix] (mean, then the squared deviations — torch.std), summed per thread, then the
+// waves in order.  k_simlar_std_grad: its backward per pixel.  OT > 0: O known at compile time
+// and 4 pixels a float4 (n_pix % 4 == 0), two of them in flight per thread and mode; OT = 0 any
+// O ≤ kSimlarMaxO, one pixel at a time.
+constexpr int kSimlarMaxO = 32;
+template <int OT>
+__device__ __forceinline__ float simlar_px(const float (&w)[OT > 0 ? OT : kSimlarMaxO], int O, float& m) {
+  constexpr int OM = OT > 0 ? OT : kSimlarMaxO;
+  float mm = 0.f;
+#pragma unroll
+  for (int o = 0; o < OM; ++o)
+    if (o < O) mm += w[o];
+  mm *= 1.0f / (float)O;
+  float v = 0.f;
+#pragma unroll
+  for (int o = 0; o < OM; ++o)
+    if (o < O) v = fmaf(w[o] - mm, w[o] - mm, v);
+  m = mm;
+  return sqrtf(v * (1.0f / (float)(O - 1)));
+}
+template <int OT>
+__global__ __launch_bounds__(256) void k_simlar_std(const float* __restrict__ x, int Odyn, long long n_planes,
+                                                    int n_pix, const float* __restrict__ occ, float* __restrict__ sums) {
+  constexpr int OM = OT > 0 ? OT : kSimlarMaxO;
+  const int O = OT > 0 ? OT : Odyn;
+  __shared__ float s_w[4];
+  const long long q = blockIdx.x;
+  const size_t ostr = (size_t)n_planes * n_pix;
+  const float* xq = x + (size_t)q * n_pix;
+  float oc[OM];
+#pragma unroll
+  for (int o = 0; o < OM; ++o) oc[o] = o < O ? occ[o] : 0.f;
   float acc = 0.f;
-  for (int i = 0; i <= 2 * h; ++i) {
-    int s[3];
-    const int k = blur_sources(u, i, h, Ny, s);
-    for (int q = 0; q < k; ++q) {
-      const float* row = g + plane + (size_t)s[q] * Nx;
-      float r = 0.f;
-      for (int e = 0; e < nx; ++e) r = fmaf(xw[e], row[xs[e]], r);
-      acc = fmaf(t.w[i], r, acc);
+  if constexpr (OT > 0) {
+    const int n4 = n_pix >> 2;
+    for (int e0 = threadIdx.x; e0 < n4; e0 += 512) {
+      float4 t[2][OT];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int o = 0; o < OT; ++o)
+          t[k][o] = e0 + 256 * k < n4 ? reinterpret_cast<const float4*>(xq + o * ostr)[e0 + 256 * k]
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (e0 + 256 * k >= n4) break;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float w[OM];
+#pragma unroll
+          for (int o = 0; o < OT; ++o) w[o] = oc[o] * (&t[k][o].x)[c];
+          float m;
+          acc += simlar_px<OT>(w, O, m);
+        }
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < n_pix; e += 256) {
+      float w[OM];
+#pragma unroll
+      for (int o = 0; o < OM; ++o) w[o] = o < O ? oc[o] * xq[o * ostr + e] : 0.f;
+      float m;
+      acc += simlar_px<OT>(w, O, m);
     }
   }
-  out[plane + (size_t)u * Nx + v] = acc;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[q] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+// grid: ceil(n_planes·n_pix / (256·PXT)) with PXT = 4 (OT > 0) or 1; thread → PXT pixels
+template <int OT>
+__global__ __launch_bounds__(256) void k_simlar_std_grad(const float* __restrict__ x, int Odyn, long long n_planes,
+                                                         int n_pix, const float* __restrict__ occ,
+                                                         const float* __restrict__ gsum, float* __restrict__ gx) {
+  constexpr int OM = OT > 0 ? OT : kSimlarMaxO;
+  constexpr int PXT = OT > 0 ? 4 : 1;
+  const int O = OT > 0 ? OT : Odyn;
+  const long long total = n_planes * n_pix;
+  const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * PXT;
+  if (i0 >= total) return;
+  const long long q = i0 / n_pix;   // (n_pix % PXT == 0: a thread's pixels share the plane)
+  const size_t ostr = (size_t)total;
+  float oc[OM];
+#pragma unroll
+  for (int o = 0; o < OM; ++o) oc[o] = o < O ? occ[o] : 0.f;
+  const float gq = gsum[q];
+  float xv[OM][PXT];
+#pragma unroll
+  for (int o = 0; o < OM; ++o) {
+    if (o >= O) break;
+    if constexpr (PXT == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(x + o * ostr + i0);
+      xv[o][0] = t.x; xv[o][1] = t.y; xv[o][2] = t.z; xv[o][3] = t.w;
+    } else {
+      xv[o][0] = x[o * ostr + i0];
+    }
+  }
+  float gv[OM][PXT];
+#pragma unroll
+  for (int c = 0; c < PXT; ++c) {
+    float w[OM];
+#pragma unroll
+    for (int o = 0; o < OM; ++o) w[o] = o < O ? oc[o] * xv[o][c] : 0.f;
+    float m;
+    const float sd = simlar_px<OT>(w, O, m);
+    const float cc = gq / (sd * (float)(O - 1));
+#pragma unroll
+    for (int o = 0; o < OM; ++o) gv[o][c] = cc * oc[o] * (w[o] - m);
+  }
+#pragma unroll
+  for (int o = 0; o < OM; ++o) {
+    if (o >= O) break;
+    if constexpr (PXT == 4) *reinterpret_cast<float4*>(gx + o * ostr + i0) = make_float4(gv[o][0], gv[o][1], gv[o][2], gv[o][3]);
+    else gx[o * ostr + i0] = gv[o][0];
+  }
 }
 
 // grid (ceil(N*N/256), B, O*Nz); block 256.  Out-of-object windows read / write nothing.

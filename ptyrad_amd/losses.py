@@ -164,10 +164,16 @@ class CombinedLoss(torch.nn.Module):
         flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches])
         model._check_indices(flat)
         dev = model.opt_obja.device
-        if getattr(model, "detector_blur", False) or self.loss_params.get("loss_simlar", {}).get("state", False):
-            # the loss sees blurred intensities / blurred patches: HIP forward → HIP blur → loss
-            # terms of this module → HIP adjoints, per mini-batch
+        if getattr(model, "detector_blur", False) or (self._simlar_on() and self.simlar_per_batch):
+            # the loss sees blurred intensities: HIP forward → HIP blur → loss terms of this module
+            # → HIP adjoints, per mini-batch
             return self._per_batch(model, batches)
+        if self._simlar_on():   # data terms on the engine (one call), loss_simlar beside it
+            total, terms = self._data_loss().fused(model, batches)
+            s_total, s_terms = self._simlar_terms(model, batches)
+            terms = terms.clone()
+            terms[:, 4] = s_terms
+            return total + s_total, terms
         cfg = LossConfig.from_loss_params(self.loss_params)
         if getattr(model, "preblur", False):
             return self._preblur_fused(model, batches, cfg)
@@ -189,7 +195,73 @@ class CombinedLoss(torch.nn.Module):
 
     def _special(self, model):
         return (getattr(model, "detector_blur", False) or getattr(model, "preblur", False) or
-                getattr(model, "otf_meas", False) or self.loss_params.get("loss_simlar", {}).get("state", False))
+                getattr(model, "otf_meas", False) or self._simlar_on())
+
+    def _simlar_on(self):
+        return bool(self.loss_params.get("loss_simlar", {}).get("state", False))
+
+    simlar_per_batch = False   # A/B: loss_simlar through the per-mini-batch generic path instead
+
+    def _data_loss(self):
+        """This loss without loss_simlar (the engine's terms; loss_simlar runs beside the call)."""
+        lp = dict(self.loss_params)
+        lp["loss_simlar"] = dict(lp.get("loss_simlar", {}), state=False)
+        return CombinedLoss(lp, device=self.device)
+
+    SIMLAR_PATCH_BYTES = 1 << 30   # patch-stack bytes per loss_simlar chunk (one type)
+
+    def _simlar_terms(self, model, batches):
+        """loss_simlar (losses.py:106-141) of every mini-batch of a call, vectorised over the call:
+        the object patches of up to SIMLAR_PATCH_BYTES at a time by the HIP patch gather (and the
+        HIP gaussian_blur, kernel 5, reflect padding; pre-blurred first when obj_preblur_std is on),
+        torch's 'area' interpolation when scale_factor ≠ 1, the occupancy-weighted std over the
+        object modes, each pattern's sum of it.  Mini-batch m's term is w·Σ_type Σ_{j∈m} S_j /
+        (B_m·count) — the reference's mean over (B, Nz, Ny, Nx) of mini-batch m alone.  Returns
+        (Σ_m term_m, differentiable — its backward is the blur adjoint and the HIP patch
+        scatter-add into the object gradients —, the (n_batches,) detached terms)."""
+        from .stages import MAX_PLANES, BlurredPatches, GaussianBlur, SimlarStd
+        p = self.loss_params["loss_simlar"]
+        dev = model.opt_obja.device
+        O, Nz = int(model.opt_obja.shape[0]), int(model.opt_obja.shape[1])
+        N = int(model.opt_probe.shape[1])
+        sigma = p.get("blur_std")
+        sigma = float(sigma) if sigma not in (None, 0) else None
+        sf = p.get("scale_factor")
+        resample = sf is not None and any(f != 1 for f in sf)
+        types = [c for c, kinds in ((0, ("amplitude", "both")), (1, ("phase", "both")))
+                 if p.get("obj_type", "both") in kinds]
+        occ = model.omode_occu.to(dev, torch.float32)
+        sizes = [len(np.asarray(b).reshape(-1)) for b in batches]
+        bid = np.repeat(np.arange(len(batches)), sizes)
+        flat = np.concatenate([np.asarray(b).reshape(-1) for b in batches]) if batches else np.zeros(0, np.int64)
+        cap = max(1, min(MAX_PLANES, self.SIMLAR_PATCH_BYTES // (4 * O * Nz * N * N)))
+        terms = torch.zeros(len(batches), dtype=torch.float64, device=dev)
+        total = torch.zeros((), dtype=torch.float32, device=dev)
+        for j0 in range(0, len(flat), cap):
+            idx_t = torch.as_tensor(flat[j0:j0 + cap], dtype=torch.int32, device=dev)
+            b_t = torch.as_tensor(bid[j0:j0 + cap], dtype=torch.long, device=dev)
+            if getattr(model, "preblur", False):
+                pre = model._blurred_patches(idx_t)
+            for c in types:
+                if getattr(model, "preblur", False):
+                    x = pre[c]
+                    if sigma:
+                        x = GaussianBlur.apply(x.contiguous(), sigma)
+                else:
+                    obj = model.opt_obja if c == 0 else model.opt_objp
+                    x = BlurredPatches.apply(obj, model.crop_pos, idx_t, N, sigma)   # (O, Nz, B, N, N)
+                if resample:   # torch 'area' on (B, O, Nz, N, N), back to modes first
+                    x = torch.nn.functional.interpolate(x.permute(2, 0, 1, 3, 4), scale_factor=list(sf), mode="area")
+                    x = x.permute(1, 2, 0, 3, 4)
+                nzr, B = int(x.shape[1]), int(x.shape[2])
+                count = nzr * int(x.shape[3]) * int(x.shape[4])
+                # the std over modes per pixel, summed per (slice, pattern) plane, on the device
+                S = SimlarStd.apply(x.reshape(O, nzr * B, -1), occ).reshape(nzr, B).sum(0)   # per pattern
+                w = torch.as_tensor(float(p["weight"]) / (np.asarray(sizes, np.float64)[bid[j0:j0 + cap]] * count),
+                                    dtype=torch.float32, device=dev)
+                total = total + (S * w).sum()
+                terms.index_add_(0, b_t, (S.detach() * w).double())
+        return total, terms.float()
 
     def supports_batch_split(self, model=None, *, model_params=None, init_variables=None) -> bool:
         """Whether ``fused_into(..., batch_sums_reduce=...)`` can take mini-batches split over ranks:
@@ -231,6 +303,14 @@ class CombinedLoss(torch.nn.Module):
                 raise NotImplementedError("mini-batches split over ranks need additive loss terms "
                                           "(no loss_pacbed / loss_simlar / blur / on-the-fly stages)")
             return self._split_into(model, batches, grad_scale, batch_sums_reduce)
+        if special and self._simlar_on() and not getattr(model, "detector_blur", False) and not self.simlar_per_batch:
+            # the data terms as without loss_simlar (one engine call), loss_simlar beside it
+            terms = self._data_loss().fused_into(model, batches, grad_scale)
+            s_total, s_terms = self._simlar_terms(model, batches)
+            if s_total.requires_grad:
+                torch.autograd.backward(s_total * grad_scale)
+            terms[:, 4] = s_terms
+            return terms
         if special:
             total, terms = self.fused(model, batches)
             if total.requires_grad:

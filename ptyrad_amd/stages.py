@@ -122,6 +122,34 @@ class BlurredPatches(torch.autograd.Function):
         return gobj, None, None, None, None
 
 
+class SimlarStd(torch.autograd.Function):
+    """loss_simlar's core (losses.py:106-141): x (O, Q, …) one type's patches (modes first), occ
+    (O) → (Q,) per-plane sums of torch.std(occ·x, dim=0) (unbiased) by ptyx_simlar_std; backward
+    ptyx_simlar_std_grad."""
+
+    @staticmethod
+    def forward(ctx, x, occ):
+        x = x.contiguous()
+        _check_f32(x, "simlar patches")
+        occ = occ.detach().to(x.device, torch.float32).contiguous()
+        O, Q = int(x.shape[0]), int(x.shape[1])
+        P = int(x[0, 0].numel()) if Q else 0
+        sums = torch.empty(Q, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().ptyx_simlar_std(_stream(x.device), _ptr(x), O, Q, P, _ptr(occ), _ptr(sums)))
+        ctx.save_for_backward(x, occ)
+        return sums
+
+    @staticmethod
+    def backward(ctx, g):
+        x, occ = ctx.saved_tensors
+        O, Q = int(x.shape[0]), int(x.shape[1])
+        P = int(x[0, 0].numel()) if Q else 0
+        g = g.contiguous().float()
+        gx = torch.empty_like(x)
+        _lib.check(_lib.load().ptyx_simlar_std_grad(_stream(x.device), _ptr(x), O, Q, P, _ptr(occ), _ptr(g), _ptr(gx)))
+        return gx, None
+
+
 def stack_crop_pos(B: int, N: int, device) -> torch.Tensor:
     """crop_pos of a (.., B·N, N) patch-stack object: patch b starts at row b·N."""
     cp = torch.zeros((B, 2), dtype=torch.int32, device=device)
@@ -129,5 +157,5 @@ def stack_crop_pos(B: int, N: int, device) -> torch.Tensor:
     return cp
 
 
-__all__ = ["GaussianBlur", "BlurredPatches", "blur_planes", "patch_gather", "patch_scatter_add",
+__all__ = ["GaussianBlur", "BlurredPatches", "SimlarStd", "blur_planes", "patch_gather", "patch_scatter_add",
            "stack_crop_pos", "KERNEL_SIZE"]

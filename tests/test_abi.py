@@ -156,4 +156,10 @@ def test_stage_entry_points_validate_without_gpu():
     assert lib.ptyx_patch_gather(None, vp, 1, 1, 64, 64, vp, vp, 70000, 32, vp) == _lib.PTYX_EUNSUPPORTED
     assert lib.ptyx_patch_scatter_add(None, vp, 1, 1, 64, 64, None, vp, 3, 32, vp) == _lib.PTYX_EINVAL
     assert lib.ptyx_patch_scatter_add(None, vp, 1, 1, 64, 64, None, None, 0, 32, None) == _lib.PTYX_OK
+    assert lib.ptyx_simlar_std(None, vp, 33, 4, 16, vp, vp) == _lib.PTYX_EUNSUPPORTED          # O > 32
+    assert lib.ptyx_simlar_std(None, vp, 0, 4, 16, vp, vp) == _lib.PTYX_EINVAL                 # no modes
+    assert lib.ptyx_simlar_std(None, None, 2, 4, 16, vp, vp) == _lib.PTYX_EINVAL               # null x
+    assert lib.ptyx_simlar_std(None, None, 2, 0, 16, None, None) == _lib.PTYX_OK               # empty
+    assert lib.ptyx_simlar_std_grad(None, vp, 2, 4, 16, vp, vp, vp) == _lib.PTYX_EINVAL        # gx aliases x
+    assert lib.ptyx_simlar_std_grad(None, None, 2, 0, 16, None, None, None) == _lib.PTYX_OK
 

@@ -35,7 +35,8 @@ def dev():
 
 
 @pytest.mark.parametrize("shape,ks,sigma", [((3, 33, 47), 5, 1.0), ((32, 128, 128), 5, 0.7), ((2, 9, 8), 7, 2.0),
-                                            ((4, 64, 64), 3, 0.5)])
+                                            ((4, 64, 64), 3, 0.5), ((2, 100, 130), 9, 1.5), ((1, 40, 70), 15, 3.0),
+                                            ((1, 17, 16), 1, 1.0)])
 def test_blur_and_adjoint_vs_oracle(shape, ks, sigma):
     device = dev()
     from ptyrad_amd.stages import blur_planes
@@ -203,3 +204,59 @@ def test_loss_pacbed_multi_batch_vs_oracle():
     gp = model.opt_probe.grad.cpu().numpy()
     assert rel(gp[..., 0] + 1j * gp[..., 1], g["probe"]) < 5e-5
 
+
+
+SIMLAR = [c for c in PACBED if "simlar" in c]
+
+
+@pytest.mark.parametrize("variant", ["fixture", "area_phase", "chunked_amp"])
+def test_loss_simlar_beside_engine_matches_per_batch_path(variant):
+    """loss_simlar with several mini-batches: the data terms in one engine call and loss_simlar
+    vectorised over the call (CombinedLoss._simlar_terms: HIP patch gather + blur, per-batch
+    normalisation) against the per-mini-batch generic path (torch loss_simlar on each mini-batch's
+    patches, losses.py:106-141) — terms and gradients, through fused() and fused_into()."""
+    import json
+    import torch
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = dict(load_case(SIMLAR[0]))
+    lp = json.loads(json.dumps(d["loss_params"]))
+    if variant == "area_phase":
+        lp["loss_simlar"].update(obj_type="phase", scale_factor=[1.0, 0.5, 0.5], blur_std=0)
+    elif variant == "chunked_amp":
+        lp["loss_simlar"].update(obj_type="amplitude", blur_std=1.5)
+    S = d["shifts"].shape[0]
+    perm = np.random.default_rng(5).permutation(S)
+    batches = [perm[:5], perm[5:6], perm[6:13], perm[13:]]
+
+    def grads(m):
+        return {k: getattr(m, "opt_" + k).grad.detach().cpu().numpy().copy() for k in ("obja", "objp", "probe")}
+
+    ref_model = _model(d, device)
+    ref = CombinedLoss(lp, device=device)
+    total, rterms = ref._per_batch(ref_model, batches)
+    total.backward()
+    g_ref = grads(ref_model)
+    rterms = rterms.detach().cpu().numpy()
+    assert np.all(np.isfinite(rterms)) and np.all(rterms[:, 4] > 0)
+
+    loss = CombinedLoss(lp, device=device)
+    if variant == "chunked_amp":
+        loss.SIMLAR_PATCH_BYTES = 4 * 2 * 2 * 32 * 32 * 3   # 3 patterns a chunk: chunks cut mini-batches
+    model = _model(d, device)
+    total, terms = loss.fused(model, batches)
+    total.backward()
+    np.testing.assert_allclose(terms.detach().cpu().numpy(), rterms, rtol=2e-5, atol=1e-7)
+    g = grads(model)
+    for k in g:
+        assert rel(g[k], g_ref[k]) < 2e-5, k
+
+    model2 = _model(d, device)
+    for k in ("obja", "objp", "probe"):
+        p = getattr(model2, "opt_" + k)
+        p.grad = torch.zeros_like(p)
+    terms2 = loss.fused_into(model2, batches, grad_scale=0.5)
+    np.testing.assert_allclose(terms2.detach().cpu().numpy(), rterms, rtol=2e-5, atol=1e-7)
+    g2 = grads(model2)
+    for k in g2:
+        assert rel(g2[k], 0.5 * g_ref[k]) < 2e-5, k

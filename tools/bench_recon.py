@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--iters", type=int, default=1)
     ap.add_argument("--pmodes", type=int, default=1, help="probe modes (tBL_WSe2 demo: 6)")
     ap.add_argument("--slices", type=int, default=1, help="object slices (tBL_WSe2 demo: 6)")
+    ap.add_argument("--omodes", type=int, default=1, help="object modes")
+    ap.add_argument("--simlar", choices=["off", "call", "batch"], default="off",
+                    help="loss_simlar (weight 0.1, both, blur 1): beside the engine call, or per mini-batch (A/B)")
     ap.add_argument("--tune", action="append", default=[], help="ptyx_set_tuning key=value (A/B runs)")
     ap.add_argument("--graphs", choices=["auto", "on", "off"], default="auto",
                     help="recon_step(graphs=...): hipGraph-replayed optimizer steps")
@@ -61,7 +64,7 @@ def main():
     n = S * S
     rng = np.random.default_rng(0)
     Ny, Nx = scan.obj_shape
-    P, Nz = a.pmodes, a.slices
+    P, Nz, O = a.pmodes, a.slices, a.omodes
     probe = np.stack([syn.stem_probe(N) * np.float32(60.0 / (1 + 2 * p)) for p in range(P)])
     g = torch.Generator(device=dev)
     g.manual_seed(5)
@@ -72,11 +75,12 @@ def main():
           "loss_poissn": {"state": False, "weight": 1.0, "dp_pow": 1.0, "eps": 1e-6},
           "loss_pacbed": {"state": False, "weight": 0.5, "dp_pow": 0.2},
           "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1},
-          "loss_simlar": {"state": False}}
+          "loss_simlar": {"state": a.simlar != "off", "weight": 0.1, "obj_type": "both",
+                          "scale_factor": [1, 1, 1], "blur_std": 1}}
     for ga in a.ga:
-        iv = {"obja": np.ones((1, Nz, Ny, Nx), np.float32),
-              "objp": (1e-8 * rng.random((1, Nz, Ny, Nx))).astype(np.float32), "obj": None,
-              "probe": probe, "probe_pos_shifts": scan.shifts, "omode_occu": np.ones(1, np.float32),
+        iv = {"obja": np.ones((O, Nz, Ny, Nx), np.float32),
+              "objp": (1e-8 * rng.random((O, Nz, Ny, Nx))).astype(np.float32), "obj": None,
+              "probe": probe, "probe_pos_shifts": scan.shifts, "omode_occu": np.full(O, 1.0 / O, np.float32),
               "H": syn.fresnel_propagator(N, syn.DX_ANG, 2.0), "measurements": meas, "crop_pos": scan.crop_pos,
               "N_scan_slow": S, "N_scan_fast": S, "slice_thickness": 2.0, "dx": syn.DX_ANG, "dk": 1.0 / (N * syn.DX_ANG),
               "lambd": syn.electron_wavelength(syn.KV), "obj_tilts": np.zeros((1, 2), np.float32)}
@@ -86,6 +90,7 @@ def main():
         model = PtychoHIP(iv, mp, device=dev, verbose=False)
         opt = create_optimizer(model.optimizer_params, model.optimizable_params)
         loss_fn = CombinedLoss(lp, device=dev)
+        loss_fn.simlar_per_batch = a.simlar == "batch"
         batches = make_batches(np.arange(n), scan.crop_pos, 32, mode="random", rng=np.random.default_rng(3))
         graphs = {"auto": None, "on": True, "off": False}[a.graphs]
         recon_step(batches, ga, model, opt, loss_fn, None, 1, verbose=False, graphs=graphs,
@@ -98,7 +103,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
         sg = getattr(model, "_step_graphs", None)
-        print(json.dumps({"ga": ga, "P": P, "Nz": Nz, "graphs": a.graphs, "rccl": a.rccl, "tune": a.tune, "replays": sg.replays if sg else 0,
+        print(json.dumps({"ga": ga, "P": P, "O": O, "Nz": Nz, "simlar": a.simlar, "graphs": a.graphs, "rccl": a.rccl, "tune": a.tune, "replays": sg.replays if sg else 0,
                           "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
