@@ -237,11 +237,12 @@ struct DeviceGuard {
 };
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
-enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneCount };
+enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
+               kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
-                                            "gen_wg_per_cu"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1};
+                                            "gen_wg_per_cu", "gather_rows"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -442,12 +443,13 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
     S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], pl->gpart_cap / parts));
   g.part = pl->gpart;
   g.pcnt = pl->gpcnt;
-  if constexpr (MP) {
-    if (S == 1 && g.n <= f3::kSmallCall) {   // mixed-state small calls: rows over waves
-      if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
-      else hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
-      return;
-    }
+  // rows over waves (k_obj_gather_rows): mixed-state small calls by default; gather_rows 1 / 0
+  // forces it on / off for every unsplit gather
+  const long long tr = g_tuning[kTuneGatherRows];
+  if (S == 1 && (tr == 1 || (tr < 0 && MP && g.n <= f3::kSmallCall))) {
+    if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
+    else hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
+    return;
   }
   if (S == 1) {
     if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);

@@ -96,6 +96,35 @@ def test_stripe_object_gradient_atomics_and_slots(tuning, O, flag):
     check_against_oracle(d, [np.array([6, 2, 3]), np.array([0, 8, 4, 1])], meas_f16=False, gather=flag == 1)
 
 
+@pytest.mark.parametrize("rows,N,P,O,Nz", [(1, 128, 1, 1, 1), (1, 128, 1, 1, 3), (0, 128, 3, 1, 2), (1, 256, 8, 2, 1)])
+def test_gather_rows_variant_vs_oracle(tuning, rows, N, P, O, Nz):
+    """k_obj_gather_rows (tuning "gather_rows" 1: every unsplit gather lists a chunk's hits and
+    gives each wave its rows) and the whole-hit k_obj_gather (0, also for mixed-state small calls
+    that take the rows form by default): the same gradients on k_fused3, k_fused3ms, the
+    mixed-state engine and the N = 256 stripe engine with slots."""
+    tuning("gather_rows", rows)
+    if N == 256:
+        tuning("s_gather", 1)
+        d = config_problem(P, O, False, seed=15)
+        check_against_oracle(d, [np.array([1, 3, 4]), np.array([7, 2, 0, 8])], meas_f16=False, gather=True)
+        return
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(N, 4, 4, P=P, O=O, Nz=Nz, seed=16)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=json.loads(json.dumps(orc_default_loss())))
+    batches = [np.array([0, 5, 9, 14]), np.array([3, 12, 6]), np.array([15, 1, 10, 7, 2])]
+    ks = {}
+    terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=False, kernels=ks)
+    assert "k_obj_gather" in ks, ks
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"])
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
 # ------------------------------------------------------------------ rank-local measurements
 def test_rank_local_measurement_block_equals_full_stack():
     """PtychoHIP holding only the DPs of the positions it uses (rows in a shuffled order, via
