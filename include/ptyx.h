@@ -398,17 +398,6 @@ int ptyx_step_store(void *stream, const float *terms, int32_t nb, const int64_t 
 int ptyx_adam_step(void *stream, int32_t n, float *const *params, const float *const *grads, float *const *exp_avgs,
                    float *const *exp_avg_sqs, const float *const *steps, const int64_t *numels, const double *lrs,
                    double beta1, double beta2, double eps, double weight_decay, int32_t flags);
-/* The same step with torch's step-count increment (torch/optim/adam.py: state_step += 1) folded
- * in: *steps[i] is read BEFORE the increment, the update uses *steps[i] + 1, and the launch
- * writes *steps[i] + 1 back once every workgroup has read it (the last workgroup to finish,
- * counted in *counter: a device uint32 the caller owns, 0 before the call and left 0 after it;
- * one counter per concurrently running optimizer).  At most 16 tensor ranges (a tensor whose
- * numel is not a multiple of 4, or that is not 16-B aligned, counts 2): else PTYX_EUNSUPPORTED
- * and nothing launched. */
-int ptyx_adam_step_inc(void *stream, int32_t n, float *const *params, const float *const *grads,
-                       float *const *exp_avgs, float *const *exp_avg_sqs, float *const *steps, const int64_t *numels,
-                       const double *lrs, double beta1, double beta2, double eps, double weight_decay, int32_t flags,
-                       uint32_t *counter);
 
 /* Patterns one ptyx_forward_loss_grad call may hold and still run on the plan's fast engine:
  * the register-resident engines' slot capacity (k_fused3 / k_fused3ms / mixed-state), the stripe

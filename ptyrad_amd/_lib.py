@@ -34,7 +34,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
            "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
-           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_adam_step_inc", "ptyx_plan_check")
+           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_plan_check")
 
 
 class PtyxError(RuntimeError):
@@ -174,8 +174,7 @@ def load(path: str | None = None):
     lib.ptyx_step_store.argtypes = [vp, vp, i32, vp, vp, vp]
     d64 = ctypes.c_double
     lib.ptyx_adam_step.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32]
-    lib.ptyx_adam_step_inc.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32, vp]
-    for name in ("ptyx_plan_check", "ptyx_adam_step", "ptyx_adam_step_inc", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+    for name in ("ptyx_plan_check", "ptyx_adam_step", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
                  "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
@@ -214,7 +213,7 @@ def set_tuning(key: str, value: int) -> None:
     check(load().ptyx_set_tuning(key.encode(), int(value)))
 
 
-TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows")   # ptyx_set_tuning's keys
+TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows", "fmm_hold_h")   # ptyx_set_tuning's keys
 
 
 def get_tuning(key: str) -> int:

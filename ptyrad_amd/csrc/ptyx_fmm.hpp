@@ -66,8 +66,12 @@ __device__ __forceinline__ size_t fmm_far(const FmArgs& m, int pat, int p) {
 }
 
 // ------------------------------------------------------------------ forward: job → far field
-template <bool SHIFT>
-__global__ __launch_bounds__(256, 2) void k_fmm_fwd(FmArgs m) {
+// HOLDH (calls of at most one workgroup per CU, e.g. the reference's default cadence): the
+// K-packed H/N² is loaded into registers once per workgroup (64 more float2 a thread: one
+// workgroup a CU, so the unified register file holds them) instead of streaming 128 KiB from L2
+// in every propagation.
+template <bool SHIFT, bool HOLDH>
+__global__ __launch_bounds__(256, HOLDH ? 1 : 2) void k_fmm_fwd(FmArgs m) {
   using namespace rf;
   const F3Args& a = m.f;
   __shared__ float2 buf[kLdsElems];
@@ -86,7 +90,23 @@ __global__ __launch_bounds__(256, 2) void k_fmm_fwd(FmArgs m) {
   const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;
   float2 v[64];
 
+  float2 hreg[HOLDH ? 64 : 1];
+  if constexpr (HOLDH) {
+    if (Nz > 1) {
+      const int vpk = 8 * threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) hreg[k] = ld2(r_hpk, vpk, 2048 * k);
+    }
+  }
   auto prop_k = [&] {   // v ← v ⊙ H/N² (K layout)
+    if constexpr (HOLDH) {
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        v[k] = pcm(v[k], hreg[k]);
+        pin(v[k]);
+      }
+      return;
+    }
     const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
     pipeline<16>(
         [&](auto C) {
@@ -301,8 +321,8 @@ __global__ __launch_bounds__(256) void k_fmm_loss(FmArgs m) {
 // BOTH: loss_single and loss_poissn; the data coefficients c_m (k_finalize, which runs before this
 // kernel) are applied to g_Ψ itself, so the slots, the probe spectrum and the position sums all
 // carry them (k_obj_gather then takes data coefficient 1: FinArgs ci = 2)
-template <bool SHIFT, bool BOTH>
-__global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
+template <bool SHIFT, bool BOTH, bool HOLDH>
+__global__ __launch_bounds__(256, HOLDH ? 1 : 2) void k_fmm_adj(FmArgs m) {
   using namespace rf;
   const F3Args& a = m.f;
   __shared__ float2 buf[kLdsElems];
@@ -324,7 +344,23 @@ __global__ __launch_bounds__(256, 2) void k_fmm_adj(FmArgs m) {
   const int lds0 = (int)(size_t)(__attribute__((address_space(3))) float2*)buf;
   float2 v[64];
 
+  float2 hreg[HOLDH ? 64 : 1];
+  if constexpr (HOLDH) {
+    if (Nz > 1) {
+      const int vpk = 8 * threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) hreg[k] = ld2(r_hpk, vpk, 2048 * k);
+    }
+  }
   auto prop_kc = [&] {   // v ← v ⊙ conj(H)/N² (K layout)
+    if constexpr (HOLDH) {
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        v[k] = pcmc(v[k], hreg[k]);
+        pin(v[k]);
+      }
+      return;
+    }
     const int vpk = rf::opaque(8 * rf::opaque(threadIdx.x));
     pipeline<16>(
         [&](auto C) {

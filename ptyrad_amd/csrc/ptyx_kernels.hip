@@ -238,11 +238,11 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneCount };
+               kTuneFmmHoldH, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
-                                            "gen_wg_per_cu", "gather_rows"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1};
+                                            "gen_wg_per_cu", "gather_rows", "fmm_hold_h"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -617,9 +617,9 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
     // and far fields are the far-field cache's planes, P·(Nz + 1) per pattern, so it needs no
     // per-pattern memory of its own and takes the same call sizes; jobs are (pattern, probe mode)
     int occ3 = 0, o2 = 0;
-    bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fmm_fwd<true>, 256, 0) == hipSuccess && occ3 > 0;
-    for (auto kf : {f3::k_fmm_fwd<false>, f3::k_fmm_adj<true, false>, f3::k_fmm_adj<false, false>,
-                    f3::k_fmm_adj<true, true>, f3::k_fmm_adj<false, true>})
+    bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, f3::k_fmm_fwd<true, false>, 256, 0) == hipSuccess && occ3 > 0;
+    for (auto kf : {f3::k_fmm_fwd<false, false>, f3::k_fmm_adj<true, false, false>, f3::k_fmm_adj<false, false, false>,
+                    f3::k_fmm_adj<true, true, false>, f3::k_fmm_adj<false, true, false>})
       if (ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kf, 256, 0) == hipSuccess) occ3 = std::min(occ3, o2);
     if (ok && occ3 > 0) {
       pl->nwg3 = (int)std::min<long long>((long long)cu * occ3, std::max<long long>(1, (long long)d.max_patterns * d.P));
@@ -1168,6 +1168,8 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   const int nj = a.n_idx * P;
   const int G = std::max(1, std::min(pl->nwg3, nj));
   const int nseg = P + G;
+  // at most one workgroup a CU (the default cadence's small calls): H/N² held in registers
+  const bool holdh = Nz > 1 && G <= pl->n_cu && g_tuning[kTuneFmmHoldH] != 0;
   const bool both = cfg->single_on && cfg->poissn_on;
   f3::FmArgs m{};
   m.f = register_args(pl, in, a, cfg, gz);
@@ -1186,8 +1188,10 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     if ((rc = register_prep(pl, in, a, cfg, st, nseg))) return rc;
     {
       ProfScope ps(pl, kKFmmFwd, st);
-      if (a.shift) hipLaunchKernelGGL(f3::k_fmm_fwd<true>, dim3(G), dim3(256), 0, st, m);
-      else hipLaunchKernelGGL(f3::k_fmm_fwd<false>, dim3(G), dim3(256), 0, st, m);
+      if (a.shift && holdh) hipLaunchKernelGGL((f3::k_fmm_fwd<true, true>), dim3(G), dim3(256), 0, st, m);
+      else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_fwd<true, false>), dim3(G), dim3(256), 0, st, m);
+      else if (holdh) hipLaunchKernelGGL((f3::k_fmm_fwd<false, true>), dim3(G), dim3(256), 0, st, m);
+      else hipLaunchKernelGGL((f3::k_fmm_fwd<false, false>), dim3(G), dim3(256), 0, st, m);
     }
     {
       ProfScope ps(pl, kKFmmLoss, st);
@@ -1224,10 +1228,17 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   if (!any_grad) return PTYX_OK;
   {
     ProfScope ps(pl, kKFmmAdj, st);
-    if (a.shift && both) hipLaunchKernelGGL((f3::k_fmm_adj<true, true>), dim3(G), dim3(256), 0, st, m);
-    else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_adj<true, false>), dim3(G), dim3(256), 0, st, m);
-    else if (both) hipLaunchKernelGGL((f3::k_fmm_adj<false, true>), dim3(G), dim3(256), 0, st, m);
-    else hipLaunchKernelGGL((f3::k_fmm_adj<false, false>), dim3(G), dim3(256), 0, st, m);
+    if (holdh) {
+      if (a.shift && both) hipLaunchKernelGGL((f3::k_fmm_adj<true, true, true>), dim3(G), dim3(256), 0, st, m);
+      else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_adj<true, false, true>), dim3(G), dim3(256), 0, st, m);
+      else if (both) hipLaunchKernelGGL((f3::k_fmm_adj<false, true, true>), dim3(G), dim3(256), 0, st, m);
+      else hipLaunchKernelGGL((f3::k_fmm_adj<false, false, true>), dim3(G), dim3(256), 0, st, m);
+    } else {
+      if (a.shift && both) hipLaunchKernelGGL((f3::k_fmm_adj<true, true, false>), dim3(G), dim3(256), 0, st, m);
+      else if (a.shift) hipLaunchKernelGGL((f3::k_fmm_adj<true, false, false>), dim3(G), dim3(256), 0, st, m);
+      else if (both) hipLaunchKernelGGL((f3::k_fmm_adj<false, true, false>), dim3(G), dim3(256), 0, st, m);
+      else hipLaunchKernelGGL((f3::k_fmm_adj<false, false, false>), dim3(G), dim3(256), 0, st, m);
+    }
   }
   if ((rc = launch_status("k_fmm_adj launch"))) return rc;
   const bool bins = a.n_idx > f3::kSmallCall;

@@ -50,7 +50,6 @@ struct AdamArgs {
   float beta1, beta2, eps, wd;
   double beta1d, beta2d;
   int adamw, maximize;
-  unsigned* counter;        // ptyx_adam_step_inc: the launch's workgroup counter (else null)
 };
 
 // β^t for the integer step count t by square-and-multiply in fp64 (a few fp64 ulps from pow(),
@@ -69,13 +68,10 @@ __device__ __forceinline__ double pow_step(double b, double t) {
 
 __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
   // the tensors' step scalars, once per workgroup (lane t of wave 0 for tensor t)
-  __shared__ float s_nstep[kMaxT], s_bc2s[kMaxT], s_stepv[kMaxT];
+  __shared__ float s_nstep[kMaxT], s_bc2s[kMaxT];
   if (threadIdx.x < (unsigned)a.nt) {
     const int t = threadIdx.x;
-    float sv = *a.step[t];
-    if (a.counter) sv += 1.0f;   // torch's state_step += 1 (f32), folded into this launch
-    s_stepv[t] = sv;
-    const double step = (double)sv;
+    const double step = (double)*a.step[t];
     const double bc1 = 1.0 - pow_step(a.beta1d, step), bc2 = 1.0 - pow_step(a.beta2d, step);
     s_nstep[t] = (float)(-(a.lr[t] / bc1));
     s_bc2s[t] = (float)sqrt(bc2);
@@ -152,18 +148,6 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
       }
     }
   }
-  if (a.counter) {   // every workgroup read the step counts at its start; the last one writes them
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      const unsigned prev = atomicAdd(a.counter, 1u);
-      if (prev == gridDim.x - 1) {
-        for (int t = 0; t < a.nt; ++t) atomicExch(const_cast<float*>(a.step[t]), s_stepv[t]);
-        __threadfence();
-        atomicExch(a.counter, 0u);
-      }
-    }
-  }
 }
 
 }  // namespace opt
@@ -173,10 +157,10 @@ using ptyx::abi::fail;
 using ptyx::abi::launch_status;
 namespace opt = ptyx::opt;
 
-static int adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
-                     float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
-                     const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
-                     double weight_decay, int32_t flags, unsigned* counter) {
+extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
+                              float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                              const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
+                              double weight_decay, int32_t flags) {
   ptyx::abi::clear_error();
   if (n < 0 || (n && (!params || !grads || !exp_avgs || !exp_avg_sqs || !steps || !numels || !lrs)))
     return fail(PTYX_EINVAL, "ptyx_adam_step: null array or negative count");
@@ -199,11 +183,7 @@ static int adam_step(void* stream, int32_t n, float* const* params, const float*
   for (int i = 0; i < n; ++i) {
     if (numels[i] < 0 || (numels[i] && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i] || !steps[i])))
       return fail(PTYX_EINVAL, "ptyx_adam_step: null tensor pointer or negative size");
-    if (counter && !steps[i]) return fail(PTYX_EINVAL, "ptyx_adam_step_inc: null step pointer");
-    if (!numels[i]) {   // no elements; its step count still advances (torch increments every state_step)
-      if (counter) rs.push_back({params[i], grads[i], exp_avgs[i], exp_avg_sqs[i], steps[i], lrs[i], 0, 0});
-      continue;
-    }
+    if (!numels[i]) continue;
     const bool aligned = al16(params[i]) && al16(grads[i]) && al16(exp_avgs[i]) && al16(exp_avg_sqs[i]);
     const int64_t body = aligned ? numels[i] / 4 * 4 : 0;
     if (body) rs.push_back({params[i], grads[i], exp_avgs[i], exp_avg_sqs[i], steps[i], lrs[i], body, 1});
@@ -211,8 +191,6 @@ static int adam_step(void* stream, int32_t n, float* const* params, const float*
       rs.push_back({params[i] + body, grads[i] + body, exp_avgs[i] + body, exp_avg_sqs[i] + body, steps[i], lrs[i],
                     numels[i] - body, 0});
   }
-  if (counter && rs.size() > (size_t)opt::kMaxT)
-    return fail(PTYX_EUNSUPPORTED, "ptyx_adam_step_inc: more than 16 tensor ranges (use ptyx_adam_step)");
   for (size_t i0 = 0; i0 < rs.size(); i0 += opt::kMaxT) {
     opt::AdamArgs a{};
     a.nt = (int)std::min<size_t>(opt::kMaxT, rs.size() - i0);
@@ -238,32 +216,11 @@ static int adam_step(void* stream, int32_t n, float* const* params, const float*
     a.wd = (float)weight_decay;
     a.adamw = flags & 1;
     a.maximize = (flags >> 1) & 1;
-    a.counter = counter;
     const int64_t total = a.off[a.nt];
-    if (!total && !counter) continue;
+    if (!total) continue;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, total / opt::kChunk));
     hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(opt::kThreads), 0, (hipStream_t)stream, a);
     if (int rc = launch_status("k_adam launch")) return rc;
   }
   return PTYX_OK;
-}
-
-extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
-                              float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
-                              const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
-                              double weight_decay, int32_t flags) {
-  return adam_step(stream, n, params, grads, exp_avgs, exp_avg_sqs, steps, numels, lrs, beta1, beta2, eps,
-                   weight_decay, flags, nullptr);
-}
-
-extern "C" int ptyx_adam_step_inc(void* stream, int32_t n, float* const* params, const float* const* grads,
-                                  float* const* exp_avgs, float* const* exp_avg_sqs, float* const* steps,
-                                  const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
-                                  double weight_decay, int32_t flags, uint32_t* counter) {
-  if (!counter) {
-    ptyx::abi::clear_error();
-    return fail(PTYX_EINVAL, "ptyx_adam_step_inc: null counter");
-  }
-  return adam_step(stream, n, params, grads, exp_avgs, exp_avg_sqs, steps, numels, lrs, beta1, beta2, eps,
-                   weight_decay, flags, counter);
 }

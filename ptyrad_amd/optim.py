@@ -7,9 +7,8 @@ for a 1033² object — so at the reference's default cadence (one optimizer ste
 mini-batch) the update is latency-bound and costs more GPU time than the engine call
 (ptyrad_amd/csrc/ptyx_optim.hip).  These classes ARE torch.optim.Adam / AdamW (same constructor,
 param_groups, state layout — 'step', 'exp_avg', 'exp_avg_sq' — and state_dict, so checkpoints
-move between them and torch's own classes); only ``step()`` differs: every group's update runs
-in one ``ptyx_adam_step_inc`` launch that also advances the step counts (torch's
-``state_step += 1``; ``torch._foreach_add_`` + ``ptyx_adam_step`` beyond 16 tensor ranges), in
+move between them and torch's own classes); only ``step()`` differs: the step counts advance in
+one ``torch._foreach_add_`` and every group's update runs in one ``ptyx_adam_step`` launch, in
 torch's single-tensor arithmetic (fp32, same operation order; bias corrections in fp64).
 
 Cases the kernel does not cover (amsgrad, complex or non-fp32 or sparse gradients, CPU tensors,
@@ -39,14 +38,6 @@ def _eligible(group, params):
 class _HipAdamMixin:
     _decoupled = False
 
-    def _step_counter(self, dev):
-        """The device uint32 ptyx_adam_step_inc counts its workgroups in (0 between launches)."""
-        cs = self.__dict__.setdefault("_ptyx_counters", {})
-        c = cs.get(dev)
-        if c is None:
-            c = cs[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-        return c
-
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -75,8 +66,9 @@ class _HipAdamMixin:
                 elif st["step"].device != p.device:   # a state loaded from a non-capturable torch Adam
                     st["step"] = st["step"].to(p.device, torch.float32)
                 b.append((p, st, float(group["lr"])))
-        lib = _lib.load()
         for (b1, b2, eps, wd, decoupled, maximize, dev), items in batches.items():
+            steps = [st["step"] for _, st, _ in items]
+            torch._foreach_add_(steps, 1)
             n = len(items)
             P = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _, _ in items])
             G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _, _ in items])
@@ -86,14 +78,8 @@ class _HipAdamMixin:
             NE = (ctypes.c_int64 * n)(*[p.numel() for p, _, _ in items])
             LR = (ctypes.c_double * n)(*[lr for _, _, lr in items])
             stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            fl = (1 if decoupled else 0) | (2 if maximize else 0)
-            # the step counts advance inside the launch (ptyx_adam_step_inc), one launch fewer
-            rc = lib.ptyx_adam_step_inc(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd, fl,
-                                        ctypes.c_void_p(self._step_counter(dev).data_ptr()))
-            if rc == _lib.PTYX_EUNSUPPORTED:   # > 16 tensor ranges: torch's increment, then the update
-                torch._foreach_add_([st["step"] for _, st, _ in items], 1)
-                rc = lib.ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd, fl)
-            _lib.check(rc)
+            _lib.check(_lib.load().ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd,
+                                                  (1 if decoupled else 0) | (2 if maximize else 0)))
         if plain:
             saved = self.param_groups
             try:

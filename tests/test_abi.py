@@ -164,14 +164,3 @@ def test_stage_entry_points_validate_without_gpu():
     assert lib.ptyx_simlar_std_grad(None, None, 2, 0, 16, None, None, None) == _lib.PTYX_OK
 
 
-def test_adam_step_inc_validates_without_gpu():
-    lib = _lib.load()
-    n = 9
-    arr = lambda: (ctypes.c_void_p * n)(*([16] * n))   # noqa: E731  (16-B aligned dummies, never read)
-    ne = (ctypes.c_int64 * n)(*([5] * n))                # 9 tensors of 5 elements: 18 ranges > 16
-    lr = (ctypes.c_double * n)(*([1e-3] * n))
-    args = (None, n, arr(), arr(), arr(), arr(), arr(), ne, lr, 0.9, 0.999, 1e-8, 0.0, 0)
-    assert lib.ptyx_adam_step_inc(*args, None) == _lib.PTYX_EINVAL                         # no counter
-    assert lib.ptyx_adam_step_inc(*args, ctypes.c_void_p(16)) == _lib.PTYX_EUNSUPPORTED    # too many ranges
-    assert b"16 tensor ranges" in lib.ptyx_last_error()
-

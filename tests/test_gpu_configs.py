@@ -96,13 +96,18 @@ def test_stripe_object_gradient_atomics_and_slots(tuning, O, flag):
     check_against_oracle(d, [np.array([6, 2, 3]), np.array([0, 8, 4, 1])], meas_f16=False, gather=flag == 1)
 
 
-@pytest.mark.parametrize("rows,N,P,O,Nz", [(1, 128, 1, 1, 1), (1, 128, 1, 1, 3), (0, 128, 3, 1, 2), (1, 256, 8, 2, 1)])
-def test_gather_rows_variant_vs_oracle(tuning, rows, N, P, O, Nz):
+@pytest.mark.parametrize("rows,N,P,O,Nz,holdh", [(1, 128, 1, 1, 1, -1), (1, 128, 1, 1, 3, -1), (0, 128, 3, 1, 2, -1),
+                                                 (-1, 128, 3, 1, 3, 0), (-1, 128, 2, 1, 4, -1),
+                                                 (1, 256, 8, 2, 1, -1)])
+def test_gather_rows_variant_vs_oracle(tuning, rows, N, P, O, Nz, holdh):
     """k_obj_gather_rows (tuning "gather_rows" 1: every unsplit gather lists a chunk's hits and
     gives each wave its rows) and the whole-hit k_obj_gather (0, also for mixed-state small calls
     that take the rows form by default): the same gradients on k_fused3, k_fused3ms, the
-    mixed-state engine and the N = 256 stripe engine with slots."""
+    mixed-state engine and the N = 256 stripe engine with slots.  Also the mixed-state engine's
+    H/N² streamed per propagation (tuning "fmm_hold_h" 0) instead of held in registers (the
+    default when the call has at most one workgroup a CU)."""
     tuning("gather_rows", rows)
+    tuning("fmm_hold_h", holdh)
     if N == 256:
         tuning("s_gather", 1)
         d = config_problem(P, O, False, seed=15)
