@@ -270,6 +270,20 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
     acc[r] = make_float2(0.f, 0.f);
     cnt[r] = 0.f;
   }
+  // the epilogue's operands of this wave's pixels (A, φ and the gradients it adds to), loaded
+  // now: they do not depend on the hits, and only this workgroup touches these pixels
+  float pa[RW], pp[RW], pga[RW], pgp[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    pa[r] = pp[r] = pga[r] = pgp[r] = 0.f;
+    if (r0 + r < ga.Ny && x < ga.Nx) {
+      const size_t off = zoff + (size_t)(r0 + r) * ga.Nx + x;
+      pa[r] = ga.obja[off];
+      pp[r] = ga.objp[off];
+      if (ga.d_obja) pga[r] = ga.d_obja[off];
+      if (ga.d_objp) pgp[r] = ga.d_objp[off];
+    }
+  }
   const int np = MP ? ga.np : 1;
   for (int base = 0; base < total; base += 64 * GW) {
     const int i = base + (int)threadIdx.x;
@@ -345,10 +359,22 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
     __syncthreads();   // the next chunk rewrites the hit list
   }
 #pragma unroll
-  for (int r = 0; r < RW; ++r) {
+  for (int r = 0; r < RW; ++r) {   // gather_apply on the prefetched operands
     const int y = r0 + r;
     if (y >= ga.Ny || x >= ga.Nx) continue;
-    gather_apply(ga, zoff + (size_t)y * ga.Nx + x, acc[r], cnt[r]);
+    const size_t off = zoff + (size_t)y * ga.Nx + x;
+    float sn, cs;
+    phase_sincos(pp[r], &sn, &cs);
+    if (ga.d_obja) ga.d_obja[off] = pga[r] + fmaf(acc[r].x, cs, acc[r].y * sn);
+    if (ga.d_objp) {
+      float dph = pa[r] * fmaf(acc[r].y, cs, -acc[r].x * sn);
+      if (cnt[r] != 0.f) {
+        const float ph = pp[r];
+        const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
+        dph += ga.sparse_n == 1 ? cnt[r] * sg : cnt[r] * powq(fabsf(ph), (float)(ga.sparse_n - 1)) * sg;
+      }
+      ga.d_objp[off] = pgp[r] + dph;
+    }
   }
 }
 
