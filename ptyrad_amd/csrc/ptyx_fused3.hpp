@@ -494,13 +494,57 @@ constexpr int kPrepRows = 4;
 __host__ __device__ constexpr int small_prep_blocks(int n, int Nz, int Ny) {
   return n + (Nz * Ny + kPrepRows - 1) / kPrepRows + 1;
 }
+// Work of the call's probe preparation that rides in k_small_prep's launch as further block roles
+// (independent of the table / object rows): the row pass of F(P_p) (k_lines_rows<128, −1>, the
+// same code: its column pass, k_lines_cols, follows as the next launch) and the K-packing of H/N²
+// (k_pack128<true>).  probe / H null: that role is absent.
+constexpr int kPrLines = 8;   // lines a row block (ptyx_general.hpp kSpecLines)
+struct PrepExtra {
+  const float2* probe = nullptr;
+  int P = 0;
+  float2* tmp = nullptr;       // (P, N, N) row-pass output
+  const float2* twg = nullptr;
+  const float2* H = nullptr;
+  float2* hpk = nullptr;
+  float hscale = 1.0f;
+  __host__ __device__ int row_blocks() const { return probe ? (kN / kPrLines) * P : 0; }
+  __host__ __device__ int h_blocks() const { return H ? kN2 / 256 : 0; }
+};
+__device__ __forceinline__ void probe_rows_body(int bx, int p, const float2* src, float2* tmp, const float2* twg) {
+  constexpr int N = kN;
+  using LT = LineTile<N, kPrLines>;
+  using P1 = Plan1D<N>;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 T[LT::kElems];
+  const int l0 = bx * kPrLines;
+  const float2* s = src + (size_t)p * N * N;
+  float2* d = tmp + (size_t)p * N * N;
+  for (int i = threadIdx.x; i < N; i += 256) s_tw[i] = twg[i];
+  const int nl = min(kPrLines, N - l0);
+  for (int e = threadIdx.x; e < nl * N; e += 256) T[LT::off(e / N, e % N)] = s[(size_t)(l0 + e / N) * N + e % N];
+  __syncthreads();
+  line_pass<N, 256, P1::R1, 1, -1, kPrLines>(T, s_tw, nl);
+  line_pass<N, 256, P1::R2, P1::R1, -1, kPrLines>(T, s_tw, nl);
+  for (int e = threadIdx.x; e < nl * N; e += 256) d[(size_t)(l0 + e / N) * N + e % N] = T[LT::off(e / N, e % N)];
+}
 template <bool SPARSE>
 __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const int* boff, int n_batches,
                                                     const int* crop, int n_scans, int Ny, int Nx, int* bid, int2* geo,
                                                     const float* obja, const float* objp, int sparse_n, float* psums,
                                                     int Nz, TableCheck tc, float2* oc, int* bbox, int* segbid,
-                                                    int nseg) {
+                                                    int nseg, PrepExtra ex) {
   const int b = blockIdx.x;
+  const int bx = b - small_prep_blocks(n, Nz, Ny);   // the PrepExtra roles
+  if (bx >= 0) {
+    if (bx < ex.row_blocks()) {
+      probe_rows_body(bx % (kN / kPrLines), bx / (kN / kPrLines), ex.probe, ex.tmp, ex.twg);
+      return;
+    }
+    const int e = (bx - ex.row_blocks()) * 256 + (int)threadIdx.x;   // H/N² K-packed
+    const float2 h = ex.H[packed_rc<true>(e & 255, e >> 8)];
+    ex.hpk[e] = make_float2(h.x * ex.hscale, h.y * ex.hscale);
+    return;
+  }
   if (b < n) {
     if constexpr (SPARSE) {
       k_pattern_table_direct_body(b, idx, n, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, objp, sparse_n, psums,

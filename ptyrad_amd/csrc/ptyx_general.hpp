@@ -882,6 +882,10 @@ struct GenLaunch {
     hipLaunchKernelGGL((k_lines_rows<N, -1>), gr, bl, 0, st, probe, tmp, twg);
     hipLaunchKernelGGL((k_lines_cols<N, -1, 0>), gr, bl, 0, st, tmp, Fp, fpk, twg);
   }
+  static void spectrum_cols(const float2* tmp, int P, float2* Fp, float2* fpk, const float2* twg, hipStream_t st) {
+    const dim3 gr((N + kSpecLines - 1) / kSpecLines, P), bl(kSpecThreads);
+    hipLaunchKernelGGL((k_lines_cols<N, -1, 0>), gr, bl, 0, st, tmp, Fp, fpk, twg);
+  }
   static void probe_finalize_lines(const float2* G, int P, float2* d_probe, float2* tmp, const float2* twg,
                                    hipStream_t st) {
     const dim3 gr((N + kSpecLines - 1) / kSpecLines, P), bl(kSpecThreads);
@@ -892,7 +896,7 @@ struct GenLaunch {
   static constexpr int blocks_per_cu() { return Geo<N>::kResident; }
   static const GenOps* ops() {
     static const GenOps o{N, NT, Geo<N>::kLds, blocks_per_cu(), &spectrum, &forward, &modesum, &adjoint, &probe_finalize,
-                          &spectrum_lines, &probe_finalize_lines};
+                          &spectrum_lines, &probe_finalize_lines, &spectrum_cols};
     return &o;
   }
 };

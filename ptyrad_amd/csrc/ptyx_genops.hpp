@@ -29,6 +29,9 @@ struct GenOps {
                          hipStream_t st);
   void (*probe_finalize_lines)(const float2* G, int P, float2* d_probe, float2* tmp, const float2* twg,
                                hipStream_t st);
+  // the column launch of spectrum_lines alone (its row pass ran inside another launch: the
+  // register engines' k_small_prep)
+  void (*spectrum_cols)(const float2* tmp, int P, float2* Fp, float2* fpk, const float2* twg, hipStream_t st);
 };
 
 // registry (ptyx_kernels.hip): gen_register is called from the size groups' static initialisers

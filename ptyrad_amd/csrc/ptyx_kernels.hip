@@ -889,35 +889,57 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
   const bool sparse = cfg->sparse_on != 0;
   const int Nz = d.Nz;
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
+  // small calls (one mini-batch per optimizer step): one-workgroup bbox that also clears the
+  // segment table, and direct loss_sparse window sums instead of the summed-area table; the
+  // probe spectrum's row pass and the H packing ride in the same launch (PrepExtra)
+  const bool small = a.n_idx <= f3::kSmallCall && pl->bbox;
+  const bool merged = small && cfg->prep == PTYX_PREP_CALL;
   if (reuse) {
   } else if (a.shift) {   // F(P_p), natural and K-packed: rows then columns, N/8 workgroups a mode each
-    ProfScope ps(pl, kKSpectrum, st);
-    pl->gen->spectrum_lines(a.probe, d.P, pl->Fp, pl->fpk, pl->Gsum, pl->twg, st);
+    if (!merged) {
+      ProfScope ps(pl, kKSpectrum, st);
+      pl->gen->spectrum_lines(a.probe, d.P, pl->Fp, pl->fpk, pl->Gsum, pl->twg, st);
+    }
   } else {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<false>, dim3(N2 / 256, d.P), dim3(256), 0, st,
                        reinterpret_cast<const float2*>(in->probe), pl->fpk);
   }
-  if (Nz > 1 && !reuse) {
+  if (Nz > 1 && !reuse && !merged) {
     ProfScope ps(pl, kKPack, st);
     hipLaunchKernelGGL(f3::k_pack128<true>, dim3(N2 / 256), dim3(256), 0, st, a.H, pl->hpk, 1.0f / N2);   // H/N²
   }
-  // small calls (one mini-batch per optimizer step): one-workgroup bbox that also clears the
-  // segment table, and direct loss_sparse window sums instead of the summed-area table
-  const bool small = a.n_idx <= f3::kSmallCall && pl->bbox;
   const bool direct_sums = sparse && small && cfg->prep == PTYX_PREP_CALL;
-  if (small && cfg->prep == PTYX_PREP_CALL) {   // table, object rows, bbox: one launch (k_small_prep)
-    ProfScope ps(pl, kKTable, st);
-    const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny)), bl(256);
-    const f3::TableCheck tc{a.err, a.mrow, a.mrows};
-    if (sparse)
-      hipLaunchKernelGGL(f3::k_small_prep<true>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop, a.n_scans,
-                         d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc, pl->oc,
-                         pl->bbox, pl->segbid, nseg);
-    else
-      hipLaunchKernelGGL(f3::k_small_prep<false>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop, a.n_scans,
-                         d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc, pl->oc,
-                         pl->bbox, pl->segbid, nseg);
+  if (merged) {   // table, object rows, bbox (+ probe rows, H packing): one launch (k_small_prep)
+    f3::PrepExtra ex;
+    if (a.shift) {
+      ex.probe = a.probe;
+      ex.P = d.P;
+      ex.tmp = pl->Gsum;
+      ex.twg = pl->twg;
+    }
+    if (Nz > 1) {
+      ex.H = a.H;
+      ex.hpk = pl->hpk;
+      ex.hscale = 1.0f / N2;
+    }
+    {
+      ProfScope ps(pl, kKTable, st);
+      const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny) + ex.row_blocks() + ex.h_blocks()), bl(256);
+      const f3::TableCheck tc{a.err, a.mrow, a.mrows};
+      if (sparse)
+        hipLaunchKernelGGL(f3::k_small_prep<true>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop,
+                           a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc,
+                           pl->oc, pl->bbox, pl->segbid, nseg, ex);
+      else
+        hipLaunchKernelGGL(f3::k_small_prep<false>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop,
+                           a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc,
+                           pl->oc, pl->bbox, pl->segbid, nseg, ex);
+    }
+    if (a.shift) {   // the spectrum's column pass (Fp natural, fpk K-packed)
+      ProfScope ps(pl, kKSpectrum, st);
+      pl->gen->spectrum_cols(pl->Gsum, d.P, pl->Fp, pl->fpk, pl->twg, st);
+    }
     return launch_status("register engine preparation (small call)");
   }
   if (small) {

@@ -73,7 +73,7 @@ def tuning():
     """ptyx_set_tuning for one test; every key back to its measured default afterwards."""
     from ptyrad_amd import _lib
     yield _lib.set_tuning
-    for k in ("s3_hold", "s_psi0", "s_gather", "s_defer_groups"):
+    for k in _lib.TUNING_KEYS:
         _lib.set_tuning(k, -1)
 
 
