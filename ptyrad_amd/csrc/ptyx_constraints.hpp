@@ -40,7 +40,7 @@ struct Taps {
 };
 
 // ------------------------------------------------------------------ obj_rblur
-constexpr int kTX = 64, kTY = 16;
+constexpr int kTX = 64;   // columns of a blur tile
 __device__ __forceinline__ int reflect_idx(int i, int n) {
   i = i < 0 ? -i : i;
   return i >= n ? 2 * (n - 1) - i : i;
@@ -94,21 +94,6 @@ __global__ __launch_bounds__(256) void k_rblur(const float* __restrict__ in, flo
 //               (get_obj_ROI, models.py:251-265); lanes along x, one 256-B row segment per wave.
 // k_patch_scatter  the transpose: gobj[crop + (y, x)] += gpatch, f32 atomics (overlapping
 //               patches; summation order is arrival order).
-__device__ __forceinline__ int blur_sources(int u, int t, int h, int n, int* s) {
-  int k = 0;
-  int c = u - t + h;
-  if (c >= 0 && c < n) s[k++] = c;
-  if (u > 0) {
-    c = -u - t + h;
-    if (c >= 0 && c < n) s[k++] = c;
-  }
-  if (u < n - 1) {
-    c = 2 * (n - 1) - u - t + h;
-    if (c >= 0 && c < n) s[k++] = c;
-  }
-  return k;
-}
-
 // grid (ceil(Nx/kTX), ceil(Ny/kBTY), planes); block 256.  The transpose of k_rblur's (horizontal,
 // then vertical) pass is the vertical transpose, then the horizontal one, tiled like k_rblur.  A
 // 1-D transpose is the transposed convolution onto the reflect-padded line, folded back: output
