@@ -378,13 +378,17 @@ int ptyx_meas_pad_resample(void *stream, const void *src, int32_t src_f16, int64
  * Optimizer-step bookkeeping for graph-replayed recon_step (reconstruction.py:658-781 at
  * grad_accumulation = 1: one step per mini-batch).  A captured step reads its mini-batch through
  * a device step counter, so one hipGraph serves every step of the same shape.
- *   ptyx_step_select: idx_out[i] = idx_all[istart[*cnt] + i] for i < n, and zeroes grad[0..grad_n)
- *                     (the flat gradient buffer every trainable parameter's .grad views).
+ *   ptyx_step_select: idx_out[i] = idx_all[istart[*cnt] + i] for i < n, zeroes grad[0..grad_n)
+ *                     (the flat gradient buffer every trainable parameter's .grad views), and
+ *                     adds 1 to *steps[j] for j < n_steps (steps: a DEVICE array of device f32
+ *                     pointers, n_steps ≤ 256 — the optimizer's step counts, torch's
+ *                     state_step += 1, so the step's Adam launch needs no increment launch of its
+ *                     own; steps may be null with n_steps 0).
  *   ptyx_step_store:  terms_all[rstart[*cnt] + b][k] = terms[b][k] (b < nb, k < 5), then ++*cnt
  *                     (one workgroup: every thread reads *cnt before it is advanced).
  * ------------------------------------------------------------------------------------------- */
 int ptyx_step_select(void *stream, const int32_t *idx_all, const int64_t *istart, const int64_t *cnt, int32_t n,
-                     int32_t *idx_out, float *grad, int64_t grad_n);
+                     int32_t *idx_out, float *grad, int64_t grad_n, float *const *steps, int32_t n_steps);
 int ptyx_step_store(void *stream, const float *terms, int32_t nb, const int64_t *rstart, int64_t *cnt,
                     float *terms_all);
 

@@ -168,7 +168,7 @@ def load(path: str | None = None):
     lib.ptyx_meas_pad_background.argtypes = [vp, vp, i32, i32, i32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                              i32, i32, i32, i32, vp]
     lib.ptyx_meas_pad_resample.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp, i32]
-    lib.ptyx_step_select.argtypes = [vp, vp, vp, vp, i32, vp, vp, i64]
+    lib.ptyx_step_select.argtypes = [vp, vp, vp, vp, i32, vp, vp, i64, vp, i32]
     lib.ptyx_simlar_std.argtypes = [vp, vp, i32, i64, i32, vp, vp]
     lib.ptyx_simlar_std_grad.argtypes = [vp, vp, i32, i64, i32, vp, vp, vp]
     lib.ptyx_step_store.argtypes = [vp, vp, i32, vp, vp, vp]

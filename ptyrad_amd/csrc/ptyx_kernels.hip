@@ -1601,9 +1601,13 @@ extern "C" int ptyx_profile_end(ptyx_plan* pl, ptyx_kernel_stat* out, int32_t ca
 // (ptyrad_amd/stepgraph.py): the step's indices by a device counter, and the flat gradient zeroed,
 // in one launch; the loss terms stored and the counter advanced in another.
 __global__ void k_step_select(const int32_t* idx_all, const int64_t* istart, const int64_t* cnt, int n,
-                              int32_t* idx_out, float* grad, int64_t grad_n) {
+                              int32_t* idx_out, float* grad, int64_t grad_n, float* const* steps, int n_steps) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
   if (t < n) idx_out[t] = idx_all[istart[*cnt] + t];
+  if (t < n_steps) {   // the optimizer's step counts (f32, as torch's state_step += 1)
+    float* s = steps[t];
+    *s = *s + 1.0f;
+  }
   float4* g4 = reinterpret_cast<float4*>(grad);
   const int64_t n4 = grad_n >> 2;
   for (int64_t i = t; i < n4; i += stride) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1619,16 +1623,19 @@ __global__ __launch_bounds__(256) void k_step_store(const float* terms, int nb, 
 }
 
 extern "C" int ptyx_step_select(void* stream, const int32_t* idx_all, const int64_t* istart, const int64_t* cnt,
-                                int32_t n, int32_t* idx_out, float* grad, int64_t grad_n) {
+                                int32_t n, int32_t* idx_out, float* grad, int64_t grad_n, float* const* steps,
+                                int32_t n_steps) {
   g_err.clear();
   if (!idx_all || !istart || !cnt || !idx_out || n < 0 || grad_n < 0 || (grad_n && !grad))
     return fail(PTYX_EINVAL, "ptyx_step_select: null pointer or negative size");
+  if (n_steps < 0 || n_steps > 256 || (n_steps && !steps))
+    return fail(PTYX_EINVAL, "ptyx_step_select: steps must be a device array of at most 256 pointers");
   if (reinterpret_cast<uintptr_t>(grad) % 16)
     return fail(PTYX_EINVAL, "ptyx_step_select: grad must be 16-byte aligned");
   const int64_t work = std::max<int64_t>(n, (grad_n + 3) / 4);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (work + 255) / 256));
   hipLaunchKernelGGL(k_step_select, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx_all, istart, cnt, n,
-                     idx_out, grad, grad_n);
+                     idx_out, grad, grad_n, steps, n_steps);
   return launch_status("k_step_select launch");
 }
 

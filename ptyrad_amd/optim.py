@@ -37,6 +37,24 @@ def _eligible(group, params):
 
 class _HipAdamMixin:
     _decoupled = False
+    # set by a graph-replayed recon_step around step(): its ptyx_step_select launch has already
+    # advanced the step counts _step_tensors() returned (ptyrad_amd/stepgraph.py)
+    _external_step_inc = False
+
+    def _step_tensors(self):
+        """The step counts the next step() advances (one per eligible parameter with a gradient),
+        or [] while any of them does not exist yet (step() creates the state and increments)."""
+        out = []
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params or not _eligible(group, params):
+                continue
+            for p in params:
+                st = self.state.get(p)
+                if not st or "step" not in st or st["step"].device != p.device:
+                    return []
+                out.append(st["step"])
+        return out
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -67,8 +85,8 @@ class _HipAdamMixin:
                     st["step"] = st["step"].to(p.device, torch.float32)
                 b.append((p, st, float(group["lr"])))
         for (b1, b2, eps, wd, decoupled, maximize, dev), items in batches.items():
-            steps = [st["step"] for _, st, _ in items]
-            torch._foreach_add_(steps, 1)
+            if not self._external_step_inc:
+                torch._foreach_add_([st["step"] for _, st, _ in items], 1)
             n = len(items)
             P = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _, _ in items])
             G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _, _ in items])

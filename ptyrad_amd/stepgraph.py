@@ -5,8 +5,8 @@ of recon_step (reconstruction.py:658-781) is one optimizer step per 32-pattern m
 steps per iteration at the c2 geometry.  Each step is ~18 small engine launches plus the fused
 Adam kernels, and issuing them from Python costs more than the GPU needs to run them
 (0.47 ms per step, 0.18 ms of it GPU time).  ``StepGraphs`` captures ONE optimizer
-step — ptyx_step_select (the step's indices by a device counter, and the flat gradient buffer
-zeroed), the ptyx_forward_loss_grad call, ``optimizer.step()``, ptyx_step_store (the loss terms,
+step — ptyx_step_select (the step's indices by a device counter, the flat gradient buffer zeroed,
+and the HIP Adam's step counts advanced), the ptyx_forward_loss_grad call, ``optimizer.step()``, ptyx_step_store (the loss terms,
 then the counter advances) — into a hipGraph
 (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it for every later step with the same
 shape.  The step's inputs are selected on the device from a per-iteration index table by a
@@ -117,6 +117,7 @@ class StepGraphs:
         self._table = None        # persistent device buffers (idx_all, istart, rstart)
         self._host = None         # the host tables last copied into them
         self._seen = set()        # keys whose first (eager) step has run
+        self._sptr = {}           # key -> (step-count pointers, their device array) for ptyx_step_select
         self._cnt = None          # (1,) i64: the step the next replay runs
         self._terms = None        # (n_batches, 5) loss terms of the iteration
         self.captures = 0
@@ -154,6 +155,17 @@ class StepGraphs:
         self.graphs.clear()
         self.static.clear()
         self._seen.clear()
+        self._sptr.clear()
+
+    def _step_ptrs(self, key, step_ts, dev):
+        """Device array of the step-count pointers ptyx_step_select advances (kept per step shape:
+        a captured graph holds its address; the key already holds the state's pointers)."""
+        want = [int(t.data_ptr()) for t in step_ts]
+        cur = self._sptr.get(key)
+        if cur is None or cur[0] != want:
+            cur = (want, torch.tensor(want, dtype=torch.int64, device=dev))
+            self._sptr[key] = cur
+        return cur[1]
 
     # ---------------------------------------------------------------- one step
     def _body(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, idx_all, istart, rstart,
@@ -165,9 +177,13 @@ class StepGraphs:
         sidx, soff, sterms, mine_t = self.static[key]
         lib = _lib.load()
         st = ctypes.c_void_p(torch.cuda.current_stream(flat_grad.device).cuda_stream)
+        # the HIP Adam's step counts advance in the same launch (its own increment launch skipped)
+        step_ts = optimizer._step_tensors() if hasattr(optimizer, "_step_tensors") else []
+        sp = self._step_ptrs(key, step_ts, flat_grad.device) if 0 < len(step_ts) <= 256 else None
         # the step's indices (device counter) + zeroed gradient buffer (and terms tail), one launch
         _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
-                                        _ptr(flat_grad), int(flat_grad.numel())))
+                                        _ptr(flat_grad), int(flat_grad.numel()), None if sp is None else _ptr(sp),
+                                        0 if sp is None else len(step_ts)))
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
              "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(),
              "tilts": None if model._tilts() is None else model._tilts().detach().contiguous()}
@@ -185,7 +201,12 @@ class StepGraphs:
             if mine_t is not None:
                 terms.index_copy_(0, mine_t, sterms)
             ctx.allreduce(flat_grad)
-        optimizer.step()
+        if sp is not None:
+            optimizer._external_step_inc = True
+        try:
+            optimizer.step()
+        finally:
+            optimizer._external_step_inc = False
         # the loss terms into the iteration's table, then the counter advances (one launch)
         _lib.check(lib.ptyx_step_store(st, _ptr(terms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all)))
 
@@ -259,6 +280,9 @@ class StepGraphs:
                     gr = torch.cuda.CUDAGraph()
                     if self.pool is None:
                         self.pool = torch.cuda.graph_pool_handle()
+                    sts = optimizer._step_tensors() if hasattr(optimizer, "_step_tensors") else []
+                    if 0 < len(sts) <= 256:   # the step-count pointer array exists before the capture
+                        self._step_ptrs(key, sts, dev)
                     torch.cuda.synchronize(dev)
                     with torch.cuda.graph(gr, pool=self.pool):
                         self._body(*args)
@@ -268,6 +292,7 @@ class StepGraphs:
                         old = next(iter(self.graphs))
                         del self.graphs[old]
                         self.static.pop(old, None)
+                        self._sptr.pop(old, None)
                         self._seen.discard(old)
                     gr.replay()
                     self.replays += 1
