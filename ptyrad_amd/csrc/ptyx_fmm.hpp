@@ -597,7 +597,8 @@ constexpr int kTailSegCap = 2048;   // segments (P + workgroups of k_fmm_adj) th
 template <bool KL>
 __global__ __launch_bounds__(256) void k_small_tail_modes(const float2* segslab, const int* segbid, int nseg,
                                                           float2* out, const int* idx, int n, int n_scans, int P,
-                                                          const float* dsu, float* d_shifts) {
+                                                          const float* dsu, float* d_shifts,
+                                                          const float2* twg = nullptr, float2* cols_out = nullptr) {
   constexpr int kSlabBlocks = kN2 / 256;
   if (blockIdx.x >= kSlabBlocks) {
     const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
@@ -647,6 +648,10 @@ __global__ __launch_bounds__(256) void k_small_tail_modes(const float2* segslab,
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
   for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[y]);
+  if (KL && cols_out) {   // (block-uniform) the column pass of the probe gradient's inverse FFT
+    tail_cols_ifft(acc, blockIdx.x, twg, cols_out + (size_t)p * kN2);
+    return;
+  }
   out[(size_t)p * kN2 + packed_rc<KL>(e & 255, e >> 8)] = acc;
 }
 

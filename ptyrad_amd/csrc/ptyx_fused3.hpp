@@ -139,10 +139,55 @@ __global__ void k_shift_apply(const int* idx, int n, int n_scans, const int* bid
 // k_segslab_final + k_shift_apply in ONE launch.  Blocks [0, N²/256) sum the segments in exactly
 // the two kernels' order (partial y = Σ_{g ≡ y mod kSegSplit} c·u, then the partials in order:
 // bit-identical results); the blocks after them apply the position gradient.
+// The probe gradient of a small call, inverse-transformed in two launches instead of three: a
+// tail block owns columns i and i + 64 of the K-packed spectrum G (element 256 i + t is row
+// fixed_of(t), column i + 64(t & 1)), so it transforms those two columns along themselves in LDS
+// (tail_cols_ifft) and stores them to tmp in natural order; k_probe_rows_acc then transforms the
+// rows and adds F⁻¹(G)/N² to d_probe (k_lines_cols<128, +1, 1>'s epilogue).  Columns before rows
+// instead of rows before columns: the same transform up to fp32 rounding.
+constexpr int kPrLinesT = 8;   // rows a k_probe_rows_acc block (ptyx_general.hpp kSpecLines)
+__device__ __forceinline__ void tail_cols_ifft(float2 acc, int i, const float2* twg, float2* tmp_plane) {
+  constexpr int N = kN;
+  using LT = LineTile<N, 2>;
+  using P1 = Plan1D<N>;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 T[LT::kElems];
+  const int t = threadIdx.x, line = t & 1, f = fixed_of(t);
+  for (int k = t; k < N; k += 256) s_tw[k] = twg[k];
+  T[LT::off(line, f)] = acc;
+  __syncthreads();
+  line_pass<N, 256, P1::R1, 1, +1, 2>(T, s_tw, 2);
+  line_pass<N, 256, P1::R2, P1::R1, +1, 2>(T, s_tw, 2);
+  tmp_plane[f * N + i + 64 * line] = T[LT::off(line, f)];
+}
+// grid (N / kPrLinesT, P), block 256: rows l0 … l0 + 7 of plane p, d_probe += F⁻¹_rows(tmp)/N²
+__global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float2* d_probe, const float2* twg) {
+  constexpr int N = kN;
+  using LT = LineTile<N, kPrLinesT>;
+  using P1 = Plan1D<N>;
+  __shared__ float2 s_tw[N];
+  __shared__ float2 T[LT::kElems];
+  const int l0 = blockIdx.x * kPrLinesT, p = blockIdx.y;
+  const float2* s = tmp + (size_t)p * N * N;
+  float2* d = d_probe + (size_t)p * N * N;
+  for (int k = threadIdx.x; k < N; k += 256) s_tw[k] = twg[k];
+  for (int e = threadIdx.x; e < kPrLinesT * N; e += 256) T[LT::off(e / N, e % N)] = s[(size_t)(l0 + e / N) * N + e % N];
+  __syncthreads();
+  line_pass<N, 256, P1::R1, 1, +1, kPrLinesT>(T, s_tw, kPrLinesT);
+  line_pass<N, 256, P1::R2, P1::R1, +1, kPrLinesT>(T, s_tw, kPrLinesT);
+  constexpr float inv_n2 = 1.0f / (float)(N * N);
+  for (int e = threadIdx.x; e < kPrLinesT * N; e += 256) {
+    float2* dp = d + (size_t)(l0 + e / N) * N + e % N;
+    const float2 v = T[LT::off(e / N, e % N)];
+    *dp = cadd(*dp, make_float2(v.x * inv_n2, v.y * inv_n2));
+  }
+}
+
 template <bool KL>
 __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const int* segbid, int nseg,
                                                     const float* coef, int ci, float2* out, const int* idx, int n,
-                                                    int n_scans, const int* bid, const float* dsu, float* d_shifts) {
+                                                    int n_scans, const int* bid, const float* dsu, float* d_shifts,
+                                                    const float2* twg = nullptr, float2* cols_out = nullptr) {
   constexpr int kSlabBlocks = kN2 / 256;
   if (blockIdx.x >= kSlabBlocks) {
     const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
@@ -184,6 +229,10 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
   for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[y]);
+  if (KL && cols_out) {   // (block-uniform) the column pass of the probe gradient's inverse FFT
+    tail_cols_ifft(acc, blockIdx.x, twg, cols_out);
+    return;
+  }
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
 }
 

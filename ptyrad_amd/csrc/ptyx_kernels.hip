@@ -1146,14 +1146,21 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
       float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
         hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts);
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
+                           gz.d_probe ? pl->slab : nullptr);
       else
         hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts);
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
     }
-    if (gz.d_probe) launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, st);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, st, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
+    }
     return launch_status("probe finalize launch");
   }
   if (d_shifts) {
@@ -1297,14 +1304,20 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
       float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
         hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts);
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, pl->twg, gz.d_probe ? pl->slab : nullptr);
       else
         hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts);
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
     }
-    if (gz.d_probe) launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, st);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, st, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
+    }
     return launch_status("k_fmm probe / position reduction launch");
   }
   if (d_shifts) {
