@@ -164,3 +164,16 @@ def test_stage_entry_points_validate_without_gpu():
     assert lib.ptyx_simlar_std_grad(None, None, 2, 0, 16, None, None, None) == _lib.PTYX_OK
 
 
+
+
+def test_tuning_keys_round_trip_without_gpu():
+    """Every key _lib.TUNING_KEYS names (the GPU tests' tuning fixture resets exactly these) is a
+    library key that takes -1 (the measured default) and reads back; unknown keys are refused."""
+    for k in _lib.TUNING_KEYS:
+        before = _lib.get_tuning(k)
+        _lib.set_tuning(k, -1)
+        assert _lib.get_tuning(k) == -1, k
+        _lib.set_tuning(k, before)
+    lib = _lib.load()
+    assert lib.ptyx_set_tuning(b"no_such_key", 1) == _lib.PTYX_EINVAL
+    assert lib.ptyx_get_tuning(b"no_such_key") == -2
