@@ -533,15 +533,17 @@ __global__ __launch_bounds__(256) void k_pattern_table_direct(const int* idx, in
 
 // Small calls with PTYX_PREP_CALL (one mini-batch per optimizer step): k_pattern_table_direct,
 // k_obj_prep and k_bbox_small as ONE launch of independent block roles —
-//   blocks [0, n)            the pattern table (+ the loss_sparse window sums when SPARSE);
+//   blocks [0, n)            the pattern table (+ the loss_sparse window sums when SPARSE; with
+//                            PrepExtra::zsum n·Nz blocks, one (pattern, slice) sum each);
 //   blocks [n, n + R)        O = A e^{iφ} for kPrepRows object rows (of the Nz·Ny) each, those any
 //                            window of the call covers (decided from the ≤ 256 windows directly,
 //                            not the bbox); R = ⌈Nz·Ny / kPrepRows⌉ (small_prep_blocks);
 //   block n + R              the bounding box (k_obj_gather) and the segment-table clear.
 // Same outputs as the three kernels (the rows no window touches are never read under PREP_CALL).
 constexpr int kPrepRows = 4;
-__host__ __device__ constexpr int small_prep_blocks(int n, int Nz, int Ny) {
-  return n + (Nz * Ny + kPrepRows - 1) / kPrepRows + 1;
+// zs (multislice calls with loss_sparse): the pattern blocks are n·Nz, one (pattern, slice) each
+__host__ __device__ constexpr int small_prep_blocks(int n, int Nz, int Ny, bool zs = false) {
+  return (zs ? n * Nz : n) + (Nz * Ny + kPrepRows - 1) / kPrepRows + 1;
 }
 // Work of the call's probe preparation that rides in k_small_prep's launch as further block roles
 // (independent of the table / object rows): the row pass of F(P_p) (k_lines_rows<128, −1>, the
@@ -556,6 +558,7 @@ struct PrepExtra {
   const float2* H = nullptr;
   float2* hpk = nullptr;
   float hscale = 1.0f;
+  double* zsum = nullptr;      // per-(pattern, slice) loss_sparse window sums (else psums, per pattern)
   __host__ __device__ int row_blocks() const { return probe ? (kN / kPrLines) * P : 0; }
   __host__ __device__ int h_blocks() const { return H ? kN2 / 256 : 0; }
 };
@@ -576,6 +579,33 @@ __device__ __forceinline__ void probe_rows_body(int bx, int p, const float2* src
   line_pass<N, 256, P1::R2, P1::R1, -1, kPrLines>(T, s_tw, nl);
   for (int e = threadIdx.x; e < nl * N; e += 256) d[(size_t)(l0 + e / N) * N + e % N] = T[LT::off(e / N, e % N)];
 }
+// one (pattern, slice)'s loss_sparse window sum: the slice pass of k_pattern_table_direct_body,
+// its fp64 wave sums added in wave order, to zsum[j·Nz + z] (k_finalize adds the slices in order)
+__device__ __forceinline__ void slice_window_sum(int j, int z, const int* idx, const int* crop, int n_scans, int Ny,
+                                                 int Nx, const float* objp, int sparse_n, int Nz, double* zsum) {
+  __shared__ double s_z[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s = min(max(idx[j], 0), n_scans - 1);
+  const int cy = min(max(crop[2 * s], 0), Ny - kN), cx = min(max(crop[2 * s + 1], 0), Nx - kN);
+  const float* ph = objp + ((size_t)z * Ny + cy + wave) * Nx + cx + lane;
+  float v[64];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    v[2 * k] = ph[(size_t)(4 * k) * Nx];
+    v[2 * k + 1] = ph[(size_t)(4 * k) * Nx + 64];
+  }
+  double acc = 0;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const float a = fabsf(v[k]);
+    acc += sparse_n == 1 ? (double)a : (double)powq(a, (float)sparse_n);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) s_z[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) zsum[(size_t)j * Nz + z] = ((s_z[0] + s_z[1]) + s_z[2]) + s_z[3];
+}
 template <bool SPARSE>
 __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const int* boff, int n_batches,
                                                     const int* crop, int n_scans, int Ny, int Nx, int* bid, int2* geo,
@@ -583,7 +613,9 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
                                                     int Nz, TableCheck tc, float2* oc, int* bbox, int* segbid,
                                                     int nseg, PrepExtra ex) {
   const int b = blockIdx.x;
-  const int bx = b - small_prep_blocks(n, Nz, Ny);   // the PrepExtra roles
+  const bool zs = SPARSE && ex.zsum != nullptr;
+  const int np = zs ? n * Nz : n;                         // pattern blocks
+  const int bx = b - small_prep_blocks(n, Nz, Ny, zs);   // the PrepExtra roles
   if (bx >= 0) {
     if (bx < ex.row_blocks()) {
       probe_rows_body(bx % (kN / kPrLines), bx / (kN / kPrLines), ex.probe, ex.tmp, ex.twg);
@@ -594,8 +626,12 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
     ex.hpk[e] = make_float2(h.x * ex.hscale, h.y * ex.hscale);
     return;
   }
-  if (b < n) {
-    if constexpr (SPARSE) {
+  if (b < np) {
+    if (zs) {   // (pattern j, slice z): z = 0 also writes the table entry
+      const int j = b / Nz, z = b - j * Nz;
+      if (z == 0 && threadIdx.x == 0) table_entry(j, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
+      slice_window_sum(j, z, idx, crop, n_scans, Ny, Nx, objp, sparse_n, Nz, ex.zsum);
+    } else if constexpr (SPARSE) {
       k_pattern_table_direct_body(b, idx, n, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, objp, sparse_n, psums,
                                   Nz, tc);
     } else if (threadIdx.x == 0) {
@@ -604,13 +640,13 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
     return;
   }
   const int nrb = (Nz * Ny + kPrepRows - 1) / kPrepRows;
-  if (b == n + nrb) {
+  if (b == np + nrb) {
     k_bbox_small_body(idx, n, crop, n_scans, Ny, Nx, bbox, kN, segbid, nseg);
     return;
   }
   // kPrepRows consecutive object rows (flattened z·Ny + r): which of them any window covers, then
   // their loads issued together
-  const int y0 = (b - n) * kPrepRows;
+  const int y0 = (b - np) * kPrepRows;
   int cy = -(1 << 29);
   if ((int)threadIdx.x < n) {
     const int s = min(max(idx[threadIdx.x], 0), n_scans - 1);

@@ -67,6 +67,8 @@ struct FinArgs {
   const double* bsums_in = nullptr;
   const float* lparts = nullptr;   // the data-term sums [0, kSumBase) as nparts partials per pattern
   int nparts = 0;                  // (k_fmm_loss, ≤ kFinMaxParts), added in part order
+  const double* zsum = nullptr;    // object mode 0's sparse sum as zNz per-slice partials per pattern
+  int zNz = 0;                     // (k_small_prep with use_zsum), added in slice order
 };
 constexpr int kFinMaxParts = 8;
 static_assert(kSumBase == 4, "k_finalize reads the data-term sums as one float4");
@@ -88,7 +90,12 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
   auto wsum = [&](int k) -> double {
     if (bin) return bin[1 + k];
     double s = 0;
-    for (int t = b0 + lane; t < b1; t += 64) s += f.psums[(size_t)t * kNSum + k];
+    if (f.zsum && k == kSumBase) {
+      for (int t = b0 + lane; t < b1; t += 64)
+        for (int z = 0; z < f.zNz; ++z) s += f.zsum[(size_t)t * f.zNz + z];
+    } else {
+      for (int t = b0 + lane; t < b1; t += 64) s += f.psums[(size_t)t * kNSum + k];
+    }
 #pragma unroll
     for (int x = 32; x >= 1; x >>= 1) s += __shfl_xor(s, x, 64);
     return s;
@@ -277,6 +284,8 @@ struct ptyx_plan {
   float* Ibuf = nullptr;
   float* Ibuf2 = nullptr;     // mixed-state register engine with both data terms: ∂ℓ_poissn/∂I planes
   float* lparts = nullptr;    // mixed-state register engine: k_fmm_loss partial sums (patterns, parts, 4)
+  double* zsum = nullptr;     // small multislice calls: loss_sparse window sums per (pattern, slice)
+  bool zsum_call = false;     // the current call's k_small_prep wrote zsum (k_finalize reads it)
   float* Imodes = nullptr;    // probe-mode split: P mode-intensity planes per pattern (≤ kModeSplitCap)
   float2* slab = nullptr;
   float2* Gsum = nullptr;
@@ -717,6 +726,11 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
       pl->ms3 = true;
     }
   }
+  // the per-slice loss_sparse window sums of small multislice calls (k_small_prep, use_zsum)
+  if (pl->bbox && d.Nz > 1 && (rc = dalloc(pl, &pl->zsum, (size_t)f3::kSmallCall * d.Nz))) {
+    free_plan(pl);
+    return rc;
+  }
   // input-error flags in host-mapped memory: the kernels set them (plain stores) and the next call
   // reads them without synchronising the stream
   e = hipHostMalloc(reinterpret_cast<void**>(&pl->err_host), sizeof(int) * kErrWords, hipHostMallocMapped);
@@ -889,6 +903,7 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
   const bool sparse = cfg->sparse_on != 0;
   const int Nz = d.Nz;
   const bool reuse = cfg->prep == PTYX_PREP_REUSE;   // object / probe / H prepared by the previous call
+  pl->zsum_call = false;
   // small calls (one mini-batch per optimizer step): one-workgroup bbox that also clears the
   // segment table, and direct loss_sparse window sums instead of the summed-area table; the
   // probe spectrum's row pass and the H packing ride in the same launch (PrepExtra)
@@ -923,9 +938,14 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
       ex.hpk = pl->hpk;
       ex.hscale = 1.0f / N2;
     }
+    if (sparse && Nz > 1 && pl->zsum) {   // the window sums one (pattern, slice) a workgroup
+      ex.zsum = pl->zsum;
+      pl->zsum_call = true;
+    }
     {
       ProfScope ps(pl, kKTable, st);
-      const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny) + ex.row_blocks() + ex.h_blocks()), bl(256);
+      const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny, ex.zsum != nullptr) + ex.row_blocks() + ex.h_blocks()),
+          bl(256);
       const f3::TableCheck tc{a.err, a.mrow, a.mrows};
       if (sparse)
         hipLaunchKernelGGL(f3::k_small_prep<true>, gr, bl, 0, st, a.idx, a.n_idx, a.boff, a.n_batches, a.crop,
@@ -1088,6 +1108,10 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   FinArgs fa{};
   fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
   fa.psums = pl->psums; fa.occu = in->omode_occu;
+  if (pl->zsum_call) {   // the sparse sums as per-slice partials (k_small_prep)
+    fa.zsum = pl->zsum;
+    fa.zNz = Nz;
+  }
   fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
   fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
@@ -1237,6 +1261,10 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   FinArgs fa{};
   fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
   fa.psums = pl->psums; fa.occu = in->omode_occu;
+  if (pl->zsum_call) {   // the sparse sums as per-slice partials (k_small_prep)
+    fa.zsum = pl->zsum;
+    fa.zNz = Nz;
+  }
   fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
   fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
   fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
