@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 206
+#define PTYX_ABI_VERSION 207
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -402,6 +402,14 @@ int ptyx_step_store(void *stream, const float *terms, int32_t nb, const int64_t 
 int ptyx_adam_step(void *stream, int32_t n, float *const *params, const float *const *grads, float *const *exp_avgs,
                    float *const *exp_avg_sqs, const float *const *steps, const int64_t *numels, const double *lrs,
                    double beta1, double beta2, double eps, double weight_decay, int32_t flags);
+/* ptyx_adam_step, then in the same launch what ptyx_step_store does (terms_all[rstart[*cnt] + b][k]
+ * = terms[b][k], ++*cnt): a graph-replayed step whose optimizer is the HIP Adam needs no store
+ * launch of its own.  Issues one bookkeeping-only launch when no tensor has elements. */
+int ptyx_adam_step_store(void *stream, int32_t n, float *const *params, const float *const *grads,
+                         float *const *exp_avgs, float *const *exp_avg_sqs, const float *const *steps,
+                         const int64_t *numels, const double *lrs, double beta1, double beta2, double eps,
+                         double weight_decay, int32_t flags, const float *terms, int32_t nb, const int64_t *rstart,
+                         int64_t *cnt, float *terms_all);
 
 /* Patterns one ptyx_forward_loss_grad call may hold and still run on the plan's fast engine:
  * the register-resident engines' slot capacity (k_fused3 / k_fused3ms / mixed-state), the stripe

@@ -50,6 +50,13 @@ struct AdamArgs {
   float beta1, beta2, eps, wd;
   double beta1d, beta2d;
   int adamw, maximize;
+  // optional graph-step bookkeeping in workgroup 0 (ptyx_adam_step_store): the step's loss terms
+  // into the iteration's table, then the device step counter advanced
+  const float* sterms;
+  const int64_t* srstart;
+  int64_t* scnt;
+  float* sterms_all;
+  int snb;
 };
 
 // β^t for the integer step count t by square-and-multiply in fp64 (a few fp64 ulps from pow(),
@@ -77,6 +84,13 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     s_bc2s[t] = (float)sqrt(bc2);
   }
   __syncthreads();
+  if (a.scnt && blockIdx.x == 0) {   // as k_step_store: every thread reads *scnt before it advances
+    const int64_t c = *a.scnt;
+    const int64_t r0 = a.srstart[c];
+    for (int i = threadIdx.x; i < a.snb * 5; i += blockDim.x) a.sterms_all[r0 * 5 + i] = a.sterms[i];
+    __syncthreads();
+    if (threadIdx.x == 0) *a.scnt = c + 1;
+  }
   const int64_t total = a.off[a.nt];
   const float w1 = (float)(1.0 - a.beta1d), c2 = (float)(1.0 - a.beta2d);
   // a workgroup takes chunks of 4·256 consecutive units of one tensor, a thread four of them 256
@@ -157,11 +171,18 @@ using ptyx::abi::fail;
 using ptyx::abi::launch_status;
 namespace opt = ptyx::opt;
 
-extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
-                              float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
-                              const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
-                              double weight_decay, int32_t flags) {
-  ptyx::abi::clear_error();
+namespace {
+struct StepStore {
+  const float* terms;
+  int32_t nb;
+  const int64_t* rstart;
+  int64_t* cnt;
+  float* terms_all;
+};
+
+int adam_step(void* stream, int32_t n, float* const* params, const float* const* grads, float* const* exp_avgs,
+              float* const* exp_avg_sqs, const float* const* steps, const int64_t* numels, const double* lrs,
+              double beta1, double beta2, double eps, double weight_decay, int32_t flags, const StepStore* ss) {
   if (n < 0 || (n && (!params || !grads || !exp_avgs || !exp_avg_sqs || !steps || !numels || !lrs)))
     return fail(PTYX_EINVAL, "ptyx_adam_step: null array or negative count");
   // Each tensor is one or two ranges: its first 4·⌊numel/4⌋ elements in float4 units when p, g,
@@ -218,9 +239,50 @@ extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, con
     a.maximize = (flags >> 1) & 1;
     const int64_t total = a.off[a.nt];
     if (!total) continue;
+    if (ss) {   // the bookkeeping rides in the first launch
+      a.sterms = ss->terms;
+      a.snb = ss->nb;
+      a.srstart = ss->rstart;
+      a.scnt = ss->cnt;
+      a.sterms_all = ss->terms_all;
+      ss = nullptr;
+    }
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, total / opt::kChunk));
     hipLaunchKernelGGL(opt::k_adam, dim3(blocks), dim3(opt::kThreads), 0, (hipStream_t)stream, a);
     if (int rc = launch_status("k_adam launch")) return rc;
   }
+  if (ss) {   // nothing to update: the bookkeeping alone (one workgroup, no tensors)
+    opt::AdamArgs a{};
+    a.sterms = ss->terms;
+    a.snb = ss->nb;
+    a.srstart = ss->rstart;
+    a.scnt = ss->cnt;
+    a.sterms_all = ss->terms_all;
+    hipLaunchKernelGGL(opt::k_adam, dim3(1), dim3(opt::kThreads), 0, (hipStream_t)stream, a);
+    if (int rc = launch_status("k_adam launch")) return rc;
+  }
   return PTYX_OK;
+}
+}  // namespace
+
+extern "C" int ptyx_adam_step(void* stream, int32_t n, float* const* params, const float* const* grads,
+                              float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                              const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
+                              double weight_decay, int32_t flags) {
+  ptyx::abi::clear_error();
+  return adam_step(stream, n, params, grads, exp_avgs, exp_avg_sqs, steps, numels, lrs, beta1, beta2, eps,
+                   weight_decay, flags, nullptr);
+}
+
+extern "C" int ptyx_adam_step_store(void* stream, int32_t n, float* const* params, const float* const* grads,
+                                    float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                                    const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
+                                    double weight_decay, int32_t flags, const float* terms, int32_t nb,
+                                    const int64_t* rstart, int64_t* cnt, float* terms_all) {
+  ptyx::abi::clear_error();
+  if (!terms || !rstart || !cnt || !terms_all || nb < 0)
+    return fail(PTYX_EINVAL, "ptyx_adam_step_store: null pointer or negative size");
+  const StepStore ss{terms, nb, rstart, cnt, terms_all};
+  return adam_step(stream, n, params, grads, exp_avgs, exp_avg_sqs, steps, numels, lrs, beta1, beta2, eps,
+                   weight_decay, flags, &ss);
 }

@@ -40,6 +40,10 @@ class _HipAdamMixin:
     # set by a graph-replayed recon_step around step(): its ptyx_step_select launch has already
     # advanced the step counts _step_tensors() returned (ptyrad_amd/stepgraph.py)
     _external_step_inc = False
+    # set likewise: (terms, nb, rstart, cnt, terms_all) pointers of the step's ptyx_step_store, done
+    # by the first Adam launch instead (ptyx_adam_step_store); _step_store_done tells the caller
+    _step_store = None
+    _step_store_done = False
 
     def _step_tensors(self):
         """The step counts the next step() advances (one per eligible parameter with a gradient),
@@ -96,8 +100,13 @@ class _HipAdamMixin:
             NE = (ctypes.c_int64 * n)(*[p.numel() for p, _, _ in items])
             LR = (ctypes.c_double * n)(*[lr for _, _, lr in items])
             stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            _lib.check(_lib.load().ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd,
-                                                  (1 if decoupled else 0) | (2 if maximize else 0)))
+            flags = (1 if decoupled else 0) | (2 if maximize else 0)
+            if self._step_store is not None and not self._step_store_done:
+                _lib.check(_lib.load().ptyx_adam_step_store(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd,
+                                                            flags, *self._step_store))
+                self._step_store_done = True
+            else:
+                _lib.check(_lib.load().ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd, flags))
         if plain:
             saved = self.param_groups
             try:

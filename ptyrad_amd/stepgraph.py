@@ -7,7 +7,7 @@ Adam kernels, and issuing them from Python costs more than the GPU needs to run 
 (0.47 ms per step, 0.18 ms of it GPU time).  ``StepGraphs`` captures ONE optimizer
 step — ptyx_step_select (the step's indices by a device counter, the flat gradient buffer zeroed,
 and the HIP Adam's step counts advanced), the ptyx_forward_loss_grad call, ``optimizer.step()``, ptyx_step_store (the loss terms,
-then the counter advances) — into a hipGraph
+then the counter advances; done by the HIP Adam's first launch when it runs one) — into a hipGraph
 (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it for every later step with the same
 shape.  The step's inputs are selected on the device from a per-iteration index table by a
 step counter that the graph itself advances, so a replay needs no host work besides the launch.
@@ -203,12 +203,21 @@ class StepGraphs:
             ctx.allreduce(flat_grad)
         if sp is not None:
             optimizer._external_step_inc = True
+        # the loss terms into the iteration's table, then the counter advances: inside the HIP
+        # Adam's first launch when it runs one, else a launch of its own
+        store = (_ptr(terms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all))
+        fold = hasattr(optimizer, "_step_store")
+        if fold:
+            optimizer._step_store, optimizer._step_store_done = store, False
         try:
             optimizer.step()
+            done = fold and optimizer._step_store_done
         finally:
             optimizer._external_step_inc = False
-        # the loss terms into the iteration's table, then the counter advances (one launch)
-        _lib.check(lib.ptyx_step_store(st, _ptr(terms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all)))
+            if fold:
+                optimizer._step_store, optimizer._step_store_done = None, False
+        if not done:
+            _lib.check(lib.ptyx_step_store(st, *store))
 
     def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad, ctx=None, extra=0):
         """All optimizer steps of one recon_step iteration; returns the (n_batches, 5) loss terms.
