@@ -26,6 +26,8 @@ Other workloads (--config; all one process per GPU, same step structure):
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
        torchrun --nproc-per-node N bench.py --gpus N ...   (driver, one rank per GPU, RCCL)
+  Without torchrun, --gpus N > 1 starts the N rank processes itself (launch_ranks: fresh
+  processes, rank 0's JSON line only, non-zero exit when a rank fails or fewer GPUs are visible).
 """
 from __future__ import annotations
 
@@ -82,6 +84,8 @@ def parse():
                          "reference: recon_step at grad_accumulation = 1 (the reference's default cadence) on "
                          "the c2 scan, every mini-batch split over the ranks, graph-replayed steps with their "
                          "RCCL collectives captured; one bench step = one recon_step iteration")
+    ap.add_argument("--rank-timeout", type=float, default=3000.0,
+                    help="--gpus N > 1 without torchrun: seconds before the launcher stops a job that has not ended")
     ap.add_argument("--always-reduce", action="store_true",
                     help="--cadence reference at one GPU: init RCCL anyway and run every collective of the "
                          "multi-rank step (split mini-batches), as an 8-GPU job would")
@@ -330,14 +334,114 @@ def reference_cadence(a, world, rank, local, cpu):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ rank launcher
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising the GPU (torch.cuda.device_count
+    does not create a HIP context on this image; is_available() would)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(n, cmd, timeout=None, env=None, poll_s=0.2, out=None):
+    """Run ``cmd`` as ``n`` fresh rank processes of one job (one per GPU, the launch torchrun would
+    make: RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR 127.0.0.1 / MASTER_PORT in
+    their environment) and forward rank 0's stdout only; every rank's stderr passes through.  The
+    launcher itself never touches the GPU.  The first rank that exits non-zero, or a job still
+    running after ``timeout`` seconds, ends the job: the other ranks' process groups are killed and
+    the exit status returned is non-zero (the failing rank's code, 124 on a timeout).  Returns 0
+    when every rank exits 0."""
+    import signal
+    import subprocess
+    out = out if out is not None else sys.stdout
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(_free_port())})
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True, text=True))
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    import threading
+    lines = []
+
+    def pump():                        # rank 0's stdout, forwarded as it arrives
+        for line in procs[0].stdout:
+            lines.append(line)
+            out.write(line)
+            out.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t0 = time.monotonic()
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"[bench] rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr)
+                status = c if c > 0 else 128 - c
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                print(f"[bench] the {n}-rank job exceeded {timeout:.0f} s; stopping it", file=sys.stderr)
+                status = 124
+                break
+            time.sleep(poll_s)
+    finally:
+        kill_all()
+        th.join(timeout=5)
+    return status
+
+
 def main():
     a = parse()
     cfg = CONFIGS[a.config]
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: start the N ranks here, one fresh process per
+        # GPU, and never touch the GPU in this process
+        have = visible_gpus()
+        if have < a.gpus:
+            print(f"[bench] --gpus {a.gpus} needs {a.gpus} visible GPUs, this host shows {have}", file=sys.stderr)
+            raise SystemExit(2)
+        raise SystemExit(launch_ranks(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      timeout=a.rank_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and not a.quiet and rank == 0:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    if world != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE {world}: the launcher must start one rank per GPU",
+              file=sys.stderr)
+        raise SystemExit(2)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -364,10 +468,10 @@ def main():
             k, v = kv.split("=")
             _lib.set_tuning(k, int(v))
             tunings[k] = int(v)
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     ctx = DistContext()
     N, P, O, Nz, f16 = cfg["N"], cfg["P"], cfg["O"], cfg["Nz"], cfg["f16"]
     gw, gr = (a.geom_world, a.geom_rank) if a.geom_world else (world, rank)

@@ -32,17 +32,18 @@ def _on(cp, name, niter):
 
 def object_footprint(cp, niter):
     """What iteration ``niter``'s object constraints read (constraints.py:83-208): 'global' for the
-    Fourier filters (kr / kz), the lateral blur and objp_postiv's subtract_min (the global
-    minimum); 'pointwise' when only per-pixel ones run (obj_zblur acts along z at one (y, x),
-    complex_ratio, mirrored_amp, obja_thresh, objp_postiv clip_neg); else 'none'.  The band
-    exchange refreshes the whole object before a 'global' iteration only."""
+    Fourier filters (kr / kz), the lateral blur, objp_postiv's subtract_min (the global minimum)
+    and complex_ratio (its Cbar = Σ|ln A| / Σ|φ| sums the whole object, constraints.py:352);
+    'pointwise' when only per-pixel ones run (obj_zblur acts along z at one (y, x), mirrored_amp,
+    obja_thresh, objp_postiv clip_neg); else 'none'.  The band exchange refreshes the whole object
+    before a 'global' iteration only."""
     blur = cp.get("obj_rblur") or {}
     pos = cp.get("objp_postiv") or {}
-    if _on(cp, "kr_filter", niter) or _on(cp, "kz_filter", niter) or \
+    if _on(cp, "kr_filter", niter) or _on(cp, "kz_filter", niter) or _on(cp, "complex_ratio", niter) or \
             (_on(cp, "obj_rblur", niter) and blur.get("std", 0) != 0) or \
             (_on(cp, "objp_postiv", niter) and pos.get("mode", "clip_neg") == "subtract_min"):
         return "global"
-    if any(_on(cp, k, niter) for k in ("obj_zblur", "complex_ratio", "mirrored_amp", "obja_thresh", "objp_postiv")):
+    if any(_on(cp, k, niter) for k in ("obj_zblur", "mirrored_amp", "obja_thresh", "objp_postiv")):
         return "pointwise"
     return "none"
 

@@ -141,7 +141,7 @@ def loss_logger(batch_losses, niter, iter_t, verbose=True):
 class DistContext:
     """Rank/world of a torch.distributed job (backend 'nccl' = RCCL on ROCm, or 'gloo' on CPU)."""
 
-    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=None):
+    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=False):
         """split_batches: None = split a group's mini-batches over the ranks only when the group has
         fewer mini-batches than ranks; True = always (accelerate's split_batches=True,
         utils/common.py:63); False = never (whole mini-batches round-robin).
@@ -149,16 +149,23 @@ class DistContext:
         band_exchange: object gradients by row band (ObjectBands): each rank sends only the rows
         its windows touched to their owners, owners run the optimizer on their band (ZeRO-1),
         then send the updated rows back to the ranks that read them; the rest of the gradient is
-        all-reduced.  None (default) = auto: by band when the ranks' touched rows line up by rank
-        within a window of their bands (a row-sharded scan), else one flat all-reduce; True /
-        False force it.  With the band exchange, call ``sync_object(model)`` on every rank before
-        reading the object outside recon_step."""
+        all-reduced.  False (default): one flat all-reduce; True: always by band; "auto": by band
+        when the ranks' touched rows line up by rank within a window of their bands (a row-sharded
+        scan), else the flat all-reduce.  The band exchange is opt-in because it changes what the
+        caller's optimizer holds: the object moments live in the band optimizer
+        (``ObjectBands.opt``), so ``optimizer.state_dict()`` lacks them (a resumed run restarts
+        them), and its steps are not graph-replayed.  With the band exchange, call
+        ``sync_object(model)`` on every rank before reading the object outside recon_step."""
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.split_batches = split_batches
         self.always_reduce = bool(always_reduce) and dist.is_initialized()
-        self.band_exchange = None if band_exchange is None else bool(band_exchange)
+        if band_exchange is None:
+            band_exchange = False
+        if band_exchange != "auto":
+            band_exchange = bool(band_exchange)
+        self.band_exchange = band_exchange
         self.bands = None
         self.block_split = None   # the split decision local_indices built a measurement block for
 
@@ -583,12 +590,12 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
     if ctx.band_exchange is not False and ctx._collective() and objs:
         # the rows each rank's windows reach this iteration (recomputed: the batches may change);
-        # band_exchange None = auto: by band when the ranks' rows line up (a row-sharded scan)
+        # band_exchange "auto": by band when the ranks' rows line up (a row-sharded scan)
         N = int(model.opt_probe.shape[1])
         lo, hi = touched_rows(model, ctx.local_batches(batches, grad_accumulation, split_ok), N)
         ranges = exchange_ranges(ctx, lo, hi, dev)
         Ny = int(model.opt_obja.shape[2])
-        if ctx.bands is None and (ctx.band_exchange or ObjectBands.disjoint(ranges, Ny, ctx.world, N)):
+        if ctx.bands is None and (ctx.band_exchange is True or ObjectBands.disjoint(ranges, Ny, ctx.world, N)):
             ctx.bands = ObjectBands(ctx, Ny, dev, ranges)
         if ctx.bands is not None:
             band = True

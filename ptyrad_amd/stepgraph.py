@@ -43,7 +43,7 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
     the same path."""
     if not torch.cuda.is_available() or model.opt_obja.device.type != "cuda":
         return "no HIP device"
-    if ctx is not None and (ctx.band_exchange or ctx.bands is not None):
+    if ctx is not None and (ctx.band_exchange is True or ctx.bands is not None):
         return "band exchange (point-to-point collectives per step)"
     if not (hasattr(loss_fn, "_special") and hasattr(loss_fn, "supports_batch_split")):
         return "loss_fn is not ptyrad_amd.losses.CombinedLoss"
@@ -184,6 +184,22 @@ class StepGraphs:
         _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
                                         _ptr(flat_grad), int(flat_grad.numel()), None if sp is None else _ptr(sp),
                                         0 if sp is None else len(step_ts)))
+        try:
+            self._body_rest(model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
+                            ctx, extra, G, split, sp, lib, st)
+        except BaseException:
+            # an eager step that raised after its step counts advanced (an engine-call check, the
+            # optimizer itself): take them back, so Adam's bias correction stays in step with the
+            # updates it really made (a capture only records the launch; nothing ran)
+            if sp is not None and not torch.cuda.is_current_stream_capturing():
+                with torch.no_grad():
+                    for t_ in step_ts:
+                        t_.sub_(1)
+            raise
+
+    def _body_rest(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
+                   ctx, extra, G, split, sp, lib, st):
+        sidx, soff, sterms, mine_t = self.static[key]
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
              "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(),
              "tilts": None if model._tilts() is None else model._tilts().detach().contiguous()}

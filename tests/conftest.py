@@ -17,3 +17,18 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _reset_engine_tuning(request):
+    """After EVERY GPU test: every ptyx_set_tuning key back to its measured default, so a variant
+    one test selects can never leak into the next (a leaked gather variant failed a
+    later test's split-invariance check)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    from ptyrad_amd import _lib
+    if _lib._lib is None:
+        return
+    for k in _lib.TUNING_KEYS:
+        _lib.set_tuning(k, -1)

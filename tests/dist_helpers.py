@@ -279,8 +279,9 @@ def row_sharded_problem(W, seed=0, N=32, rows_per_rank=2, n_fast=3, step_px=18.0
     """A trajectory-fixture-shaped problem whose scan is sharded by rows over W ranks: rank r's
     mini-batches hold only scan rows [r·rows_per_rank, (r+1)·rows_per_rank) (grad_accumulation =
     W, whole mini-batches dealt round-robin), and the scan step is large enough that every object
-    pixel is reached by at most two ranks.  Pointwise object constraints every iteration and a
-    Fourier filter (a global footprint) in the last one."""
+    pixel is reached by at most two ranks.  Pointwise object constraints every iteration,
+    complex_ratio (a whole-object sum) in the second and a Fourier filter (a global footprint) in
+    the last one."""
     from ptyrad_amd import synthetic as syn
     rng = np.random.default_rng(seed)
     sc = syn.raster_scan(W * rows_per_rank, n_fast, N, step_px=step_px, seed=seed)
@@ -317,13 +318,15 @@ def row_sharded_problem(W, seed=0, N=32, rows_per_rank=2, n_fast=3, step_px=18.0
         "mirrored_amp": {"freq": 1, "relax": 0.1, "scale": 0.03, "power": 4.0},
         "obja_thresh": {"freq": 1, "relax": 0.0, "thresh": [0.98, 1.02]},
         "objp_postiv": {"freq": 1, "relax": 0.0, "mode": "clip_neg"},
+        # Cbar sums the whole object (a global footprint): iteration 2 of 3
+        "complex_ratio": {"freq": 2, "obj_type": "both", "alpha1": 0.7, "alpha2": 0.2},
         "kr_filter": {"freq": niter, "obj_type": "both", "radius": 0.15, "width": 0.05}}))
     z["probe_int_sum"] = np.array(float(np.sum(np.abs(z["init_probe"]) ** 2)))
     return z
 
 
 def band_worker(rank, world, port, out_path, band):
-    """One gloo rank of the row-sharded problem with band_exchange = band (None: auto)."""
+    """One gloo rank of the row-sharded problem with band_exchange = band ("auto", True or False)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)

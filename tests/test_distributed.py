@@ -1,4 +1,4 @@
-"""Data-parallel driver (replacement of PtyRAD's DDP wrapper) on CPU with gloo, world_size 2.
+"""Data-parallel driver (replacement of PtyRAD's DDP wrapper) on CPU with gloo, world_size 2 to 8.
 
 The mini-batches of every optimizer step are dealt round-robin to the ranks, gradients are summed
 by ONE all-reduce, and every rank takes the same Adam step.  Expected: identical replicas, and
@@ -189,20 +189,23 @@ def test_oracle_split_mini_batches_equal_whole_batches(world):
         np.testing.assert_allclose(got, whole[k], rtol=1e-10, atol=1e-13 * np.abs(whole[k]).max(), err_msg=k)
 
 
-def test_three_ranks_ga1_split_batches_reproduce_single_rank(tmp_path):
-    """grad_accumulation = 1 (the reference default) on 3 gloo ranks: every mini-batch of 4 is split
-    2/1/1 over the ranks, each rank holds only its parts' DPs (the rest NaN), and the trajectory
-    equals the single-rank one (fp32 summation order) and the reference's."""
+@pytest.mark.parametrize("world", [3, 8])
+def test_ga1_split_batches_reproduce_single_rank(tmp_path, world):
+    """grad_accumulation = 1 (the reference default) on 3 and 8 gloo ranks: every mini-batch of 4
+    is split over the ranks (2/1/1 at three; at eight, four ranks hold one position and four hold
+    none but still join every collective), each rank holds only its parts' DPs (the rest NaN), and
+    the trajectory equals the single-rank one (fp32 summation order) and the reference's."""
     path = [p for p in TRAJ if "traj_n64_b4_ga1" in p][0]
     z = np.load(path, allow_pickle=False)
     single, _ = run_recon(z)
     out = str(tmp_path / "r.npz")
-    mp.start_processes(dist_worker, args=(3, free_port(), path, out, {"shard": True}), nprocs=3,
+    mp.start_processes(dist_worker, args=(world, free_port(), path, out, {"shard": True}), nprocs=world,
                        start_method="spawn")
-    r = [np.load(out)] + [np.load(out.replace(".npz", f"_r{i}.npz")) for i in (1, 2)]
+    r = [np.load(out)] + [np.load(out.replace(".npz", f"_r{i}.npz")) for i in range(1, world)]
     for k in ("obja", "objp", "probe", "shifts"):
         assert np.all(np.isfinite(r[0][k])), k
-        assert np.array_equal(r[0][k], r[1][k]) and np.array_equal(r[0][k], r[2][k]), f"replicas diverged in {k}"
+        for i in range(1, world):
+            assert np.array_equal(r[0][k], r[i][k]), f"replicas diverged in {k} (rank {i})"
         np.testing.assert_allclose(r[0][k], single[k], rtol=0, atol=2e-6)
     for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
         assert float(np.sqrt(np.mean((r[0][k].astype(np.float64) - ref) ** 2))) < 1e-5
@@ -229,14 +232,16 @@ def test_band_exchange_equals_flat_allreduce(tmp_path, name, start):
         assert np.array_equal(outs[True][0][k], outs[False][0][k]), f"band != all-reduce in {k}"
 
 
-def test_mismatched_ranks_refuse_instead_of_hanging(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_mismatched_ranks_refuse_instead_of_hanging(tmp_path, world):
     """A rank iterating another batching would pair mismatched collectives: recon_step's
     fingerprint all-reduce makes EVERY rank raise before the first step collective."""
     from tests.dist_helpers import mismatch_worker
     path = [p for p in TRAJ if "traj_n32_p2_ga2" in p][0]
     out = str(tmp_path / "m.npz")
-    mp.start_processes(mismatch_worker, args=(2, free_port(), path, out, "batches"), nprocs=2, start_method="spawn")
-    for r in range(2):
+    mp.start_processes(mismatch_worker, args=(world, free_port(), path, out, "batches"), nprocs=world,
+                       start_method="spawn")
+    for r in range(world):
         z = np.load(out.replace(".npz", f"_r{r}.npz"))
         assert int(z["ok"]) == 0 and "disagree" in str(z["msg"])
 
@@ -269,10 +274,10 @@ def test_agree_and_step_plan_single_process():
     assert p1 != ctx.step_plan(b, 2, True, False, 100, None)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_band_exchange_row_sharded_auto_equals_flat(tmp_path, world):
     """A row-sharded scan (each rank's mini-batches from its own scan rows, every pixel reached by
-    at most two ranks): the default DistContext picks the band exchange by itself (halo rows to
+    at most two ranks): DistContext(band_exchange="auto") picks the band exchange by itself (halo rows to
     the owners, Adam on the owned band, updated rows back to their readers, no per-step
     all-gather; the whole object is synced only before the Fourier-filter constraint of the last
     iteration and at the end).  3 iterations with object constraints: every rank holds the same
@@ -282,23 +287,23 @@ def test_band_exchange_row_sharded_auto_equals_flat(tmp_path, world):
     to fp32 summation order (2e-6), as is the one-rank run."""
     from tests.dist_helpers import band_worker, row_sharded_problem
     outs = {}
-    for band in (None, False):
+    for band in ("auto", False):
         out = str(tmp_path / f"b{band}.npz")
         mp.start_processes(band_worker, args=(world, free_port(), out, band), nprocs=world, start_method="spawn")
         outs[band] = [np.load(out.replace(".npz", f"_r{r}.npz")) for r in range(world)]
     single, _ = run_recon(row_sharded_problem(world))
     for r in range(world):
-        assert bool(outs[None][r]["banded"]) and not bool(outs[False][r]["banded"])
+        assert bool(outs["auto"][r]["banded"]) and not bool(outs[False][r]["banded"])
         # halo traffic: a few window heights, far below the object's rows
-        assert 0 < int(outs[None][r]["sent_rows"]) + int(outs[None][r]["halo_rows"]) <= 4 * 32
+        assert 0 < int(outs["auto"][r]["sent_rows"]) + int(outs["auto"][r]["halo_rows"]) <= 4 * 32
         for k in ("obja", "objp", "probe", "shifts"):
-            assert np.array_equal(outs[None][r][k], outs[None][0][k]), f"band replicas diverged in {k}"
+            assert np.array_equal(outs["auto"][r][k], outs["auto"][0][k]), f"band replicas diverged in {k}"
             if world == 2:
-                assert np.array_equal(outs[None][r][k], outs[False][0][k]), f"band != all-reduce in {k}"
+                assert np.array_equal(outs["auto"][r][k], outs[False][0][k]), f"band != all-reduce in {k}"
             else:
-                np.testing.assert_allclose(outs[None][r][k], outs[False][0][k], rtol=0, atol=2e-6)
+                np.testing.assert_allclose(outs["auto"][r][k], outs[False][0][k], rtol=0, atol=2e-6)
     for k in ("obja", "objp", "probe", "shifts"):
-        np.testing.assert_allclose(outs[None][0][k], single[k], rtol=0, atol=2e-6)
+        np.testing.assert_allclose(outs["auto"][0][k], single[k], rtol=0, atol=2e-6)
 
 
 def test_band_edges_and_auto_rule():

@@ -181,3 +181,47 @@ def test_graphs_follow_hyperparameters_and_reuse_reshuffled_tables():
     # second has a new key; iterations 2 and 3 each capture once for their new betas / loss weight
     assert caps[0] >= 2, caps
     assert caps[1] == caps[0], caps      # reshuffled batches: same graphs
+
+
+def test_graphs_two_beta_groups_and_a_failed_step_keep_adam_state():
+    """ptyx_step_select advances the HIP Adam's step counts before the engine call and
+    the update; an eager step that raises in between (here the optimizer itself) must take them
+    back.  Param groups with different betas (several Adam launches a step), a step that raises
+    at iteration 3, then the iterations rerun: graphs vs eager, parameters AND optimizer state
+    (step counts, moments) bitwise equal."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    from ptyrad_amd.reconstruction import recon_step
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    out = []
+    for graphs in (False, True):
+        model, opt, loss_fn, batches, _ = gpu_recon(z, niter=0, ret_all=True)
+        opt.param_groups[0]["betas"] = (0.85, 0.995)           # two Adam batches a step
+        for it in (1, 2):
+            recon_step(batches, 1, model, opt, loss_fn, None, it, verbose=False, graphs=graphs)
+        plist = [p for g in opt.param_groups for p in g["params"]]
+        before = [opt.state[p]["step"].clone() for p in plist if p in opt.state]
+        opt.param_groups[-1]["eps"] = 1e-7                      # a new step key: the next step runs eagerly
+
+        def boom(*a, **k):
+            raise RuntimeError("injected optimizer failure")
+        opt.step = boom
+        with pytest.raises(RuntimeError, match="injected"):
+            recon_step(batches, 1, model, opt, loss_fn, None, 3, verbose=False, graphs=graphs)
+        del opt.step
+        after = [opt.state[p]["step"].clone() for p in plist if p in opt.state]
+        assert len(before) == len(after) > 0
+        for b, a in zip(before, after):
+            assert torch.equal(b, a), (b, a)                    # no step count moved without an update
+        for it in (3, 4):
+            recon_step(batches, 1, model, opt, loss_fn, None, it, verbose=False, graphs=graphs)
+        st = [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist if p in opt.state]
+        out.append((_params(model), st))
+        if graphs:
+            assert model._step_graphs.replays > 0
+    for k in out[0][0]:
+        assert np.array_equal(out[0][0][k], out[1][0][k]), k
+    for se, sg_ in zip(out[0][1], out[1][1]):
+        assert se.keys() == sg_.keys()
+        for k in se:
+            assert torch.equal(se[k], sg_[k]), k
