@@ -84,6 +84,9 @@ def parse():
                          "reference: recon_step at grad_accumulation = 1 (the reference's default cadence) on "
                          "the c2 scan, every mini-batch split over the ranks, graph-replayed steps with their "
                          "RCCL collectives captured; one bench step = one recon_step iteration")
+    ap.add_argument("--flat-exchange", action="store_true",
+                    help="--cadence reference: all-reduce the whole flat gradient in split steps instead of the "
+                         "slot exchange (DistContext(slot_exchange=False))")
     ap.add_argument("--rank-timeout", type=float, default=3000.0,
                     help="--gpus N > 1 without torchrun: seconds before the launcher stops a job that has not ended")
     ap.add_argument("--always-reduce", action="store_true",
@@ -109,50 +112,76 @@ def host_cores() -> int:
     return n
 
 
+def _alg_flops(cfg):
+    """SURVEY §8d F_alg per pattern: n_fft 5 N² log2 N², n_fft = 2 P O (2 Nz - 1) + 2 P (shifts on)."""
+    N, P, O, Nz = cfg["N"], cfg["P"], cfg["O"], cfg["Nz"]
+    return (2 * P * O * (2 * Nz - 1) + 2 * P) * 5 * N * N * math.log2(N * N)
+
+
 def _cpu_worker(args):
-    n, seed, nbatch, bsize = args
+    config, seed, nbatch, bsize = args
     from oracle import ptyx_oracle as orc
     from ptyrad_amd import synthetic as syn
-    pr = syn.random_problem(n, 16, 16, seed=seed)
+    cfg = CONFIGS[config]
+    N = cfg["N"]
+    pr = syn.random_problem(N, 16, 16, P=cfg["P"], O=cfg["O"], Nz=cfg["Nz"], seed=seed)
     lp = {"loss_single": {"state": True, "weight": 1.0, "dp_pow": 0.5},
           "loss_poissn": {"state": False}, "loss_pacbed": {"state": False},
           "loss_sparse": {"state": True, "weight": 0.1, "ln_order": 1}, "loss_simlar": {"state": False}}
     rng = np.random.default_rng(seed)
     batches = [rng.choice(256, bsize, replace=False) for _ in range(nbatch)]
     t = time.perf_counter()
-    orc.forward_loss_grad(pr.obja, pr.objp, pr.probe * np.float32(60.0), pr.shifts, pr.crop_pos, pr.H, pr.occu,
-                          pr.meas, batches, lp, cdt=np.complex64)
+    orc.forward_loss_grad(pr.obja, pr.objp, pr.probe * np.float32(60.0 if N == 128 else 30.0), pr.shifts,
+                          pr.crop_pos, pr.H, pr.occu, pr.meas, batches, lp, cdt=np.complex64)
     return nbatch * bsize, time.perf_counter() - t
 
 
-def cpu_baseline(n, bsize, sample):
-    """Oracle (NumPy port of the reference path) on the host cores, one process per core, before
-    any GPU call.  sample 0: about 20 s of work (≈ 110 patterns/s per core measured)."""
+def cpu_baseline(config, bsize, sample):
+    """Oracle (NumPy port of the reference path) at the config's own shape (N, P, O, Nz) on the
+    host cores, one process per core, before any GPU call.  sample 0: about 20 s of work (≈ 110
+    patterns/s per core at the c2 shape, scaled by the shape's FFT work, at least one mini-batch
+    per core)."""
     import multiprocessing as mp
+    cfg = CONFIGS[config]
     cores = host_cores()
     if not sample:
-        sample = 110 * 20 * cores
+        per_core_rate = 110.0 * _alg_flops(CONFIGS["c2"]) / _alg_flops(cfg)
+        sample = int(per_core_rate * 20 * cores)
     nb_total = max(cores, sample // bsize)
     per = [nb_total // cores + (1 if i < nb_total % cores else 0) for i in range(cores)]
-    jobs = [(n, 100 + i, per[i], bsize) for i in range(cores) if per[i] > 0]
+    jobs = [(config, 100 + i, per[i], bsize) for i in range(cores) if per[i] > 0]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(len(jobs)) as pool:
         res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
     pats = sum(r[0] for r in res)
     busy = max(r[1] for r in res)     # the workers' compute (they run concurrently), pool start excluded
+    shape = f"N={cfg['N']}, P={cfg['P']}, O={cfg['O']}, Nz={cfg['Nz']}"
     out = {"value": round(pats / busy, 1), "unit": "patterns/s", "cores": len(jobs), "kind": "port",
-           "sample": f"{pats} patterns of the c2 shape ({len(jobs)} processes x mini-batches of {bsize}), N={n}, "
-                     f"P=O=Nz=1, shifts on, oracle/ptyx_oracle.py complex64 NumPy; rate over the slowest worker's "
-                     f"compute time {busy:.1f}s (wall {wall:.1f}s incl. pool start: {pats / wall:.1f} patterns/s)"}
-    ratio = os.path.join(ROOT, "tests", "golden", "cpu_ratio.json")
-    if os.path.exists(ratio):   # reference CPU path vs this port, same cores, measured in the build container
-        r = json.load(open(ratio))
+           "shape": f"{config}: {shape}",
+           "sample": f"{pats} patterns of the {config} shape ({shape}, f32 DPs; {len(jobs)} processes x mini-batches "
+                     f"of {bsize}), shifts on, loss_single(q=0.5)+loss_sparse(L1), oracle/ptyx_oracle.py complex64 "
+                     f"NumPy; rate over the slowest worker's compute time {busy:.1f}s (wall {wall:.1f}s incl. pool "
+                     f"start: {pats / wall:.1f} patterns/s)"}
+    r = cpu_ratio(config)
+    if r:   # reference CPU path vs this port at the same shape, same cores, measured in the build container
         out["ratio_to_reference"] = r["ratio_reference_over_port"]
         out["reference_equivalent"] = round(out["value"] * r["ratio_reference_over_port"], 1)
         out["ratio_measured"] = f"{r['host']}: reference {r['reference_patterns_per_s']} / port " \
-                                f"{r['port_patterns_per_s']} patterns/s (tests/golden/measure_cpu_ratio.py)"
+                                f"{r['port_patterns_per_s']} patterns/s at the {config} shape " \
+                                f"(tests/golden/measure_cpu_ratio.py)"
     return out
+
+
+def cpu_ratio(key):
+    """tests/golden/cpu_ratio.json's entry for `key` (a config, or 'c2_refcad': recon_step with
+    Adam at grad_accumulation = 1), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "cpu_ratio.json")
+    if not os.path.exists(path):
+        return None
+    r = json.load(open(path))
+    e = r.get("configs", {}).get(key)
+    return {**e, "host": r["host"]} if e else None
 
 
 def cpu_adam_ms(shapes, reps=5):
@@ -192,6 +221,14 @@ def with_adam(cpu, shapes, bsize):
     out["sample"] = cpu["sample"] + (f"; plus one NumPy fp32 Adam step (torch single-tensor order) over the c2 "
                                      f"parameters {[list(s) for s in shapes]} per mini-batch of {bsize}, "
                                      f"{ms:.1f} ms on one core (grad_accumulation = 1, like for like)")
+    for k in ("ratio_to_reference", "reference_equivalent", "ratio_measured"):
+        out.pop(k, None)
+    r = cpu_ratio("c2_refcad")
+    if r:   # the reference's own recon_step WITH Adam at grad_accumulation = 1 vs this Adam-inclusive port
+        out["ratio_to_reference"] = r["ratio_reference_over_port"]
+        out["reference_equivalent"] = round(out["value"] * r["ratio_reference_over_port"], 1)
+        out["ratio_measured"] = f"{r['host']}: reference recon_step + Adam {r['reference_patterns_per_s']} / port + " \
+                                f"Adam {r['port_patterns_per_s']} patterns/s (tests/golden/measure_cpu_ratio.py)"
     return out
 
 
@@ -241,7 +278,8 @@ def reference_cadence(a, world, rank, local, cpu):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    ctx = DistContext(split_batches=True if a.always_reduce else None, always_reduce=a.always_reduce)
+    ctx = DistContext(split_batches=True if a.always_reduce else None, always_reduce=a.always_reduce,
+                      slot_exchange=not a.flat_exchange)
     N = 128
     crop_pos, shifts, (Ny, Nx), _, _ = syn.bench_geometry("c2", 1, 0, scan=a.scan)
     n = crop_pos.shape[0]
@@ -306,6 +344,17 @@ def reference_cadence(a, world, rank, local, cpu):
     sg = getattr(model, "_step_graphs", None)
     n_steps = len(batches)
     last = float(model.loss_iters[-1][1])
+    # bytes a rank sends per optimizer step in the gradient exchange of a W-rank job (ring
+    # collectives: an all-reduce sends 2(W-1)/W of its buffer, an all-gather (W-1) x the rank's
+    # share).  Slot exchange: ⌈B/W⌉ slots (N² complex64) + table rows all-gathered, the probe
+    # gradient and loss terms all-reduced; flat: the object, probe and position gradients all-reduced
+    W_x = a.geom_world or world
+    n_obj, n_pr, n_sh = 2 * Ny * Nx, 2 * N * N, 2 * n
+    cap_x = -(-a.batch // W_x)
+    ring = 2 * (W_x - 1) / W_x
+    slot_b = (W_x - 1) * cap_x * (2 * N * N + 8) * 4 + ring * (n_pr + 5) * 4
+    flat_b = ring * (n_obj + n_pr + n_sh + 5) * 4
+    use_slots = bool(ctx.slot_exchange) and (world > 1 or a.always_reduce or a.geom_world > 1)
     assert math.isfinite(last), "non-finite loss"
     out = {
         "metric": "diffraction-patterns/sec/iter (fwd+bwd), 256x256 probe positions, 128x128 DP",
@@ -318,9 +367,17 @@ def reference_cadence(a, world, rank, local, cpu):
                                "loss_single(q=0.5)+loss_sparse(L1), HIP Adam; one bench step = one iteration",
                    "cadence": "reference", "N": N, "P": 1, "O": 1, "Nz": 1, "mini_batch": a.batch,
                    "optimizer_steps_per_iteration": n_steps, "object": [Ny, Nx],
-                   "parallelism": f"dp{world} (split mini-batches; RCCL loss-sum + gradient all-reduce per "
-                                  f"optimizer step{', forced at world size 1' if a.always_reduce and world == 1 else ''})"},
+                   "parallelism": f"dp{world} (split mini-batches; per optimizer step an RCCL loss-sum all-reduce, then "
+                                  + ("the slot exchange: object-gradient slots all-gathered, probe gradient and "
+                                     "loss terms all-reduced" if use_slots else "the flat gradient all-reduce")
+                                  + f"{', forced at world size 1' if a.always_reduce and world == 1 else ''})"},
         "ms_per_optimizer_step": round(1e3 * elapsed / a.steps / n_steps, 4),
+        "exchange": {"mode": ("slots" if use_slots else "allreduce") if (world > 1 or a.always_reduce) else None,
+                     "world_for_bytes": W_x,
+                     "bytes_sent_per_rank_per_step": int(slot_b if use_slots else flat_b),
+                     "slot_exchange_bytes": int(slot_b), "flat_allreduce_bytes": int(flat_b),
+                     **({"geometry_only": f"bytes of a {W_x}-rank job; this run has {world} rank(s)"}
+                        if a.geom_world else {})},
         "graphs": {"captures": sg.captures, "replays": sg.replays, "eager": sg.eager} if sg else None,
         "loss_last_iteration": last,
         "roofline": None,
@@ -445,7 +502,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(128, a.batch, a.cpu_sample)          # before the GPU is touched
+        cpu = cpu_baseline("c2" if a.cadence == "reference" or a.config == "c2-strong" else a.config,
+                           a.batch, a.cpu_sample)                # before the GPU is touched
     if a.cadence == "reference":
         if a.config != "c2":
             raise SystemExit("--cadence reference runs the c2 geometry")

@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 207
+#define PTYX_ABI_VERSION 208
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -60,6 +60,11 @@ extern "C" {
  * every call on the plan must pass the same d_probe.  Engines without a deferred epilogue
  * ignore the bit. */
 #define PTYX_PREP_DEFER_PROBE 4
+/* PTYX_PREP_DEFER_GATHER (ptyx_forward_loss_grad_begin / _end only, ABI 208): the register engines
+ * (k_fused3 / k_fused3ms: ptyx_plan_slot_floats > 0) leave the object gradient untouched and keep
+ * the call's per-pattern object-gradient slots for ptyx_slots_export; the caller all-gathers them
+ * over the ranks and runs ptyx_obj_gather_slots.  Another engine: PTYX_EUNSUPPORTED. */
+#define PTYX_PREP_DEFER_GATHER 8
 /* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
  * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
  * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
@@ -190,6 +195,27 @@ int ptyx_forward_loss_grad_begin(ptyx_plan *plan, void *stream, const ptyx_input
                                  const ptyx_loss_cfg *cfg, float *dp_out, const ptyx_grads *grads,
                                  double *batch_sums);
 int ptyx_forward_loss_grad_end(ptyx_plan *plan, void *stream, const double *batch_sums, float *loss_terms);
+
+/* Slot exchange for mini-batches split over ranks (ABI 208; replaces the object part of the DDP
+ * gradient all-reduce, reconstruction.py:753, for a split step).  A _begin / _end call with
+ * PTYX_PREP_DEFER_GATHER keeps, per pattern, its unit-coefficient object-gradient slot
+ * (ptyx_plan_slot_floats floats, an internal row order that ptyx_obj_gather_slots reads back),
+ * window origin and mini-batch coefficients.
+ *   ptyx_slots_export: slots_out (n_pad x slot floats) gets the last such call's slots, meta_out
+ *     (n_pad x PTYX_SLOT_META floats) their table rows and, with d_shifts, each pattern's row of
+ *     the (n_scans, 2) position gradient; rows past the call's patterns are padding (no effect).
+ *     use_last 0: padding only (a rank with no part in the step).
+ *   ptyx_obj_gather_slots: the object gradient of ALL n rows (the ranks' exports, all-gathered
+ *     rank by rank) accumulated into d_obja / d_objp (deterministic, fixed order: identical on
+ *     every rank that passes the same buffers), and the position-gradient rows outside
+ *     [skip0, skip1) (the other ranks') added into d_shifts. */
+#define PTYX_SLOT_META 8
+int64_t ptyx_plan_slot_floats(const ptyx_plan *plan);   /* 0: the plan keeps no slots */
+int ptyx_slots_export(ptyx_plan *plan, void *stream, int32_t use_last, int32_t n_pad, float *slots_out,
+                      float *meta_out, const float *d_shifts);
+int ptyx_obj_gather_slots(ptyx_plan *plan, void *stream, const float *slots, const float *meta, int32_t n,
+                          const float *obja, const float *objp, float *d_obja, float *d_objp, int32_t sparse_n,
+                          float *d_shifts, int32_t skip0, int32_t skip1);
 
 /* Adjoint for an external loss: given dLdI (n_idx,N,N) = dL/d(dp_fwd) for the patterns idx,
  * accumulate the object / probe / position gradients (autograd of PtychoAD.forward). */

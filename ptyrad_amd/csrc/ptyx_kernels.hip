@@ -362,6 +362,13 @@ struct ptyx_plan {
   int32_t pend_nb = 0, pend_n = 0;
   float* pend_dp = nullptr;
   int pend_engine = -1;
+  bool pend_defer_gather = false;   // PTYX_PREP_DEFER_GATHER on the call in flight
+  // the last split call that deferred its object gather (ptyx_slots_export reads it): its slots,
+  // pattern table and coefficients stay in the plan until the next compute call
+  bool gather_deferred = false;     // set while that call's _end runs (run_fused3 skips the gather)
+  bool slots_ready = false;
+  int32_t slots_n = 0;
+  const int32_t* slots_idx = nullptr;
   // ptyx_profile_begin/end: HIP events around every launch (kind, start, stop)
   bool prof = false;
   struct ProfRec {
@@ -1134,7 +1141,10 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   // small calls: every tile scans the call's few patterns directly (no binning launches)
   const bool bins = a.n_idx > f3::kSmallCall;
-  if ((gz.d_obja || gz.d_objp) && bins) {
+  // PTYX_PREP_DEFER_GATHER: the slots, pattern table and coefficients stay for ptyx_slots_export
+  // and the caller's ptyx_obj_gather_slots over every rank's patterns (split mini-batches)
+  const bool gather_here = (gz.d_obja || gz.d_objp) && !pl->gather_deferred;
+  if (gather_here && bins) {
     // candidate bins of the gather: the patterns by object tile of their window origin
     ProfScope ps(pl, kKTable, st);
     const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
@@ -1146,7 +1156,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
-  if (gz.d_obja || gz.d_objp) {
+  if (gather_here) {
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
     g.boff = bins ? pl->boff : nullptr;
@@ -1698,6 +1708,7 @@ extern "C" int ptyx_forward(ptyx_plan* pl, void* stream, const ptyx_inputs* in, 
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
   if ((rc = busy(pl))) return rc;
+  pl->slots_ready = false;
   if (n_idx == 0) return PTYX_OK;
   if (!idx || !dp_out) return fail(PTYX_EINVAL, "idx / dp_out is null");
   DeviceGuard dg(pl->device);
@@ -1744,7 +1755,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  if ((cfg->prep & ~PTYX_PREP_DEFER_PROBE) > PTYX_PREP_REUSE || cfg->prep < 0) return fail(PTYX_EINVAL, "unknown cfg.prep");
+  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER)) > PTYX_PREP_REUSE || cfg->prep < 0)
+    return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
   a.boff = boff;
   a.n_batches = n_batches;
@@ -1901,8 +1913,11 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   if (grads) gz = *grads;
   KArgs a{};
   int engine = kEngTwoPass;
+  if (cfg && (cfg->prep & PTYX_PREP_DEFER_GATHER))
+    return fail(PTYX_EINVAL, "PTYX_PREP_DEFER_GATHER is for ptyx_forward_loss_grad_begin / _end");
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
+  pl->slots_ready = false;
   ptyx_loss_cfg c = *cfg;
   const bool defer = (c.prep & PTYX_PREP_DEFER_PROBE) != 0;
   c.prep &= ~PTYX_PREP_DEFER_PROBE;
@@ -1928,7 +1943,12 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;
-  c.prep &= ~PTYX_PREP_DEFER_PROBE;   // a split call is one piece: it closes its own probe gradient
+  const bool defer_gather = (c.prep & PTYX_PREP_DEFER_GATHER) != 0;
+  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER);   // a split call is one piece: it closes its own probe gradient
+  if (defer_gather && engine != kEngFused3)
+    return fail(PTYX_EUNSUPPORTED, "PTYX_PREP_DEFER_GATHER needs the k_fused3 / k_fused3ms engine "
+                                   "(ptyx_plan_slot_floats > 0, f32 DPs, the call within the register capacity)");
+  pl->slots_ready = false;
   resolve_prep(pl, in, engine, &c);
   if ((rc = run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), nullptr, kPhaseBegin,
                      batch_sums, false)))
@@ -1937,6 +1957,7 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   pl->pend_in = *in; pl->pend_gz = gz; pl->pend_cfg = c;
   pl->pend_idx = idx; pl->pend_boff = boff; pl->pend_nb = n_batches; pl->pend_n = n_idx;
   pl->pend_dp = dp_out; pl->pend_engine = engine;
+  pl->pend_defer_gather = defer_gather;
   return PTYX_OK;
 }
 
@@ -1953,8 +1974,143 @@ extern "C" int ptyx_forward_loss_grad_end(ptyx_plan* pl, void* stream, const dou
   if (rc) return rc;
   if (engine != pl->pend_engine) return fail(PTYX_EINVAL, "internal: engine changed between _begin and _end");
   DeviceGuard dg(pl->device);
-  return run_call(pl, &pl->pend_in, a, &pl->pend_cfg, pl->pend_gz, engine, reinterpret_cast<hipStream_t>(stream),
-                  loss_terms, kPhaseEnd, const_cast<double*>(batch_sums), false);
+  pl->gather_deferred = pl->pend_defer_gather;
+  rc = run_call(pl, &pl->pend_in, a, &pl->pend_cfg, pl->pend_gz, engine, reinterpret_cast<hipStream_t>(stream),
+                loss_terms, kPhaseEnd, const_cast<double*>(batch_sums), false);
+  pl->gather_deferred = false;
+  if (rc == PTYX_OK && pl->pend_defer_gather) {
+    pl->slots_ready = true;
+    pl->slots_n = pl->pend_n;
+    pl->slots_idx = pl->pend_idx;
+  }
+  return rc;
+}
+
+// ---------------------------------------------------------------- slot exchange (split mini-batches)
+constexpr int kSlotMeta = PTYX_SLOT_META;
+// A split call with PTYX_PREP_DEFER_GATHER leaves its patterns' unit-coefficient object-gradient
+// slots (g_O = conj(ψ⁰)·g, ptyx_gather.hpp), their window origins and mini-batch coefficients in
+// the plan.  ptyx_slots_export copies them into caller buffers padded to a common count, the
+// caller all-gathers those over the ranks, and ptyx_obj_gather_slots runs the deterministic
+// gather over EVERY rank's patterns: each rank forms the whole object gradient itself, bitwise
+// the same on every rank, with no object all-reduce.
+extern "C" int64_t ptyx_plan_slot_floats(const ptyx_plan* pl) {
+  if (!pl || pl->nwg3 <= 0 || pl->og_cap <= 0 || (pl->d.flags & PTYX_MEAS_F16) || pl->d.N != 128 ||
+      pl->d.P * pl->d.O != 1)
+    return 0;
+  return (int64_t)2 * pl->d.Nz * pl->d.N * pl->d.N;
+}
+
+// meta row per pattern (8 floats): geo (2 × int bits), pcoef (2), scan index (int bits), the
+// pattern's position-gradient row (2), 0; padding rows: geo far outside the object (no tile hits
+// it), pcoef 0, index -1
+__global__ void k_slots_meta(const int2* geo, const float2* pcoef, const int32_t* idx, int n, int n_pad,
+                             const float* d_shifts, float* meta) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_pad) return;
+  float* m = meta + (size_t)j * kSlotMeta;
+  if (j < n) {
+    const int2 o = geo[j];
+    const float2 c = pcoef[j];
+    const int s = idx[j];
+    m[0] = __int_as_float(o.x); m[1] = __int_as_float(o.y);
+    m[2] = c.x; m[3] = c.y;
+    m[4] = __int_as_float(s);
+    m[5] = d_shifts ? d_shifts[2 * (size_t)s] : 0.f;
+    m[6] = d_shifts ? d_shifts[2 * (size_t)s + 1] : 0.f;
+  } else {
+    m[0] = __int_as_float(-(1 << 29)); m[1] = __int_as_float(-(1 << 29));
+    m[2] = 0.f; m[3] = 0.f;
+    m[4] = __int_as_float(-1);
+    m[5] = 0.f; m[6] = 0.f;
+  }
+  m[7] = 0.f;
+}
+
+// geo / pcoef columns of the all-gathered meta rows, for GatherArgs
+__global__ void k_slots_unpack(const float* meta, int n, int2* geo, float2* pcoef) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const float* m = meta + (size_t)j * kSlotMeta;
+  geo[j] = make_int2(__float_as_int(m[0]), __float_as_int(m[1]));
+  pcoef[j] = make_float2(m[2], m[3]);
+}
+
+// the other ranks' position-gradient rows added to this rank's dense d_shifts (every scan index
+// occurs once in a call, so no two threads touch one row; this rank's own rows are skipped)
+__global__ void k_slots_rows_add(const float* meta, int n, int skip0, int skip1, float* d_shifts) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || (j >= skip0 && j < skip1)) return;
+  const float* m = meta + (size_t)j * kSlotMeta;
+  const int s = __float_as_int(m[4]);
+  if (s < 0) return;
+  d_shifts[2 * (size_t)s] += m[5];
+  d_shifts[2 * (size_t)s + 1] += m[6];
+}
+
+extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, int32_t n_pad, float* slots_out,
+                                 float* meta_out, const float* d_shifts) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
+  const int64_t sf = ptyx_plan_slot_floats(pl);
+  if (sf <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no object-gradient slots");
+  if (use_last && !pl->slots_ready) return fail(PTYX_EINVAL, "no split call with PTYX_PREP_DEFER_GATHER to export");
+  const int n = use_last ? pl->slots_n : 0;
+  if (n_pad < n || n_pad < 1) return fail(PTYX_EINVAL, "n_pad must be >= 1 and cover the call's patterns");
+  if (!meta_out || (n > 0 && !slots_out)) return fail(PTYX_EINVAL, "null output buffer");
+  DeviceGuard dg(pl->device);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n > 0) {
+    hipError_t e = hipMemcpyAsync(slots_out, pl->ogscr, (size_t)n * sf * sizeof(float), hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(slots)");
+  }
+  hipLaunchKernelGGL(k_slots_meta, dim3((n_pad + 255) / 256), dim3(256), 0, st, pl->geo, pl->pcoef,
+                     use_last ? pl->slots_idx : nullptr, n, n_pad, d_shifts, meta_out);
+  return launch_status("k_slots_meta launch");
+}
+
+extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* slots, const float* meta, int32_t n,
+                                     const float* obja, const float* objp, float* d_obja, float* d_objp,
+                                     int32_t sparse_n, float* d_shifts, int32_t skip0, int32_t skip1) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
+  if (ptyx_plan_slot_floats(pl) <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no object-gradient slots");
+  if (n < 1 || n > pl->d.max_patterns) return fail(PTYX_EINVAL, "n must be in [1, max_patterns]");
+  if (!slots || !meta || !obja || !objp) return fail(PTYX_EINVAL, "null input");
+  if (skip0 < 0 || skip1 < skip0 || skip1 > n) return fail(PTYX_EINVAL, "skip range outside [0, n]");
+  const int sn = sparse_n < 1 ? 1 : sparse_n;
+  DeviceGuard dg(pl->device);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the unpacked table reuses the plan's per-call geo / pcoef arrays (capacity max_patterns)
+  hipLaunchKernelGGL(k_slots_unpack, dim3((n + 255) / 256), dim3(256), 0, st, meta, n, pl->geo, pl->pcoef);
+  int rc = launch_status("k_slots_unpack launch");
+  if (rc) return rc;
+  pl->slots_ready = false;
+  pl->prep.valid = false;
+  if (d_obja || d_objp) {
+#if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
+    constexpr int N = 128;
+    GatherArgs g{};
+    g.ogscr = reinterpret_cast<const float2*>(slots); g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = n;
+    g.boff = nullptr; g.blist = nullptr; g.bbox = nullptr;
+    g.Ny = pl->d.Ny; g.Nx = pl->d.Nx; g.tiles_x = (pl->d.Nx + kGTX - 1) / kGTX; g.sparse_n = sn;
+    g.obja = obja; g.objp = objp; g.d_obja = d_obja; g.d_objp = d_objp;
+    const int tiles = g.tiles_x * ((pl->d.Ny + kGTY - 1) / kGTY);
+    const bool sparse_tiles = (long long)n * BinReach<N>::n < 64LL * tiles;
+    g.nz = pl->d.Nz;
+    g.zgrid = 1;
+    ProfScope ps(pl, kKGather, st);
+    launch_gather<N, true, false>(pl, g, tiles, pl->d.Nz, sparse_tiles, st);
+    if ((rc = launch_status("k_obj_gather (slots) launch"))) return rc;
+#endif
+  }
+  if (d_shifts) {
+    hipLaunchKernelGGL(k_slots_rows_add, dim3((n + 255) / 256), dim3(256), 0, st, meta, n, skip0, skip1, d_shifts);
+    if ((rc = launch_status("k_slots_rows_add launch"))) return rc;
+  }
+  return PTYX_OK;
 }
 
 extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
@@ -1966,6 +2122,7 @@ extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs*
   if (rc) return rc;
   if (n_idx < 0 || n_idx > pl->d.max_patterns) return fail(PTYX_EINVAL, "n_idx out of range [0, max_patterns]");
   if ((rc = busy(pl))) return rc;
+  pl->slots_ready = false;
   if (n_idx == 0 || !grads) return PTYX_OK;
   if (!idx || !dLdI) return fail(PTYX_EINVAL, "idx / dLdI is null");
   pl->prep.valid = false;   // F(P) is rewritten

@@ -221,7 +221,7 @@ class Plan:
 
     def forward_loss_grad(self, t: dict, idx, batch_offsets, loss_cfg: LossConfig, grads: dict,
                           grad_scale: float = 1.0, loss_terms=None, dp_out=None, max_batch=None, prep=0,
-                          batch_sums_reduce=None, _rows_checked=False):
+                          batch_sums_reduce=None, slot_exchange=None, _rows_checked=False):
         """ptyx_forward_loss_grad over consecutive mini-batches; returns loss_terms (n_batches, 5).
 
         batch_offsets on the host (numpy / list / CPU tensor) let calls larger than the plan's
@@ -233,11 +233,18 @@ class Plan:
         device tensor of the parts' additive loss sums and must sum it over the ranks in place
         (one all-reduce); the loss terms and gradient coefficients then belong to the whole
         mini-batches.  Such a call is never split, so it must fit the plan's capacity.
+
+        slot_exchange (with batch_sums_reduce; plans with ``slot_floats`` > 0): the call leaves the
+        object gradient to ``slot_exchange(plan, t, grads, loss_cfg)``, which exports this rank's
+        per-pattern slots, all-gathers them and runs ``gather_slots`` over every rank's patterns
+        (reconstruction.SlotExchange).
         """
         self._prev_errors()   # (_rows_checked: kept for callers; the device checks every call)
         if batch_sums_reduce is not None:
             return self._split_call(t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out,
-                                    batch_sums_reduce)
+                                    batch_sums_reduce, slot_exchange)
+        if slot_exchange is not None:
+            raise ValueError("slot_exchange is for split-batch calls (batch_sums_reduce)")
         host_off = not (isinstance(batch_offsets, torch.Tensor) and batch_offsets.device.type != "cpu")
         if max_batch is None:
             if not host_off:
@@ -327,8 +334,10 @@ class Plan:
                                    _rows_checked=True)
         return loss_terms
 
-    def _split_call(self, t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out, reduce):
-        """ptyx_forward_loss_grad_begin → reduce(batch sums) → ptyx_forward_loss_grad_end."""
+    def _split_call(self, t, idx, batch_offsets, loss_cfg, grads, grad_scale, loss_terms, dp_out, reduce,
+                    slot_exchange=None):
+        """ptyx_forward_loss_grad_begin → reduce(batch sums) → ptyx_forward_loss_grad_end
+        (→ slot_exchange: the object gradient over every rank's patterns)."""
         idx_t = self._idx(idx)
         off_t = self._idx(batch_offsets)
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
@@ -341,7 +350,8 @@ class Plan:
         inp, _keep = self._inputs(t["obja"], t["objp"], t["probe"], t["shifts"], t.get("H"), t["occu"],
                                   t["crop_pos"], t["meas"], t.get("tilts"), t.get("kvec"), t.get("dz", 0.0),
                                   t.get("meas_rows"))
-        cfg = loss_cfg.to_c(grad_scale, 0, _lib.PTYX_PREP_CALL)
+        cfg = loss_cfg.to_c(grad_scale, 0, _lib.PTYX_PREP_CALL |
+                            (_lib.PTYX_PREP_DEFER_GATHER if slot_exchange is not None else 0))
         g = self._grads(grads)
         _lib.check(self.lib.ptyx_forward_loss_grad_begin(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
                                                          _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(dp_out),
@@ -350,7 +360,46 @@ class Plan:
             reduce(sums)
         finally:   # always close the call (the plan refuses other work while one is open)
             _lib.check(self.lib.ptyx_forward_loss_grad_end(self._h, self._stream(), _ptr(sums), _ptr(loss_terms)))
+        if slot_exchange is not None:
+            slot_exchange(self, t, grads, loss_cfg)
         return loss_terms
+
+    # ------------------------------------------------------------------ slot exchange (ABI 208)
+    @property
+    def slot_floats(self) -> int:
+        """Floats per pattern of the object-gradient slots this plan's split calls can export
+        (ptyx_plan_slot_floats; 0: no slot exchange for this geometry)."""
+        return int(self.lib.ptyx_plan_slot_floats(self._h))
+
+    def export_slots(self, n_pad: int, slots_out, meta_out, d_shifts=None, use_last=True):
+        """ptyx_slots_export: the last deferred split call's slots into slots_out (n_pad, slot_floats)
+        and table rows into meta_out (n_pad, PTYX_SLOT_META); use_last False: padding rows only."""
+        sf = self.slot_floats
+        if tuple(slots_out.shape) != (n_pad, sf) or tuple(meta_out.shape) != (n_pad, _lib.PTYX_SLOT_META):
+            raise ValueError("export buffers must be (n_pad, slot_floats) and (n_pad, PTYX_SLOT_META)")
+        for name, x in (("slots_out", slots_out), ("meta_out", meta_out)):
+            _need(x, torch.float32, name, self.device)
+        if d_shifts is not None:
+            _need(d_shifts, torch.float32, "d_shifts", self.device)
+        _lib.check(self.lib.ptyx_slots_export(self._h, self._stream(), int(bool(use_last)), int(n_pad), _ptr(slots_out),
+                                              _ptr(meta_out), _ptr(d_shifts)))
+
+    def gather_slots(self, slots, meta, t: dict, grads: dict, sparse_n: int, skip=(0, 0)):
+        """ptyx_obj_gather_slots: object gradient of every row of the all-gathered (n, slot_floats)
+        slots / (n, PTYX_SLOT_META) table into grads['obja'] / ['objp'], and the rows outside
+        ``skip`` (the other ranks') of the position gradient into grads['shifts']."""
+        n = int(slots.shape[0])
+        for name, x in (("slots", slots), ("meta", meta)):
+            _need(x, torch.float32, name, self.device)
+        if tuple(slots.shape) != (n, self.slot_floats) or tuple(meta.shape) != (n, _lib.PTYX_SLOT_META):
+            raise ValueError("gather buffers must be (n, slot_floats) and (n, PTYX_SLOT_META)")
+        g = {k: grads.get(k) for k in ("obja", "objp", "shifts")}
+        for k, v in g.items():
+            if v is not None:
+                _need(v, torch.float32, f"grad {k}", self.device)
+        _lib.check(self.lib.ptyx_obj_gather_slots(self._h, self._stream(), _ptr(slots), _ptr(meta), n,
+                                                  _ptr(t["obja"]), _ptr(t["objp"]), _ptr(g["obja"]), _ptr(g["objp"]),
+                                                  int(sparse_n), _ptr(g["shifts"]), int(skip[0]), int(skip[1])))
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):
         """ptyx_adjoint_dldi: accumulate gradients for an external dL/d(dp)."""

@@ -278,7 +278,7 @@ class CombinedLoss(torch.nn.Module):
         return not (self.loss_params.get("loss_simlar", {}).get("state", False) or
                     model_stages(model_params, init_variables))
 
-    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None):
+    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None, slot_exchange=None):
         """The hot path without autograd: gradients of (Σ_m loss_m)·grad_scale are ACCUMULATED
         straight into the ``.grad`` tensors of the optimisable parameters the loss reaches
         (created, zeroed, when missing) — the engine writes them in place, no temporaries.
@@ -291,7 +291,12 @@ class CombinedLoss(torch.nn.Module):
         ``batch_sums_reduce(t)`` sums a float64 device tensor over the ranks in place.  The engine
         normalises every loss by its WHOLE mini-batch (ptyx_forward_loss_grad_begin / _end), so the
         ranks' gradients sum to the single-device gradient.  Rows of parts this rank does not hold
-        are zero in the returned terms."""
+        are zero in the returned terms.
+
+        slot_exchange (with batch_sums_reduce; reconstruction.SlotExchange): the object gradient of
+        the split mini-batches is formed on every rank from every rank's per-pattern slots
+        (all-gathered), and the position-gradient rows are exchanged likewise, instead of being
+        left for an all-reduce of the whole object."""
         names = model.engine_grad_names()
         for k in names:
             p = model.optimizable_tensors[k]
@@ -302,7 +307,9 @@ class CombinedLoss(torch.nn.Module):
             if not self.supports_batch_split(model):
                 raise NotImplementedError("mini-batches split over ranks need additive loss terms "
                                           "(no loss_pacbed / loss_simlar / blur / on-the-fly stages)")
-            return self._split_into(model, batches, grad_scale, batch_sums_reduce)
+            return self._split_into(model, batches, grad_scale, batch_sums_reduce, slot_exchange)
+        if slot_exchange is not None:
+            raise ValueError("slot_exchange needs split mini-batches (batch_sums_reduce)")
         if special and self._simlar_on() and not getattr(model, "detector_blur", False) and not self.simlar_per_batch:
             # the data terms as without loss_simlar (one engine call), loss_simlar beside it
             terms = self._data_loss().fused_into(model, batches, grad_scale)
@@ -344,7 +351,17 @@ class CombinedLoss(torch.nn.Module):
             torch.autograd.backward(H_rv, grads["H"])
         return terms
 
-    def _split_into(self, model, parts, grad_scale, reduce):
+    def slot_exchange_ok(self, model):
+        """Whether a split step of this loss on this model can exchange per-pattern object-gradient
+        slots (reconstruction.SlotExchange): the register engines keep them (ptyx_plan_slot_floats)
+        and the call is the plain fused one (no autograd stage, no optimised propagator, no
+        per-position tilts)."""
+        plan = getattr(model, "plan", None)
+        return (plan is not None and plan.slot_floats > 0 and not self._special(model) and
+                not getattr(model, "prop_opt", False) and model._dz_t() is None and model._tilts() is None and
+                self.supports_batch_split(model))
+
+    def _split_into(self, model, parts, grad_scale, reduce, slot_exchange=None):
         """fused_into for this rank's parts of mini-batches split over ranks."""
         from .engine import LossConfig as _LC
         dev = model.opt_obja.device
@@ -352,8 +369,22 @@ class CombinedLoss(torch.nn.Module):
         parts = [np.asarray(b).reshape(-1) for b in parts]
         held = [m for m, b in enumerate(parts) if b.size]
         terms = torch.zeros((G, 5), dtype=torch.float32, device=dev)
-        if not held:   # nothing here: still join the reduction of the group's sums
+        H_rv = model._H_rv()
+        if model._tilts() is not None:
+            raise NotImplementedError("split mini-batches with per-position tilts are not supported")
+        t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
+             "shifts": model.opt_probe_pos_shifts.detach(), "H": H_rv.detach(), "tilts": None}
+        t.update(model._base())
+        live = lambda p: p is not None and p.requires_grad and p.grad is not None  # noqa: E731
+        grads = {k: p.grad for k, p in (("obja", model.opt_obja), ("objp", model.opt_objp),
+                                         ("probe", model.opt_probe)) if live(p)}
+        if model.shift_probes and live(model.opt_probe_pos_shifts):
+            grads["shifts"] = model.opt_probe_pos_shifts.grad
+        cfg = _LC.from_loss_params(self.loss_params)
+        if not held:   # nothing here: still join the reduction of the group's sums (and the slot exchange)
             reduce(torch.zeros((G, _lib.PTYX_BATCH_SUMS), dtype=torch.float64, device=dev))
+            if slot_exchange is not None:
+                slot_exchange(model.plan, t, grads, cfg, used=False)
             return terms
         local = [parts[m] for m in held]
         flat = np.concatenate(local)
@@ -368,22 +399,11 @@ class CombinedLoss(torch.nn.Module):
             sums.copy_(full.index_select(0, sel))
 
         idx_t = torch.as_tensor(flat, dtype=torch.int32).to(dev, non_blocking=True)
-        H_rv = model._H_rv()
-        if model._tilts() is not None:
-            raise NotImplementedError("split mini-batches with per-position tilts are not supported")
-        t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
-             "shifts": model.opt_probe_pos_shifts.detach(), "H": H_rv.detach(), "tilts": None}
-        t.update(model._base())
-        live = lambda p: p is not None and p.requires_grad and p.grad is not None  # noqa: E731
-        grads = {k: p.grad for k, p in (("obja", model.opt_obja), ("objp", model.opt_objp),
-                                         ("probe", model.opt_probe)) if live(p)}
-        if model.shift_probes and live(model.opt_probe_pos_shifts):
-            grads["shifts"] = model.opt_probe_pos_shifts.grad
         if H_rv.requires_grad:          # optimised dz / tilts: this rank's share of dL/dH, then autograd
             grads["H"] = torch.zeros_like(H_rv)
-        local_terms = model.plan.forward_loss_grad(t, idx_t, batch_offsets(local), _LC.from_loss_params(self.loss_params),
+        local_terms = model.plan.forward_loss_grad(t, idx_t, batch_offsets(local), cfg,
                                                    grads, grad_scale=float(grad_scale), batch_sums_reduce=group_reduce,
-                                                   _rows_checked=True)   # _check_held above
+                                                   slot_exchange=slot_exchange, _rows_checked=True)   # _check_held above
         if "H" in grads:
             torch.autograd.backward(H_rv, grads["H"])
         terms.index_copy_(0, sel, local_terms)

@@ -141,7 +141,8 @@ def loss_logger(batch_losses, niter, iter_t, verbose=True):
 class DistContext:
     """Rank/world of a torch.distributed job (backend 'nccl' = RCCL on ROCm, or 'gloo' on CPU)."""
 
-    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=False):
+    def __init__(self, group=None, split_batches=None, always_reduce=False, band_exchange=False,
+                 slot_exchange=True):
         """split_batches: None = split a group's mini-batches over the ranks only when the group has
         fewer mini-batches than ranks; True = always (accelerate's split_batches=True,
         utils/common.py:63); False = never (whole mini-batches round-robin).
@@ -155,7 +156,14 @@ class DistContext:
         caller's optimizer holds: the object moments live in the band optimizer
         (``ObjectBands.opt``), so ``optimizer.state_dict()`` lacks them (a resumed run restarts
         them), and its steps are not graph-replayed.  With the band exchange, call
-        ``sync_object(model)`` on every rank before reading the object outside recon_step."""
+        ``sync_object(model)`` on every rank before reading the object outside recon_step.
+        slot_exchange: in a SPLIT optimizer step (every mini-batch split over the ranks), the
+        object gradient is formed on every rank from all ranks' per-pattern object-gradient slots
+        (one all-gather of 32/W slots a rank at the default cadence, then the deterministic gather
+        over all of them: bitwise the same on every rank) and the step's position-gradient rows are
+        exchanged with them, so only the probe gradient and the loss terms are all-reduced — instead
+        of an all-reduce of the whole object (SlotExchange).  Used when the engine keeps slots
+        (CombinedLoss.slot_exchange_ok); False: the flat all-reduce."""
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -166,6 +174,8 @@ class DistContext:
         if band_exchange != "auto":
             band_exchange = bool(band_exchange)
         self.band_exchange = band_exchange
+        self.slot_exchange = bool(slot_exchange)
+        self._slot_bufs = {}
         self.bands = None
         self.block_split = None   # the split decision local_indices built a measurement block for
 
@@ -314,6 +324,36 @@ class DistContext:
         if self._collective() and flat is not None and flat.numel():
             dist.all_reduce(flat, group=self.group)
 
+    def all_gather_into(self, out, inp):
+        """out (W·k, ...) = every rank's inp (k, ...), rank by rank (one all-gather)."""
+        if not self._collective():
+            out.copy_(inp)
+        elif dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(self.world)), inp, group=self.group)
+
+    def slot_cap(self, group):
+        """Patterns per rank of a split engine call over ``group``'s mini-batches, padded to the
+        largest rank's share (rank 0's: Σ ⌈|b| / W⌉), the same on every rank."""
+        return sum(-(-len(np.asarray(b).reshape(-1)) // self.world) for b in group)
+
+    def slot_buffers(self, device, cap, sf):
+        """Persistent (send slots, send table, received slots, received table) buffers of the slot
+        exchange (a captured step holds their addresses)."""
+        key = (str(device), int(cap), int(sf))
+        b = self._slot_bufs.get(key)
+        if b is None:
+            from . import _lib
+            M = _lib.PTYX_SLOT_META
+            b = (torch.zeros((cap, sf), dtype=torch.float32, device=device),
+                 torch.zeros((cap, M), dtype=torch.float32, device=device),
+                 torch.zeros((self.world * cap, sf), dtype=torch.float32, device=device),
+                 torch.zeros((self.world * cap, M), dtype=torch.float32, device=device))
+            self._slot_bufs[key] = b
+        return b
+
+
     @staticmethod
     def terms_tail(flat, extra, G):
         """The (G, 5) loss-term rows at the start of the ``extra`` floats grad_views appended."""
@@ -329,6 +369,45 @@ class DistContext:
             else:
                 tail[torch.as_tensor(idx_local, device=tail.device)] = terms_local.to(tail.device)
 
+
+class SlotExchange:
+    """The object-gradient exchange of one split engine call (DistContext.slot_exchange; replaces
+    the object part of DDP's gradient all-reduce, reconstruction.py:753, at the default cadence).
+
+    Every rank runs its parts of the step's mini-batches with the object gather deferred
+    (ptyx_forward_loss_grad_begin / _end with PTYX_PREP_DEFER_GATHER), exports its patterns'
+    unit-coefficient object-gradient slots and table rows (window origin, mini-batch coefficients,
+    scan index and position-gradient row) padded to ``cap`` rows, all-gathers them (two
+    all-gathers: slots and rows), and runs the deterministic slot gather over all W·cap rows: the
+    object gradient of the whole step, identical on every rank, and the other ranks'
+    position-gradient rows added to its own.  Bytes a rank sends: its cap slots (128 KiB each at
+    N = 128) and rows, against 2·(W−1)/W of the object and position gradients for the all-reduce."""
+
+    def __init__(self, ctx, cap):
+        self.ctx, self.cap = ctx, int(cap)
+
+    def __call__(self, plan, t, grads, cfg, used=True):
+        ctx, cap = self.ctx, self.cap
+        sf = plan.slot_floats
+        send_s, send_m, recv_s, recv_m = ctx.slot_buffers(plan.device, cap, sf)
+        plan.export_slots(cap, send_s, send_m, grads.get("shifts"), use_last=used)
+        ctx.all_gather_into(recv_s, send_s)
+        ctx.all_gather_into(recv_m, send_m)
+        plan.gather_slots(recv_s, recv_m, t, grads, cfg.sparse_n if cfg.sparse_on else 1,
+                          skip=(ctx.rank * cap, (ctx.rank + 1) * cap))
+
+    def dense(self, tensors):
+        """The same exchange for a loss without slots (the CPU test doubles): each tensor holds
+        this rank's contribution and becomes, on every rank, the sum of all ranks' contributions
+        in rank order (one all-gather each)."""
+        W = self.ctx.world
+        for x in tensors:
+            buf = torch.empty((W,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+            self.ctx.all_gather_into(buf.view((W * x.shape[0],) + tuple(x.shape[1:])) if x.dim() else buf, x)
+            acc = buf[0].clone()
+            for r in range(1, W):
+                acc = acc + buf[r]
+            x.copy_(acc)
 
 class ObjectBands:
     """Row-band ownership of the object for the band-sized gradient exchange (the
@@ -603,6 +682,23 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             if ctx.bands.stale:
                 ctx.bands.halo(obj_all)      # rows this iteration reads, current from their owners
             live = objs + [p for p in live if not any(p is q for q in objs)]   # objects first in the flat buffer
+    # slot exchange (split steps): the object gradient from every rank's per-pattern slots, the
+    # position-gradient rows with them; only the rest of the flat buffer is all-reduced
+    slots = False
+    if ctx.slot_exchange and ctx._collective() and split_ok and not band and objs and \
+            getattr(loss_fn, "slot_exchange_ok", None) is not None and loss_fn.slot_exchange_ok(model):
+        plan_ = getattr(model, "plan", None)
+        cap_ = plan_.call_capacity if plan_ is not None else None
+        maxp = int(plan_.dims.max_patterns) if plan_ is not None else None
+        sgroups = [batches[g0:g0 + ga] for g0 in range(0, len(batches), ga) if ctx.splits(batches[g0:g0 + ga])]
+        slots = bool(sgroups) and (maxp is None or all(
+            ctx.world * ctx.slot_cap(g[a:b]) <= maxp for g in sgroups for a, b in ctx.split_ranges(g, cap_)))
+    ar_skip = 0
+    if slots:
+        sp_ = model.opt_probe_pos_shifts
+        sh = [p for p in live if p is sp_]
+        live = objs + sh + [p for p in live if not any(p is q for q in objs) and p is not sp_]
+        ar_skip = sum(p.numel() for p in objs + sh)
     rows = []
     use_graphs = False
     if graphs is not False and not band:
@@ -618,7 +714,8 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         # refuse on every rank instead of hanging in RCCL), and take the same graph decision
         # (else every rank runs the eager steps)
         cap = model.plan.call_capacity if hasattr(model, "plan") else None
-        plan_fp = ctx.step_plan(batches, ga, split_ok, band, sum(p.numel() for p in live) + extra, cap)
+        plan_fp = ctx.step_plan(batches, ga, split_ok, band, sum(p.numel() for p in live) + extra, cap) + \
+            (("slots", bool(slots), int(ar_skip)),)
         same_plan, same_mode = ctx.agree(plan_fp, ("graphs", bool(use_graphs)), device=dev)
         if not same_plan:
             raise RuntimeError(f"recon_step iteration {niter} (rank {ctx.rank}): the ranks disagree on the "
@@ -636,7 +733,8 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         if sg is None:
             sg = model._step_graphs = StepGraphs()
         flat = ctx.grad_views(live, extra, dev)
-        rows.append(sg.run(model, optimizer, loss_fn, batches, ga, live, flat, ctx=ctx, extra=extra))
+        rows.append(sg.run(model, optimizer, loss_fn, batches, ga, live, flat, ctx=ctx, extra=extra,
+                           slots=slots, ar_skip=ar_skip))
         optimizer.zero_grad(set_to_none=True)
         model.clear_cache()
     for g0 in (range(0, len(batches), ga) if not use_graphs else ()):
@@ -648,7 +746,9 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             # every mini-batch is non-empty: its terms are the group's.
             cap = model.plan.call_capacity if hasattr(model, "plan") else None
             terms = torch.cat([loss_fn.fused_into(model, [ctx.my_part(b) for b in group[a:b]], grad_scale=1.0 / ga,
-                                                  batch_sums_reduce=ctx.allreduce_sums)
+                                                  batch_sums_reduce=ctx.allreduce_sums,
+                                                  **({"slot_exchange": SlotExchange(ctx, ctx.slot_cap(group[a:b]))}
+                                                     if slots else {}))
                                for a, b in ctx.split_ranges(group, cap)])
             mine = list(range(len(group))) if ctx.rank == 0 else []
             if ctx.rank:
@@ -680,7 +780,8 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
             ctx.bands.step(optimizer, objs, obj_all)
             ctx.bands.halo(objs)                       # updated rows back to the ranks that read them
         else:
-            ctx.allreduce(flat)
+            # (a split step's object and position gradients came with the slot exchange)
+            ctx.allreduce(flat[ar_skip:] if slots and ctx.splits(group) else flat)
             optimizer.step()
         optimizer.zero_grad(set_to_none=True)
         # the loss terms stay on the device until the iteration ends (no host sync per step)

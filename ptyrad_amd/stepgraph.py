@@ -90,18 +90,19 @@ def ineligible_reason(model, optimizer, loss_fn, ctx, batches, grad_accumulation
 
 def _local_steps(ctx, batches, ga):
     """Per optimizer step of the iteration: (this rank's mini-batch pieces, the group size, whether
-    the group is split, the group rows this rank's terms fill).  One rank: the whole groups."""
+    the group is split, the group rows this rank's terms fill, the slot-exchange rows per rank of a
+    split group).  One rank: the whole groups."""
     out = []
     for g0 in range(0, len(batches), ga):
         group = batches[g0:g0 + ga]
         if ctx is None or not ctx._collective():
-            out.append(([np.asarray(b).reshape(-1) for b in group], len(group), False, tuple(range(len(group)))))
+            out.append(([np.asarray(b).reshape(-1) for b in group], len(group), False, tuple(range(len(group))), 0))
         elif ctx.splits(group):
             out.append(([ctx.my_part(b) for b in group], len(group), True,
-                        tuple(range(len(group))) if ctx.rank == 0 else ()))
+                        tuple(range(len(group))) if ctx.rank == 0 else (), ctx.slot_cap(group)))
         else:
             mine = ctx.my_batches(group)
-            out.append(([np.asarray(group[i]).reshape(-1) for i in mine], len(group), False, tuple(mine)))
+            out.append(([np.asarray(group[i]).reshape(-1) for i in mine], len(group), False, tuple(mine), 0))
     return out
 
 
@@ -169,7 +170,7 @@ class StepGraphs:
 
     # ---------------------------------------------------------------- one step
     def _body(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, idx_all, istart, rstart,
-              terms_all, ctx, extra, G, split):
+              terms_all, ctx, extra, G, split, scap=0, ar_skip=0):
         """Exactly recon_step's step, on static buffers: captured or run eagerly.  With collectives
         (RCCL, captured into the graph like the kernels): a split step all-reduces the engine's
         per-mini-batch loss sums between its halves, and the gradient all-reduce carries the
@@ -186,7 +187,7 @@ class StepGraphs:
                                         0 if sp is None else len(step_ts)))
         try:
             self._body_rest(model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
-                            ctx, extra, G, split, sp, lib, st)
+                            ctx, extra, G, split, sp, lib, st, scap, ar_skip)
         except BaseException:
             # an eager step that raised after its step counts advanced (an engine-call check, the
             # optimizer itself): take them back, so Adam's bias correction stays in step with the
@@ -198,7 +199,7 @@ class StepGraphs:
             raise
 
     def _body_rest(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
-                   ctx, extra, G, split, sp, lib, st):
+                   ctx, extra, G, split, sp, lib, st, scap=0, ar_skip=0):
         sidx, soff, sterms, mine_t = self.static[key]
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
              "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(),
@@ -207,8 +208,10 @@ class StepGraphs:
         cfg = LossConfig.from_loss_params(loss_fn.loss_params)
         terms = sterms
         if split:
+            from .reconstruction import SlotExchange
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                         batch_sums_reduce=ctx.allreduce_sums, _rows_checked=True)
+                                         batch_sums_reduce=ctx.allreduce_sums,
+                                         slot_exchange=SlotExchange(ctx, scap) if scap else None, _rows_checked=True)
         else:
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
                                          max_batch=max(key[0]), _rows_checked=True)
@@ -216,7 +219,8 @@ class StepGraphs:
             terms = ctx.terms_tail(flat_grad, extra, G)
             if mine_t is not None:
                 terms.index_copy_(0, mine_t, sterms)
-            ctx.allreduce(flat_grad)
+            # (with the slot exchange the object / position gradients are already whole)
+            ctx.allreduce(flat_grad[ar_skip:] if (split and scap) else flat_grad)
         if sp is not None:
             optimizer._external_step_inc = True
         # the loss terms into the iteration's table, then the counter advances: inside the HIP
@@ -235,10 +239,13 @@ class StepGraphs:
         if not done:
             _lib.check(lib.ptyx_step_store(st, *store))
 
-    def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad, ctx=None, extra=0):
+    def run(self, model, optimizer, loss_fn, batches, ga, live, flat_grad, ctx=None, extra=0, slots=False,
+            ar_skip=0):
         """All optimizer steps of one recon_step iteration; returns the (n_batches, 5) loss terms.
         ``live``: the parameters whose ``.grad`` are views of ``flat_grad`` (DistContext.grad_views);
-        ``extra``: the floats after them that carry a step's loss terms through the all-reduce."""
+        ``extra``: the floats after them that carry a step's loss terms through the all-reduce;
+        ``slots``: split steps exchange object-gradient slots (reconstruction.SlotExchange) and
+        all-reduce only ``flat_grad[ar_skip:]``."""
         dev = model.opt_obja.device
         ga = max(1, int(ga))
         steps = _local_steps(ctx, batches, ga)
@@ -285,9 +292,10 @@ class StepGraphs:
                          if isinstance(v, torch.Tensor))
 
         try:
-            for pieces, G, split, mine in steps:
+            for pieces, G, split, mine, scap in steps:
+                scap = scap if (split and slots) else 0
                 sizes = tuple(len(p) for p in pieces)
-                key = (sizes, G, split, mine, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs())
+                key = (sizes, G, split, mine, scap, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs())
                 if key not in self.static:
                     n, nb = sum(sizes), len(sizes)
                     self.static[key] = (torch.zeros(n, dtype=torch.int32, device=dev),
@@ -295,7 +303,7 @@ class StepGraphs:
                                         torch.zeros((nb, 5), dtype=torch.float32, device=dev),
                                         torch.as_tensor(mine, dtype=torch.long).to(dev) if (extra and mine) else None)
                 args = (model, optimizer, loss_fn, flat_grad, grads, key, 1.0 / ga, cnt, idx_all, istart, rstart,
-                        terms_all, ctx, extra, G, split)
+                        terms_all, ctx, extra, G, split, scap, ar_skip)
                 gr = self.graphs.get(key)
                 if gr is not None:
                     gr.replay()

@@ -92,6 +92,11 @@ class OracleLoss:
     def supports_batch_split(self, model=None, **_stages):
         return not self.loss_params.get("loss_pacbed", {}).get("state", False)
 
+    def slot_exchange_ok(self, model):
+        """The oracle keeps no slots; SlotExchange.dense exchanges its dense per-rank contributions
+        the same way (all-gather, sum in rank order on every rank)."""
+        return getattr(self, "slots", True)
+
     def _split_grads(self, model, parts, reduce):
         """oracle of ptyx_forward_loss_grad_begin → reduce → _end on this rank's parts."""
         flat = np.concatenate([np.asarray(b).reshape(-1) for b in parts])
@@ -108,7 +113,7 @@ class OracleLoss:
             model.opt_probe_pos_shifts.detach().numpy(), model.crop_pos_np, model.H_np, model.occu_np,
             model.meas_np, parts, self.loss_params, reduce_np, shift_probes=True)
 
-    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None):
+    def fused_into(self, model, batches, grad_scale=1.0, batch_sums_reduce=None, slot_exchange=None):
         """recon_step's direct path: accumulate the oracle's gradients into the existing .grad."""
         if batch_sums_reduce is not None:
             terms, g = self._split_grads(model, batches, batch_sums_reduce)
@@ -116,12 +121,18 @@ class OracleLoss:
             terms, g = _oracle_grads(model, batches, self.loss_params)
         vals = {"obja": g["obja"], "objp": g["objp"], "probe": np.stack([g["probe"].real, g["probe"].imag], -1),
                 "probe_pos_shifts": g["shifts"]}
+        contrib = {}
         for k in model.engine_grad_names():
             p = model.optimizable_tensors[k]
             if p.requires_grad:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-                p.grad += torch.tensor(vals[k], dtype=torch.float32) * grad_scale
+                contrib[k] = torch.tensor(vals[k], dtype=torch.float32) * grad_scale
+        if slot_exchange is not None:   # objects and positions: every rank's contribution, summed in rank order
+            slot_exchange.dense([contrib[k] for k in ("obja", "objp", "probe_pos_shifts") if k in contrib])
+        for k, c in contrib.items():
+            p = model.optimizable_tensors[k]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            p.grad += c
         return torch.tensor(terms, dtype=torch.float32)
 
     def fused(self, model, batches):
@@ -129,7 +140,7 @@ class OracleLoss:
                                   model, batches, self.loss_params)
 
 
-def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band=False):
+def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band=False, slots=True):
     """Run the trajectory fixture through ptyrad_amd.reconstruction.recon_step; returns final params.
 
     start_iter: per-tensor overrides (staggered toggle_grad_requires); shard: each rank keeps only
@@ -137,7 +148,7 @@ def run_recon(z, rank_world=None, niter=None, start_iter=None, shard=False, band
     from ptyrad_amd.reconstruction import DistContext, recon_step
     sizes = z["batch_sizes"]
     batches = np.split(z["batches"], np.cumsum(sizes)[:-1])
-    ctx = DistContext(band_exchange=band)
+    ctx = DistContext(band_exchange=band, slot_exchange=slots)
     mi = ctx.local_indices(batches, int(z["grad_accumulation"])) if shard else None
     model = OracleModel(z, start_iter=start_iter, meas_index=mi)
     lp = json.loads(str(z["loss_params"]))
@@ -219,15 +230,16 @@ def gpu_recon(z, dist_ctx=None, shard=False, niter=None, ret_all=False, graphs=N
     return model
 
 
-def gpu_dist_worker(rank, world, port, path, out_path):
-    """One rank of a gloo job whose engine runs on cuda:0 (both ranks share the one GPU)."""
+def gpu_dist_worker(rank, world, port, path, out_path, kw=None):
+    """One rank of a gloo job whose engine runs on cuda:0 (both ranks share the one GPU).
+    kw: DistContext keywords (split_batches, slot_exchange)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ptyrad_amd.reconstruction import DistContext
         z = np.load(path, allow_pickle=False)
-        model = gpu_recon(z, DistContext(), shard=True)
+        model = gpu_recon(z, DistContext(**(kw or {})), shard=True)
         np.savez(out_path.replace(".npz", f"_r{rank}.npz"), obja=model.opt_obja.detach().cpu().numpy(),
                  objp=model.opt_objp.detach().cpu().numpy(), probe=model.opt_probe.detach().cpu().numpy(),
                  held=np.array(model.measurements.shape[0]))

@@ -189,18 +189,21 @@ def test_oracle_split_mini_batches_equal_whole_batches(world):
         np.testing.assert_allclose(got, whole[k], rtol=1e-10, atol=1e-13 * np.abs(whole[k]).max(), err_msg=k)
 
 
-@pytest.mark.parametrize("world", [3, 8])
-def test_ga1_split_batches_reproduce_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,slots", [(2, True), (3, False), (4, True), (8, True), (8, False)])
+def test_ga1_split_batches_reproduce_single_rank(tmp_path, world, slots):
     """grad_accumulation = 1 (the reference default) on 3 and 8 gloo ranks: every mini-batch of 4
     is split over the ranks (2/1/1 at three; at eight, four ranks hold one position and four hold
     none but still join every collective), each rank holds only its parts' DPs (the rest NaN), and
-    the trajectory equals the single-rank one (fp32 summation order) and the reference's."""
+    the trajectory equals the single-rank one (fp32 summation order) and the reference's.  slots:
+    the split steps' object and position gradients by SlotExchange (all-gathered per-rank
+    contributions summed in rank order on every rank; only the probe gradient and the loss terms
+    all-reduced), else the flat all-reduce."""
     path = [p for p in TRAJ if "traj_n64_b4_ga1" in p][0]
     z = np.load(path, allow_pickle=False)
     single, _ = run_recon(z)
     out = str(tmp_path / "r.npz")
-    mp.start_processes(dist_worker, args=(world, free_port(), path, out, {"shard": True}), nprocs=world,
-                       start_method="spawn")
+    mp.start_processes(dist_worker, args=(world, free_port(), path, out, {"shard": True, "slots": slots}),
+                       nprocs=world, start_method="spawn")
     r = [np.load(out)] + [np.load(out.replace(".npz", f"_r{i}.npz")) for i in range(1, world)]
     for k in ("obja", "objp", "probe", "shifts"):
         assert np.all(np.isfinite(r[0][k])), k

@@ -281,6 +281,79 @@ def test_recon_step_under_rccl_matches_reference(tmp_path, split, band):
         assert float(np.sqrt(np.mean((r[k].astype(np.float64) - ref) ** 2))) < 1e-5, k
 
 
+def _nccl_slot_worker(rank, port, path, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from ptyrad_amd.reconstruction import DistContext
+        from tests.dist_helpers import gpu_recon
+        z = np.load(path, allow_pickle=False)
+        res = {}
+        for slots in (False, True):
+            for graphs in (False, True):
+                ctx = DistContext(split_batches=True, always_reduce=True, slot_exchange=slots)
+                model, _, _, _, last = gpu_recon(z, ctx, shard=True, graphs=graphs, ret_all=True)
+                tag = f"{'s' if slots else 'f'}{'g' if graphs else 'e'}"
+                res.update({f"{tag}_obja": model.opt_obja.detach().cpu().numpy(),
+                            f"{tag}_objp": model.opt_objp.detach().cpu().numpy(),
+                            f"{tag}_probe": model.opt_probe.detach().cpu().numpy(),
+                            f"{tag}_shifts": model.opt_probe_pos_shifts.detach().cpu().numpy(),
+                            f"{tag}_terms": np.array([np.asarray(v) for v in last.values()]),
+                            f"{tag}_bufs": np.array(len(ctx._slot_bufs))})
+        np.savez(out, **res)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_slot_exchange_under_rccl_equals_flat_allreduce(tmp_path):
+    """a split step's object gradient from all-gathered per-pattern slots
+    (ptyx_forward_loss_grad_begin / _end with PTYX_PREP_DEFER_GATHER, ptyx_slots_export, RCCL
+    all-gather, ptyx_obj_gather_slots) and its position-gradient rows exchanged the same way; only
+    the probe gradient and the loss terms all-reduced.  At world size 1 under RCCL (always_reduce)
+    the slot gather runs over the very patterns, in the very order, the engine's own gather takes:
+    the trajectory is BITWISE the flat all-reduce's, eager and graph-replayed (the all-gathers
+    captured), and matches the reference's (RMS < 1e-5)."""
+    dev()
+    import torch.multiprocessing as mp
+    path = os.path.join(GOLDEN, "traj_c1_n128.npz")
+    out = str(tmp_path / "slots.npz")
+    mp.start_processes(_nccl_slot_worker, args=(_free_port(), path, out), nprocs=1, start_method="spawn")
+    r = np.load(out)
+    assert int(r["sg_bufs"]) >= 1 and int(r["fe_bufs"]) == 0          # the exchange really ran (and only there)
+    for tag in ("se", "sg", "fg"):
+        for k in ("obja", "objp", "probe", "shifts", "terms"):
+            assert np.array_equal(r["fe_" + k], r[f"{tag}_" + k]), (tag, k)
+    z = np.load(path, allow_pickle=False)
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((r["sg_" + k].astype(np.float64) - ref) ** 2))) < 1e-5, k
+
+
+@pytest.mark.parametrize("slots", [True, False], ids=["slot_exchange", "flat_allreduce"])
+def test_two_gloo_ranks_split_steps_on_one_gpu(tmp_path, slots):
+    """Two gloo ranks sharing cuda:0, the reference's default cadence (grad_accumulation = 1) with
+    every 32-pattern mini-batch split 16 / 16 (k_fused3), each rank holding only its parts' DPs:
+    with the slot exchange (all-gathered slots, each rank gathers the whole object gradient) and
+    with the flat all-reduce, the two replicas are bitwise equal and the final object is the
+    reference's (RMS < 1e-5)."""
+    dev()
+    import torch.multiprocessing as mp
+    from tests.dist_helpers import gpu_dist_worker
+    path = os.path.join(GOLDEN, "traj_c1_n128.npz")
+    z = np.load(path, allow_pickle=False)
+    out = str(tmp_path / "r.npz")
+    mp.start_processes(gpu_dist_worker, args=(2, _free_port(), path, out,
+                                              {"split_batches": True, "slot_exchange": slots}),
+                       nprocs=2, start_method="spawn")
+    r0, r1 = np.load(out.replace(".npz", "_r0.npz")), np.load(out.replace(".npz", "_r1.npz"))
+    assert int(r0["held"]) + int(r1["held"]) == z["batches"].size
+    for k in ("obja", "objp", "probe"):
+        assert np.array_equal(r0[k], r1[k]), k
+    for k, ref in (("obja", z["final_obja"]), ("objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((r0[k].astype(np.float64) - ref) ** 2))) < 1e-5, k
+
+
 # (engine geometry, bad input): every engine flags out-of-range indices, windows and meas rows on the
 # device and the C ABI reports PTYX_EINVAL at the next call instead of reading out of bounds
 BAD = [("fused3", "idx"), ("fused3", "crop"), ("fused3ms", "crop"), ("fmm", "idx"), ("stripe", "crop"),
