@@ -200,22 +200,24 @@ int ptyx_forward_loss_grad_end(ptyx_plan *plan, void *stream, const double *batc
  * gradient all-reduce, reconstruction.py:753, for a split step).  A _begin / _end call with
  * PTYX_PREP_DEFER_GATHER keeps, per pattern, its unit-coefficient object-gradient slot
  * (ptyx_plan_slot_floats floats, an internal row order that ptyx_obj_gather_slots reads back),
- * window origin and mini-batch coefficients.
- *   ptyx_slots_export: slots_out (n_pad x slot floats) gets the last such call's slots, meta_out
- *     (n_pad x PTYX_SLOT_META floats) their table rows and, with d_shifts, each pattern's row of
- *     the (n_scans, 2) position gradient; rows past the call's patterns are padding (no effect).
- *     use_last 0: padding only (a rank with no part in the step).
- *   ptyx_obj_gather_slots: the object gradient of ALL n rows (the ranks' exports, all-gathered
- *     rank by rank) accumulated into d_obja / d_objp (deterministic, fixed order: identical on
- *     every rank that passes the same buffers), and the position-gradient rows outside
- *     [skip0, skip1) (the other ranks') added into d_shifts. */
+ * window origin and mini-batch coefficients.  A rank's block (ptyx_slot_block_floats(cap) floats)
+ * holds cap slots, then cap table rows of PTYX_SLOT_META floats (window origin, coefficients, scan
+ * index, the pattern's row of the (n_scans, 2) position gradient); rows past the call's patterns
+ * are padding (no effect).
+ *   ptyx_slots_export: this rank's block from the last such call (use_last 0: padding only, for a
+ *     rank with no part in the step); d_shifts (or NULL) is read for the position rows.
+ *   ptyx_obj_gather_slots: `blocks` = the n_ranks blocks all-gathered rank by rank.  The object
+ *     gradient of all n_ranks x cap rows is accumulated into d_obja / d_objp (deterministic, fixed
+ *     order: identical on every rank that passes the same blocks) and the position-gradient rows
+ *     of the other ranks' blocks are added into d_shifts. */
 #define PTYX_SLOT_META 8
-int64_t ptyx_plan_slot_floats(const ptyx_plan *plan);   /* 0: the plan keeps no slots */
-int ptyx_slots_export(ptyx_plan *plan, void *stream, int32_t use_last, int32_t n_pad, float *slots_out,
-                      float *meta_out, const float *d_shifts);
-int ptyx_obj_gather_slots(ptyx_plan *plan, void *stream, const float *slots, const float *meta, int32_t n,
-                          const float *obja, const float *objp, float *d_obja, float *d_objp, int32_t sparse_n,
-                          float *d_shifts, int32_t skip0, int32_t skip1);
+int64_t ptyx_plan_slot_floats(const ptyx_plan *plan);               /* 0: the plan keeps no slots */
+int64_t ptyx_slot_block_floats(const ptyx_plan *plan, int32_t cap);  /* floats of one rank's block */
+int ptyx_slots_export(ptyx_plan *plan, void *stream, int32_t use_last, int32_t cap, float *block,
+                      const float *d_shifts);
+int ptyx_obj_gather_slots(ptyx_plan *plan, void *stream, const float *blocks, int32_t n_ranks, int32_t cap,
+                          int32_t self_rank, const float *obja, const float *objp, float *d_obja, float *d_objp,
+                          int32_t sparse_n, float *d_shifts);
 
 /* Adjoint for an external loss: given dLdI (n_idx,N,N) = dL/d(dp_fwd) for the patterns idx,
  * accumulate the object / probe / position gradients (autograd of PtychoAD.forward). */

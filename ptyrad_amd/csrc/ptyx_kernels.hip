@@ -365,6 +365,10 @@ struct ptyx_plan {
   bool pend_defer_gather = false;   // PTYX_PREP_DEFER_GATHER on the call in flight
   // the last split call that deferred its object gather (ptyx_slots_export reads it): its slots,
   // pattern table and coefficients stay in the plan until the next compute call
+  // small calls: the object gather runs on the caller's stream while the probe / position sums
+  // run on this side stream (fork / join by events: captured into a graph as two branches)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool gather_deferred = false;     // set while that call's _end runs (run_fused3 skips the gather)
   bool slots_ready = false;
   int32_t slots_n = 0;
@@ -480,6 +484,9 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
 
 static void free_plan(ptyx_plan* pl) {
   if (pl->err_host) (void)hipHostFree(pl->err_host);
+  if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
+  if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
+  if (pl->side) (void)hipStreamDestroy(pl->side);
   for (void* q : pl->allocs) (void)hipFree(q);
   delete pl;
 }
@@ -530,6 +537,12 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->device = device;
   pl->n_cu = cu;
   pl->gen = gen;
+  if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming)) != hipSuccess) {
+    free_plan(pl);
+    return hip_fail(e, "side stream / events");
+  }
   const int wg_cu = g_tuning[kTuneGenWg] >= 1 ? (int)g_tuning[kTuneGenWg] : gen->blocks_per_cu;
   pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * wg_cu));
   const size_t N2 = (size_t)d.N * d.N;
@@ -1099,6 +1112,20 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   return launch_status("k_fused3 launch");
 }
 
+// Fork the plan's side stream off `st` (it starts after everything queued on `st` so far) and join
+// it back (`st` continues after everything queued on the side stream).  Under stream capture the
+// pair becomes two graph branches.
+static int fork_side(ptyx_plan* pl, hipStream_t st) {
+  hipError_t e = hipEventRecord(pl->ev_fork, st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(pl->side, pl->ev_fork, 0);
+  return e == hipSuccess ? PTYX_OK : hip_fail(e, "fork (side stream)");
+}
+static int join_side(ptyx_plan* pl, hipStream_t st) {
+  hipError_t e = hipEventRecord(pl->ev_join, pl->side);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st, pl->ev_join, 0);
+  return e == hipSuccess ? PTYX_OK : hip_fail(e, "join (side stream)");
+}
+
 static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
                       const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
   constexpr int N = 128, N2 = N * N;
@@ -1156,6 +1183,35 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  // small call: the probe / position sums (k_small_tail, k_probe_rows_acc) do not read what the
+  // gather writes nor the reverse: they run on the side stream, concurrently with it
+  const bool tail_small = !bins && (gz.d_probe || d_shifts);
+  const bool forked = tail_small && gather_here;
+  hipStream_t tst = forked ? pl->side : st;
+  if (forked && (rc = fork_side(pl, st))) return rc;
+  if (tail_small) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, tst);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
+        hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
+                           gz.d_probe ? pl->slab : nullptr);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
+    }
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, tst);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, tst, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, tst, gz.d_probe, 1);
+    }
+    if ((rc = launch_status("probe finalize launch"))) return rc;
+  }
   if (gather_here) {
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
@@ -1174,29 +1230,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
-    {
-      ProfScope ps(pl, kKSlabReduce, st);
-      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
-      float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
-        hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
-                           gz.d_probe ? pl->slab : nullptr);
-      else
-        hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
-    }
-    if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, st);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, st, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
-    } else if (gz.d_probe) {
-      launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
-    }
-    return launch_status("probe finalize launch");
-  }
+  if (forked && (rc = join_side(pl, st))) return rc;
+  if (tail_small) return PTYX_OK;
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.n_scans,
@@ -1320,6 +1355,34 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  // small call: the probe / position sums on the side stream, concurrently with the gather (they
+  // read the segment slabs, it reads the slots; neither writes what the other reads)
+  const bool tail_small = !bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts);
+  const bool forked = tail_small && (gz.d_obja || gz.d_objp);
+  hipStream_t tst = forked ? pl->side : st;
+  if (forked && (rc = fork_side(pl, st))) return rc;
+  if (tail_small) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, tst);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
+        hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, pl->twg, gz.d_probe ? pl->slab : nullptr);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
+    }
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, tst);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, tst, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, tst, gz.d_probe, P);
+    }
+    if ((rc = launch_status("k_fmm probe / position reduction launch"))) return rc;
+  }
   if (gz.d_obja || gz.d_objp) {
     GatherArgs g{};
     g.ogscr = pl->ffc; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
@@ -1336,28 +1399,8 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  if (!bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
-    {
-      ProfScope ps(pl, kKSlabReduce, st);
-      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
-      float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
-        hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, pl->twg, gz.d_probe ? pl->slab : nullptr);
-      else
-        hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
-    }
-    if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, st);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, st, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
-    } else if (gz.d_probe) {
-      launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
-    }
-    return launch_status("k_fmm probe / position reduction launch");
-  }
+  if (forked && (rc = join_side(pl, st))) return rc;
+  if (tail_small) return PTYX_OK;
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply_modes, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx,
@@ -2001,9 +2044,10 @@ extern "C" int64_t ptyx_plan_slot_floats(const ptyx_plan* pl) {
   return (int64_t)2 * pl->d.Nz * pl->d.N * pl->d.N;
 }
 
-// meta row per pattern (8 floats): geo (2 × int bits), pcoef (2), scan index (int bits), the
-// pattern's position-gradient row (2), 0; padding rows: geo far outside the object (no tile hits
-// it), pcoef 0, index -1
+// Rank block of the slot exchange (floats): cap slots of sf floats, then cap table rows of
+// kSlotMeta floats: geo (2 × int bits), pcoef (2), scan index (int bits), the pattern's
+// position-gradient row (2), 0.  Padding rows: geo far outside the object (no tile hits it),
+// pcoef 0, index -1.
 __global__ void k_slots_meta(const int2* geo, const float2* pcoef, const int32_t* idx, int n, int n_pad,
                              const float* d_shifts, float* meta) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2027,29 +2071,40 @@ __global__ void k_slots_meta(const int2* geo, const float2* pcoef, const int32_t
   m[7] = 0.f;
 }
 
-// geo / pcoef columns of the all-gathered meta rows, for GatherArgs
-__global__ void k_slots_unpack(const float* meta, int n, int2* geo, float2* pcoef) {
+__device__ __forceinline__ const float* block_meta(const float* buf, int j, int cap, long long bfl, long long sf) {
+  return buf + (size_t)(j / cap) * bfl + (size_t)cap * sf + (size_t)(j % cap) * kSlotMeta;
+}
+
+// geo / pcoef columns of every rank block's table rows, for GatherArgs
+__global__ void k_slots_unpack(const float* buf, int n, int cap, long long bfl, long long sf, int2* geo,
+                               float2* pcoef) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  const float* m = meta + (size_t)j * kSlotMeta;
+  const float* m = block_meta(buf, j, cap, bfl, sf);
   geo[j] = make_int2(__float_as_int(m[0]), __float_as_int(m[1]));
   pcoef[j] = make_float2(m[2], m[3]);
 }
 
 // the other ranks' position-gradient rows added to this rank's dense d_shifts (every scan index
-// occurs once in a call, so no two threads touch one row; this rank's own rows are skipped)
-__global__ void k_slots_rows_add(const float* meta, int n, int skip0, int skip1, float* d_shifts) {
+// occurs once in a call, so no two threads touch one row; this rank's own block is skipped)
+__global__ void k_slots_rows_add(const float* buf, int n, int cap, long long bfl, long long sf, int self,
+                                 float* d_shifts) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n || (j >= skip0 && j < skip1)) return;
-  const float* m = meta + (size_t)j * kSlotMeta;
+  if (j >= n || j / cap == self) return;
+  const float* m = block_meta(buf, j, cap, bfl, sf);
   const int s = __float_as_int(m[4]);
   if (s < 0) return;
   d_shifts[2 * (size_t)s] += m[5];
   d_shifts[2 * (size_t)s + 1] += m[6];
 }
 
-extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, int32_t n_pad, float* slots_out,
-                                 float* meta_out, const float* d_shifts) {
+extern "C" int64_t ptyx_slot_block_floats(const ptyx_plan* pl, int32_t cap) {
+  const int64_t sf = ptyx_plan_slot_floats(pl);
+  return sf > 0 && cap > 0 ? (int64_t)cap * (sf + kSlotMeta) : 0;
+}
+
+extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, int32_t cap, float* block,
+                                 const float* d_shifts) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
   if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
@@ -2057,43 +2112,48 @@ extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, 
   if (sf <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no object-gradient slots");
   if (use_last && !pl->slots_ready) return fail(PTYX_EINVAL, "no split call with PTYX_PREP_DEFER_GATHER to export");
   const int n = use_last ? pl->slots_n : 0;
-  if (n_pad < n || n_pad < 1) return fail(PTYX_EINVAL, "n_pad must be >= 1 and cover the call's patterns");
-  if (!meta_out || (n > 0 && !slots_out)) return fail(PTYX_EINVAL, "null output buffer");
+  if (cap < n || cap < 1) return fail(PTYX_EINVAL, "cap must be >= 1 and cover the call's patterns");
+  if (!block) return fail(PTYX_EINVAL, "null output block");
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n > 0) {
-    hipError_t e = hipMemcpyAsync(slots_out, pl->ogscr, (size_t)n * sf * sizeof(float), hipMemcpyDeviceToDevice, st);
+    hipError_t e = hipMemcpyAsync(block, pl->ogscr, (size_t)n * sf * sizeof(float), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(slots)");
   }
-  hipLaunchKernelGGL(k_slots_meta, dim3((n_pad + 255) / 256), dim3(256), 0, st, pl->geo, pl->pcoef,
-                     use_last ? pl->slots_idx : nullptr, n, n_pad, d_shifts, meta_out);
+  hipLaunchKernelGGL(k_slots_meta, dim3((cap + 255) / 256), dim3(256), 0, st, pl->geo, pl->pcoef,
+                     use_last ? pl->slots_idx : nullptr, n, cap, d_shifts, block + (size_t)cap * sf);
   return launch_status("k_slots_meta launch");
 }
 
-extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* slots, const float* meta, int32_t n,
-                                     const float* obja, const float* objp, float* d_obja, float* d_objp,
-                                     int32_t sparse_n, float* d_shifts, int32_t skip0, int32_t skip1) {
+extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_t n_ranks, int32_t cap,
+                                     int32_t self_rank, const float* obja, const float* objp, float* d_obja,
+                                     float* d_objp, int32_t sparse_n, float* d_shifts) {
   g_err.clear();
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
   if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
-  if (ptyx_plan_slot_floats(pl) <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no object-gradient slots");
-  if (n < 1 || n > pl->d.max_patterns) return fail(PTYX_EINVAL, "n must be in [1, max_patterns]");
-  if (!slots || !meta || !obja || !objp) return fail(PTYX_EINVAL, "null input");
-  if (skip0 < 0 || skip1 < skip0 || skip1 > n) return fail(PTYX_EINVAL, "skip range outside [0, n]");
+  const int64_t sf = ptyx_plan_slot_floats(pl);
+  if (sf <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no object-gradient slots");
+  if (n_ranks < 1 || cap < 1 || (int64_t)n_ranks * cap > pl->d.max_patterns)
+    return fail(PTYX_EINVAL, "n_ranks x cap must be in [1, max_patterns]");
+  if (self_rank < 0 || self_rank >= n_ranks) return fail(PTYX_EINVAL, "self_rank outside [0, n_ranks)");
+  if (!blocks || !obja || !objp) return fail(PTYX_EINVAL, "null input");
+  const int n = n_ranks * cap;
+  const long long bfl = (long long)cap * (sf + kSlotMeta);
   const int sn = sparse_n < 1 ? 1 : sparse_n;
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // the unpacked table reuses the plan's per-call geo / pcoef arrays (capacity max_patterns)
-  hipLaunchKernelGGL(k_slots_unpack, dim3((n + 255) / 256), dim3(256), 0, st, meta, n, pl->geo, pl->pcoef);
+  hipLaunchKernelGGL(k_slots_unpack, dim3((n + 255) / 256), dim3(256), 0, st, blocks, n, cap, bfl, (long long)sf,
+                     pl->geo, pl->pcoef);
   int rc = launch_status("k_slots_unpack launch");
   if (rc) return rc;
   pl->slots_ready = false;
-  pl->prep.valid = false;
   if (d_obja || d_objp) {
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
     constexpr int N = 128;
     GatherArgs g{};
-    g.ogscr = reinterpret_cast<const float2*>(slots); g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = n;
+    g.ogscr = reinterpret_cast<const float2*>(blocks); g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = n;
+    g.blk = cap; g.bstride = bfl / 2;   // (float2 units)
     g.boff = nullptr; g.blist = nullptr; g.bbox = nullptr;
     g.Ny = pl->d.Ny; g.Nx = pl->d.Nx; g.tiles_x = (pl->d.Nx + kGTX - 1) / kGTX; g.sparse_n = sn;
     g.obja = obja; g.objp = objp; g.d_obja = d_obja; g.d_objp = d_objp;
@@ -2106,8 +2166,9 @@ extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* s
     if ((rc = launch_status("k_obj_gather (slots) launch"))) return rc;
 #endif
   }
-  if (d_shifts) {
-    hipLaunchKernelGGL(k_slots_rows_add, dim3((n + 255) / 256), dim3(256), 0, st, meta, n, skip0, skip1, d_shifts);
+  if (d_shifts && n_ranks > 1) {
+    hipLaunchKernelGGL(k_slots_rows_add, dim3((n + 255) / 256), dim3(256), 0, st, blocks, n, cap, bfl, (long long)sf,
+                       self_rank, d_shifts);
     if ((rc = launch_status("k_slots_rows_add launch"))) return rc;
   }
   return PTYX_OK;

@@ -371,35 +371,35 @@ class Plan:
         (ptyx_plan_slot_floats; 0: no slot exchange for this geometry)."""
         return int(self.lib.ptyx_plan_slot_floats(self._h))
 
-    def export_slots(self, n_pad: int, slots_out, meta_out, d_shifts=None, use_last=True):
-        """ptyx_slots_export: the last deferred split call's slots into slots_out (n_pad, slot_floats)
-        and table rows into meta_out (n_pad, PTYX_SLOT_META); use_last False: padding rows only."""
-        sf = self.slot_floats
-        if tuple(slots_out.shape) != (n_pad, sf) or tuple(meta_out.shape) != (n_pad, _lib.PTYX_SLOT_META):
-            raise ValueError("export buffers must be (n_pad, slot_floats) and (n_pad, PTYX_SLOT_META)")
-        for name, x in (("slots_out", slots_out), ("meta_out", meta_out)):
-            _need(x, torch.float32, name, self.device)
+    def slot_block_floats(self, cap: int) -> int:
+        """Floats of one rank's slot-exchange block of ``cap`` patterns (slots, then table rows)."""
+        return int(self.lib.ptyx_slot_block_floats(self._h, int(cap)))
+
+    def export_slots(self, cap: int, block, d_shifts=None, use_last=True):
+        """ptyx_slots_export: this rank's block (slot_block_floats(cap) floats) from the last
+        deferred split call; use_last False: padding rows only."""
+        _need(block, torch.float32, "block", self.device)
+        if block.numel() != self.slot_block_floats(cap):
+            raise ValueError(f"block must hold slot_block_floats({cap}) floats")
         if d_shifts is not None:
             _need(d_shifts, torch.float32, "d_shifts", self.device)
-        _lib.check(self.lib.ptyx_slots_export(self._h, self._stream(), int(bool(use_last)), int(n_pad), _ptr(slots_out),
-                                              _ptr(meta_out), _ptr(d_shifts)))
+        _lib.check(self.lib.ptyx_slots_export(self._h, self._stream(), int(bool(use_last)), int(cap), _ptr(block),
+                                              _ptr(d_shifts)))
 
-    def gather_slots(self, slots, meta, t: dict, grads: dict, sparse_n: int, skip=(0, 0)):
-        """ptyx_obj_gather_slots: object gradient of every row of the all-gathered (n, slot_floats)
-        slots / (n, PTYX_SLOT_META) table into grads['obja'] / ['objp'], and the rows outside
-        ``skip`` (the other ranks') of the position gradient into grads['shifts']."""
-        n = int(slots.shape[0])
-        for name, x in (("slots", slots), ("meta", meta)):
-            _need(x, torch.float32, name, self.device)
-        if tuple(slots.shape) != (n, self.slot_floats) or tuple(meta.shape) != (n, _lib.PTYX_SLOT_META):
-            raise ValueError("gather buffers must be (n, slot_floats) and (n, PTYX_SLOT_META)")
+    def gather_slots(self, blocks, n_ranks: int, cap: int, rank: int, t: dict, grads: dict, sparse_n: int):
+        """ptyx_obj_gather_slots: object gradient of every rank block's patterns (the all-gathered
+        ``blocks``) into grads['obja'] / ['objp'], and the other ranks' position-gradient rows
+        into grads['shifts']."""
+        _need(blocks, torch.float32, "blocks", self.device)
+        if blocks.numel() != n_ranks * self.slot_block_floats(cap):
+            raise ValueError("blocks must hold n_ranks x slot_block_floats(cap) floats")
         g = {k: grads.get(k) for k in ("obja", "objp", "shifts")}
         for k, v in g.items():
             if v is not None:
                 _need(v, torch.float32, f"grad {k}", self.device)
-        _lib.check(self.lib.ptyx_obj_gather_slots(self._h, self._stream(), _ptr(slots), _ptr(meta), n,
-                                                  _ptr(t["obja"]), _ptr(t["objp"]), _ptr(g["obja"]), _ptr(g["objp"]),
-                                                  int(sparse_n), _ptr(g["shifts"]), int(skip[0]), int(skip[1])))
+        _lib.check(self.lib.ptyx_obj_gather_slots(self._h, self._stream(), _ptr(blocks), int(n_ranks), int(cap),
+                                                  int(rank), _ptr(t["obja"]), _ptr(t["objp"]), _ptr(g["obja"]),
+                                                  _ptr(g["objp"]), int(sparse_n), _ptr(g["shifts"])))
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):
         """ptyx_adjoint_dldi: accumulate gradients for an external dL/d(dp)."""

@@ -338,36 +338,16 @@ class DistContext:
         largest rank's share (rank 0's: Σ ⌈|b| / W⌉), the same on every rank."""
         return sum(-(-len(np.asarray(b).reshape(-1)) // self.world) for b in group)
 
-    def slot_buffers(self, device, cap, sf):
-        """Persistent (send slots, send table, received slots, received table) buffers of the slot
-        exchange (a captured step holds their addresses)."""
-        key = (str(device), int(cap), int(sf))
+    def slot_buffers(self, device, block):
+        """Persistent (this rank's block, all ranks' blocks) buffers of the slot exchange (a
+        captured step holds their addresses)."""
+        key = (str(device), int(block))
         b = self._slot_bufs.get(key)
         if b is None:
-            from . import _lib
-            M = _lib.PTYX_SLOT_META
-            b = (torch.zeros((cap, sf), dtype=torch.float32, device=device),
-                 torch.zeros((cap, M), dtype=torch.float32, device=device),
-                 torch.zeros((self.world * cap, sf), dtype=torch.float32, device=device),
-                 torch.zeros((self.world * cap, M), dtype=torch.float32, device=device))
+            b = (torch.zeros(block, dtype=torch.float32, device=device),
+                 torch.zeros(self.world * block, dtype=torch.float32, device=device))
             self._slot_bufs[key] = b
         return b
-
-
-    @staticmethod
-    def terms_tail(flat, extra, G):
-        """The (G, 5) loss-term rows at the start of the ``extra`` floats grad_views appended."""
-        n0 = flat.numel() - int(extra)
-        return flat[n0:n0 + 5 * G].view(G, 5)
-
-    def put_terms(self, tail, terms_local, idx_local):
-        """Rows of the group's loss terms this rank owns, into the (zeroed) tail of the flat
-        buffer: after the gradient all-reduce every rank holds the whole group's terms."""
-        if len(idx_local):
-            if list(idx_local) == list(range(tail.shape[0])):
-                tail.copy_(terms_local)
-            else:
-                tail[torch.as_tensor(idx_local, device=tail.device)] = terms_local.to(tail.device)
 
 
 class SlotExchange:
@@ -377,8 +357,8 @@ class SlotExchange:
     Every rank runs its parts of the step's mini-batches with the object gather deferred
     (ptyx_forward_loss_grad_begin / _end with PTYX_PREP_DEFER_GATHER), exports its patterns'
     unit-coefficient object-gradient slots and table rows (window origin, mini-batch coefficients,
-    scan index and position-gradient row) padded to ``cap`` rows, all-gathers them (two
-    all-gathers: slots and rows), and runs the deterministic slot gather over all W·cap rows: the
+    scan index and position-gradient row) padded to ``cap`` patterns as ONE block, all-gathers the
+    blocks (one collective), and runs the deterministic slot gather over all W·cap rows: the
     object gradient of the whole step, identical on every rank, and the other ranks'
     position-gradient rows added to its own.  Bytes a rank sends: its cap slots (128 KiB each at
     N = 128) and rows, against 2·(W−1)/W of the object and position gradients for the all-reduce."""
@@ -388,13 +368,10 @@ class SlotExchange:
 
     def __call__(self, plan, t, grads, cfg, used=True):
         ctx, cap = self.ctx, self.cap
-        sf = plan.slot_floats
-        send_s, send_m, recv_s, recv_m = ctx.slot_buffers(plan.device, cap, sf)
-        plan.export_slots(cap, send_s, send_m, grads.get("shifts"), use_last=used)
-        ctx.all_gather_into(recv_s, send_s)
-        ctx.all_gather_into(recv_m, send_m)
-        plan.gather_slots(recv_s, recv_m, t, grads, cfg.sparse_n if cfg.sparse_on else 1,
-                          skip=(ctx.rank * cap, (ctx.rank + 1) * cap))
+        send, recv = ctx.slot_buffers(plan.device, plan.slot_block_floats(cap))
+        plan.export_slots(cap, send, grads.get("shifts"), use_last=used)
+        ctx.all_gather_into(recv, send)
+        plan.gather_slots(recv, ctx.world, cap, ctx.rank, t, grads, cfg.sparse_n if cfg.sparse_on else 1)
 
     def dense(self, tensors):
         """The same exchange for a loss without slots (the CPU test doubles): each tensor holds
