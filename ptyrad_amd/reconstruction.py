@@ -349,6 +349,21 @@ class DistContext:
             self._slot_bufs[key] = b
         return b
 
+    @staticmethod
+    def terms_tail(flat, extra, G):
+        """The (G, 5) loss-term rows at the start of the ``extra`` floats grad_views appended."""
+        n0 = flat.numel() - int(extra)
+        return flat[n0:n0 + 5 * G].view(G, 5)
+
+    def put_terms(self, tail, terms_local, idx_local):
+        """Rows of the group's loss terms this rank owns, into the (zeroed) tail of the flat
+        buffer: after the gradient all-reduce every rank holds the whole group's terms."""
+        if len(idx_local):
+            if list(idx_local) == list(range(tail.shape[0])):
+                tail.copy_(terms_local)
+            else:
+                tail[torch.as_tensor(idx_local, device=tail.device)] = terms_local.to(tail.device)
+
 
 class SlotExchange:
     """The object-gradient exchange of one split engine call (DistContext.slot_exchange; replaces
@@ -644,7 +659,15 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
     objs = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in live)]
     band = False
     obj_all = [p for p in (model.opt_obja, model.opt_objp) if any(p is q for q in params)]
-    if ctx.band_exchange is not False and ctx._collective() and objs:
+    # "auto" remembers a batching it found not row-sharded (every rank iterates the same global
+    # batches, so every rank skips alike): no touched-rows pass or range all-gather for it again
+    auto_key = None
+    if ctx.band_exchange == "auto" and ctx.bands is None and ctx._collective() and objs:
+        crc = zlib.crc32(np.ascontiguousarray(np.concatenate([np.asarray(b).reshape(-1) for b in batches]),
+                                              dtype=np.int64).tobytes()) if len(batches) else 0
+        auto_key = (crc, len(batches), ga, bool(split_ok))
+    if ctx.band_exchange is not False and ctx._collective() and objs and \
+            not (auto_key is not None and getattr(ctx, "_not_banded", None) == auto_key):
         # the rows each rank's windows reach this iteration (recomputed: the batches may change);
         # band_exchange "auto": by band when the ranks' rows line up (a row-sharded scan)
         N = int(model.opt_probe.shape[1])
@@ -653,6 +676,8 @@ def recon_step(batches, grad_accumulation, model, optimizer, loss_fn, constraint
         Ny = int(model.opt_obja.shape[2])
         if ctx.bands is None and (ctx.band_exchange is True or ObjectBands.disjoint(ranges, Ny, ctx.world, N)):
             ctx.bands = ObjectBands(ctx, Ny, dev, ranges)
+        elif ctx.bands is None:
+            ctx._not_banded = auto_key
         if ctx.bands is not None:
             band = True
             ctx.bands.ranges = ranges
