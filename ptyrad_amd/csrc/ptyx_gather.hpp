@@ -230,10 +230,12 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
 // wave whole hits, 16 rows × np planes each, and at np = 6 the compiler issues them row by row (16
 // round trips a hit); here a hit costs one.  Each wave owns its rows to the end, so there is no
 // wave-partial reduction either.  Hits are summed in candidate order (deterministic) with a
-// compensated (Kahan) accumulator: one sequential fp32 sum over every hit of a pixel (≈ 2,000 at
-// the c2 coverage) drifts by ≈ 5e-6 of the gradient's norm between call splits (VERDICT r05
-// weak 1: a full-c2 split-invariance failure that is summation order, not a hit-list defect —
-// a missing or doubled hit moves the norm by ≈ 6e-5); the compensation keeps it at fp32 rounding.
+// compensated (Kahan) accumulators, for the g_O sum and the loss_sparse count alike: one
+// sequential fp32 sum over every hit of a pixel (≈ 2,000 at the c2 coverage) drifts by ≈ 5e-6 of
+// the gradient's norm between call splits (a full-c2 split-invariance failure
+// of dφ — the count adds ≈ 2,000 near-equal c_sparse terms, whose rounding is systematic, not
+// random; a missing or doubled hit would move the norm by ≈ 6e-5); compensated, both stay at fp32
+// rounding.
 template <int N, bool ROWPERM, int GW, bool MP>
 __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
   constexpr int N2 = N * N;
@@ -277,12 +279,13 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
   const int x = tx + lane;
   const int r0 = ty + wave * RW;   // this wave's first object row
   float2 acc[RW], cmp[RW];   // running sums and their Kahan compensations
-  float cnt[RW];
+  float cnt[RW], ccmp[RW];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
     acc[r] = make_float2(0.f, 0.f);
     cmp[r] = make_float2(0.f, 0.f);
     cnt[r] = 0.f;
+    ccmp[r] = 0.f;
   }
   // the epilogue's operands of this wave's pixels (A, φ and the gradients it adds to), loaded
   // now: they do not depend on the hits, and only this workgroup touches these pixels
@@ -369,7 +372,12 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
           cmp[r].y = (sy - acc[r].y) - yy;
           acc[r] = make_float2(sx, sy);
           const int row = r0 + r - H.x;
-          if (colok && row >= 0 && row < N) cnt[r] += cs;
+          if (colok && row >= 0 && row < N) {   // (≈ 2,000 near-equal c_sparse terms: compensated too)
+            const float yc = cs - ccmp[r];
+            const float sc = cnt[r] + yc;
+            ccmp[r] = (sc - cnt[r]) - yc;
+            cnt[r] = sc;
+          }
         }
       }
     }
