@@ -213,6 +213,11 @@ int ptyx_forward_loss_grad_end(ptyx_plan *plan, void *stream, const double *batc
 #define PTYX_SLOT_META 8
 int64_t ptyx_plan_slot_floats(const ptyx_plan *plan);               /* 0: the plan keeps no slots */
 int64_t ptyx_slot_block_floats(const ptyx_plan *plan, int32_t cap);  /* floats of one rank's block */
+/* ptyx_plan_slot_target: the NEXT _begin / _end call with PTYX_PREP_DEFER_GATHER (of at most cap
+ * patterns) writes its slots straight into `block` (this rank's block, e.g. its slice of the
+ * all-gather's output: an in-place all-gather), so ptyx_slots_export only adds the table rows.
+ * One call's target: cleared when that call ends; NULL clears it. */
+int ptyx_plan_slot_target(ptyx_plan *plan, float *block, int32_t cap);
 int ptyx_slots_export(ptyx_plan *plan, void *stream, int32_t use_last, int32_t cap, float *block,
                       const float *d_shifts);
 int ptyx_obj_gather_slots(ptyx_plan *plan, void *stream, const float *blocks, int32_t n_ranks, int32_t cap,

@@ -365,10 +365,12 @@ struct ptyx_plan {
   bool pend_defer_gather = false;   // PTYX_PREP_DEFER_GATHER on the call in flight
   // the last split call that deferred its object gather (ptyx_slots_export reads it): its slots,
   // pattern table and coefficients stay in the plan until the next compute call
-  // small calls: the object gather runs on the caller's stream while the probe / position sums
-  // run on this side stream (fork / join by events: captured into a graph as two branches)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // ptyx_plan_slot_target: the next deferring call writes its slots straight into the caller's
+  // block (no copy in ptyx_slots_export); consumed by that call
+  float* slot_tgt = nullptr;
+  int32_t slot_tgt_cap = 0;
+  bool use_tgt = false;             // the call in flight writes its slots to slot_tgt
+  float* slots_at = nullptr;        // where the last deferring call's slots are
   bool gather_deferred = false;     // set while that call's _end runs (run_fused3 skips the gather)
   bool slots_ready = false;
   int32_t slots_n = 0;
@@ -484,9 +486,6 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
 
 static void free_plan(ptyx_plan* pl) {
   if (pl->err_host) (void)hipHostFree(pl->err_host);
-  if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
-  if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
-  if (pl->side) (void)hipStreamDestroy(pl->side);
   for (void* q : pl->allocs) (void)hipFree(q);
   delete pl;
 }
@@ -537,12 +536,6 @@ extern "C" int ptyx_plan_create(ptyx_plan** out, const ptyx_dims* dims, int devi
   pl->device = device;
   pl->n_cu = cu;
   pl->gen = gen;
-  if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming)) != hipSuccess) {
-    free_plan(pl);
-    return hip_fail(e, "side stream / events");
-  }
   const int wg_cu = g_tuning[kTuneGenWg] >= 1 ? (int)g_tuning[kTuneGenWg] : gen->blocks_per_cu;
   pl->nwg = std::max(d.P, std::min(d.max_patterns, cu * wg_cu));
   const size_t N2 = (size_t)d.N * d.N;
@@ -1038,7 +1031,7 @@ static f3::F3Args register_args(const ptyx_plan* pl, const ptyx_inputs* in, cons
   f.q = single ? cfg->single_q : cfg->poissn_q;
   f.eps2 = cfg->poissn_eps;
   f.psums = pl->psums;
-  f.slots = pl->ogscr; f.segslab = pl->segslab; f.segbid = pl->segbid; f.dsu = pl->dsu;
+  f.slots = pl->use_tgt ? reinterpret_cast<float2*>(pl->slot_tgt) : pl->ogscr; f.segslab = pl->segslab; f.segbid = pl->segbid; f.dsu = pl->dsu;
   f.tail = (gz.d_probe != nullptr || (a.shift && gz.d_shifts != nullptr)) ? 1 : 0;
   f.dp_out = a.dp_out;
   f.Nz = d.Nz;
@@ -1112,20 +1105,6 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   return launch_status("k_fused3 launch");
 }
 
-// Fork the plan's side stream off `st` (it starts after everything queued on `st` so far) and join
-// it back (`st` continues after everything queued on the side stream).  Under stream capture the
-// pair becomes two graph branches.
-static int fork_side(ptyx_plan* pl, hipStream_t st) {
-  hipError_t e = hipEventRecord(pl->ev_fork, st);
-  if (e == hipSuccess) e = hipStreamWaitEvent(pl->side, pl->ev_fork, 0);
-  return e == hipSuccess ? PTYX_OK : hip_fail(e, "fork (side stream)");
-}
-static int join_side(ptyx_plan* pl, hipStream_t st) {
-  hipError_t e = hipEventRecord(pl->ev_join, pl->side);
-  if (e == hipSuccess) e = hipStreamWaitEvent(st, pl->ev_join, 0);
-  return e == hipSuccess ? PTYX_OK : hip_fail(e, "join (side stream)");
-}
-
 static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
                       const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
   constexpr int N = 128, N2 = N * N;
@@ -1183,35 +1162,6 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  // small call: the probe / position sums (k_small_tail, k_probe_rows_acc) do not read what the
-  // gather writes nor the reverse: they run on the side stream, concurrently with it
-  const bool tail_small = !bins && (gz.d_probe || d_shifts);
-  const bool forked = tail_small && gather_here;
-  hipStream_t tst = forked ? pl->side : st;
-  if (forked && (rc = fork_side(pl, st))) return rc;
-  if (tail_small) {   // small call: one launch for the probe / position sums
-    {
-      ProfScope ps(pl, kKSlabReduce, tst);
-      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
-      float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
-        hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
-                           gz.d_probe ? pl->slab : nullptr);
-      else
-        hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, pl->coef, ci,
-                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
-    }
-    if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, tst);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, tst, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
-    } else if (gz.d_probe) {
-      launch_probe_fin_reg(pl, a, tst, gz.d_probe, 1);
-    }
-    if ((rc = launch_status("probe finalize launch"))) return rc;
-  }
   if (gather_here) {
     GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
@@ -1230,8 +1180,29 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  if (forked && (rc = join_side(pl, st))) return rc;
-  if (tail_small) return PTYX_OK;
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
+        hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
+                           gz.d_probe ? pl->slab : nullptr);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
+                           out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
+    }
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, st);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, st, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
+    }
+    return launch_status("probe finalize launch");
+  }
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.n_scans,
@@ -1355,34 +1326,6 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  // small call: the probe / position sums on the side stream, concurrently with the gather (they
-  // read the segment slabs, it reads the slots; neither writes what the other reads)
-  const bool tail_small = !bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts);
-  const bool forked = tail_small && (gz.d_obja || gz.d_objp);
-  hipStream_t tst = forked ? pl->side : st;
-  if (forked && (rc = fork_side(pl, st))) return rc;
-  if (tail_small) {   // small call: one launch for the probe / position sums
-    {
-      ProfScope ps(pl, kKSlabReduce, tst);
-      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
-      float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
-        hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, pl->twg, gz.d_probe ? pl->slab : nullptr);
-      else
-        hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, tst, pl->segslab, pl->segbid, nseg, out,
-                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
-    }
-    if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, tst);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, tst, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
-    } else if (gz.d_probe) {
-      launch_probe_fin_reg(pl, a, tst, gz.d_probe, P);
-    }
-    if ((rc = launch_status("k_fmm probe / position reduction launch"))) return rc;
-  }
   if (gz.d_obja || gz.d_objp) {
     GatherArgs g{};
     g.ogscr = pl->ffc; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
@@ -1399,8 +1342,28 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  if (forked && (rc = join_side(pl, st))) return rc;
-  if (tail_small) return PTYX_OK;
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  if (!bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+    {
+      ProfScope ps(pl, kKSlabReduce, st);
+      const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
+      float2* out = gz.d_probe ? pl->Gsum : nullptr;
+      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
+        hipLaunchKernelGGL(f3::k_small_tail_modes<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, pl->twg, gz.d_probe ? pl->slab : nullptr);
+      else
+        hipLaunchKernelGGL(f3::k_small_tail_modes<false>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, out,
+                           a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
+    }
+    if (gz.d_probe && a.shift) {
+      ProfScope ps(pl, kKProbeFinalize, st);
+      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, st, pl->slab,
+                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+    } else if (gz.d_probe) {
+      launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
+    }
+    return launch_status("k_fmm probe / position reduction launch");
+  }
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply_modes, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx,
@@ -1992,10 +1955,14 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
     return fail(PTYX_EUNSUPPORTED, "PTYX_PREP_DEFER_GATHER needs the k_fused3 / k_fused3ms engine "
                                    "(ptyx_plan_slot_floats > 0, f32 DPs, the call within the register capacity)");
   pl->slots_ready = false;
+  pl->use_tgt = defer_gather && pl->slot_tgt && n_idx <= pl->slot_tgt_cap;
   resolve_prep(pl, in, engine, &c);
   if ((rc = run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), nullptr, kPhaseBegin,
-                     batch_sums, false)))
+                     batch_sums, false))) {
+    pl->use_tgt = false;
+    pl->slot_tgt = nullptr;
     return rc;
+  }
   pl->pend = true;
   pl->pend_in = *in; pl->pend_gz = gz; pl->pend_cfg = c;
   pl->pend_idx = idx; pl->pend_boff = boff; pl->pend_nb = n_batches; pl->pend_n = n_idx;
@@ -2025,7 +1992,10 @@ extern "C" int ptyx_forward_loss_grad_end(ptyx_plan* pl, void* stream, const dou
     pl->slots_ready = true;
     pl->slots_n = pl->pend_n;
     pl->slots_idx = pl->pend_idx;
+    pl->slots_at = pl->use_tgt ? pl->slot_tgt : reinterpret_cast<float*>(pl->ogscr);
   }
+  pl->use_tgt = false;
+  pl->slot_tgt = nullptr;   // one call's target
   return rc;
 }
 
@@ -2103,6 +2073,17 @@ extern "C" int64_t ptyx_slot_block_floats(const ptyx_plan* pl, int32_t cap) {
   return sf > 0 && cap > 0 ? (int64_t)cap * (sf + kSlotMeta) : 0;
 }
 
+extern "C" int ptyx_plan_slot_target(ptyx_plan* pl, float* block, int32_t cap) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
+  if (block && ptyx_plan_slot_floats(pl) <= 0) return fail(PTYX_EUNSUPPORTED, "this plan's calls keep no slots");
+  if (block && cap < 1) return fail(PTYX_EINVAL, "cap must be >= 1");
+  pl->slot_tgt = block;
+  pl->slot_tgt_cap = block ? cap : 0;
+  return PTYX_OK;
+}
+
 extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, int32_t cap, float* block,
                                  const float* d_shifts) {
   g_err.clear();
@@ -2116,8 +2097,8 @@ extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, 
   if (!block) return fail(PTYX_EINVAL, "null output block");
   DeviceGuard dg(pl->device);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (n > 0) {
-    hipError_t e = hipMemcpyAsync(block, pl->ogscr, (size_t)n * sf * sizeof(float), hipMemcpyDeviceToDevice, st);
+  if (n > 0 && pl->slots_at != block) {   // (written in place when the block was the call's target)
+    hipError_t e = hipMemcpyAsync(block, pl->slots_at, (size_t)n * sf * sizeof(float), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(slots)");
   }
   hipLaunchKernelGGL(k_slots_meta, dim3((cap + 255) / 256), dim3(256), 0, st, pl->geo, pl->pcoef,

@@ -353,6 +353,8 @@ class Plan:
         cfg = loss_cfg.to_c(grad_scale, 0, _lib.PTYX_PREP_CALL |
                             (_lib.PTYX_PREP_DEFER_GATHER if slot_exchange is not None else 0))
         g = self._grads(grads)
+        if slot_exchange is not None:   # the slots go straight into this rank's exchange block
+            self.set_slot_target(*slot_exchange.target(self))
         _lib.check(self.lib.ptyx_forward_loss_grad_begin(self._h, self._stream(), ctypes.byref(inp), _ptr(idx_t),
                                                          _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(dp_out),
                                                          ctypes.byref(g), _ptr(sums)))
@@ -374,6 +376,14 @@ class Plan:
     def slot_block_floats(self, cap: int) -> int:
         """Floats of one rank's slot-exchange block of ``cap`` patterns (slots, then table rows)."""
         return int(self.lib.ptyx_slot_block_floats(self._h, int(cap)))
+
+    def set_slot_target(self, block, cap: int):
+        """ptyx_plan_slot_target: the next deferring split call writes its slots into ``block``."""
+        if block is not None:
+            _need(block, torch.float32, "block", self.device)
+            if block.numel() != self.slot_block_floats(cap):
+                raise ValueError(f"block must hold slot_block_floats({cap}) floats")
+        _lib.check(self.lib.ptyx_plan_slot_target(self._h, _ptr(block), int(cap)))
 
     def export_slots(self, cap: int, block, d_shifts=None, use_last=True):
         """ptyx_slots_export: this rank's block (slot_block_floats(cap) floats) from the last

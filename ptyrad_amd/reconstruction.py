@@ -381,11 +381,24 @@ class SlotExchange:
     def __init__(self, ctx, cap):
         self.ctx, self.cap = ctx, int(cap)
 
+    def _block(self, plan):
+        """(this rank's block, all blocks): with RCCL the rank's block IS its slice of the
+        all-gather output (in place: the engine writes its slots there, nothing is copied)."""
+        ctx = self.ctx
+        bf = plan.slot_block_floats(self.cap)
+        send, recv = ctx.slot_buffers(plan.device, bf)
+        inplace = ctx._collective() and dist.get_backend(ctx.group) == "nccl"
+        return (recv[ctx.rank * bf:(ctx.rank + 1) * bf] if inplace else send), recv
+
+    def target(self, plan):
+        """(block, cap) for ptyx_plan_slot_target before the engine call."""
+        return self._block(plan)[0], self.cap
+
     def __call__(self, plan, t, grads, cfg, used=True):
         ctx, cap = self.ctx, self.cap
-        send, recv = ctx.slot_buffers(plan.device, plan.slot_block_floats(cap))
-        plan.export_slots(cap, send, grads.get("shifts"), use_last=used)
-        ctx.all_gather_into(recv, send)
+        mine, recv = self._block(plan)
+        plan.export_slots(cap, mine, grads.get("shifts"), use_last=used)
+        ctx.all_gather_into(recv, mine)
         plan.gather_slots(recv, ctx.world, cap, ctx.rank, t, grads, cfg.sparse_n if cfg.sparse_on else 1)
 
     def dense(self, tensors):
