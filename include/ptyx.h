@@ -65,6 +65,12 @@ extern "C" {
  * the call's per-pattern object-gradient slots for ptyx_slots_export; the caller all-gathers them
  * over the ranks and runs ptyx_obj_gather_slots.  Another engine: PTYX_EUNSUPPORTED. */
 #define PTYX_PREP_DEFER_GATHER 8
+/* PTYX_PREP_GRAD_STORE (ABI 208): the call OVERWRITES d_obja / d_objp with its own object
+ * gradient instead of accumulating into them (their content on entry is ignored), so a caller
+ * that would zero them first need not: the register engines' gathers store, the other engines
+ * clear the two arrays on the stream before they accumulate.  The other gradients accumulate as
+ * usual.  (A graph-replayed optimizer step zeroes only the rest of its flat gradient buffer.) */
+#define PTYX_PREP_GRAD_STORE 16
 /* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
  * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
  * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
@@ -412,7 +418,9 @@ int ptyx_meas_pad_resample(void *stream, const void *src, int32_t src_f16, int64
  * grad_accumulation = 1: one step per mini-batch).  A captured step reads its mini-batch through
  * a device step counter, so one hipGraph serves every step of the same shape.
  *   ptyx_step_select: idx_out[i] = idx_all[istart[*cnt] + i] for i < n, zeroes grad[0..grad_n)
- *                     (the flat gradient buffer every trainable parameter's .grad views), and
+ *                     (the flat gradient buffer every trainable parameter's .grad views, or the
+ *                     part of it a PTYX_PREP_GRAD_STORE call does not overwrite; any 4-byte
+ *                     aligned start), and
  *                     adds 1 to *steps[j] for j < n_steps (steps: a DEVICE array of device f32
  *                     pointers, n_steps ≤ 256 — the optimizer's step counts, torch's
  *                     state_step += 1, so the step's Adam launch needs no increment launch of its

@@ -18,6 +18,7 @@ PTYX_ABI_VERSION = 208     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_PREP_DEFER_PROBE = 4  # flag bit: the probe-gradient reduction may wait for a later piece
 PTYX_PREP_DEFER_GATHER = 8  # flag bit (_begin / _end): keep the object-gradient slots for the slot exchange
+PTYX_PREP_GRAD_STORE = 16  # flag bit: the call overwrites d_obja / d_objp (no zeroing needed before)
 PTYX_SLOT_META = 8         # floats per table row of a slot-exchange rank block
 PTYX_BATCH_SUMS = 37      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4

@@ -48,6 +48,9 @@ struct GatherArgs {
   // j / blk, row j % blk, blocks bstride float2 apart (blk 0: plain pattern rows)
   int blk = 0;
   long long bstride = 0;
+  // PTYX_PREP_GRAD_STORE: d_obja / d_objp are OVERWRITTEN with this call's gradient (tiles no
+  // window touches get zeros), so the caller need not zero them and no old value is read
+  int store = 0;
 };
 // float2 offset of pattern j's slot plane zp (non-MP layouts)
 __device__ __forceinline__ size_t slot_plane(const GatherArgs& ga, int j, int zp, int N2) {
@@ -65,19 +68,35 @@ __device__ __forceinline__ void gather_apply(const GatherArgs& ga, size_t off, f
   const float A = ga.obja[off], ph = ga.objp[off];
   float sn, cs;
   phase_sincos(ph, &sn, &cs);
-  if (ga.d_obja) ga.d_obja[off] += fmaf(S.x, cs, S.y * sn);
+  if (ga.d_obja) {
+    const float da = fmaf(S.x, cs, S.y * sn);
+    ga.d_obja[off] = (ga.store ? 0.f : ga.d_obja[off]) + da;   // (0 + x: bitwise the accumulate into zeros)
+  }
   if (ga.d_objp) {
     float dph = A * fmaf(S.y, cs, -S.x * sn);
     if (C != 0.f) {
       const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
       dph += ga.sparse_n == 1 ? C * sg : C * powq(fabsf(ph), (float)(ga.sparse_n - 1)) * sg;
     }
-    ga.d_objp[off] += dph;
+    ga.d_objp[off] = (ga.store ? 0.f : ga.d_objp[off]) + dph;
   }
 }
+// A tile no window of the call reaches: its contribution is zero (store mode writes the zeros).
 template <int N>
 __device__ __forceinline__ bool gather_tile_skip(const GatherArgs& ga, int ty, int tx) {
-  return ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] || tx >= ga.bbox[3] + N);
+  const bool skip = ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] ||
+                                tx >= ga.bbox[3] + N);
+  if (skip && ga.store) {
+    const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;
+    for (int e = threadIdx.x; e < kGTY * kGTX; e += blockDim.x) {
+      const int y = ty + e / kGTX, x = tx + e % kGTX;
+      if (y >= ga.Ny || x >= ga.Nx) continue;
+      const size_t off = zoff + (size_t)y * ga.Nx + x;
+      if (ga.d_obja) ga.d_obja[off] = 0.f;
+      if (ga.d_objp) ga.d_objp[off] = 0.f;
+    }
+  }
+  return skip;
 }
 
 // ROWPERM: slots written by k_fused3 (N = 128), row y stored at row 2(y & 63) + (y >> 6).
@@ -297,8 +316,8 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
       const size_t off = zoff + (size_t)(r0 + r) * ga.Nx + x;
       pa[r] = ga.obja[off];
       pp[r] = ga.objp[off];
-      if (ga.d_obja) pga[r] = ga.d_obja[off];
-      if (ga.d_objp) pgp[r] = ga.d_objp[off];
+      if (ga.d_obja && !ga.store) pga[r] = ga.d_obja[off];
+      if (ga.d_objp && !ga.store) pgp[r] = ga.d_objp[off];
     }
   }
   const int np = MP ? ga.np : 1;

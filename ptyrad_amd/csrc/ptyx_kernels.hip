@@ -363,6 +363,7 @@ struct ptyx_plan {
   float* pend_dp = nullptr;
   int pend_engine = -1;
   bool pend_defer_gather = false;   // PTYX_PREP_DEFER_GATHER on the call in flight
+  bool pend_store = false;          // PTYX_PREP_GRAD_STORE served by its engine's gather
   // the last split call that deferred its object gather (ptyx_slots_export reads it): its slots,
   // pattern table and coefficients stay in the plan until the next compute call
   // ptyx_plan_slot_target: the next deferring call writes its slots straight into the caller's
@@ -372,6 +373,7 @@ struct ptyx_plan {
   bool use_tgt = false;             // the call in flight writes its slots to slot_tgt
   float* slots_at = nullptr;        // where the last deferring call's slots are
   bool gather_deferred = false;     // set while that call's _end runs (run_fused3 skips the gather)
+  bool grad_store = false;          // PTYX_PREP_GRAD_STORE on the call in flight
   bool slots_ready = false;
   int32_t slots_n = 0;
   const int32_t* slots_idx = nullptr;
@@ -1177,6 +1179,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     g.nz = Nz;
     g.bbox = pl->bbox;   // also for Nz = 1
     g.zgrid = 1;         // every slice plane in one launch (blockIdx.y = slice)
+    g.store = pl->grad_store;
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
@@ -1336,6 +1339,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     g.nz = Nz; g.np = P; g.pstride = m.pstride;
     g.bbox = pl->bbox;
     g.zgrid = 1;
+    g.store = pl->grad_store;
     const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
     const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
     ProfScope ps(pl, kKGather, st);
@@ -1665,10 +1669,13 @@ __global__ void k_step_select(const int32_t* idx_all, const int64_t* istart, con
     float* s = steps[t];
     *s = *s + 1.0f;
   }
-  float4* g4 = reinterpret_cast<float4*>(grad);
-  const int64_t n4 = grad_n >> 2;
+  // scalar head up to 16-byte alignment, float4 body, scalar tail
+  const int64_t head = std::min<int64_t>(grad_n, ((16 - (reinterpret_cast<uintptr_t>(grad) & 15)) & 15) >> 2);
+  if (t < head) grad[t] = 0.f;
+  float4* g4 = reinterpret_cast<float4*>(grad + head);
+  const int64_t n4 = (grad_n - head) >> 2;
   for (int64_t i = t; i < n4; i += stride) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t i = 4 * n4 + t; i < grad_n; i += stride) grad[i] = 0.f;
+  for (int64_t i = head + 4 * n4 + t; i < grad_n; i += stride) grad[i] = 0.f;
 }
 __global__ __launch_bounds__(256) void k_step_store(const float* terms, int nb, const int64_t* rstart, int64_t* cnt,
                                                     float* terms_all) {
@@ -1687,8 +1694,8 @@ extern "C" int ptyx_step_select(void* stream, const int32_t* idx_all, const int6
     return fail(PTYX_EINVAL, "ptyx_step_select: null pointer or negative size");
   if (n_steps < 0 || n_steps > 256 || (n_steps && !steps))
     return fail(PTYX_EINVAL, "ptyx_step_select: steps must be a device array of at most 256 pointers");
-  if (reinterpret_cast<uintptr_t>(grad) % 16)
-    return fail(PTYX_EINVAL, "ptyx_step_select: grad must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(grad) % 4)
+    return fail(PTYX_EINVAL, "ptyx_step_select: grad must be 4-byte aligned");
   const int64_t work = std::max<int64_t>(n, (grad_n + 3) / 4);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (work + 255) / 256));
   hipLaunchKernelGGL(k_step_select, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx_all, istart, cnt, n,
@@ -1761,7 +1768,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER)) > PTYX_PREP_REUSE || cfg->prep < 0)
+  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE)) > PTYX_PREP_REUSE ||
+      cfg->prep < 0)
     return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
   a.boff = boff;
@@ -1821,6 +1829,24 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (pl->slab_live && *engine != kEngStripe)
     return fail(PTYX_EINVAL, "a deferred stripe probe gradient awaits the step's last piece on this plan");
   *out = a;
+  return PTYX_OK;
+}
+
+// PTYX_PREP_GRAD_STORE: the register engines' gathers overwrite the object gradient (returns
+// true: pl->grad_store for the call); any other engine accumulates, so its two arrays are cleared
+// on the stream first.
+static int grad_store_setup(ptyx_plan* pl, int engine, const ptyx_grads& gz, hipStream_t st, bool* gather_store) {
+  *gather_store = false;
+  if (engine == kEngFused3 || engine == kEngFmm) {
+    *gather_store = true;
+    return PTYX_OK;
+  }
+  const size_t bytes = sizeof(float) * (size_t)pl->d.O * pl->d.Nz * pl->d.Ny * pl->d.Nx;
+  for (float* p : {gz.d_obja, gz.d_objp}) {
+    if (!p) continue;
+    hipError_t e = hipMemsetAsync(p, 0, bytes, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(object gradient, PTYX_PREP_GRAD_STORE)");
+  }
   return PTYX_OK;
 }
 
@@ -1926,10 +1952,16 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   pl->slots_ready = false;
   ptyx_loss_cfg c = *cfg;
   const bool defer = (c.prep & PTYX_PREP_DEFER_PROBE) != 0;
-  c.prep &= ~PTYX_PREP_DEFER_PROBE;
+  const bool store = (c.prep & PTYX_PREP_GRAD_STORE) != 0;
+  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_GRAD_STORE);
   resolve_prep(pl, in, engine, &c);
-  return run_call(pl, in, a, &c, gz, engine, reinterpret_cast<hipStream_t>(stream), loss_terms, kPhaseAll, nullptr,
-                  defer);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  bool gstore = false;
+  if (store && (rc = grad_store_setup(pl, engine, gz, st, &gstore))) return rc;
+  pl->grad_store = gstore;
+  rc = run_call(pl, in, a, &c, gz, engine, st, loss_terms, kPhaseAll, nullptr, defer);
+  pl->grad_store = false;
+  return rc;
 }
 
 extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
@@ -1950,10 +1982,16 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;
   const bool defer_gather = (c.prep & PTYX_PREP_DEFER_GATHER) != 0;
-  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER);   // a split call is one piece: it closes its own probe gradient
+  const bool store = (c.prep & PTYX_PREP_GRAD_STORE) != 0;
+  // a split call is one piece: it closes its own probe gradient
+  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE);
   if (defer_gather && engine != kEngFused3)
     return fail(PTYX_EUNSUPPORTED, "PTYX_PREP_DEFER_GATHER needs the k_fused3 / k_fused3ms engine "
                                    "(ptyx_plan_slot_floats > 0, f32 DPs, the call within the register capacity)");
+  if (defer_gather && store)
+    return fail(PTYX_EINVAL, "PTYX_PREP_GRAD_STORE with PTYX_PREP_DEFER_GATHER: the slot gather accumulates");
+  bool gstore = false;
+  if (store && (rc = grad_store_setup(pl, engine, gz, reinterpret_cast<hipStream_t>(stream), &gstore))) return rc;
   pl->slots_ready = false;
   pl->use_tgt = defer_gather && pl->slot_tgt && n_idx <= pl->slot_tgt_cap;
   resolve_prep(pl, in, engine, &c);
@@ -1968,6 +2006,7 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   pl->pend_idx = idx; pl->pend_boff = boff; pl->pend_nb = n_batches; pl->pend_n = n_idx;
   pl->pend_dp = dp_out; pl->pend_engine = engine;
   pl->pend_defer_gather = defer_gather;
+  pl->pend_store = gstore;
   return PTYX_OK;
 }
 
@@ -1985,9 +2024,11 @@ extern "C" int ptyx_forward_loss_grad_end(ptyx_plan* pl, void* stream, const dou
   if (engine != pl->pend_engine) return fail(PTYX_EINVAL, "internal: engine changed between _begin and _end");
   DeviceGuard dg(pl->device);
   pl->gather_deferred = pl->pend_defer_gather;
+  pl->grad_store = pl->pend_store;
   rc = run_call(pl, &pl->pend_in, a, &pl->pend_cfg, pl->pend_gz, engine, reinterpret_cast<hipStream_t>(stream),
                 loss_terms, kPhaseEnd, const_cast<double*>(batch_sums), false);
   pl->gather_deferred = false;
+  pl->grad_store = false;
   if (rc == PTYX_OK && pl->pend_defer_gather) {
     pl->slots_ready = true;
     pl->slots_n = pl->pend_n;

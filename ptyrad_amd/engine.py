@@ -258,7 +258,8 @@ class Plan:
             off = np.asarray(batch_offsets.cpu() if isinstance(batch_offsets, torch.Tensor) else batch_offsets,
                              dtype=np.int64)
             if off[-1] - off[0] > cap and np.max(np.diff(off)) <= cap:
-                return self._chunked(t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch)
+                return self._chunked(t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch,
+                                     store=bool(prep & _lib.PTYX_PREP_GRAD_STORE))
         idx_t = self._idx(idx)
         off_t = self._idx(batch_offsets)
         n, nb = int(idx_t.numel()), int(off_t.numel()) - 1
@@ -306,9 +307,10 @@ class Plan:
         """Patterns per call the register-resident engines take (0: none for this geometry)."""
         return int(self.lib.ptyx_plan_register_capacity(self._h))
 
-    def _chunked(self, t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch):
+    def _chunked(self, t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch, store=False):
         """Split a call at mini-batch boundaries into groups of <= cap patterns (each batch keeps
-        its own normalisation; gradients accumulate across the group calls)."""
+        its own normalisation; gradients accumulate across the group calls; with ``store`` the
+        first piece overwrites the object gradient, PTYX_PREP_GRAD_STORE)."""
         nb = off.size - 1
         if loss_terms is None:
             loss_terms = torch.empty((nb, 5), dtype=torch.float32, device=self.device)
@@ -326,6 +328,8 @@ class Plan:
             prep = _lib.PTYX_PREP_FULL if i == 0 else _lib.PTYX_PREP_REUSE
             if i < len(pieces) - 1:
                 prep |= _lib.PTYX_PREP_DEFER_PROBE
+            if i == 0 and store:
+                prep |= _lib.PTYX_PREP_GRAD_STORE
             sub_off = (off[b0:b1 + 1] - off[b0]).astype(np.int32)
             sub_idx = idx_t[int(off[b0]):int(off[b1])]
             sub_dp = None if dp_out is None else dp_out[int(off[b0]):int(off[b1])]

@@ -124,6 +124,7 @@ class StepGraphs:
         self.captures = 0
         self.replays = 0
         self.eager = 0
+        self._store_from = 0      # floats at the flat buffer's head a whole-batch step's call overwrites
 
     # ---------------------------------------------------------------- per-iteration tables
     def _tables(self, steps, ga, dev):
@@ -182,8 +183,12 @@ class StepGraphs:
         step_ts = optimizer._step_tensors() if hasattr(optimizer, "_step_tensors") else []
         sp = self._step_ptrs(key, step_ts, flat_grad.device) if 0 < len(step_ts) <= 256 else None
         # the step's indices (device counter) + zeroed gradient buffer (and terms tail), one launch
+        # a whole-batch step's engine call overwrites the object gradient at the buffer's head
+        # (PTYX_PREP_GRAD_STORE): only the rest is zeroed
+        z0 = 0 if split else self._store_from
+        zbuf = flat_grad[z0:]
         _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
-                                        _ptr(flat_grad), int(flat_grad.numel()), None if sp is None else _ptr(sp),
+                                        _ptr(zbuf), int(zbuf.numel()), None if sp is None else _ptr(sp),
                                         0 if sp is None else len(step_ts)))
         try:
             self._body_rest(model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
@@ -214,7 +219,8 @@ class StepGraphs:
                                          slot_exchange=SlotExchange(ctx, scap) if scap else None, _rows_checked=True)
         else:
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                         max_batch=max(key[0]), _rows_checked=True)
+                                         max_batch=max(key[0]), _rows_checked=True,
+                                         prep=_lib.PTYX_PREP_GRAD_STORE if self._store_from else 0)
         if extra:
             terms = ctx.terms_tail(flat_grad, extra, G)
             if mine_t is not None:
@@ -266,6 +272,14 @@ class StepGraphs:
                      ("tilts", model._tilts())):
             if p is not None and any(p is q for q in live):
                 grads[k] = p.grad
+        # the object gradients at the head of the flat buffer (live order): a whole-batch step's
+        # call overwrites them, so its select launch zeroes only what follows
+        self._store_from = 0
+        for p in live:
+            if p is model.opt_obja or p is model.opt_objp:
+                self._store_from += p.numel()
+            else:
+                break
         if model.shift_probes and any(model.opt_probe_pos_shifts is q for q in live):
             grads["shifts"] = model.opt_probe_pos_shifts.grad
         base = model._base()

@@ -119,6 +119,52 @@ def test_split_batches_sum_to_whole_call(geom, world):
     assert rel(got["shifts"], og["shifts"]) < TOL_SH
 
 
+@pytest.mark.parametrize("geom", ["fused3", "fused3ms", "fmm", "stripe", "stripe_o2", "two_pass"])
+def test_grad_store_overwrites_the_object_gradient(geom):
+    """PTYX_PREP_GRAD_STORE (ABI 208): the call overwrites d_obja / d_objp with its own gradient —
+    whatever they held before — and accumulates the probe / position gradients as usual.  Every
+    engine (the register engines' gathers store, including the tiles no window reaches; the others
+    clear the arrays first): bitwise the accumulate-into-zeros call; and, split over two calls at
+    mini-batch boundaries (the Plan's pieces), only the first piece stores."""
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import LossConfig, batch_offsets
+    device = dev()
+    d = problem(*GEOMS[geom], seed=31)
+    t = tensors(d, device)
+    cfg = LossConfig.from_loss_params(d["loss_params"])
+    batches = [np.array([3, 0, 9, 7, 11]), np.array([5, 1, 10, 2]), np.array([4, 8, 6])]
+    idx, off = np.concatenate(batches), batch_offsets(batches)
+    plan = plan_for(d, device)
+    ref = zero_grads(t)
+    plan.forward_loss_grad(t, idx, off, cfg, ref)
+    got = zero_grads(t)
+    for k in ("obja", "objp"):
+        got[k].fill_(123.0)                    # stale values: must not survive
+    got["probe"].copy_(ref["probe"])           # these accumulate: start from a known value
+    got["shifts"].copy_(ref["shifts"])
+    plan.forward_loss_grad(t, idx, off, cfg, got, prep=_lib.PTYX_PREP_GRAD_STORE)
+    torch.cuda.synchronize()
+    atomics = geom in ("stripe", "two_pass")     # f32 object atomics: last bits follow arrival order
+    for k in ("obja", "objp"):
+        if atomics:
+            assert rel(got[k].cpu().numpy(), ref[k].cpu().numpy()) < 1e-6, k
+        else:
+            assert torch.equal(got[k], ref[k]), k
+    for k in ("probe", "shifts"):
+        assert torch.equal(got[k], 2 * ref[k]) or rel(got[k].cpu().numpy(), 2 * ref[k].cpu().numpy()) < 1e-6, k
+    # pieces: a plan whose capacity splits the call; the first piece stores, the second accumulates
+    small = plan_for(d, device, max_patterns=9)
+    pc = zero_grads(t)
+    small.forward_loss_grad(t, idx, off, cfg, pc)
+    ps = zero_grads(t)
+    for k in ("obja", "objp"):
+        ps[k].fill_(-7.0)
+    small.forward_loss_grad(t, idx, off, cfg, ps, prep=_lib.PTYX_PREP_GRAD_STORE)
+    torch.cuda.synchronize()
+    for k in ("obja", "objp"):
+        assert rel(ps[k].cpu().numpy(), pc[k].cpu().numpy()) < 1e-6, k
+
+
 def test_plan_refuses_work_between_begin_and_end():
     from ptyrad_amd import _lib
     from ptyrad_amd.engine import LossConfig, batch_offsets
