@@ -8,7 +8,7 @@ O="$R/gpurun_out/r06/${1:-c}"
 mkdir -p "$O"
 cd "$R"
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_stepgraph.py tests/test_gpu_fullsize.py -x -v --timeout 180 --timeout-method thread > "$O/targeted.log" 2>&1 &&
+timeout -k 10 500 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_stepgraph.py tests/test_gpu_fullsize.py tests/test_gpu_model.py -x -v --timeout 180 --timeout-method thread > "$O/targeted.log" 2>&1 &&
 echo "targeted: $(tail -1 "$O/targeted.log")" &&
 timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 180 --timeout-method thread > "$O/gpu_tests.log" 2>&1 &&
 echo "suite: $(tail -1 "$O/gpu_tests.log")" &&
