@@ -110,6 +110,7 @@ class StepGraphs:
     """Captured optimizer steps of one (model, optimizer, loss_fn), keyed by step shape."""
 
     MAX_GRAPHS = 16               # captured steps kept (insertion order; the oldest is dropped)
+    STORE = True                  # whole-batch steps' calls overwrite the object gradient (A/B switch)
 
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
@@ -275,7 +276,7 @@ class StepGraphs:
         # the object gradients at the head of the flat buffer (live order): a whole-batch step's
         # call overwrites them, so its select launch zeroes only what follows
         self._store_from = 0
-        for p in live:
+        for p in (live if self.STORE else ()):
             if p is model.opt_obja or p is model.opt_objp:
                 self._store_from += p.numel()
             else:
