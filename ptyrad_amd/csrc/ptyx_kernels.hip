@@ -386,6 +386,20 @@ struct ptyx_plan {
   mutable std::vector<ProfRec> recs;
 };
 
+// Fill n 32-bit words with v on the stream: a kernel, not hipMemsetAsync — a memset captured into a
+// hipGraph (graph-replayed optimizer steps) was measured to leave a buffer's unaligned 8-byte tail
+// untouched on replay (the PTYX_PREP_GRAD_STORE clear of a 19,208-byte object plane,
+// tools/diag_store.py), so every in-stream fill of the engine is this kernel.
+__global__ void k_fill32(uint32_t* p, int64_t n, uint32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+static int fill32(void* p, int64_t n, uint32_t v, hipStream_t st) {
+  if (n <= 0) return PTYX_OK;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+  hipLaunchKernelGGL(k_fill32, dim3(blocks), dim3(256), 0, st, reinterpret_cast<uint32_t*>(p), n, v);
+  return launch_status("k_fill32 launch");
+}
+
 static int busy(const ptyx_plan* pl) {
   return pl->pend ? fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting for its _end on this plan") : 0;
 }
@@ -1014,8 +1028,8 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
                          f3::TableCheck{a.err, a.mrow, a.mrows});
   }
   if (!small) {
-    hipError_t e = hipMemsetAsync(pl->segbid, 0xFF, sizeof(int) * (size_t)nseg, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(segbid)");
+    int rc0 = fill32(pl->segbid, nseg, 0xFFFFFFFFu, st);
+    if (rc0) return rc0;
   }
   return launch_status("register engine preparation");
 }
@@ -1156,8 +1170,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     // candidate bins of the gather: the patterns by object tile of their window origin
     ProfScope ps(pl, kKTable, st);
     const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
-    hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
-    if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+    if (int rc2 = fill32(pl->bcnt, pl->nbins, 0u, st)) return rc2;
     const dim3 gn((a.n_idx + 255) / 256);
     hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
@@ -1321,8 +1334,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   if ((gz.d_obja || gz.d_objp) && bins) {
     ProfScope ps(pl, kKTable, st);
     const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
-    hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
-    if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+    if (int rc2 = fill32(pl->bcnt, pl->nbins, 0u, st)) return rc2;
     const dim3 gn((a.n_idx + 255) / 256);
     hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
@@ -1562,8 +1574,7 @@ static int run_stripe(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
     {
       ProfScope ps(pl, kKTable, st);
-      hipError_t e2 = hipMemsetAsync(pl->bcnt, 0, sizeof(int) * (size_t)pl->nbins, st);
-      if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(bcnt)");
+      if (int rc2 = fill32(pl->bcnt, pl->nbins, 0u, st)) return rc2;
       const dim3 gn((n + 255) / 256);
       hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, n, tiles_x, pl->bcnt, pl->bkey);
       hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
@@ -1841,11 +1852,10 @@ static int grad_store_setup(ptyx_plan* pl, int engine, const ptyx_grads& gz, hip
     *gather_store = true;
     return PTYX_OK;
   }
-  const size_t bytes = sizeof(float) * (size_t)pl->d.O * pl->d.Nz * pl->d.Ny * pl->d.Nx;
+  const int64_t n = (int64_t)pl->d.O * pl->d.Nz * pl->d.Ny * pl->d.Nx;
   for (float* p : {gz.d_obja, gz.d_objp}) {
     if (!p) continue;
-    hipError_t e = hipMemsetAsync(p, 0, bytes, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(object gradient, PTYX_PREP_GRAD_STORE)");
+    if (int rc = fill32(p, n, 0u, st)) return rc;
   }
   return PTYX_OK;
 }
