@@ -386,6 +386,12 @@ struct ptyx_plan {
   mutable std::vector<ProfRec> recs;
 };
 
+static int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, what);
+  return PTYX_OK;
+}
+
 // Fill n 32-bit words with v on the stream: a kernel, not hipMemsetAsync — a memset captured into a
 // hipGraph (graph-replayed optimizer steps) was measured to leave a buffer's unaligned 8-byte tail
 // untouched on replay (the PTYX_PREP_GRAD_STORE clear of a 19,208-byte object plane,
@@ -899,12 +905,6 @@ static void launch_probe_finalize(const ptyx_plan* pl, const KArgs& a, hipStream
                        per, pl->Gsum);
   }
   launch_probe_fin(pl, a, st, d_probe, pl->d.P);
-}
-
-static int launch_status(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, what);
-  return PTYX_OK;
 }
 
 // shared with the other translation units of libptyx.so (ptyx_abi.hpp)
