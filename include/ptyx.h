@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 208
+#define PTYX_ABI_VERSION 209
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -71,6 +71,14 @@ extern "C" {
  * clear the two arrays on the stream before they accumulate.  The other gradients accumulate as
  * usual.  (A graph-replayed optimizer step zeroes only the rest of its flat gradient buffer.) */
 #define PTYX_PREP_GRAD_STORE 16
+/* PTYX_PREP_FUSED_ADAM (ptyx_forward_loss_grad only, ABI 209): the call ends with the optimizer step
+ * that ptyx_plan_set_adam registered on the plan (consumed by this call): what ptyx_adam_step (or
+ * ptyx_adam_step_store) with those arguments would do right after the call, on the same stream.
+ * The k_fused3 engine's small calls (one mini-batch per optimizer step) fold it into their epilogue
+ * (k_gather_adam: the object gather, the probe gradient's row pass and the update of every tensor
+ * in one launch); any other call issues the ordinary k_adam launch after its own epilogue.  Either
+ * way the gradients are written as without the flag, and the results are bitwise the same. */
+#define PTYX_PREP_FUSED_ADAM 32
 /* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
  * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
  * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
@@ -451,6 +459,16 @@ int ptyx_adam_step_store(void *stream, int32_t n, float *const *params, const fl
                          const int64_t *numels, const double *lrs, double beta1, double beta2, double eps,
                          double weight_decay, int32_t flags, const float *terms, int32_t nb, const int64_t *rstart,
                          int64_t *cnt, float *terms_all);
+
+/* Registers the optimizer step the plan's next ptyx_forward_loss_grad call with PTYX_PREP_FUSED_ADAM
+ * takes (arguments as ptyx_adam_step's; the host arrays are copied, the device pointers must stay
+ * valid until that call).  terms non-NULL: also what ptyx_step_store(stream, terms, nb, rstart,
+ * cnt, terms_all) does (ptyx_adam_step_store).  A later ptyx_plan_set_adam replaces it. */
+int ptyx_plan_set_adam(ptyx_plan *plan, int32_t n, float *const *params, const float *const *grads,
+                       float *const *exp_avgs, float *const *exp_avg_sqs, const float *const *steps,
+                       const int64_t *numels, const double *lrs, double beta1, double beta2, double eps,
+                       double weight_decay, int32_t flags, const float *terms, int32_t nb, const int64_t *rstart,
+                       int64_t *cnt, float *terms_all);
 
 /* Patterns one ptyx_forward_loss_grad call may hold and still run on the plan's fast engine:
  * the register-resident engines' slot capacity (k_fused3 / k_fused3ms / mixed-state), the stripe

@@ -160,14 +160,17 @@ __device__ __forceinline__ void tail_cols_ifft(float2 acc, int i, const float2* 
   line_pass<N, 256, P1::R2, P1::R1, +1, 2>(T, s_tw, 2);
   tmp_plane[f * N + i + 64 * line] = T[LT::off(line, f)];
 }
-// grid (N / kPrLinesT, P), block 256: rows l0 … l0 + 7 of plane p, d_probe += F⁻¹_rows(tmp)/N²
-__global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float2* d_probe, const float2* twg) {
+// Rows l0 … l0 + kPrLinesT − 1 of probe plane p (256 threads): g = d_probe + F⁻¹_rows(tmp)/N² per
+// element, handed to epi(pointer into d_probe, element index in the plane stack, g), which stores it
+// (k_probe_rows_acc) or also takes the optimizer step on it (k_gather_adam, ptyx_stepfuse.hpp).
+template <class Epi>
+__device__ __forceinline__ void probe_rows_block(const float2* tmp, float2* d_probe, const float2* twg, int l0, int p,
+                                                 Epi epi) {
   constexpr int N = kN;
   using LT = LineTile<N, kPrLinesT>;
   using P1 = Plan1D<N>;
   __shared__ float2 s_tw[N];
   __shared__ float2 T[LT::kElems];
-  const int l0 = blockIdx.x * kPrLinesT, p = blockIdx.y;
   const float2* s = tmp + (size_t)p * N * N;
   float2* d = d_probe + (size_t)p * N * N;
   for (int k = threadIdx.x; k < N; k += 256) s_tw[k] = twg[k];
@@ -177,10 +180,16 @@ __global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float
   line_pass<N, 256, P1::R2, P1::R1, +1, kPrLinesT>(T, s_tw, kPrLinesT);
   constexpr float inv_n2 = 1.0f / (float)(N * N);
   for (int e = threadIdx.x; e < kPrLinesT * N; e += 256) {
-    float2* dp = d + (size_t)(l0 + e / N) * N + e % N;
+    const size_t el = (size_t)(l0 + e / N) * N + e % N;
+    float2* dp = d + el;
     const float2 v = T[LT::off(e / N, e % N)];
-    *dp = cadd(*dp, make_float2(v.x * inv_n2, v.y * inv_n2));
+    epi(dp, (size_t)p * N * N + el, cadd(*dp, make_float2(v.x * inv_n2, v.y * inv_n2)));
   }
+}
+// grid (N / kPrLinesT, P), block 256: rows l0 … l0 + 7 of plane p, d_probe += F⁻¹_rows(tmp)/N²
+__global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float2* d_probe, const float2* twg) {
+  probe_rows_block(tmp, d_probe, twg, blockIdx.x * kPrLinesT, blockIdx.y,
+                   [](float2* dp, size_t, float2 g) { *dp = g; });
 }
 
 template <bool KL>

@@ -106,21 +106,17 @@ struct BinReach {
   static constexpr int rows = (N + kGTY - 1) / kGTY + 1, cols = (N + kGTX - 1) / kGTX + 1, n = rows * cols;
 };
 
-// GW: waves per tile (kGWaves for dense calls; 4 when a tile has only a few candidates, so that
-// the per-tile fixed cost, the wave-partial reduction, stays small)
-template <int N, bool ROWPERM = false, int GW = kGWaves, bool MP = false, bool SPLIT = false>
-__global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
+// A tile's sums S (s_acc) and sparse counts C (s_cnt) over its candidates, in fixed order (the
+// workgroup's GW waves; LDS results valid after the final barrier).  Tile (tyi, txi), slot plane zp;
+// split s of S.
+template <int N, bool ROWPERM, int GW, bool MP, bool SPLIT>
+__device__ __forceinline__ void gather_tile_sums(const GatherArgs& ga, int tyi, int txi, int zp, float2* s_acc,
+                                                 float* s_cnt) {
   constexpr int N2 = N * N;
   constexpr int NB = BinReach<N>::n;
-  __shared__ float2 s_acc[kGTY * kGTX];
-  __shared__ float s_cnt[kGTY * kGTX];
   __shared__ int s_b0[NB], s_pre[NB + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
-  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;                        // slot plane
-  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;   // object plane
   const int ty = tyi * kGTY, tx = txi * kGTX;
-  if (gather_tile_skip<N>(ga, ty, tx)) return;   // no window of this call touches the tile: its contribution is zero
   const int S = SPLIT ? (int)gridDim.z : 1, s = SPLIT ? (int)blockIdx.z : 0;
   int total = ga.n;
   if (ga.boff) {
@@ -228,6 +224,21 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
     }
     __syncthreads();
   }
+}
+
+// GW: waves per tile (kGWaves for dense calls; 4 when a tile has only a few candidates, so that
+// the per-tile fixed cost, the wave-partial reduction, stays small)
+template <int N, bool ROWPERM = false, int GW = kGWaves, bool MP = false, bool SPLIT = false>
+__global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
+  __shared__ float2 s_acc[kGTY * kGTX];
+  __shared__ float s_cnt[kGTY * kGTX];
+  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
+  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;                        // slot plane
+  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;   // object plane
+  const int ty = tyi * kGTY, tx = txi * kGTX;
+  if (gather_tile_skip<N>(ga, ty, tx)) return;   // no window of this call touches the tile: its contribution is zero
+  gather_tile_sums<N, ROWPERM, GW, MP, SPLIT>(ga, tyi, txi, zp, s_acc, s_cnt);
+  const int S = SPLIT ? (int)gridDim.z : 1, s = SPLIT ? (int)blockIdx.z : 0;
   if constexpr (SPLIT) {   // this split's tile sums; k_obj_gather_fin adds the splits in order
     const size_t pb = (((size_t)blockIdx.y * gridDim.x + blockIdx.x) * S + s) * (kGTY * kGTX);
     for (int e = threadIdx.x; e < kGTY * kGTX; e += 64 * GW) {

@@ -28,6 +28,7 @@
 #include "ptyx_fmm.hpp"
 #include "ptyx_stripe.hpp"
 #include "ptyx_abi.hpp"
+#include "ptyx_adam.hpp"
 #include "ptyx_genops.hpp"
 
 namespace ptyx {
@@ -193,6 +194,7 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
 
 
 #include "ptyx_gather.hpp"
+#include "ptyx_stepfuse.hpp"
 
 // d_H += Σ over workgroup propagator-gradient slabs, fixed order.
 __global__ void k_hslab_reduce(const float2* hslab, int nwg, int n2, float2* d_H) {
@@ -245,11 +247,11 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneFmmHoldH, kTuneCount };
+               kTuneFmmHoldH, kTuneFuseAdam, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
-                                            "gen_wg_per_cu", "gather_rows", "fmm_hold_h"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1};
+                                            "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -377,6 +379,14 @@ struct ptyx_plan {
   bool slots_ready = false;
   int32_t slots_n = 0;
   const int32_t* slots_idx = nullptr;
+  // ptyx_plan_set_adam: the optimizer step the next PTYX_PREP_FUSED_ADAM call takes (one-shot)
+  bool fadam_set = false;
+  bool fadam_on = false;            // the call in flight takes it
+  bool fadam_done = false;          // its engine fused it into the epilogue (else a k_adam launch follows)
+  std::vector<opt::AdamTensor> fadam_ts;
+  opt::AdamHyper fadam_h{};
+  bool fadam_store = false;
+  opt::StepStore fadam_ss{};
   // ptyx_profile_begin/end: HIP events around every launch (kind, start, stop)
   bool prof = false;
   struct ProfRec {
@@ -412,7 +422,7 @@ static int busy(const ptyx_plan* pl) {
 
 enum KernelKind {
   kKSpectrum, kKForward, kKFinalize, kKAdjoint, kKSlabReduce, kKProbeFinalize, kKFused, kKTable, kKGather,
-  kKObjPrep, kKPack, kKS1, kKS2, kKS3, kKS4, kKS5, kKFmmFwd, kKFmmLoss, kKFmmAdj, kKCount
+  kKObjPrep, kKPack, kKS1, kKS2, kKS3, kKS4, kKS5, kKFmmFwd, kKFmmLoss, kKFmmAdj, kKGatherAdam, kKCount
 };
 static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward",        "k_finalize",
                                                   "k_adjoint",        "k_slab_reduce",    "k_probe_finalize",
@@ -420,7 +430,7 @@ static const char* const kKernelNames[kKCount] = {"k_probe_spectrum", "k_forward
                                                   "k_obj_prep",       "k_pack",           "k_s1",
                                                   "k_s2",             "k_s3",             "k_s4",
                                                   "k_s5",             "k_fmm_fwd",        "k_fmm_loss",
-                                                  "k_fmm_adj"};
+                                                  "k_fmm_adj",        "k_gather_adam"};
 
 // Brackets one launch with HIP events on its stream while the plan is profiling.
 struct ProfScope {
@@ -1121,6 +1131,82 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
   return launch_status("k_fused3 launch");
 }
 
+// PTYX_PREP_FUSED_ADAM: k_gather_adam's arguments for a small single-slice k_fused3 call, or false
+// (then the call runs its ordinary epilogue and the registered step is a k_adam launch after it).
+// The Adam tensors that ARE obja / objp (parameter = the call's object, gradient = its d_obja /
+// d_objp) take their step in the tile blocks, the probe's in the probe-row blocks; every other
+// tensor must fit one k_adam launch and must not overlap what those blocks write.
+static bool fused_adam_setup(const ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_grads& gz,
+                             const GatherArgs& g, int tiles, FusedAdamArgs* f) {
+  constexpr int N = 128;
+  const ptyx_dims& d = pl->d;
+  if (d.O != 1 || d.Nz != 1 || d.P != 1) return false;
+  const int64_t nobj = (int64_t)d.Ny * d.Nx, nprobe = 2LL * N * N;
+  const bool probe_rows = gz.d_probe && a.shift;   // (else the probe gradient is final before the launch)
+  *f = FusedAdamArgs{};
+  f->ga = g;
+  f->h = pl->fadam_h;
+  f->tiles = tiles;
+  std::vector<opt::AdamTensor> rest;
+  struct Span {
+    uintptr_t lo, hi;
+  };
+  std::vector<Span> owned;   // what the tile / probe blocks read or write
+  const auto span = [](const void* p, int64_t n) {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+    return Span{lo, lo + (uintptr_t)(4 * n)};
+  };
+  owned.push_back(span(a.obja, nobj));
+  owned.push_back(span(a.objp, nobj));
+  if (gz.d_obja) owned.push_back(span(gz.d_obja, nobj));
+  if (gz.d_objp) owned.push_back(span(gz.d_objp, nobj));
+  if (probe_rows) owned.push_back(span(gz.d_probe, nprobe));
+  for (const opt::AdamTensor& t : pl->fadam_ts) {
+    if (!t.numel) continue;
+    int plane = -1;
+    if (t.numel == nobj && gz.d_obja && t.g == gz.d_obja && t.p == a.obja) plane = 0;
+    else if (t.numel == nobj && gz.d_objp && t.g == gz.d_objp && t.p == a.objp) plane = 1;
+    if (plane >= 0) {
+      if (f->om[plane]) return false;   // (the same tensor twice)
+      f->op[plane] = t.p; f->om[plane] = t.m; f->ov[plane] = t.v; f->ostep[plane] = t.step; f->olr[plane] = t.lr;
+      owned.push_back(span(t.m, nobj));
+      owned.push_back(span(t.v, nobj));
+      continue;
+    }
+    if (probe_rows && t.numel == nprobe && t.g == gz.d_probe && t.p == in->probe) {
+      if (f->pp) return false;
+      f->pp = t.p; f->pm = t.m; f->pv = t.v; f->pstep = t.step; f->plr = t.lr;
+      owned.push_back(span(t.p, nprobe));
+      owned.push_back(span(t.m, nprobe));
+      owned.push_back(span(t.v, nprobe));
+      continue;
+    }
+    rest.push_back(t);
+  }
+  for (const opt::AdamTensor& t : rest)
+    for (const void* q : {(const void*)t.p, (const void*)t.g, (const void*)t.m, (const void*)t.v}) {
+      const Span r = span(q, t.numel);
+      for (const Span& o : owned)
+        if (r.lo < o.hi && o.lo < r.hi) return false;
+    }
+  const std::vector<opt::AdamArgs> packs = opt::adam_pack(rest, f->h);
+  if (packs.size() > 1) return false;
+  if (!packs.empty()) {
+    f->rest = packs[0];
+    f->rblocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, f->rest.off[f->rest.nt] / opt::kChunk));
+  } else {
+    f->rest.h = f->h;
+  }
+  if (pl->fadam_store) opt::adam_set_store(f->rest, pl->fadam_ss);
+  if (probe_rows) {
+    f->pblocks = N / f3::kPrLinesT;
+    f->ptmp = pl->slab;
+    f->d_probe = reinterpret_cast<float2*>(gz.d_probe);
+    f->twg = pl->twg;
+  }
+  return true;
+}
+
 static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
                       const ptyx_grads& gz, hipStream_t st, float* loss_terms, int ph, double* bsums) {
   constexpr int N = 128, N2 = N * N;
@@ -1177,26 +1263,35 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
+  GatherArgs g{};
+  int tiles = 0;
+  bool sparse_tiles = false;
   if (gather_here) {
-    GatherArgs g{};
     g.ogscr = pl->ogscr; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
     g.boff = bins ? pl->boff : nullptr;
     g.blist = bins ? pl->blist : nullptr;
     g.Ny = d.Ny; g.Nx = d.Nx; g.tiles_x = (d.Nx + kGTX - 1) / kGTX; g.sparse_n = sparse ? cfg->sparse_n : 1;
     g.obja = a.obja; g.objp = a.objp; g.d_obja = gz.d_obja; g.d_objp = gz.d_objp;
-    const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
     // fewer than 64 candidates per tile on average (c4's 8,192-pattern calls over 13,340 tiles:
     // ≈ 17): 4 waves a tile instead of kGWaves
-    const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
-    ProfScope ps(pl, kKGather, st);
+    sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
     g.nz = Nz;
     g.bbox = pl->bbox;   // also for Nz = 1
     g.zgrid = 1;         // every slice plane in one launch (blockIdx.y = slice)
     g.store = pl->grad_store;
+  }
+  // PTYX_PREP_FUSED_ADAM on a small single-slice call: the gather, the probe rows and the optimizer
+  // step in one launch after the probe / position sums (ptyx_stepfuse.hpp)
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  FusedAdamArgs fz{};
+  const bool fuse = pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles && g_tuning[kTuneGatherRows] != 1 &&
+                    g_tuning[kTuneFuseAdam] != 0 && fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+  if (gather_here && !fuse) {
+    ProfScope ps(pl, kKGather, st);
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
   if (!bins && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
     {
       ProfScope ps(pl, kKSlabReduce, st);
@@ -1211,14 +1306,23 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
                            out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
     }
     if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, st);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, st, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+      if (!fuse) {
+        ProfScope ps(pl, kKProbeFinalize, st);
+        hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, 1), dim3(256), 0, st, pl->slab,
+                           reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+      }
     } else if (gz.d_probe) {
       launch_probe_fin_reg(pl, a, st, gz.d_probe, 1);
     }
-    return launch_status("probe finalize launch");
+    if ((rc = launch_status("probe finalize launch"))) return rc;
   }
+  if (fuse) {
+    ProfScope ps(pl, kKGatherAdam, st);
+    hipLaunchKernelGGL((k_gather_adam<N, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+    pl->fadam_done = true;
+    return launch_status("k_gather_adam launch");
+  }
+  if (!bins && (gz.d_probe || d_shifts)) return PTYX_OK;
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);
     hipLaunchKernelGGL(f3::k_shift_apply, dim3((a.n_idx + 255) / 256), dim3(256), 0, st, a.idx, a.n_idx, a.n_scans,
@@ -1779,7 +1883,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE)) > PTYX_PREP_REUSE ||
+  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM)) >
+          PTYX_PREP_REUSE ||
       cfg->prep < 0)
     return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
@@ -1963,15 +2068,49 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   ptyx_loss_cfg c = *cfg;
   const bool defer = (c.prep & PTYX_PREP_DEFER_PROBE) != 0;
   const bool store = (c.prep & PTYX_PREP_GRAD_STORE) != 0;
-  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_GRAD_STORE);
+  const bool fadam = (c.prep & PTYX_PREP_FUSED_ADAM) != 0;
+  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM);
+  if (fadam && !pl->fadam_set) return fail(PTYX_EINVAL, "PTYX_PREP_FUSED_ADAM without ptyx_plan_set_adam");
   resolve_prep(pl, in, engine, &c);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   bool gstore = false;
   if (store && (rc = grad_store_setup(pl, engine, gz, st, &gstore))) return rc;
   pl->grad_store = gstore;
+  pl->fadam_on = fadam;
+  pl->fadam_done = false;
   rc = run_call(pl, in, a, &c, gz, engine, st, loss_terms, kPhaseAll, nullptr, defer);
   pl->grad_store = false;
+  if (fadam) {   // the registered step, consumed: fused into the epilogue, or its own launch now
+    if (!rc && !pl->fadam_done)
+      rc = opt::adam_launch(st, pl->fadam_ts, pl->fadam_h, pl->fadam_store ? &pl->fadam_ss : nullptr);
+    pl->fadam_on = pl->fadam_set = pl->fadam_done = false;
+  }
   return rc;
+}
+
+extern "C" int ptyx_plan_set_adam(ptyx_plan* pl, int32_t n, float* const* params, const float* const* grads,
+                                  float* const* exp_avgs, float* const* exp_avg_sqs, const float* const* steps,
+                                  const int64_t* numels, const double* lrs, double beta1, double beta2, double eps,
+                                  double weight_decay, int32_t flags, const float* terms, int32_t nb,
+                                  const int64_t* rstart, int64_t* cnt, float* terms_all) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (n < 0 || (n && (!params || !grads || !exp_avgs || !exp_avg_sqs || !steps || !numels || !lrs)))
+    return fail(PTYX_EINVAL, "ptyx_plan_set_adam: null array or negative count");
+  if (terms && (!rstart || !cnt || !terms_all || nb < 0))
+    return fail(PTYX_EINVAL, "ptyx_plan_set_adam: null step-store pointer or negative size");
+  std::vector<opt::AdamTensor> ts;
+  for (int i = 0; i < n; ++i) {
+    if (numels[i] < 0 || (numels[i] && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i] || !steps[i])))
+      return fail(PTYX_EINVAL, "ptyx_plan_set_adam: null tensor pointer or negative size");
+    ts.push_back({params[i], grads[i], exp_avgs[i], exp_avg_sqs[i], steps[i], lrs[i], numels[i]});
+  }
+  pl->fadam_ts = std::move(ts);
+  pl->fadam_h = opt::hyper(beta1, beta2, eps, weight_decay, flags);
+  pl->fadam_store = terms != nullptr;
+  pl->fadam_ss = opt::StepStore{terms, nb, rstart, cnt, terms_all};
+  pl->fadam_set = true;
+  return PTYX_OK;
 }
 
 extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,
@@ -1988,6 +2127,9 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   if (grads) gz = *grads;
   KArgs a{};
   int engine = kEngTwoPass;
+  if (cfg && (cfg->prep & PTYX_PREP_FUSED_ADAM))
+    return fail(PTYX_EINVAL, "PTYX_PREP_FUSED_ADAM is for ptyx_forward_loss_grad (a split step's gradients "
+                             "are complete only after the caller's exchange)");
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;

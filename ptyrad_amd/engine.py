@@ -258,6 +258,8 @@ class Plan:
             off = np.asarray(batch_offsets.cpu() if isinstance(batch_offsets, torch.Tensor) else batch_offsets,
                              dtype=np.int64)
             if off[-1] - off[0] > cap and np.max(np.diff(off)) <= cap:
+                if prep & _lib.PTYX_PREP_FUSED_ADAM:
+                    raise ValueError("PTYX_PREP_FUSED_ADAM on a call larger than one engine call")
                 return self._chunked(t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch,
                                      store=bool(prep & _lib.PTYX_PREP_GRAD_STORE))
         idx_t = self._idx(idx)
@@ -274,6 +276,13 @@ class Plan:
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
                                                    _ptr(dp_out), ctypes.byref(g)))
         return loss_terms
+
+    def set_adam(self, args, store=None):
+        """ptyx_plan_set_adam: the optimizer step the next forward_loss_grad call with
+        PTYX_PREP_FUSED_ADAM takes.  ``args``: ptyrad_amd.optim's ``fused_step_args()``; ``store``:
+        (terms, nb, rstart, cnt, terms_all) device pointers of the step's ptyx_step_store, or None."""
+        st = store if store is not None else (None, 0, None, None, None)
+        _lib.check(self.lib.ptyx_plan_set_adam(self._h, *args, *st))
 
     def loss_pacbed(self, t: dict, idx, batch_offsets, dp, loss_cfg: LossConfig, loss_terms, grad_scale=1.0,
                     want_dldi=True):

@@ -60,12 +60,10 @@ class _HipAdamMixin:
                 out.append(st["step"])
         return out
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
+    def _hip_batches(self, create=True):
+        """(batches, plain): the eligible groups' (param, state, lr) by Adam hyperparameter key, and
+        the groups torch's own step() takes.  ``create``: make missing state as step() does; else
+        None while any eligible parameter has no state yet."""
         plain = []
         batches = {}
         for group in self.param_groups:
@@ -82,31 +80,65 @@ class _HipAdamMixin:
             for p in params:
                 st = self.state[p]
                 if len(st) == 0:
+                    if not create:
+                        return None
                     st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 elif st["step"].device != p.device:   # a state loaded from a non-capturable torch Adam
+                    if not create:
+                        return None
                     st["step"] = st["step"].to(p.device, torch.float32)
                 b.append((p, st, float(group["lr"])))
-        for (b1, b2, eps, wd, decoupled, maximize, dev), items in batches.items():
+        return batches, plain
+
+    @staticmethod
+    def _launch_args(key, items):
+        """ptyx_adam_step's arguments after the stream: (n, params, grads, exp_avgs, exp_avg_sqs,
+        steps, numels, lrs, beta1, beta2, eps, weight_decay, flags)."""
+        b1, b2, eps, wd, decoupled, maximize, _ = key
+        n = len(items)
+        P = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _, _ in items])
+        G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _, _ in items])
+        M = (ctypes.c_void_p * n)(*[st["exp_avg"].data_ptr() for _, st, _ in items])
+        V = (ctypes.c_void_p * n)(*[st["exp_avg_sq"].data_ptr() for _, st, _ in items])
+        S = (ctypes.c_void_p * n)(*[st["step"].data_ptr() for _, st, _ in items])
+        NE = (ctypes.c_int64 * n)(*[p.numel() for p, _, _ in items])
+        LR = (ctypes.c_double * n)(*[lr for _, _, lr in items])
+        flags = (1 if decoupled else 0) | (2 if maximize else 0)
+        return (n, P, G, M, V, S, NE, LR, b1, b2, eps, wd, flags)
+
+    def fused_step_args(self):
+        """ptyx_plan_set_adam's arguments (after the plan) when ONE HIP launch is the whole step:
+        every group eligible, one hyperparameter batch, every state created — what a graph-replayed
+        recon_step folds into its engine call (PTYX_PREP_FUSED_ADAM, ptyrad_amd/stepgraph.py) —
+        else None.  The step counts are the caller's to advance (ptyx_step_select)."""
+        got = self._hip_batches(create=False)
+        if got is None:
+            return None
+        batches, plain = got
+        if plain or len(batches) != 1:
+            return None
+        key, items = next(iter(batches.items()))
+        return self._launch_args(key, items)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        batches, plain = self._hip_batches()
+        for key, items in batches.items():
             if not self._external_step_inc:
                 torch._foreach_add_([st["step"] for _, st, _ in items], 1)
-            n = len(items)
-            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p, _, _ in items])
-            G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _, _ in items])
-            M = (ctypes.c_void_p * n)(*[st["exp_avg"].data_ptr() for _, st, _ in items])
-            V = (ctypes.c_void_p * n)(*[st["exp_avg_sq"].data_ptr() for _, st, _ in items])
-            S = (ctypes.c_void_p * n)(*[st["step"].data_ptr() for _, st, _ in items])
-            NE = (ctypes.c_int64 * n)(*[p.numel() for p, _, _ in items])
-            LR = (ctypes.c_double * n)(*[lr for _, _, lr in items])
-            stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            flags = (1 if decoupled else 0) | (2 if maximize else 0)
+            args = self._launch_args(key, items)
+            stream = ctypes.c_void_p(torch.cuda.current_stream(key[-1]).cuda_stream)
             if self._step_store is not None and not self._step_store_done:
-                _lib.check(_lib.load().ptyx_adam_step_store(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd,
-                                                            flags, *self._step_store))
+                _lib.check(_lib.load().ptyx_adam_step_store(stream, *args, *self._step_store))
                 self._step_store_done = True
             else:
-                _lib.check(_lib.load().ptyx_adam_step(stream, n, P, G, M, V, S, NE, LR, b1, b2, eps, wd, flags))
+                _lib.check(_lib.load().ptyx_adam_step(stream, *args))
         if plain:
             saved = self.param_groups
             try:

@@ -13,7 +13,9 @@ shape.  The step's inputs are selected on the device from a per-iteration index 
 step counter that the graph itself advances, so a replay needs no host work besides the launch.
 
 Same kernels, same order, same arguments as the eager step: the trajectory is bitwise identical
-(tests/test_gpu_stepgraph.py).  The first step of every new shape runs eagerly through the same
+(tests/test_gpu_stepgraph.py).  With one rank and one HIP Adam batch the optimizer step rides in
+the engine call (PTYX_PREP_FUSED_ADAM, ABI 209: the k_fused3 engine's small calls fold the object
+gather, the probe gradient's rows and the update into one launch), bitwise the separate launch.  The first step of every new shape runs eagerly through the same
 body (it creates the optimizer state a capture must not allocate), the next is captured.
 
 Eligible: the plain fused engine path (no autograd stages, no loss_pacbed, no optimised
@@ -111,6 +113,7 @@ class StepGraphs:
 
     MAX_GRAPHS = 16               # captured steps kept (insertion order; the oldest is dropped)
     STORE = True                  # whole-batch steps' calls overwrite the object gradient (A/B switch)
+    FUSE_ADAM = True              # one-rank steps fold the optimizer step into the engine call (A/B switch)
 
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
@@ -219,9 +222,19 @@ class StepGraphs:
                                          batch_sums_reduce=ctx.allreduce_sums,
                                          slot_exchange=SlotExchange(ctx, scap) if scap else None, _rows_checked=True)
         else:
+            prep = _lib.PTYX_PREP_GRAD_STORE if self._store_from else 0
+            # one rank, the step counts already advanced, one HIP Adam launch for the whole step: the
+            # call takes the optimizer step itself (PTYX_PREP_FUSED_ADAM; the k_fused3 engine's small
+            # calls fold it into their last launch), the loss-term store included
+            fargs = optimizer.fused_step_args() if (self.FUSE_ADAM and not extra and sp is not None and
+                                                    hasattr(optimizer, "fused_step_args")) else None
+            if fargs is not None:
+                model.plan.set_adam(fargs, (_ptr(sterms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all)))
+                prep |= _lib.PTYX_PREP_FUSED_ADAM
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                         max_batch=max(key[0]), _rows_checked=True,
-                                         prep=_lib.PTYX_PREP_GRAD_STORE if self._store_from else 0)
+                                         max_batch=max(key[0]), _rows_checked=True, prep=prep)
+            if fargs is not None:
+                return
         if extra:
             terms = ctx.terms_tail(flat_grad, extra, G)
             if mine_t is not None:

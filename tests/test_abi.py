@@ -177,3 +177,14 @@ def test_tuning_keys_round_trip_without_gpu():
     lib = _lib.load()
     assert lib.ptyx_set_tuning(b"no_such_key", 1) == _lib.PTYX_EINVAL
     assert lib.ptyx_get_tuning(b"no_such_key") == -2
+
+
+def test_plan_set_adam_validates_without_gpu():
+    """ptyx_plan_set_adam (ABI 209) refuses a null plan and null arrays before touching the device;
+    a PTYX_PREP_FUSED_ADAM call needs a registered step (checked in tests/test_gpu_stepgraph.py)."""
+    lib = _lib.load()
+    rc = lib.ptyx_plan_set_adam(None, 0, None, None, None, None, None, None, None, 0.9, 0.999, 1e-8, 0.0, 0,
+                                None, 0, None, None, None)
+    assert rc == _lib.PTYX_EINVAL and b"plan is null" in lib.ptyx_last_error()
+    assert _lib.PTYX_PREP_FUSED_ADAM == 32
+    assert _lib.get_tuning("fuse_adam") == -1

@@ -225,3 +225,101 @@ def test_graphs_two_beta_groups_and_a_failed_step_keep_adam_state():
         assert se.keys() == sg_.keys()
         for k in se:
             assert torch.equal(se[k], sg_[k]), k
+
+
+def _one_step(model, opt, loss_fn, idx, mode, store):
+    """One optimizer step of the mini-batch idx through the engine call: 'off' = the call, then the
+    HIP Adam; 'fast' / 'fallback' = the call with PTYX_PREP_FUSED_ADAM (fallback: tuning fuse_adam 0,
+    the step as a k_adam launch after the epilogue).  Returns the kernels the plan launched."""
+    from ptyrad_amd import _lib
+    from ptyrad_amd.engine import LossConfig
+    t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
+         "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(), "tilts": None}
+    t.update(model._base())
+    live = [p for g in opt.param_groups for p in g["params"] if p.requires_grad]
+    for p in live:
+        p.grad = torch.zeros_like(p) if p.grad is None else p.grad.zero_()
+    grads = {k: p.grad for k, p in (("obja", model.opt_obja), ("objp", model.opt_objp), ("probe", model.opt_probe),
+                                    ("shifts", model.opt_probe_pos_shifts)) if any(p is q for q in live)}
+    if store:   # the call overwrites the object gradient: leave garbage there to prove it
+        for k in ("obja", "objp"):
+            if k in grads:
+                grads[k].fill_(3.0)
+    cfg = LossConfig.from_loss_params(loss_fn.loss_params)
+    idx_t = torch.as_tensor(np.asarray(idx), dtype=torch.int32, device=model.opt_obja.device)
+    off = np.array([0, len(idx)], np.int32)
+    with torch.no_grad():
+        for s in opt._step_tensors():
+            s.add_(1)
+    prep = _lib.PTYX_PREP_GRAD_STORE if store else 0
+    opt._external_step_inc = True
+    _lib.set_tuning("fuse_adam", 0 if mode == "fallback" else -1)
+    model.plan.profile_begin()
+    try:
+        if mode == "off":
+            model.plan.forward_loss_grad(t, idx_t, off, cfg, grads, prep=prep)
+            opt.step()
+        else:
+            model.plan.set_adam(opt.fused_step_args())
+            model.plan.forward_loss_grad(t, idx_t, off, cfg, grads, prep=prep | _lib.PTYX_PREP_FUSED_ADAM)
+    finally:
+        prof = model.plan.profile_end()
+        opt._external_step_inc = False
+        _lib.set_tuning("fuse_adam", -1)
+    torch.cuda.synchronize()
+    return prof
+
+
+@pytest.mark.parametrize("store", [False, True])
+def test_fused_adam_call_bitwise_the_call_then_adam(store):
+    """PTYX_PREP_FUSED_ADAM (ABI 209): the k_fused3 small call with the optimizer step folded into
+    its last launch (k_gather_adam: object gather + Adam of obja / objp per tile, the probe
+    gradient's rows + its Adam, k_adam's chunks for the positions) leaves parameters, gradients and
+    optimizer state BITWISE what the call followed by the HIP Adam leaves; so does the fallback
+    (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue)."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    res = {}
+    for mode in ("off", "fast", "fallback"):
+        model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
+        prof = _one_step(model, opt, loss_fn, batches[0], mode, store)
+        plist = [p for g in opt.param_groups for p in g["params"] if p in opt.state]
+        res[mode] = (_params(model), [p.grad.detach().cpu().clone() for p in plist],
+                     [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist], prof)
+    assert "k_gather_adam" in res["fast"][3] and "k_obj_gather" not in res["fast"][3], res["fast"][3]
+    assert "k_gather_adam" not in res["fallback"][3] and "k_obj_gather" in res["fallback"][3]
+    for mode in ("fast", "fallback"):
+        for k in res["off"][0]:
+            assert np.array_equal(res["off"][0][k], res[mode][0][k]), (mode, k)
+        for a, b in zip(res["off"][1], res[mode][1]):
+            assert torch.equal(a, b), mode
+        for se, sf in zip(res["off"][2], res[mode][2]):
+            for k in se:
+                assert torch.equal(se[k], sf[k]), (mode, k)
+    # the step moved the parameters
+    model0, *_ = gpu_recon(z, niter=1, ret_all=True)
+    assert not np.array_equal(_params(model0)["opt_obja"], res["fast"][0]["opt_obja"])
+
+
+def test_graphs_fused_adam_bitwise_unfused_and_reference():
+    """Graph-replayed recon_step with the optimizer step folded into the engine call
+    (StepGraphs.FUSE_ADAM, the default) against the same with the separate HIP Adam launch: bitwise
+    equal trajectories, both at the reference's (RMS < 1e-5)."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    from ptyrad_amd.stepgraph import StepGraphs
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    out = {}
+    try:
+        for fuse in (False, True):
+            StepGraphs.FUSE_ADAM = fuse
+            m = gpu_recon(z, graphs=True)
+            assert m._step_graphs.replays >= 1
+            out[fuse] = _params(m)
+    finally:
+        StepGraphs.FUSE_ADAM = True
+    for k in out[False]:
+        assert np.array_equal(out[False][k], out[True][k]), k
+    for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
+        assert float(np.sqrt(np.mean((out[True][k].astype(np.float64) - ref) ** 2))) < 1e-5, k
