@@ -45,12 +45,12 @@ __device__ __forceinline__ void gather_adam_tile(const FusedAdamArgs& f, int b) 
   __shared__ float2 s_acc[kGTY * kGTX];
   __shared__ float s_cnt[kGTY * kGTX];
   __shared__ float s_ns[2], s_bc[2];
-  const GatherArgs& ga = f.ga;
+  const GatherArgs ga = f.ga;   // (a copy: a reference into the kernel argument put the whole struct in scratch)
   const int tyi = b / ga.tiles_x, txi = b % ga.tiles_x;
   const int ty = tyi * kGTY, tx = txi * kGTX;
   constexpr int PX = kGTY * kGTX / 256;   // pixels a thread
-  if (threadIdx.x < 2 && f.om[threadIdx.x])
-    opt::adam_step_scalars(f.h, f.olr[threadIdx.x], *f.ostep[threadIdx.x], &s_ns[threadIdx.x], &s_bc[threadIdx.x]);
+  if (threadIdx.x == 0 && f.om[0]) opt::adam_step_scalars(f.h, f.olr[0], *f.ostep[0], &s_ns[0], &s_bc[0]);
+  if (threadIdx.x == 64 && f.om[1]) opt::adam_step_scalars(f.h, f.olr[1], *f.ostep[1], &s_ns[1], &s_bc[1]);
   // the epilogue's operands, loaded before the candidate scan (only this workgroup touches them)
   float A[PX], ph[PX], ma[PX], va[PX], mp[PX], vp[PX], ga0[PX], gp0[PX];
 #pragma unroll
