@@ -192,17 +192,20 @@ __global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float
                    [](float2* dp, size_t, float2 g) { *dp = g; });
 }
 
-template <bool KL>
-__global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const int* segbid, int nseg,
-                                                    const float* coef, int ci, float2* out, const int* idx, int n,
-                                                    int n_scans, const int* bid, const float* dsu, float* d_shifts,
-                                                    const float2* twg = nullptr, float2* cols_out = nullptr) {
+// The tail's body with the mini-batch coefficient coef_of(m) (c of segment / pattern batch m for the
+// data term ci; ci 2: already applied): k_small_tail reads it from k_finalize's coef, the small
+// calls' k_small_tail_fin (ptyx_kernels.hip) computes it in the workgroup.
+template <bool KL, class CoefOf>
+__device__ __forceinline__ void small_tail_body(const float2* segslab, const int* segbid, int nseg, CoefOf coef_of,
+                                                float2* out, const int* idx, int n, int n_scans, const int* bid,
+                                                const float* dsu, float* d_shifts, const float2* twg,
+                                                float2* cols_out) {
   constexpr int kSlabBlocks = kN2 / 256;
   if (blockIdx.x >= kSlabBlocks) {
     const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
     if (!d_shifts || j >= n) return;
     const int s = min(max(idx[j], 0), n_scans - 1);
-    const float k = 6.283185307179586f * (ci >= 2 ? 1.f : coef[(size_t)bid[j] * kNCoef + ci]) * (1.0f / kN2);
+    const float k = 6.283185307179586f * coef_of(bid[j]) * (1.0f / kN2);
     atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
     atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
     return;
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
       u[y] = make_float2(0.f, 0.f);
       c[y] = 0.f;
       if (m >= 0) {
-        c[y] = ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci];
+        c[y] = coef_of(m);
         u[y] = segslab[(size_t)g * kN2 + e];
       }
     }
@@ -243,6 +246,16 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
     return;
   }
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
+}
+
+template <bool KL>
+__global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const int* segbid, int nseg,
+                                                    const float* coef, int ci, float2* out, const int* idx, int n,
+                                                    int n_scans, const int* bid, const float* dsu, float* d_shifts,
+                                                    const float2* twg = nullptr, float2* cols_out = nullptr) {
+  small_tail_body<KL>(segslab, segbid, nseg,
+                      [&](int m) { return ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci]; }, out, idx, n, n_scans,
+                      bid, dsu, d_shifts, twg, cols_out);
 }
 
 // Per call: complex object O = A e^{iφ} (the fused kernel then needs no transcendental per
@@ -568,7 +581,10 @@ struct PrepExtra {
   float2* hpk = nullptr;
   float hscale = 1.0f;
   double* zsum = nullptr;      // per-(pattern, slice) loss_sparse window sums (else psums, per pattern)
-  __host__ __device__ int row_blocks() const { return probe ? (kN / kPrLines) * P : 0; }
+  float2* fpk = nullptr;       // non-null: F(P_p) straight to the K-packed fpk, one leading workgroup a
+                               // mode (probe_spectrum_reg), instead of the row pass into tmp
+  __host__ __device__ int lead_blocks() const { return probe && fpk ? P : 0; }
+  __host__ __device__ int row_blocks() const { return probe && !fpk ? (kN / kPrLines) * P : 0; }
   __host__ __device__ int h_blocks() const { return H ? kN2 / 256 : 0; }
 };
 __device__ __forceinline__ void probe_rows_body(int bx, int p, const float2* src, float2* tmp, const float2* twg) {
@@ -587,6 +603,22 @@ __device__ __forceinline__ void probe_rows_body(int bx, int p, const float2* src
   line_pass<N, 256, P1::R1, 1, -1, kPrLines>(T, s_tw, nl);
   line_pass<N, 256, P1::R2, P1::R1, -1, kPrLines>(T, s_tw, nl);
   for (int e = threadIdx.x; e < nl * N; e += 256) d[(size_t)(l0 + e / N) * N + e % N] = T[LT::off(e / N, e % N)];
+}
+// The shifted probe's spectrum F(P) of a small call in ONE workgroup: the register-resident 2-D FFT
+// (ptyx_regfft.hpp) from the natural probe straight to the K-packed layout the register engines
+// read (fpk[256 k + t] = F[ky][k + 64 l0] of thread t, as k_lines_cols packs it), instead of a row
+// pass here and a column launch (k_lines_cols) after.  Same transform up to fp32 rounding.
+__device__ __forceinline__ void probe_spectrum_reg(const float2* probe, float2* fpk) {
+  using namespace rf;
+  __shared__ float2 buf[kLdsElems];
+  const Coord cd = coord(threadIdx.x);
+  const LaneCtx lc = lane_ctx(cd.lane);
+  float2 v[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) v[j] = probe[(size_t)(j + 64 * cd.l0) * kN + cd.fixed];
+  fft_fwd(v, buf, lc, cd.wsign);
+#pragma unroll
+  for (int k = 0; k < 64; ++k) fpk[(size_t)k * 256 + threadIdx.x] = v[k];
 }
 // one (pattern, slice)'s loss_sparse window sum: the slice pass of k_pattern_table_direct_body,
 // its fp64 wave sums added in wave order, to zsum[j·Nz + z] (k_finalize adds the slices in order)
@@ -621,7 +653,11 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
                                                     const float* obja, const float* objp, int sparse_n, float* psums,
                                                     int Nz, TableCheck tc, float2* oc, int* bbox, int* segbid,
                                                     int nseg, PrepExtra ex) {
-  const int b = blockIdx.x;
+  if ((int)blockIdx.x < ex.lead_blocks()) {   // (first: the longest chain of the launch starts first)
+    probe_spectrum_reg(ex.probe + (size_t)blockIdx.x * kN2, ex.fpk + (size_t)blockIdx.x * kN2);
+    return;
+  }
+  const int b = blockIdx.x - ex.lead_blocks();
   const bool zs = SPARSE && ex.zsum != nullptr;
   const int np = zs ? n * Nz : n;                         // pattern blocks
   const int bx = b - small_prep_blocks(n, Nz, Ny, zs);   // the PrepExtra roles

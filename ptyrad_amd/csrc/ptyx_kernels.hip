@@ -80,11 +80,12 @@ static_assert(kSumBase == 4, "k_finalize reads the data-term sums as one float4"
 // coefficients; lane 0 stores them, every lane writes its share of the per-pattern coefficients.
 // The object modes are a runtime loop with one accumulator at a time (no per-mode register arrays:
 // indexed by the runtime O they went to scratch).
+// finalize_batch: one wave, mini-batch m.  write: store the terms and coefficients (k_finalize);
+// else only return the data-term coefficients (c_single, c_pois) in cdata — the small calls' tail
+// launch recomputes them per workgroup instead of waiting for a k_finalize launch (one of its
+// workgroups also writes, the same bits).
 constexpr int kFinWaves = 2;   // mini-batches per 128-thread workgroup
-__global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
-  const int m = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (m >= f.n_batches) return;   // (wave-uniform)
+__device__ __forceinline__ void finalize_batch(const FinArgs& f, int m, int lane, bool write, float* cdata) {
   const int b0 = f.boff[m], b1 = f.boff[m + 1];
   const double* bin = f.bsums_in ? f.bsums_in + (size_t)m * kNBatchSum : nullptr;
   // additive sum k of the mini-batch (k < kSumBase: the data terms, kSumBase + o: sparse mode o)
@@ -163,6 +164,11 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
     c_pois = (float)(-f.w2 / (mu * K) * f.grad_scale);
   }
   float* cfo = f.coef + (size_t)m * kNCoef;
+  if (cdata) {
+    cdata[0] = c_single;
+    cdata[1] = c_pois;
+  }
+  if (!write) return;
   if (lane == 0) {
     cfo[0] = c_single;
     cfo[1] = c_pois;
@@ -190,6 +196,30 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
   if (sparse) terms[3] = (float)(f.ws * t_sp);
   if (lane == 0 && f.loss_terms)
     for (int i = 0; i < 5; ++i) f.loss_terms[(size_t)m * 5 + i] = terms[i];
+}
+__global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
+  const int m = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (m >= f.n_batches) return;   // (wave-uniform)
+  finalize_batch(f, m, threadIdx.x & 63, true, nullptr);
+}
+
+// Small calls of at most kTailFinBatches mini-batches: k_finalize folded into the probe / position
+// tail launch (f3::small_tail_body).  Wave w of every workgroup computes mini-batch w's data-term
+// coefficients (finalize_batch: the same fixed-order fp64 sums, so the same bits in every
+// workgroup); workgroup 0 also stores the loss terms, coef and pcoef (the next launch's object
+// gather reads pcoef).  One launch and its gap fewer per optimizer step at the default cadence.
+constexpr int kTailFinBatches = 4;
+template <bool KL>
+__global__ __launch_bounds__(256) void k_small_tail_fin(FinArgs fa, const float2* segslab, const int* segbid, int nseg,
+                                                        int ci, float2* out, const int* idx, int n, int n_scans,
+                                                        const int* bid, const float* dsu, float* d_shifts,
+                                                        const float2* twg, float2* cols_out) {
+  __shared__ float s_c[kTailFinBatches][2];
+  const int wave = threadIdx.x >> 6;
+  if (wave < fa.n_batches) finalize_batch(fa, wave, threadIdx.x & 63, blockIdx.x == 0, s_c[wave]);
+  __syncthreads();
+  f3::small_tail_body<KL>(segslab, segbid, nseg, [&](int m) { return ci >= 2 ? 1.f : s_c[m][ci]; }, out, idx, n,
+                          n_scans, bid, dsu, d_shifts, twg, cols_out);
 }
 
 
@@ -247,11 +277,12 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneFmmHoldH, kTuneFuseAdam, kTuneCount };
+               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
-                                            "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                            "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
+                                            "tail_fin", "small_spec"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -971,6 +1002,7 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
       ex.P = d.P;
       ex.tmp = pl->Gsum;
       ex.twg = pl->twg;
+      if (g_tuning[kTuneSmallSpec] != 0) ex.fpk = pl->fpk;   // the whole spectrum in this launch
     }
     if (Nz > 1) {
       ex.H = a.H;
@@ -983,7 +1015,8 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
     }
     {
       ProfScope ps(pl, kKTable, st);
-      const dim3 gr(f3::small_prep_blocks(a.n_idx, Nz, d.Ny, ex.zsum != nullptr) + ex.row_blocks() + ex.h_blocks()),
+      const dim3 gr(ex.lead_blocks() + f3::small_prep_blocks(a.n_idx, Nz, d.Ny, ex.zsum != nullptr) + ex.row_blocks() +
+                    ex.h_blocks()),
           bl(256);
       const f3::TableCheck tc{a.err, a.mrow, a.mrows};
       if (sparse)
@@ -995,7 +1028,7 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
                            a.n_scans, d.Ny, d.Nx, pl->bid, pl->geo, a.obja, a.objp, cfg->sparse_n, pl->psums, Nz, tc,
                            pl->oc, pl->bbox, pl->segbid, nseg, ex);
     }
-    if (a.shift) {   // the spectrum's column pass (Fp natural, fpk K-packed)
+    if (a.shift && !ex.fpk) {   // the spectrum's column pass (Fp natural, fpk K-packed)
       ProfScope ps(pl, kKSpectrum, st);
       pl->gen->spectrum_cols(pl->Gsum, d.P, pl->Fp, pl->fpk, pl->twg, st);
     }
@@ -1220,49 +1253,11 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const int nseg = a.n_batches + G;
   int rc = PTYX_OK;
   if (ph != kPhaseEnd && (rc = fused3_pass(pl, in, a, cfg, gz, st))) return rc;
-  FinArgs fa{};
-  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
-  fa.psums = pl->psums; fa.occu = in->omode_occu;
-  if (pl->zsum_call) {   // the sparse sums as per-slice partials (k_small_prep)
-    fa.zsum = pl->zsum;
-    fa.zNz = Nz;
-  }
-  fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
-  fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
-  fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
-  if (gz.d_obja || gz.d_objp) {
-    fa.pcoef = pl->pcoef;
-    fa.ci = ci;
-  }
-  fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
-  fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
-  {
-    ProfScope ps(pl, kKFinalize, st);
-    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
-  }
-  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
-  if (both) {   // the adjoint pass, now that the coefficients are known (dp_out written by MODE 1)
-    f3::F3Args f = register_args(pl, in, a, cfg, gz);
-    f.dp_out = nullptr;
-    launch_fused3_both(pl, f, a.shift, 2, G, st);
-    if ((rc = launch_status("k_fused3 (both terms) launch"))) return rc;
-  }
   // small calls: every tile scans the call's few patterns directly (no binning launches)
   const bool bins = a.n_idx > f3::kSmallCall;
   // PTYX_PREP_DEFER_GATHER: the slots, pattern table and coefficients stay for ptyx_slots_export
   // and the caller's ptyx_obj_gather_slots over every rank's patterns (split mini-batches)
   const bool gather_here = (gz.d_obja || gz.d_objp) && !pl->gather_deferred;
-  if (gather_here && bins) {
-    // candidate bins of the gather: the patterns by object tile of their window origin
-    ProfScope ps(pl, kKTable, st);
-    const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
-    if (int rc2 = fill32(pl->bcnt, pl->nbins, 0u, st)) return rc2;
-    const dim3 gn((a.n_idx + 255) / 256);
-    hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
-    hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
-    hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
-  }
   GatherArgs g{};
   int tiles = 0;
   bool sparse_tiles = false;
@@ -1285,8 +1280,52 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   // step in one launch after the probe / position sums (ptyx_stepfuse.hpp)
   float* d_shifts = a.shift ? gz.d_shifts : nullptr;
   FusedAdamArgs fz{};
-  const bool fuse = pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles && g_tuning[kTuneGatherRows] != 1 &&
-                    g_tuning[kTuneFuseAdam] != 0 && fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+  const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles &&
+                    g_tuning[kTuneGatherRows] != 1 && g_tuning[kTuneFuseAdam] != 0 &&
+                    fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+  // k_finalize folded into the small call's tail launch when nothing between them needs the
+  // coefficients (one data term; the object gather, if any, after the tail: k_gather_adam)
+  const bool tail_small = !bins && (gz.d_probe || d_shifts);
+  const bool fold_fin = ph == kPhaseAll && !both && tail_small && a.n_batches <= kTailFinBatches &&
+                        (fuse || !gather_here) && g_tuning[kTuneTailFin] != 0;
+  FinArgs fa{};
+  fa.boff = a.boff; fa.n_batches = a.n_batches; fa.N = N; fa.Nz = Nz; fa.O = 1;
+  fa.psums = pl->psums; fa.occu = in->omode_occu;
+  if (pl->zsum_call) {   // the sparse sums as per-slice partials (k_small_prep)
+    fa.zsum = pl->zsum;
+    fa.zNz = Nz;
+  }
+  fa.single_on = cfg->single_on; fa.pois_on = cfg->poissn_on; fa.sparse_on = cfg->sparse_on;
+  fa.sparse_n = cfg->sparse_n; fa.w1 = cfg->single_w; fa.w2 = cfg->poissn_w; fa.ws = cfg->sparse_w;
+  fa.grad_scale = cfg->grad_scale; fa.coef = pl->coef; fa.loss_terms = loss_terms;
+  if (gz.d_obja || gz.d_objp) {
+    fa.pcoef = pl->pcoef;
+    fa.ci = ci;
+  }
+  fa.bsums_out = ph == kPhaseBegin ? bsums : nullptr;
+  fa.bsums_in = ph == kPhaseEnd ? bsums : nullptr;
+  if (!fold_fin) {
+    ProfScope ps(pl, kKFinalize, st);
+    hipLaunchKernelGGL(k_finalize, dim3((a.n_batches + kFinWaves - 1) / kFinWaves), dim3(64 * kFinWaves), 0, st, fa);
+  }
+  if ((rc = launch_status("k_finalize launch")) || ph == kPhaseBegin) return rc;
+  if (both) {   // the adjoint pass, now that the coefficients are known (dp_out written by MODE 1)
+    f3::F3Args f = register_args(pl, in, a, cfg, gz);
+    f.dp_out = nullptr;
+    launch_fused3_both(pl, f, a.shift, 2, G, st);
+    if ((rc = launch_status("k_fused3 (both terms) launch"))) return rc;
+  }
+  if (gather_here && bins) {
+    // candidate bins of the gather: the patterns by object tile of their window origin
+    ProfScope ps(pl, kKTable, st);
+    const int tiles_x = (d.Nx + kGTX - 1) / kGTX;
+    if (int rc2 = fill32(pl->bcnt, pl->nbins, 0u, st)) return rc2;
+    const dim3 gn((a.n_idx + 255) / 256);
+    hipLaunchKernelGGL(k_bin_count, gn, dim3(256), 0, st, pl->geo, a.n_idx, tiles_x, pl->bcnt, pl->bkey);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, pl->bcnt, pl->nbins, pl->boff, pl->bcur);
+    hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
+    hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
+  }
   if (gather_here && !fuse) {
     ProfScope ps(pl, kKGather, st);
     launch_gather<N, true, false>(pl, g, tiles, Nz, sparse_tiles, st);
@@ -1297,7 +1336,14 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
       float2* out = gz.d_probe ? pl->Gsum : nullptr;
-      if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
+      if (fold_fin && a.shift)
+        hipLaunchKernelGGL(k_small_tail_fin<true>, gr, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
+                           a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
+                           gz.d_probe ? pl->slab : nullptr);
+      else if (fold_fin)
+        hipLaunchKernelGGL(k_small_tail_fin<false>, gr, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
+                           a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
+      else if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
         hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
                            out, a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
                            gz.d_probe ? pl->slab : nullptr);

@@ -258,3 +258,27 @@ def test_c5_shape_call_split_by_stripe_capacity(monkeypatch):
     for k in ("obja", "objp", "probe"):
         assert rel(g[k], og[k]) < TOL_G, k
     assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+@pytest.mark.parametrize("spec,P,Nz", [(-1, 1, 1), (0, 1, 1), (-1, 3, 2), (0, 3, 2)])
+def test_small_call_probe_spectrum_variants_vs_oracle(tuning, spec, P, Nz):
+    """Small calls (one mini-batch per optimizer step) take the shifted probe's spectrum F(P) in
+    k_small_prep's leading workgroups, one register-resident 2-D FFT a mode (tuning "small_spec",
+    the default), or as the row pass there plus a k_lines_cols launch (0): both against the oracle
+    on k_fused3 / k_fused3ms and the mixed-state engine, and against each other to fp32 rounding."""
+    tuning("small_spec", spec)
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(128, 4, 4, P=P, O=1, Nz=Nz, seed=21)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=json.loads(json.dumps(orc_default_loss())))
+    batches = [np.array([0, 5, 9, 14, 3, 12])]
+    ks = {}
+    terms, dp, g, _ = run_fused(d, dev(), batches, meas_f16=False, kernels=ks)
+    assert ("k_probe_spectrum" in ks) == (spec == 0), ks
+    oterms, odps, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                             d["occu"], d["meas"], batches, d["loss_params"])
+    assert rel(dp, np.concatenate(odps)) < TOL_DP
+    np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g[k], og[k]) < TOL_G, k
+    assert rel(g["shifts"], og["shifts"]) < TOL_SH

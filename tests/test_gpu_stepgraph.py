@@ -254,6 +254,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
     prep = _lib.PTYX_PREP_GRAD_STORE if store else 0
     opt._external_step_inc = True
     _lib.set_tuning("fuse_adam", 0 if mode == "fallback" else -1)
+    _lib.set_tuning("tail_fin", 0 if mode == "nofold" else -1)
     model.plan.profile_begin()
     try:
         if mode == "off":
@@ -266,6 +267,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
         prof = model.plan.profile_end()
         opt._external_step_inc = False
         _lib.set_tuning("fuse_adam", -1)
+        _lib.set_tuning("tail_fin", -1)
     torch.cuda.synchronize()
     return prof
 
@@ -276,12 +278,14 @@ def test_fused_adam_call_bitwise_the_call_then_adam(store):
     its last launch (k_gather_adam: object gather + Adam of obja / objp per tile, the probe
     gradient's rows + its Adam, k_adam's chunks for the positions) leaves parameters, gradients and
     optimizer state BITWISE what the call followed by the HIP Adam leaves; so does the fallback
-    (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue)."""
+    (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue).  The fused
+    call also folds k_finalize into its tail launch (k_small_tail_fin: every workgroup recomputes
+    the mini-batch coefficients); tail_fin 0 ("nofold") keeps the k_finalize launch: the same bits."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
     z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
     res = {}
-    for mode in ("off", "fast", "fallback"):
+    for mode in ("off", "fast", "fallback", "nofold"):
         model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
         prof = _one_step(model, opt, loss_fn, batches[0], mode, store)
         plist = [p for g in opt.param_groups for p in g["params"] if p in opt.state]
@@ -289,7 +293,9 @@ def test_fused_adam_call_bitwise_the_call_then_adam(store):
                      [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist], prof)
     assert "k_gather_adam" in res["fast"][3] and "k_obj_gather" not in res["fast"][3], res["fast"][3]
     assert "k_gather_adam" not in res["fallback"][3] and "k_obj_gather" in res["fallback"][3]
-    for mode in ("fast", "fallback"):
+    assert "k_finalize" not in res["fast"][3] and "k_finalize" in res["nofold"][3], res["fast"][3]
+    assert "k_gather_adam" in res["nofold"][3]
+    for mode in ("fast", "fallback", "nofold"):
         for k in res["off"][0]:
             assert np.array_equal(res["off"][0][k], res[mode][0][k]), (mode, k)
         for a, b in zip(res["off"][1], res[mode][1]):
