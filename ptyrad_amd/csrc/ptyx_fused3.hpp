@@ -192,57 +192,68 @@ __global__ __launch_bounds__(256) void k_probe_rows_acc(const float2* tmp, float
                    [](float2* dp, size_t, float2 g) { *dp = g; });
 }
 
-// The tail's body with the mini-batch coefficient coef_of(m) (c of segment / pattern batch m for the
-// data term ci; ci 2: already applied): k_small_tail reads it from k_finalize's coef, the small
-// calls' k_small_tail_fin (ptyx_kernels.hip) computes it in the workgroup.
-template <bool KL, class CoefOf>
-__device__ __forceinline__ void small_tail_body(const float2* segslab, const int* segbid, int nseg, CoefOf coef_of,
-                                                float2* out, const int* idx, int n, int n_scans, const int* bid,
-                                                const float* dsu, float* d_shifts, const float2* twg,
-                                                float2* cols_out) {
+// The tail's body, workgroup bx, with the mini-batch coefficient coef_of(m) (c of segment / pattern
+// batch m for the data term ci; ci 2: already applied): k_small_tail reads it from k_finalize's coef,
+// the small calls' k_small_tail_fin (ptyx_kernels.hip) computes it in the workgroup — pre() runs
+// once the workgroup's first loads are in flight and before coef_of is first called.
+template <bool KL, class CoefOf, class Pre>
+__device__ __forceinline__ void small_tail_body(int bx, const float2* segslab, const int* segbid, int nseg,
+                                                CoefOf coef_of, Pre pre, float2* out, const int* idx, int n,
+                                                int n_scans, const int* bid, const float* dsu, float* d_shifts,
+                                                const float2* twg, float2* cols_out) {
   constexpr int kSlabBlocks = kN2 / 256;
-  if (blockIdx.x >= kSlabBlocks) {
-    const int j = (blockIdx.x - kSlabBlocks) * 256 + threadIdx.x;
-    if (!d_shifts || j >= n) return;
-    const int s = min(max(idx[j], 0), n_scans - 1);
-    const float k = 6.283185307179586f * coef_of(bid[j]) * (1.0f / kN2);
-    atomicAdd(d_shifts + 2 * s, dsu[2 * j] * k);
-    atomicAdd(d_shifts + 2 * s + 1, dsu[2 * j + 1] * k);
+  if (bx >= kSlabBlocks) {
+    const int j = (bx - kSlabBlocks) * 256 + threadIdx.x;
+    const bool on = d_shifts && j < n;
+    int s = 0, bj = 0;
+    float2 dj = make_float2(0.f, 0.f);
+    if (on) {
+      s = min(max(idx[j], 0), n_scans - 1);
+      bj = bid[j];
+      dj = make_float2(dsu[2 * j], dsu[2 * j + 1]);
+    }
+    pre();
+    if (!on) return;
+    const float k = 6.283185307179586f * coef_of(bj) * (1.0f / kN2);
+    atomicAdd(d_shifts + 2 * s, dj.x * k);
+    atomicAdd(d_shifts + 2 * s + 1, dj.y * k);
     return;
   }
-  if (!out) return;
+  if (!out) {
+    pre();
+    return;
+  }
   // the kSegSplit partial chains are independent: each round issues the loads of all of them, then
   // adds (a missing segment adds 0·0 = +0 to a partial that is never −0: unchanged), so the sums
   // and their order are k_segslab_reduce + k_segslab_final's
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int e = bx * 256 + threadIdx.x;
   float2 part[kSegSplit];
 #pragma unroll
   for (int y = 0; y < kSegSplit; ++y) part[y] = make_float2(0.f, 0.f);
   for (int g0 = 0; g0 < nseg; g0 += kSegSplit) {
     float2 u[kSegSplit];
-    float c[kSegSplit];
+    int mm[kSegSplit];
 #pragma unroll
     for (int y = 0; y < kSegSplit; ++y) {
       const int g = g0 + y;
-      const int m = g < nseg ? segbid[g] : -1;
+      mm[y] = g < nseg ? segbid[g] : -1;
       u[y] = make_float2(0.f, 0.f);
-      c[y] = 0.f;
-      if (m >= 0) {
-        c[y] = coef_of(m);
-        u[y] = segslab[(size_t)g * kN2 + e];
-      }
+      if (mm[y] >= 0) u[y] = segslab[(size_t)g * kN2 + e];
     }
+    if (g0 == 0) pre();
 #pragma unroll
     for (int y = 0; y < kSegSplit; ++y) {
-      part[y].x = fmaf(c[y], u[y].x, part[y].x);
-      part[y].y = fmaf(c[y], u[y].y, part[y].y);
+      const float c = mm[y] >= 0 ? coef_of(mm[y]) : 0.f;
+      part[y].x = fmaf(c, u[y].x, part[y].x);
+      part[y].y = fmaf(c, u[y].y, part[y].y);
     }
   }
+  if (nseg <= 0) pre();
   float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
   for (int y = 0; y < kSegSplit; ++y) acc = cadd(acc, part[y]);
   if (KL && cols_out) {   // (block-uniform) the column pass of the probe gradient's inverse FFT
-    tail_cols_ifft(acc, blockIdx.x, twg, cols_out);
+    tail_cols_ifft(acc, bx, twg, cols_out);
     return;
   }
   out[packed_rc<KL>(e & 255, e >> 8)] = acc;
@@ -253,9 +264,9 @@ __global__ __launch_bounds__(256) void k_small_tail(const float2* segslab, const
                                                     const float* coef, int ci, float2* out, const int* idx, int n,
                                                     int n_scans, const int* bid, const float* dsu, float* d_shifts,
                                                     const float2* twg = nullptr, float2* cols_out = nullptr) {
-  small_tail_body<KL>(segslab, segbid, nseg,
-                      [&](int m) { return ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci]; }, out, idx, n, n_scans,
-                      bid, dsu, d_shifts, twg, cols_out);
+  small_tail_body<KL>(blockIdx.x, segslab, segbid, nseg,
+                      [&](int m) { return ci >= 2 ? 1.f : coef[(size_t)m * kNCoef + ci]; }, [] {}, out, idx, n,
+                      n_scans, bid, dsu, d_shifts, twg, cols_out);
 }
 
 // Per call: complex object O = A e^{iφ} (the fused kernel then needs no transcendental per

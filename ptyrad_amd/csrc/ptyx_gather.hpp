@@ -266,24 +266,22 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
 // of dφ — the count adds ≈ 2,000 near-equal c_sparse terms, whose rounding is systematic, not
 // random; a missing or doubled hit would move the norm by ≈ 6e-5); compensated, both stay at fp32
 // rounding.
+// The row-split gather's sums of one tile: wave w's rows ty + w·RW … (acc, cnt: running sums after
+// the Kahan-compensated accumulation over every hit, candidate order).  Tile (tyi, txi), slot plane zp.
 template <int N, bool ROWPERM, int GW, bool MP>
-__global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
+__device__ __forceinline__ void gather_rows_sums(const GatherArgs& ga, int tyi, int txi, int zp,
+                                                 float2 (&acc)[kGTY / GW], float (&cnt)[kGTY / GW]) {
   constexpr int N2 = N * N;
   constexpr int NB = BinReach<N>::n;
   constexpr int RW = kGTY / GW;                          // rows per wave
   constexpr int NPL = MP ? kGatherMaxNp : 1;             // planes per row and hit (≤; np at run time)
   constexpr int HU = 32 / (RW * NPL) > 0 ? 32 / (RW * NPL) : 1;   // hits in flight per wave
-  static_assert(kGTY % GW == 0, "rows split evenly over the waves");
   __shared__ int4 s_hit[64 * GW];     // (cy, cx, j, c) of the chunk's hits, candidate order
   __shared__ float s_hcs[64 * GW];
   __shared__ int s_wcnt[GW];
   __shared__ int s_b0[NB], s_pre[NB + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
-  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;
-  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;
   const int ty = tyi * kGTY, tx = txi * kGTX;
-  if (gather_tile_skip<N>(ga, ty, tx)) return;
   int total = ga.n;
   if (ga.boff) {
     if (threadIdx.x < NB) {
@@ -308,28 +306,14 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
   }
   const int x = tx + lane;
   const int r0 = ty + wave * RW;   // this wave's first object row
-  float2 acc[RW], cmp[RW];   // running sums and their Kahan compensations
-  float cnt[RW], ccmp[RW];
+  float2 cmp[RW];   // the running sums' Kahan compensations
+  float ccmp[RW];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
     acc[r] = make_float2(0.f, 0.f);
     cmp[r] = make_float2(0.f, 0.f);
     cnt[r] = 0.f;
     ccmp[r] = 0.f;
-  }
-  // the epilogue's operands of this wave's pixels (A, φ and the gradients it adds to), loaded
-  // now: they do not depend on the hits, and only this workgroup touches these pixels
-  float pa[RW], pp[RW], pga[RW], pgp[RW];
-#pragma unroll
-  for (int r = 0; r < RW; ++r) {
-    pa[r] = pp[r] = pga[r] = pgp[r] = 0.f;
-    if (r0 + r < ga.Ny && x < ga.Nx) {
-      const size_t off = zoff + (size_t)(r0 + r) * ga.Nx + x;
-      pa[r] = ga.obja[off];
-      pp[r] = ga.objp[off];
-      if (ga.d_obja && !ga.store) pga[r] = ga.d_obja[off];
-      if (ga.d_objp && !ga.store) pgp[r] = ga.d_objp[off];
-    }
   }
   const int np = MP ? ga.np : 1;
   for (int base = 0; base < total; base += 64 * GW) {
@@ -413,6 +397,36 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
     }
     __syncthreads();   // the next chunk rewrites the hit list
   }
+}
+
+template <int N, bool ROWPERM, int GW, bool MP>
+__global__ __launch_bounds__(64 * GW) void k_obj_gather_rows(GatherArgs ga) {
+  constexpr int RW = kGTY / GW;                          // rows per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tyi = blockIdx.x / ga.tiles_x, txi = blockIdx.x % ga.tiles_x;
+  const int zp = ga.zgrid ? (int)blockIdx.y : ga.z;
+  const size_t zoff = ga.zgrid ? (size_t)blockIdx.y * ga.Ny * ga.Nx : 0;
+  const int ty = tyi * kGTY, tx = txi * kGTX;
+  if (gather_tile_skip<N>(ga, ty, tx)) return;
+  const int x = tx + lane;
+  const int r0 = ty + wave * RW;   // this wave's first object row
+  // the epilogue's operands of this wave's pixels (A, φ and the gradients it adds to), loaded
+  // now: they do not depend on the hits, and only this workgroup touches these pixels
+  float pa[RW], pp[RW], pga[RW], pgp[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    pa[r] = pp[r] = pga[r] = pgp[r] = 0.f;
+    if (r0 + r < ga.Ny && x < ga.Nx) {
+      const size_t off = zoff + (size_t)(r0 + r) * ga.Nx + x;
+      pa[r] = ga.obja[off];
+      pp[r] = ga.objp[off];
+      if (ga.d_obja && !ga.store) pga[r] = ga.d_obja[off];
+      if (ga.d_objp && !ga.store) pgp[r] = ga.d_objp[off];
+    }
+  }
+  float2 acc[RW];
+  float cnt[RW];
+  gather_rows_sums<N, ROWPERM, GW, MP>(ga, tyi, txi, zp, acc, cnt);
 #pragma unroll
   for (int r = 0; r < RW; ++r) {   // gather_apply on the prefetched operands
     const int y = r0 + r;

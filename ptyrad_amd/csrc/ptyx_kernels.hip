@@ -204,10 +204,11 @@ __global__ __launch_bounds__(64 * kFinWaves) void k_finalize(FinArgs f) {
 }
 
 // Small calls of at most kTailFinBatches mini-batches: k_finalize folded into the probe / position
-// tail launch (f3::small_tail_body).  Wave w of every workgroup computes mini-batch w's data-term
-// coefficients (finalize_batch: the same fixed-order fp64 sums, so the same bits in every
-// workgroup); workgroup 0 also stores the loss terms, coef and pcoef (the next launch's object
-// gather reads pcoef).  One launch and its gap fewer per optimizer step at the default cadence.
+// tail launch (f3::small_tail_body).  Workgroup 0 is k_finalize (terms, coef, pcoef — the next
+// launch's object gather reads pcoef); every other workgroup issues its first segment loads, then
+// wave w computes mini-batch w's data-term coefficients (finalize_batch without the stores: the
+// same fixed-order fp64 sums, so the same bits as workgroup 0's) while they are in flight.  One
+// launch and its gap fewer per optimizer step at the default cadence; the same results.
 constexpr int kTailFinBatches = 4;
 template <bool KL>
 __global__ __launch_bounds__(256) void k_small_tail_fin(FinArgs fa, const float2* segslab, const int* segbid, int nseg,
@@ -215,13 +216,19 @@ __global__ __launch_bounds__(256) void k_small_tail_fin(FinArgs fa, const float2
                                                         const int* bid, const float* dsu, float* d_shifts,
                                                         const float2* twg, float2* cols_out) {
   __shared__ float s_c[kTailFinBatches][2];
-  const int wave = threadIdx.x >> 6;
-  if (wave < fa.n_batches) finalize_batch(fa, wave, threadIdx.x & 63, blockIdx.x == 0, s_c[wave]);
-  __syncthreads();
-  f3::small_tail_body<KL>(segslab, segbid, nseg, [&](int m) { return ci >= 2 ? 1.f : s_c[m][ci]; }, out, idx, n,
-                          n_scans, bid, dsu, d_shifts, twg, cols_out);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (blockIdx.x == 0) {
+    if (wave < fa.n_batches) finalize_batch(fa, wave, lane, true, nullptr);
+    return;
+  }
+  f3::small_tail_body<KL>(
+      (int)blockIdx.x - 1, segslab, segbid, nseg, [&](int m) { return ci >= 2 ? 1.f : s_c[m][ci]; },
+      [&] {
+        if (wave < fa.n_batches) finalize_batch(fa, wave, lane, false, s_c[wave]);
+        __syncthreads();
+      },
+      out, idx, n, n_scans, bid, dsu, d_shifts, twg, cols_out);
 }
-
 
 #include "ptyx_gather.hpp"
 #include "ptyx_stepfuse.hpp"
@@ -1173,13 +1180,14 @@ static bool fused_adam_setup(const ptyx_plan* pl, const ptyx_inputs* in, const K
                              const GatherArgs& g, int tiles, FusedAdamArgs* f) {
   constexpr int N = 128;
   const ptyx_dims& d = pl->d;
-  if (d.O != 1 || d.Nz != 1 || d.P != 1) return false;
-  const int64_t nobj = (int64_t)d.Ny * d.Nx, nprobe = 2LL * N * N;
+  if (d.O != 1) return false;
+  const int64_t nobj = (int64_t)d.Nz * d.Ny * d.Nx, nprobe = 2LL * N * N * d.P;
   const bool probe_rows = gz.d_probe && a.shift;   // (else the probe gradient is final before the launch)
   *f = FusedAdamArgs{};
   f->ga = g;
   f->h = pl->fadam_h;
-  f->tiles = tiles;
+  f->ptiles = tiles;       // (per object plane)
+  f->tiles = tiles * d.Nz;
   std::vector<opt::AdamTensor> rest;
   struct Span {
     uintptr_t lo, hi;
@@ -1232,7 +1240,7 @@ static bool fused_adam_setup(const ptyx_plan* pl, const ptyx_inputs* in, const K
   }
   if (pl->fadam_store) opt::adam_set_store(f->rest, pl->fadam_ss);
   if (probe_rows) {
-    f->pblocks = N / f3::kPrLinesT;
+    f->pblocks = N / f3::kPrLinesT * d.P;
     f->ptmp = pl->slab;
     f->d_probe = reinterpret_cast<float2*>(gz.d_probe);
     f->twg = pl->twg;
@@ -1335,13 +1343,14 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
     {
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0));
+      const dim3 grf(gr.x + 1);   // (+ k_small_tail_fin's finalize workgroup)
       float2* out = gz.d_probe ? pl->Gsum : nullptr;
       if (fold_fin && a.shift)
-        hipLaunchKernelGGL(k_small_tail_fin<true>, gr, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
+        hipLaunchKernelGGL(k_small_tail_fin<true>, grf, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
                            a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, pl->twg,
                            gz.d_probe ? pl->slab : nullptr);
       else if (fold_fin)
-        hipLaunchKernelGGL(k_small_tail_fin<false>, gr, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
+        hipLaunchKernelGGL(k_small_tail_fin<false>, grf, dim3(256), 0, st, fa, pl->segslab, pl->segbid, nseg, ci, out,
                            a.idx, a.n_idx, a.n_scans, pl->bid, pl->dsu, d_shifts, nullptr, nullptr);
       else if (a.shift)   // (with the probe gradient: its column IFFT in the same launch, into pl->slab)
         hipLaunchKernelGGL(f3::k_small_tail<true>, gr, dim3(256), 0, st, pl->segslab, pl->segbid, nseg, pl->coef, ci,
@@ -1491,8 +1500,11 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     hipLaunchKernelGGL(k_bin_fill, gn, dim3(256), 0, st, pl->bkey, a.n_idx, pl->bcur, pl->blist);
     hipLaunchKernelGGL(k_bin_sort, dim3(pl->nbins), dim3(256), 0, st, pl->boff, pl->blist);
   }
-  if (gz.d_obja || gz.d_objp) {
-    GatherArgs g{};
+  const bool gather_here = gz.d_obja || gz.d_objp;
+  GatherArgs g{};
+  int tiles = 0;
+  bool sparse_tiles = false;
+  if (gather_here) {
     g.ogscr = pl->ffc; g.geo = pl->geo; g.pcoef = pl->pcoef; g.n = a.n_idx;
     g.boff = bins ? pl->boff : nullptr;
     g.blist = bins ? pl->blist : nullptr;
@@ -1502,14 +1514,29 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     g.bbox = pl->bbox;
     g.zgrid = 1;
     g.store = pl->grad_store;
-    const int tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
-    const bool sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
+    tiles = g.tiles_x * ((d.Ny + kGTY - 1) / kGTY);
+    sparse_tiles = (long long)a.n_idx * BinReach<N>::n < 64LL * tiles;
+  }
+  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
+  const bool small_tail = !bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts);
+  // PTYX_PREP_FUSED_ADAM on a small call whose gather is the default row-split one: the gather, the
+  // probe rows and the optimizer step in one launch after the probe / position sums
+  FusedAdamArgs fz{};
+  const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && sparse_tiles && P <= kGatherMaxNp &&
+                    g_tuning[kTuneGatherRows] != 0 && g_tuning[kTuneGatherSplit] < 1 && g_tuning[kTuneFuseAdam] != 0 &&
+                    (small_tail || !(gz.d_probe || d_shifts)) && fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+  if (gather_here && !fuse) {
     ProfScope ps(pl, kKGather, st);
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  float* d_shifts = a.shift ? gz.d_shifts : nullptr;
-  if (!bins && nseg <= f3::kTailSegCap && (gz.d_probe || d_shifts)) {   // small call: one launch for the probe / position sums
+  if (fuse && !small_tail) {
+    ProfScope ps(pl, kKGatherAdam, st);
+    hipLaunchKernelGGL((k_gather_adam<N, true, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+    pl->fadam_done = true;
+    return launch_status("k_gather_adam launch");
+  }
+  if (small_tail) {   // small call: one launch for the probe / position sums
     {
       ProfScope ps(pl, kKSlabReduce, st);
       const dim3 gr(N2 / 256 + (d_shifts ? (a.n_idx + 255) / 256 : 0), P);
@@ -1522,13 +1549,23 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
                            a.idx, a.n_idx, a.n_scans, P, pl->dsu, d_shifts, nullptr, nullptr);
     }
     if (gz.d_probe && a.shift) {
-      ProfScope ps(pl, kKProbeFinalize, st);
-      hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, st, pl->slab,
-                         reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+      if (!fuse) {
+        ProfScope ps(pl, kKProbeFinalize, st);
+        hipLaunchKernelGGL(f3::k_probe_rows_acc, dim3(N / f3::kPrLinesT, P), dim3(256), 0, st, pl->slab,
+                           reinterpret_cast<float2*>(gz.d_probe), pl->twg);
+      }
     } else if (gz.d_probe) {
       launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
     }
-    return launch_status("k_fmm probe / position reduction launch");
+    if ((rc = launch_status("k_fmm probe / position reduction launch"))) return rc;
+    if (fuse) {
+      ProfScope ps(pl, kKGatherAdam, st);
+      hipLaunchKernelGGL((k_gather_adam<N, true, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st,
+                         fz);
+      pl->fadam_done = true;
+      return launch_status("k_gather_adam launch");
+    }
+    return PTYX_OK;
   }
   if (d_shifts) {
     ProfScope ps(pl, kKSlabReduce, st);

@@ -18,15 +18,16 @@
 // so the trajectory is bitwise the gather + rows + k_adam one (tests/test_gpu_stepgraph.py).
 
 struct FusedAdamArgs {
-  GatherArgs ga;           // the object gather of the call (slot plane 0, object plane 0: Nz = 1)
+  GatherArgs ga;           // the object gather of the call
   opt::AdamHyper h;
-  int tiles;               // object tile blocks
+  int tiles;               // object tile blocks: ptiles tiles of each of the nz object planes
+  int ptiles;
   float* op[2];            // obja (0) / objp (1) as Adam parameters (= ga.obja / ga.objp) with their
   float* om[2];            // state; om[i] null: that plane takes no step here
   float* ov[2];
   const float* ostep[2];
   double olr[2];
-  int pblocks;             // probe-row blocks (N / kPrLinesT), 0: no probe gradient
+  int pblocks;             // probe-row blocks (N / kPrLinesT a probe mode), 0: no probe gradient
   const float2* ptmp;      // the probe gradient's column-transformed spectrum (k_small_tail)
   float2* d_probe;
   const float2* twg;
@@ -131,7 +132,101 @@ __device__ __forceinline__ void gather_adam_tile(const FusedAdamArgs& f, int b) 
   }
 }
 
-template <int N, bool ROWPERM>
+// The same for the mixed-state engine's row-split gather (k_obj_gather_rows, 4 waves, the probe
+// modes' slot planes summed): tile b % ptiles of object plane (slice) b / ptiles.
+template <int N, bool ROWPERM, bool MP>
+__device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, int b) {
+  constexpr int GW = 4, RW = kGTY / GW;
+  __shared__ float s_ns[2], s_bc[2];
+  const GatherArgs ga = f.ga;   // (a copy, as gather_adam_tile)
+  const int tile = b % f.ptiles, z = b / f.ptiles;
+  const int tyi = tile / ga.tiles_x, txi = tile % ga.tiles_x;
+  const int ty = tyi * kGTY, tx = txi * kGTX;
+  const size_t zoff = (size_t)z * ga.Ny * ga.Nx;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = tx + lane, r0 = ty + wave * RW;
+  if (threadIdx.x == 0 && f.om[0]) opt::adam_step_scalars(f.h, f.olr[0], *f.ostep[0], &s_ns[0], &s_bc[0]);
+  if (threadIdx.x == 64 && f.om[1]) opt::adam_step_scalars(f.h, f.olr[1], *f.ostep[1], &s_ns[1], &s_bc[1]);
+  float pa[RW], pp[RW], pga[RW], pgp[RW], ma[RW], va[RW], mp[RW], vp[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    pa[r] = pp[r] = pga[r] = pgp[r] = ma[r] = va[r] = mp[r] = vp[r] = 0.f;
+    if (r0 + r < ga.Ny && x < ga.Nx) {
+      const size_t off = zoff + (size_t)(r0 + r) * ga.Nx + x;
+      pa[r] = ga.obja[off];
+      pp[r] = ga.objp[off];
+      if (ga.d_obja && !ga.store) pga[r] = ga.d_obja[off];
+      if (ga.d_objp && !ga.store) pgp[r] = ga.d_objp[off];
+      if (f.om[0]) {
+        ma[r] = f.om[0][off];
+        va[r] = f.ov[0][off];
+      }
+      if (f.om[1]) {
+        mp[r] = f.om[1][off];
+        vp[r] = f.ov[1][off];
+      }
+    }
+  }
+  const bool skip = ga.bbox && (ty + kGTY <= ga.bbox[0] || ty >= ga.bbox[1] + N || tx + kGTX <= ga.bbox[2] ||
+                                tx >= ga.bbox[3] + N);
+  float2 acc[RW];
+  float cnt[RW];
+  if (!skip) {
+    gather_rows_sums<N, ROWPERM, GW, MP>(ga, tyi, txi, z, acc, cnt);
+  } else {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      acc[r] = make_float2(0.f, 0.f);
+      cnt[r] = 0.f;
+    }
+  }
+  __syncthreads();   // (the step scalars)
+  const float dec0 = (float)(1.0 - f.olr[0] * (double)f.h.wd), dec1 = (float)(1.0 - f.olr[1] * (double)f.h.wd);
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {   // k_obj_gather_rows' epilogue, then the Adam step on its gradient
+    const int y = r0 + r;
+    if (y >= ga.Ny || x >= ga.Nx) continue;
+    const size_t off = zoff + (size_t)y * ga.Nx + x;
+    float sn, cs;
+    phase_sincos(pp[r], &sn, &cs);
+    if (ga.d_obja) {
+      const float g = skip ? (ga.store ? 0.f : pga[r]) : pga[r] + fmaf(acc[r].x, cs, acc[r].y * sn);
+      ga.d_obja[off] = g;
+      if (f.om[0]) {
+        float p = pa[r];
+        opt::adam_elem(f.h, s_ns[0], s_bc[0], dec0, g, p, ma[r], va[r]);
+        f.op[0][off] = p;
+        f.om[0][off] = ma[r];
+        f.ov[0][off] = va[r];
+      }
+    }
+    if (ga.d_objp) {
+      float g;
+      if (skip) {
+        g = ga.store ? 0.f : pgp[r];
+      } else {
+        float dph = pa[r] * fmaf(acc[r].y, cs, -acc[r].x * sn);
+        if (cnt[r] != 0.f) {
+          const float ph = pp[r];
+          const float sg = ph > 0.f ? 1.f : (ph < 0.f ? -1.f : 0.f);
+          dph += ga.sparse_n == 1 ? cnt[r] * sg : cnt[r] * powq(fabsf(ph), (float)(ga.sparse_n - 1)) * sg;
+        }
+        g = pgp[r] + dph;
+      }
+      ga.d_objp[off] = g;
+      if (f.om[1]) {
+        float p = pp[r];
+        opt::adam_elem(f.h, s_ns[1], s_bc[1], dec1, g, p, mp[r], vp[r]);
+        f.op[1][off] = p;
+        f.om[1][off] = mp[r];
+        f.ov[1][off] = vp[r];
+      }
+    }
+  }
+}
+
+// ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine), else gather_adam_tile's.
+template <int N, bool ROWPERM, bool ROWS = false>
 __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
   const int b = blockIdx.x;
   if (b == 0 && f.rest.scnt) {   // as k_step_store: every thread reads *scnt before it advances
@@ -142,7 +237,8 @@ __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
     if (threadIdx.x == 0) *f.rest.scnt = c + 1;
   }
   if (b < f.tiles) {
-    gather_adam_tile<N, ROWPERM>(f, b);
+    if constexpr (ROWS) gather_rows_adam_tile<N, ROWPERM, true>(f, b);
+    else gather_adam_tile<N, ROWPERM>(f, b);
     return;
   }
   if (b < f.tiles + f.pblocks) {
@@ -155,7 +251,9 @@ __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
     float* pm = f.pm;
     float* pv = f.pv;
     const opt::AdamHyper h = f.h;
-    f3::probe_rows_block(f.ptmp, f.d_probe, f.twg, (b - f.tiles) * f3::kPrLinesT, 0,
+    constexpr int kRowBlocks = N / f3::kPrLinesT;   // a probe mode's
+    const int pb = b - f.tiles;
+    f3::probe_rows_block(f.ptmp, f.d_probe, f.twg, (pb % kRowBlocks) * f3::kPrLinesT, pb / kRowBlocks,
                          [&](float2* dp, size_t el, float2 g) {
                            *dp = g;
                            if (!pp) return;

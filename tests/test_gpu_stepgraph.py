@@ -272,18 +272,21 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
     return prof
 
 
-@pytest.mark.parametrize("store", [False, True])
-def test_fused_adam_call_bitwise_the_call_then_adam(store):
+@pytest.mark.parametrize("name,store", [("traj_c1_n128", False), ("traj_c1_n128", True),
+                                        ("traj_n128_p6z6_ga1", True)])
+def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     """PTYX_PREP_FUSED_ADAM (ABI 209): the k_fused3 small call with the optimizer step folded into
     its last launch (k_gather_adam: object gather + Adam of obja / objp per tile, the probe
     gradient's rows + its Adam, k_adam's chunks for the positions) leaves parameters, gradients and
     optimizer state BITWISE what the call followed by the HIP Adam leaves; so does the fallback
     (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue).  The fused
     call also folds k_finalize into its tail launch (k_small_tail_fin: every workgroup recomputes
-    the mini-batch coefficients); tail_fin 0 ("nofold") keeps the k_finalize launch: the same bits."""
+    the mini-batch coefficients); tail_fin 0 ("nofold") keeps the k_finalize launch: the same bits.
+    traj_n128_p6z6_ga1 (the tBL demo's 6 probe modes, 6 slices): the mixed-state engine, whose fused
+    launch runs the row-split gather over the slices and the probe rows of every mode."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
-    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     res = {}
     for mode in ("off", "fast", "fallback", "nofold"):
         model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
@@ -293,7 +296,8 @@ def test_fused_adam_call_bitwise_the_call_then_adam(store):
                      [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist], prof)
     assert "k_gather_adam" in res["fast"][3] and "k_obj_gather" not in res["fast"][3], res["fast"][3]
     assert "k_gather_adam" not in res["fallback"][3] and "k_obj_gather" in res["fallback"][3]
-    assert "k_finalize" not in res["fast"][3] and "k_finalize" in res["nofold"][3], res["fast"][3]
+    if name == "traj_c1_n128":   # (the mixed-state engine needs k_finalize before its adjoint)
+        assert "k_finalize" not in res["fast"][3] and "k_finalize" in res["nofold"][3], res["fast"][3]
     assert "k_gather_adam" in res["nofold"][3]
     for mode in ("fast", "fallback", "nofold"):
         for k in res["off"][0]:
@@ -308,14 +312,15 @@ def test_fused_adam_call_bitwise_the_call_then_adam(store):
     assert not np.array_equal(_params(model0)["opt_obja"], res["fast"][0]["opt_obja"])
 
 
-def test_graphs_fused_adam_bitwise_unfused_and_reference():
+@pytest.mark.parametrize("name", ["traj_c1_n128", "traj_n128_p6z6_ga1"])
+def test_graphs_fused_adam_bitwise_unfused_and_reference(name):
     """Graph-replayed recon_step with the optimizer step folded into the engine call
     (StepGraphs.FUSE_ADAM, the default) against the same with the separate HIP Adam launch: bitwise
     equal trajectories, both at the reference's (RMS < 1e-5)."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
     from ptyrad_amd.stepgraph import StepGraphs
-    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     out = {}
     try:
         for fuse in (False, True):
