@@ -499,8 +499,8 @@ def test_register_engine_both_terms_vs_oracle(shift, q1, n):
                                              shift_probes=shift, grad_scale=0.25)
     assert rel(dp, np.concatenate(odps)) < TOL_DP
     np.testing.assert_allclose(terms, oterms, rtol=TOL_TERMS, atol=1e-7)
-    for k in ("obja", "objp", "probe"):
-        assert rel(g[k], og[k]) < TOL_G, k
+    for k in ("obja", "objp", "probe"):   # (the probe: both terms' cancellation, TOL_G_BOTH as elsewhere)
+        assert rel(g[k], og[k]) < (TOL_G_BOTH if k == "probe" else TOL_G), k
     if shift:
         assert rel(g["shifts"], og["shifts"]) < TOL_SH
 
