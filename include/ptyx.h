@@ -38,7 +38,7 @@ extern "C" {
 
 /* ABI version: ptyx_dims.abi_version must equal it (ptyx_plan_create rejects a binding built
  * against another revision of this header); ptyx_version() returns it too. */
-#define PTYX_ABI_VERSION 209
+#define PTYX_ABI_VERSION 210
 
 #define PTYX_OK 0
 #define PTYX_EINVAL 1
@@ -79,6 +79,14 @@ extern "C" {
  * in one launch); any other call issues the ordinary k_adam launch after its own epilogue.  Either
  * way the gradients are written as without the flag, and the results are bitwise the same. */
 #define PTYX_PREP_FUSED_ADAM 32
+/* PTYX_PREP_SELECT (ptyx_forward_loss_grad only, ABI 210): the call begins with what
+ * ptyx_step_select(stream, idx_all, istart, cnt, n_idx, idx, grad, grad_n, steps, n_steps) does,
+ * with the arguments ptyx_plan_set_select registered on the plan (consumed by this call) and the
+ * call's own idx as idx_out: its pattern indices are picked on the device by the step counter, the
+ * gradient buffer zeroed and the step counts advanced before any kernel reads them.  The register
+ * engines' small calls do it inside their preparation launch (one launch fewer per graph-replayed
+ * step); any other call issues the k_step_select launch first.  The same results either way. */
+#define PTYX_PREP_SELECT 64
 /* The plan records what a PTYX_PREP_FULL call prepared (engine, input pointers, loss_sparse order).
  * A PTYX_PREP_REUSE call whose engine or inputs do not match that record (or that follows a
  * PTYX_PREP_CALL call, ptyx_forward or ptyx_adjoint_dldi on the plan) prepares in full instead of
@@ -459,6 +467,11 @@ int ptyx_adam_step_store(void *stream, int32_t n, float *const *params, const fl
                          const int64_t *numels, const double *lrs, double beta1, double beta2, double eps,
                          double weight_decay, int32_t flags, const float *terms, int32_t nb, const int64_t *rstart,
                          int64_t *cnt, float *terms_all);
+
+/* Registers the step selection the plan's next ptyx_forward_loss_grad call with PTYX_PREP_SELECT
+ * takes (arguments as ptyx_step_select's; steps is a DEVICE array of at most 256 pointers). */
+int ptyx_plan_set_select(ptyx_plan *plan, const int32_t *idx_all, const int64_t *istart, const int64_t *cnt,
+                         float *grad, int64_t grad_n, float *const *steps, int32_t n_steps);
 
 /* Registers the optimizer step the plan's next ptyx_forward_loss_grad call with PTYX_PREP_FUSED_ADAM
  * takes (arguments as ptyx_adam_step's; the host arrays are copied, the device pointers must stay

@@ -14,12 +14,13 @@ import torch  # noqa: F401  (load torch's HIP runtime before libptyx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTYX_LIB", os.path.join(_HERE, "lib", "libptyx.so"))
 
-PTYX_ABI_VERSION = 209     # include/ptyx.h
+PTYX_ABI_VERSION = 210     # include/ptyx.h
 PTYX_PREP_CALL, PTYX_PREP_FULL, PTYX_PREP_REUSE = 0, 1, 2
 PTYX_PREP_DEFER_PROBE = 4  # flag bit: the probe-gradient reduction may wait for a later piece
 PTYX_PREP_DEFER_GATHER = 8  # flag bit (_begin / _end): keep the object-gradient slots for the slot exchange
 PTYX_PREP_GRAD_STORE = 16  # flag bit: the call overwrites d_obja / d_objp (no zeroing needed before)
 PTYX_PREP_FUSED_ADAM = 32  # flag bit: the call ends with the step ptyx_plan_set_adam registered
+PTYX_PREP_SELECT = 64      # flag bit: the call begins with the selection ptyx_plan_set_select registered
 PTYX_SLOT_META = 8         # floats per table row of a slot-exchange rank block
 PTYX_BATCH_SUMS = 37      # doubles per mini-batch of ptyx_forward_loss_grad_begin / _end
 PTYX_OK, PTYX_EINVAL, PTYX_ENOMEM, PTYX_EHIP, PTYX_EUNSUPPORTED = 0, 1, 2, 3, 4
@@ -38,7 +39,7 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_obj_constrain", "ptyx_probe_fix_int", "ptyx_probe_ortho",
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
            "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
-           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_check",
+           "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_set_select", "ptyx_plan_check",
            "ptyx_plan_slot_floats", "ptyx_slot_block_floats", "ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots")
 
 
@@ -181,6 +182,7 @@ def load(path: str | None = None):
     lib.ptyx_adam_step.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32]
     lib.ptyx_adam_step_store.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32, vp, i32, vp, vp, vp]
     lib.ptyx_plan_set_adam.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, d64, d64, d64, d64, i32, vp, i32, vp, vp, vp]
+    lib.ptyx_plan_set_select.argtypes = [vp, vp, vp, vp, vp, i64, vp, i32]
     lib.ptyx_plan_slot_floats.argtypes = [vp]
     lib.ptyx_plan_slot_floats.restype = ctypes.c_int64
     lib.ptyx_plan_slot_target.argtypes = [vp, vp, i32]
@@ -188,7 +190,7 @@ def load(path: str | None = None):
     lib.ptyx_slot_block_floats.restype = ctypes.c_int64
     lib.ptyx_slots_export.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ptyx_obj_gather_slots.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, i32, vp]
-    for name in ("ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots", "ptyx_plan_check", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+    for name in ("ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots", "ptyx_plan_check", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_set_select", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
                  "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",
@@ -227,7 +229,7 @@ def set_tuning(key: str, value: int) -> None:
     check(load().ptyx_set_tuning(key.encode(), int(value)))
 
 
-TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam", "tail_fin", "small_spec")   # ptyx_set_tuning's keys
+TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam", "tail_fin", "small_spec", "sel_fold")   # ptyx_set_tuning's keys
 
 
 def get_tuning(key: str) -> int:

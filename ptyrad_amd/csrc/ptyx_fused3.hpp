@@ -594,7 +594,23 @@ struct PrepExtra {
   double* zsum = nullptr;      // per-(pattern, slice) loss_sparse window sums (else psums, per pattern)
   float2* fpk = nullptr;       // non-null: F(P_p) straight to the K-packed fpk, one leading workgroup a
                                // mode (probe_spectrum_reg), instead of the row pass into tmp
+  // PTYX_PREP_SELECT folded in (a graph-replayed step's ptyx_step_select): the call's indices are
+  // sel_all[sel_start[*sel_cnt] + j], which the pattern workgroups also store to sel_out (the call's
+  // idx, read by the later launches); sel workgroups zero zero[0, zero_n) and advance *steps[t]
+  const int32_t* sel_all = nullptr;
+  const int64_t* sel_start = nullptr;
+  const int64_t* sel_cnt = nullptr;
+  int32_t* sel_out = nullptr;
+  float* zero = nullptr;
+  long long zero_n = 0;
+  float* const* steps = nullptr;
+  int n_steps = 0;
   __host__ __device__ int lead_blocks() const { return probe && fpk ? P : 0; }
+  __host__ __device__ int sel_blocks() const {
+    if (!sel_all) return 0;
+    const long long zb = (zero_n + 4095) / 4096;
+    return (int)(zb < 1 ? 1 : zb > 64 ? 64 : zb);
+  }
   __host__ __device__ int row_blocks() const { return probe && !fpk ? (kN / kPrLines) * P : 0; }
   __host__ __device__ int h_blocks() const { return H ? kN2 / 256 : 0; }
 };
@@ -668,7 +684,25 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
     probe_spectrum_reg(ex.probe + (size_t)blockIdx.x * kN2, ex.fpk + (size_t)blockIdx.x * kN2);
     return;
   }
-  const int b = blockIdx.x - ex.lead_blocks();
+  if ((int)blockIdx.x < ex.lead_blocks() + ex.sel_blocks()) {   // the folded step selection
+    const int sb = (int)blockIdx.x - ex.lead_blocks(), nsb = ex.sel_blocks();
+    if (sb == 0 && (int)threadIdx.x < ex.n_steps) {   // the optimizer's step counts (torch's state_step += 1)
+      float* s = ex.steps[threadIdx.x];
+      *s = *s + 1.0f;
+    }
+    // scalar head up to 16-byte alignment, float4 body, scalar tail (as k_step_select)
+    float* g = ex.zero;
+    const long long n = ex.zero_n, t = (long long)sb * 256 + threadIdx.x, stride = (long long)nsb * 256;
+    const long long head = min(n, (long long)(((16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15) >> 2));
+    if (t < head) g[t] = 0.f;
+    float4* g4 = reinterpret_cast<float4*>(g + head);
+    const long long n4 = (n - head) >> 2;
+    for (long long i = t; i < n4; i += stride) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long long i = head + 4 * n4 + t; i < n; i += stride) g[i] = 0.f;
+    return;
+  }
+  const int b = blockIdx.x - ex.lead_blocks() - ex.sel_blocks();
+  if (ex.sel_all) idx = ex.sel_all + ex.sel_start[*ex.sel_cnt];
   const bool zs = SPARSE && ex.zsum != nullptr;
   const int np = zs ? n * Nz : n;                         // pattern blocks
   const int bx = b - small_prep_blocks(n, Nz, Ny, zs);   // the PrepExtra roles
@@ -686,11 +720,14 @@ __global__ __launch_bounds__(256) void k_small_prep(const int* idx, int n, const
     if (zs) {   // (pattern j, slice z): z = 0 also writes the table entry
       const int j = b / Nz, z = b - j * Nz;
       if (z == 0 && threadIdx.x == 0) table_entry(j, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
+      if (z == 0 && threadIdx.x == 0 && ex.sel_out) ex.sel_out[j] = idx[j];
       slice_window_sum(j, z, idx, crop, n_scans, Ny, Nx, objp, sparse_n, Nz, ex.zsum);
     } else if constexpr (SPARSE) {
+      if (threadIdx.x == 0 && ex.sel_out) ex.sel_out[b] = idx[b];
       k_pattern_table_direct_body(b, idx, n, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, objp, sparse_n, psums,
                                   Nz, tc);
     } else if (threadIdx.x == 0) {
+      if (ex.sel_out) ex.sel_out[b] = idx[b];
       table_entry(b, idx, boff, n_batches, crop, n_scans, Ny, Nx, bid, geo, tc);
     }
     return;

@@ -284,12 +284,12 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneCount };
+               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
-                                            "tail_fin", "small_spec"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                            "tail_fin", "small_spec", "sel_fold"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -417,6 +417,17 @@ struct ptyx_plan {
   bool slots_ready = false;
   int32_t slots_n = 0;
   const int32_t* slots_idx = nullptr;
+  // ptyx_plan_set_select: the step selection the next PTYX_PREP_SELECT call takes (one-shot); sel_fold:
+  // the call in flight does it inside k_small_prep (register_prep)
+  bool sel_set = false;
+  bool sel_fold = false;
+  const int32_t* sel_all = nullptr;
+  const int64_t* sel_start = nullptr;
+  const int64_t* sel_cnt = nullptr;
+  float* sel_grad = nullptr;
+  int64_t sel_grad_n = 0;
+  float* const* sel_steps = nullptr;
+  int32_t sel_n_steps = 0;
   // ptyx_plan_set_adam: the optimizer step the next PTYX_PREP_FUSED_ADAM call takes (one-shot)
   bool fadam_set = false;
   bool fadam_on = false;            // the call in flight takes it
@@ -1011,6 +1022,16 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
       ex.twg = pl->twg;
       if (g_tuning[kTuneSmallSpec] != 0) ex.fpk = pl->fpk;   // the whole spectrum in this launch
     }
+    if (pl->sel_fold) {   // PTYX_PREP_SELECT: the step's indices, gradient zeroing and step counts here
+      ex.sel_all = pl->sel_all;
+      ex.sel_start = pl->sel_start;
+      ex.sel_cnt = pl->sel_cnt;
+      ex.sel_out = const_cast<int32_t*>(a.idx);
+      ex.zero = pl->sel_grad;
+      ex.zero_n = pl->sel_grad_n;
+      ex.steps = pl->sel_steps;
+      ex.n_steps = pl->sel_n_steps;
+    }
     if (Nz > 1) {
       ex.H = a.H;
       ex.hpk = pl->hpk;
@@ -1022,8 +1043,8 @@ static int register_prep(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, c
     }
     {
       ProfScope ps(pl, kKTable, st);
-      const dim3 gr(ex.lead_blocks() + f3::small_prep_blocks(a.n_idx, Nz, d.Ny, ex.zsum != nullptr) + ex.row_blocks() +
-                    ex.h_blocks()),
+      const dim3 gr(ex.lead_blocks() + ex.sel_blocks() + f3::small_prep_blocks(a.n_idx, Nz, d.Ny, ex.zsum != nullptr) +
+                    ex.row_blocks() + ex.h_blocks()),
           bl(256);
       const f3::TableCheck tc{a.err, a.mrow, a.mrows};
       if (sparse)
@@ -1884,16 +1905,23 @@ __global__ __launch_bounds__(256) void k_step_store(const float* terms, int nb, 
   if (threadIdx.x == 0) *cnt = c + 1;
 }
 
-extern "C" int ptyx_step_select(void* stream, const int32_t* idx_all, const int64_t* istart, const int64_t* cnt,
-                                int32_t n, int32_t* idx_out, float* grad, int64_t grad_n, float* const* steps,
-                                int32_t n_steps) {
-  g_err.clear();
-  if (!idx_all || !istart || !cnt || !idx_out || n < 0 || grad_n < 0 || (grad_n && !grad))
+static int step_select_check(const int32_t* idx_all, const int64_t* istart, const int64_t* cnt, float* grad,
+                             int64_t grad_n, float* const* steps, int32_t n_steps) {
+  if (!idx_all || !istart || !cnt || grad_n < 0 || (grad_n && !grad))
     return fail(PTYX_EINVAL, "ptyx_step_select: null pointer or negative size");
   if (n_steps < 0 || n_steps > 256 || (n_steps && !steps))
     return fail(PTYX_EINVAL, "ptyx_step_select: steps must be a device array of at most 256 pointers");
   if (reinterpret_cast<uintptr_t>(grad) % 4)
     return fail(PTYX_EINVAL, "ptyx_step_select: grad must be 4-byte aligned");
+  return PTYX_OK;
+}
+
+extern "C" int ptyx_step_select(void* stream, const int32_t* idx_all, const int64_t* istart, const int64_t* cnt,
+                                int32_t n, int32_t* idx_out, float* grad, int64_t grad_n, float* const* steps,
+                                int32_t n_steps) {
+  g_err.clear();
+  if (!idx_out || n < 0) return fail(PTYX_EINVAL, "ptyx_step_select: null pointer or negative size");
+  if (int rc = step_select_check(idx_all, istart, cnt, grad, grad_n, steps, n_steps)) return rc;
   const int64_t work = std::max<int64_t>(n, (grad_n + 3) / 4);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (work + 255) / 256));
   hipLaunchKernelGGL(k_step_select, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx_all, istart, cnt, n,
@@ -1966,8 +1994,8 @@ static int setup_call(ptyx_plan* pl, const ptyx_inputs* in, const int32_t* idx, 
   if (!cfg->single_on && !cfg->poissn_on)
     return fail(PTYX_EINVAL, "at least one data-error loss term (loss_single / loss_poissn) must be on");
   if (cfg->sparse_on && cfg->sparse_n < 1) return fail(PTYX_EINVAL, "sparse_n must be >= 1");
-  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM)) >
-          PTYX_PREP_REUSE ||
+  if ((cfg->prep & ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_DEFER_GATHER | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM |
+                     PTYX_PREP_SELECT)) > PTYX_PREP_REUSE ||
       cfg->prep < 0)
     return fail(PTYX_EINVAL, "unknown cfg.prep");
   KArgs a = make_args(pl, in, idx, n_idx);
@@ -2152,10 +2180,25 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   const bool defer = (c.prep & PTYX_PREP_DEFER_PROBE) != 0;
   const bool store = (c.prep & PTYX_PREP_GRAD_STORE) != 0;
   const bool fadam = (c.prep & PTYX_PREP_FUSED_ADAM) != 0;
-  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM);
+  const bool sel = (c.prep & PTYX_PREP_SELECT) != 0;
+  c.prep &= ~(PTYX_PREP_DEFER_PROBE | PTYX_PREP_GRAD_STORE | PTYX_PREP_FUSED_ADAM | PTYX_PREP_SELECT);
   if (fadam && !pl->fadam_set) return fail(PTYX_EINVAL, "PTYX_PREP_FUSED_ADAM without ptyx_plan_set_adam");
+  if (sel && !pl->sel_set) return fail(PTYX_EINVAL, "PTYX_PREP_SELECT without ptyx_plan_set_select");
   resolve_prep(pl, in, engine, &c);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // PTYX_PREP_SELECT: inside the register engines' small-call preparation launch, else first here
+  pl->sel_fold = sel && (engine == kEngFused3 || engine == kEngFmm) && a.n_idx <= f3::kSmallCall && pl->bbox &&
+                 c.prep == PTYX_PREP_CALL && g_tuning[kTuneSelFold] != 0;
+  if (sel) {
+    pl->sel_set = false;
+    if (!pl->sel_fold) {
+      const int64_t work = std::max<int64_t>(n_idx, (pl->sel_grad_n + 3) / 4);
+      const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (work + 255) / 256));
+      hipLaunchKernelGGL(k_step_select, dim3(blocks), dim3(256), 0, st, pl->sel_all, pl->sel_start, pl->sel_cnt, n_idx,
+                         const_cast<int32_t*>(idx), pl->sel_grad, pl->sel_grad_n, pl->sel_steps, pl->sel_n_steps);
+      if ((rc = launch_status("k_step_select launch"))) return rc;
+    }
+  }
   bool gstore = false;
   if (store && (rc = grad_store_setup(pl, engine, gz, st, &gstore))) return rc;
   pl->grad_store = gstore;
@@ -2163,12 +2206,29 @@ extern "C" int ptyx_forward_loss_grad(ptyx_plan* pl, void* stream, const ptyx_in
   pl->fadam_done = false;
   rc = run_call(pl, in, a, &c, gz, engine, st, loss_terms, kPhaseAll, nullptr, defer);
   pl->grad_store = false;
+  pl->sel_fold = false;
   if (fadam) {   // the registered step, consumed: fused into the epilogue, or its own launch now
     if (!rc && !pl->fadam_done)
       rc = opt::adam_launch(st, pl->fadam_ts, pl->fadam_h, pl->fadam_store ? &pl->fadam_ss : nullptr);
     pl->fadam_on = pl->fadam_set = pl->fadam_done = false;
   }
   return rc;
+}
+
+extern "C" int ptyx_plan_set_select(ptyx_plan* pl, const int32_t* idx_all, const int64_t* istart, const int64_t* cnt,
+                                    float* grad, int64_t grad_n, float* const* steps, int32_t n_steps) {
+  g_err.clear();
+  if (!pl) return fail(PTYX_EINVAL, "plan is null");
+  if (int rc = step_select_check(idx_all, istart, cnt, grad, grad_n, steps, n_steps)) return rc;
+  pl->sel_all = idx_all;
+  pl->sel_start = istart;
+  pl->sel_cnt = cnt;
+  pl->sel_grad = grad;
+  pl->sel_grad_n = grad_n;
+  pl->sel_steps = steps;
+  pl->sel_n_steps = n_steps;
+  pl->sel_set = true;
+  return PTYX_OK;
 }
 
 extern "C" int ptyx_plan_set_adam(ptyx_plan* pl, int32_t n, float* const* params, const float* const* grads,
@@ -2210,9 +2270,9 @@ extern "C" int ptyx_forward_loss_grad_begin(ptyx_plan* pl, void* stream, const p
   if (grads) gz = *grads;
   KArgs a{};
   int engine = kEngTwoPass;
-  if (cfg && (cfg->prep & PTYX_PREP_FUSED_ADAM))
-    return fail(PTYX_EINVAL, "PTYX_PREP_FUSED_ADAM is for ptyx_forward_loss_grad (a split step's gradients "
-                             "are complete only after the caller's exchange)");
+  if (cfg && (cfg->prep & (PTYX_PREP_FUSED_ADAM | PTYX_PREP_SELECT)))
+    return fail(PTYX_EINVAL, "PTYX_PREP_FUSED_ADAM / PTYX_PREP_SELECT are for ptyx_forward_loss_grad (a split "
+                             "step's gradients are complete only after the caller's exchange)");
   if ((rc = setup_call(pl, in, idx, boff, n_batches, n_idx, cfg, dp_out, gz, &a, &engine))) return rc;
   DeviceGuard dg(pl->device);
   ptyx_loss_cfg c = *cfg;

@@ -258,8 +258,8 @@ class Plan:
             off = np.asarray(batch_offsets.cpu() if isinstance(batch_offsets, torch.Tensor) else batch_offsets,
                              dtype=np.int64)
             if off[-1] - off[0] > cap and np.max(np.diff(off)) <= cap:
-                if prep & _lib.PTYX_PREP_FUSED_ADAM:
-                    raise ValueError("PTYX_PREP_FUSED_ADAM on a call larger than one engine call")
+                if prep & (_lib.PTYX_PREP_FUSED_ADAM | _lib.PTYX_PREP_SELECT):
+                    raise ValueError("PTYX_PREP_FUSED_ADAM / PTYX_PREP_SELECT on a call larger than one engine call")
                 return self._chunked(t, idx, off, cap, loss_cfg, grads, grad_scale, loss_terms, dp_out, max_batch,
                                      store=bool(prep & _lib.PTYX_PREP_GRAD_STORE))
         idx_t = self._idx(idx)
@@ -276,6 +276,13 @@ class Plan:
                                                    _ptr(off_t), nb, n, ctypes.byref(cfg), _ptr(loss_terms),
                                                    _ptr(dp_out), ctypes.byref(g)))
         return loss_terms
+
+    def set_select(self, idx_all, istart, cnt, grad, grad_n, steps, n_steps):
+        """ptyx_plan_set_select: the step selection (ptyx_step_select's arguments, device pointers)
+        the next forward_loss_grad call with PTYX_PREP_SELECT begins with; the call's idx is then
+        the output buffer its indices are picked into."""
+        _lib.check(self.lib.ptyx_plan_set_select(self._h, idx_all, istart, cnt, grad, int(grad_n), steps,
+                                                 int(n_steps)))
 
     def set_adam(self, args, store=None):
         """ptyx_plan_set_adam: the optimizer step the next forward_loss_grad call with

@@ -114,6 +114,7 @@ class StepGraphs:
     MAX_GRAPHS = 16               # captured steps kept (insertion order; the oldest is dropped)
     STORE = True                  # whole-batch steps' calls overwrite the object gradient (A/B switch)
     FUSE_ADAM = True              # one-rank steps fold the optimizer step into the engine call (A/B switch)
+    SELECT = True                 # whole-batch steps' calls pick their own indices (PTYX_PREP_SELECT; A/B switch)
 
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
@@ -186,29 +187,34 @@ class StepGraphs:
         # the HIP Adam's step counts advance in the same launch (its own increment launch skipped)
         step_ts = optimizer._step_tensors() if hasattr(optimizer, "_step_tensors") else []
         sp = self._step_ptrs(key, step_ts, flat_grad.device) if 0 < len(step_ts) <= 256 else None
-        # the step's indices (device counter) + zeroed gradient buffer (and terms tail), one launch
+        # the step's indices (device counter) + zeroed gradient buffer (and terms tail), one launch;
         # a whole-batch step's engine call overwrites the object gradient at the buffer's head
-        # (PTYX_PREP_GRAD_STORE): only the rest is zeroed
+        # (PTYX_PREP_GRAD_STORE): only the rest is zeroed.  A whole-batch step's call does the
+        # selection itself (PTYX_PREP_SELECT: inside the small call's preparation launch).
         z0 = 0 if split else self._store_from
         zbuf = flat_grad[z0:]
-        _lib.check(lib.ptyx_step_select(st, _ptr(idx_all), _ptr(istart), _ptr(cnt), int(sidx.numel()), _ptr(sidx),
-                                        _ptr(zbuf), int(zbuf.numel()), None if sp is None else _ptr(sp),
-                                        0 if sp is None else len(step_ts)))
+        sel = (_ptr(idx_all), _ptr(istart), _ptr(cnt), _ptr(zbuf), int(zbuf.numel()),
+               None if sp is None else _ptr(sp), 0 if sp is None else len(step_ts))
+        fold = self.SELECT and not split
+        done = [False]   # the step counts have advanced
+        if not fold:
+            _lib.check(lib.ptyx_step_select(st, sel[0], sel[1], sel[2], int(sidx.numel()), _ptr(sidx), *sel[3:]))
+            done[0] = True
         try:
             self._body_rest(model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
-                            ctx, extra, G, split, sp, lib, st, scap, ar_skip)
+                            ctx, extra, G, split, sp, lib, st, scap, ar_skip, sel if fold else None, done)
         except BaseException:
             # an eager step that raised after its step counts advanced (an engine-call check, the
             # optimizer itself): take them back, so Adam's bias correction stays in step with the
             # updates it really made (a capture only records the launch; nothing ran)
-            if sp is not None and not torch.cuda.is_current_stream_capturing():
+            if sp is not None and done[0] and not torch.cuda.is_current_stream_capturing():
                 with torch.no_grad():
                     for t_ in step_ts:
                         t_.sub_(1)
             raise
 
     def _body_rest(self, model, optimizer, loss_fn, flat_grad, grads, key, grad_scale, cnt, rstart, terms_all,
-                   ctx, extra, G, split, sp, lib, st, scap=0, ar_skip=0):
+                   ctx, extra, G, split, sp, lib, st, scap=0, ar_skip=0, sel=None, done=None):
         sidx, soff, sterms, mine_t = self.static[key]
         t = {"obja": model.opt_obja.detach(), "objp": model.opt_objp.detach(), "probe": model.opt_probe.detach(),
              "shifts": model.opt_probe_pos_shifts.detach(), "H": model._H_rv().detach(),
@@ -223,6 +229,9 @@ class StepGraphs:
                                          slot_exchange=SlotExchange(ctx, scap) if scap else None, _rows_checked=True)
         else:
             prep = _lib.PTYX_PREP_GRAD_STORE if self._store_from else 0
+            if sel is not None:
+                model.plan.set_select(*sel)
+                prep |= _lib.PTYX_PREP_SELECT
             # one rank, the step counts already advanced, one HIP Adam launch for the whole step: the
             # call takes the optimizer step itself (PTYX_PREP_FUSED_ADAM; the k_fused3 engine's small
             # calls fold it into their last launch), the loss-term store included
@@ -233,6 +242,8 @@ class StepGraphs:
                 prep |= _lib.PTYX_PREP_FUSED_ADAM
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
                                          max_batch=max(key[0]), _rows_checked=True, prep=prep)
+            if sel is not None and done is not None:
+                done[0] = True
             if fargs is not None:
                 return
         if extra:

@@ -188,3 +188,11 @@ def test_plan_set_adam_validates_without_gpu():
     assert rc == _lib.PTYX_EINVAL and b"plan is null" in lib.ptyx_last_error()
     assert _lib.PTYX_PREP_FUSED_ADAM == 32
     assert _lib.get_tuning("fuse_adam") == -1
+
+
+def test_plan_set_select_validates_without_gpu():
+    """ptyx_plan_set_select (ABI 210) refuses a null plan before touching the device."""
+    lib = _lib.load()
+    rc = lib.ptyx_plan_set_select(None, None, None, None, None, 0, None, 0)
+    assert rc == _lib.PTYX_EINVAL and b"plan is null" in lib.ptyx_last_error()
+    assert _lib.PTYX_PREP_SELECT == 64 and _lib.get_tuning("sel_fold") == -1

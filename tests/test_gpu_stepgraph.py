@@ -315,22 +315,32 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
 @pytest.mark.parametrize("name", ["traj_c1_n128", "traj_n128_p6z6_ga1"])
 def test_graphs_fused_adam_bitwise_unfused_and_reference(name):
     """Graph-replayed recon_step with the optimizer step folded into the engine call
-    (StepGraphs.FUSE_ADAM, the default) against the same with the separate HIP Adam launch: bitwise
-    equal trajectories, both at the reference's (RMS < 1e-5)."""
+    (StepGraphs.FUSE_ADAM, the default) and the step selection too (StepGraphs.SELECT,
+    PTYX_PREP_SELECT: inside the small call's preparation launch, or its own launch first with
+    tuning sel_fold 0) against the separate ptyx_step_select / HIP Adam launches: bitwise equal
+    trajectories, at the reference's (RMS < 1e-5)."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
     from ptyrad_amd.stepgraph import StepGraphs
+    from ptyrad_amd import _lib
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     out = {}
+    # (fuse, select, sel_fold): the optimizer step in the call or not; the step selection in the
+    # call (inside k_small_prep, or its k_step_select launch first with sel_fold 0) or not
+    variants = [(False, False, -1), (True, False, -1), (True, True, -1), (True, True, 0), (False, True, -1)]
     try:
-        for fuse in (False, True):
-            StepGraphs.FUSE_ADAM = fuse
+        for fuse, sel, fold in variants:
+            StepGraphs.FUSE_ADAM, StepGraphs.SELECT = fuse, sel
+            _lib.set_tuning("sel_fold", fold)
             m = gpu_recon(z, graphs=True)
             assert m._step_graphs.replays >= 1
-            out[fuse] = _params(m)
+            out[(fuse, sel, fold)] = _params(m)
     finally:
-        StepGraphs.FUSE_ADAM = True
-    for k in out[False]:
-        assert np.array_equal(out[False][k], out[True][k]), k
+        StepGraphs.FUSE_ADAM, StepGraphs.SELECT = True, True
+        _lib.set_tuning("sel_fold", -1)
+    base = out[variants[0]]
+    for v in variants[1:]:
+        for k in base:
+            assert np.array_equal(base[k], out[v][k]), (v, k)
     for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
-        assert float(np.sqrt(np.mean((out[True][k].astype(np.float64) - ref) ** 2))) < 1e-5, k
+        assert float(np.sqrt(np.mean((out[(True, True, -1)][k].astype(np.float64) - ref) ** 2))) < 1e-5, k
