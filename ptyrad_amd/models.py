@@ -293,12 +293,29 @@ class PtychoHIP(nn.Module):
         self.register_buffer("propagator_grid", torch.stack([Ky, Kx], dim=0))
         k = 2 * torch.pi / self.lambd
         self.register_buffer("Kz", torch.sqrt(k ** 2 - Kx ** 2 - Ky ** 2))
+        # Kz − k without the cancellation, fp64 from the f32 grid: the dz gradient's kernel (_dz_phase)
+        q2, k64 = Kx.double() ** 2 + Ky.double() ** 2, float(k)
+        self.register_buffer("Kz0", (-q2 / (k64 + torch.sqrt(k64 ** 2 - q2))).float())
+
+    def _dz_phase(self, H, dz, extra=None):
+        """H — the reference's value, exp(i dz Kz) (× the tilt ramps) in f32 — with the gradient in dz
+        taken as Re Σ conj(g_H) i (Kz − k + extra) H instead of through exp(i dz Kz).  The constant
+        part k of the phase is a global phase of every propagation, so the loss does not depend on
+        it and its term Re Σ conj(g_H) i k H is exactly 0 — but in f32 (k ≈ 150 Å⁻¹, dz·k ≈ 300 rad)
+        its rounding is ≈ 1e-3 of the gradient (the reference's own floor, tests/test_oracle_golden.py);
+        dropping it leaves the same exact-arithmetic gradient without that noise (pinned to the fp64
+        oracle in tests/test_gpu_propagator.py).  The value is H bit for bit (× exp(0) = 1)."""
+        kern = self.Kz0 if extra is None else self.Kz0 + extra.detach()
+        return H.detach() * torch.exp(1j * (dz - dz.detach()) * kern)
 
     def _propagator(self):
         """get_propagators (models.py:300-360) for a global tilt: the (N, N) complex64 H every
         position uses, differentiable in opt_slice_thickness / opt_obj_tilts when they are optimised."""
         if self.pos_tilts:   # the engine applies the per-position ramps; H is exp(i dz Kz) or the fixed H
-            return torch.exp(1j * self.opt_slice_thickness * self.Kz) if self.change_thickness else self.H_eff
+            if not self.change_thickness:
+                return self.H_eff
+            dz = self.opt_slice_thickness
+            return self._dz_phase(torch.exp(1j * dz.detach() * self.Kz), dz)
         if not self.prop_opt:
             return self.H_eff
         Ky, Kx = self.propagator_grid
@@ -306,11 +323,14 @@ class PtychoHIP(nn.Module):
         ty = self.opt_obj_tilts[:, 0, None, None] / 1e3
         tx = self.opt_obj_tilts[:, 1, None, None] / 1e3
         if self.tilt_obj and self.change_thickness:                       # case 1
-            H = torch.exp(1j * dz * self.Kz) * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx)))
+            ramp = Ky * torch.tan(ty) + Kx * torch.tan(tx)
+            d0 = dz.detach()
+            H = torch.exp(1j * d0 * self.Kz) * torch.exp(1j * d0 * ramp)   # (the tilts' gradient: through ramp)
+            H = self._dz_phase(H, dz, ramp) * torch.exp(1j * d0 * (ramp - ramp.detach()))
         elif self.tilt_obj:                                                # case 2A
             H = self.H * torch.exp(1j * dz * (Ky * torch.tan(ty) + Kx * torch.tan(tx)))
         else:                                                              # case 3
-            H = torch.exp(1j * dz * self.Kz)[None]
+            H = self._dz_phase(torch.exp(1j * dz.detach() * self.Kz), dz)[None]
         return H[0]
 
     def _H_rv(self):
@@ -462,7 +482,9 @@ class PtychoHIP(nn.Module):
             ramp_arg = Ky * torch.tan(t[:, 0, None, None]) + Kx * torch.tan(t[:, 1, None, None])
             if self.change_thickness:            # case 1 (models.py:339-342): the current dz
                 dz = self.opt_slice_thickness
-                return torch.exp(1j * dz * self.Kz) * torch.exp(1j * dz * ramp_arg)
+                d0 = dz.detach()
+                H = torch.exp(1j * d0 * self.Kz) * torch.exp(1j * d0 * ramp_arg)
+                return self._dz_phase(H, dz, ramp_arg) * torch.exp(1j * d0 * (ramp_arg - ramp_arg.detach()))
             return self.H * torch.exp(1j * self._dz * ramp_arg)
         return self._propagator()[None,]
 

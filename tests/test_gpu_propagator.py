@@ -4,10 +4,12 @@ carries it through PtychoHIP's rebuilt H to opt_slice_thickness / opt_obj_tilts.
 
 Fixtures tests/golden/n*_opt*.npz come from the reference itself (make_golden.py --prop-only).
 Tolerances: H ≤ 1e-5 (its f32 phase dz·Kz ≈ 300 rad); dp ≤ 1e-5; loss terms rtol 2e-5;
-object / probe gradients ≤ 5e-5; dL/dH vs the oracle ≤ 1e-4; the dz gradient rtol 1e-2 (the
-constant part dz·k of the phase, k ≈ 150 Å⁻¹, cancels in the sum Re Σ conj(g_H) i Kz H, and
-the f32 reference's own rounding of that cancellation is ≈ 1e-3 relative); tilt gradients
-rtol 1e-3.
+object / probe gradients ≤ 5e-5; dL/dH vs the oracle ≤ 1e-4; against the reference the dz gradient
+rtol 1e-2 (the constant part dz·k of the phase, k ≈ 150 Å⁻¹, cancels in the sum Re Σ conj(g_H) i Kz H,
+and the f32 reference's own rounding of that cancellation is ≈ 1e-3 relative) and the tilt gradients
+rtol 1e-3.  Against the fp64 oracle's chain (test_propagator_gradients_vs_fp64_oracle) the engine's
+dz gradient is held to 5e-5 and the tilt gradients to 2e-5: PtychoHIP drops the exactly-zero
+global-phase term k from the dz chain (models.py _dz_phase), so it is not bound by that floor.
 """
 import glob
 import json
@@ -199,3 +201,42 @@ def test_per_position_tilts_compose_with_blur_stages(stages):
     gp = model.opt_probe.grad.cpu().numpy()
     assert rel(gp[..., 0] + 1j * gp[..., 1], g["probe"]) < 5e-5
     assert rel(model.opt_probe_pos_shifts.grad.cpu().numpy(), g["shifts"]) < 2e-4
+
+
+# the dz gradient against the fp64 oracle: PtychoHIP takes it as Re Σ conj(g_H) i (Kz − k + ramp) H
+# (models.py _dz_phase: the global-phase term k, exactly 0, dropped), so it is not bounded by the
+# f32 reference's ≈ 1e-3 cancellation floor of the rtol 1e-2 comparison above — only by the engine's
+# fp32 dL/dH (≤ 1e-4 of the oracle's, test_engine_dH_vs_oracle)
+TOL_DZ_F64 = 5e-5     # measured 9.1e-6 / 6.0e-6 (the reference's own: 5.2e-4 / 1.5e-4)
+TOL_TILT_F64 = 2e-5   # measured 1.1e-6 / 6.1e-7 (the reference's own: 7.4e-7 / 2.8e-6)
+
+
+@pytest.mark.parametrize("path", PROP, ids=[os.path.basename(p)[:-4] for p in PROP])
+def test_propagator_gradients_vs_fp64_oracle(path):
+    """The dz and global-tilt gradients (get_propagators cases 1 / 2A / 3) against the fp64 oracle's
+    chain from its dL/dH on the same H: tighter than the comparison with the f32 reference."""
+    device = dev()
+    from ptyrad_amd.losses import CombinedLoss
+    d = load_case(path)
+    model = _model(d, device)
+    model.zero_grad(set_to_none=True)
+    total, _ = CombinedLoss(d["loss_params"], device=device).fused(model, [d["batch"]])
+    total.backward()
+    Hm = model.get_propagators([0])[0].detach().cpu().numpy()
+    _, _, g = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], Hm, d["occu"],
+                                    d["meas"], [d["batch"]], d["loss_params"], shift_probes=bool(d["shift_probes"]))
+    case = prop_case(d)
+    gdz, gt = orc.propagator_param_grads(g["H"], Hm, float(d["slice_thickness"]), d["obj_tilts"][0].astype(np.float64),
+                                        float(d["dx"]), float(d["lambd"]), case)
+    if case in (1, 3):
+        got = model.opt_slice_thickness.grad.item()
+        err = abs(got - gdz) / abs(gdz)
+        ref_err = abs(float(d["g_slice_thickness"]) - gdz) / abs(gdz)   # the f32 reference's own distance
+        print(f"{os.path.basename(path)}: dz gradient rel err vs fp64 oracle {err:.2e} (reference {ref_err:.2e})")
+        assert err < TOL_DZ_F64, (err, ref_err)
+    if case in (1, 2):
+        gt_got = model.opt_obj_tilts.grad.cpu().numpy()[0].astype(np.float64)
+        err = float(np.abs(gt_got - gt).max() / np.abs(gt).max())
+        ref_err = float(np.abs(d["g_obj_tilts"][0] - gt).max() / np.abs(gt).max())
+        print(f"{os.path.basename(path)}: tilt gradient rel err vs fp64 oracle {err:.2e} (reference {ref_err:.2e})")
+        assert err < TOL_TILT_F64, (err, ref_err)
