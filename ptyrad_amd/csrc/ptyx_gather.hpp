@@ -268,14 +268,15 @@ __global__ __launch_bounds__(64 * GW) void k_obj_gather(GatherArgs ga) {
 // rounding.
 // The row-split gather's sums of one tile: wave w's rows ty + w·RW … (acc, cnt: running sums after
 // the Kahan-compensated accumulation over every hit, candidate order).  Tile (tyi, txi), slot plane zp.
-template <int N, bool ROWPERM, int GW, bool MP>
+// HUX > 0: that many hits in flight per wave instead of what 32 registers' worth of loads allow.
+template <int N, bool ROWPERM, int GW, bool MP, int HUX = 0>
 __device__ __forceinline__ void gather_rows_sums(const GatherArgs& ga, int tyi, int txi, int zp,
                                                  float2 (&acc)[kGTY / GW], float (&cnt)[kGTY / GW]) {
   constexpr int N2 = N * N;
   constexpr int NB = BinReach<N>::n;
   constexpr int RW = kGTY / GW;                          // rows per wave
   constexpr int NPL = MP ? kGatherMaxNp : 1;             // planes per row and hit (≤; np at run time)
-  constexpr int HU = 32 / (RW * NPL) > 0 ? 32 / (RW * NPL) : 1;   // hits in flight per wave
+  constexpr int HU = HUX > 0 ? HUX : (32 / (RW * NPL) > 0 ? 32 / (RW * NPL) : 1);   // hits in flight per wave
   __shared__ int4 s_hit[64 * GW];     // (cy, cx, j, c) of the chunk's hits, candidate order
   __shared__ float s_hcs[64 * GW];
   __shared__ int s_wcnt[GW];

@@ -284,12 +284,12 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneCount };
+               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneRowsHu, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
-                                            "tail_fin", "small_spec", "sel_fold"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                            "tail_fin", "small_spec", "sel_fold", "rows_hu"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -1551,12 +1551,16 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
   }
   if ((rc = launch_status("k_obj_gather launch"))) return rc;
-  if (fuse && !small_tail) {
+  // (tuning rows_hu 2: two hits' loads in flight a wave, at two workgroups a CU instead of three)
+  const auto launch_fused = [&] {
     ProfScope ps(pl, kKGatherAdam, st);
-    hipLaunchKernelGGL((k_gather_adam<N, true, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+    const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
+    if (g_tuning[kTuneRowsHu] == 2) hipLaunchKernelGGL((k_gather_adam<N, true, true, 2>), gr, dim3(256), 0, st, fz);
+    else hipLaunchKernelGGL((k_gather_adam<N, true, true, 1>), gr, dim3(256), 0, st, fz);
     pl->fadam_done = true;
     return launch_status("k_gather_adam launch");
-  }
+  };
+  if (fuse && !small_tail) return launch_fused();
   if (small_tail) {   // small call: one launch for the probe / position sums
     {
       ProfScope ps(pl, kKSlabReduce, st);
@@ -1579,13 +1583,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
       launch_probe_fin_reg(pl, a, st, gz.d_probe, P);
     }
     if ((rc = launch_status("k_fmm probe / position reduction launch"))) return rc;
-    if (fuse) {
-      ProfScope ps(pl, kKGatherAdam, st);
-      hipLaunchKernelGGL((k_gather_adam<N, true, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st,
-                         fz);
-      pl->fadam_done = true;
-      return launch_status("k_gather_adam launch");
-    }
+    if (fuse) return launch_fused();
     return PTYX_OK;
   }
   if (d_shifts) {

@@ -134,7 +134,7 @@ __device__ __forceinline__ void gather_adam_tile(const FusedAdamArgs& f, int b) 
 
 // The same for the mixed-state engine's row-split gather (k_obj_gather_rows, 4 waves, the probe
 // modes' slot planes summed): tile b % ptiles of object plane (slice) b / ptiles.
-template <int N, bool ROWPERM, bool MP>
+template <int N, bool ROWPERM, bool MP, int HU>
 __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, int b) {
   constexpr int GW = 4, RW = kGTY / GW;
   __shared__ float s_ns[2], s_bc[2];
@@ -172,7 +172,7 @@ __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, in
   float2 acc[RW];
   float cnt[RW];
   if (!skip) {
-    gather_rows_sums<N, ROWPERM, GW, MP>(ga, tyi, txi, z, acc, cnt);
+    gather_rows_sums<N, ROWPERM, GW, MP, HU>(ga, tyi, txi, z, acc, cnt);
   } else {
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
@@ -225,8 +225,9 @@ __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, in
   }
 }
 
-// ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine), else gather_adam_tile's.
-template <int N, bool ROWPERM, bool ROWS = false>
+// ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine; HU hits in flight a wave),
+// else gather_adam_tile's.
+template <int N, bool ROWPERM, bool ROWS = false, int HU = 1>
 __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
   const int b = blockIdx.x;
   if (b == 0 && f.rest.scnt) {   // as k_step_store: every thread reads *scnt before it advances
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
     if (threadIdx.x == 0) *f.rest.scnt = c + 1;
   }
   if (b < f.tiles) {
-    if constexpr (ROWS) gather_rows_adam_tile<N, ROWPERM, true>(f, b);
+    if constexpr (ROWS) gather_rows_adam_tile<N, ROWPERM, true, HU>(f, b);
     else gather_adam_tile<N, ROWPERM>(f, b);
     return;
   }

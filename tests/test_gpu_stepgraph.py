@@ -255,6 +255,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
     opt._external_step_inc = True
     _lib.set_tuning("fuse_adam", 0 if mode == "fallback" else -1)
     _lib.set_tuning("tail_fin", 0 if mode == "nofold" else -1)
+    _lib.set_tuning("rows_hu", 2 if mode == "hu2" else -1)
     model.plan.profile_begin()
     try:
         if mode == "off":
@@ -268,6 +269,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
         opt._external_step_inc = False
         _lib.set_tuning("fuse_adam", -1)
         _lib.set_tuning("tail_fin", -1)
+        _lib.set_tuning("rows_hu", -1)
     torch.cuda.synchronize()
     return prof
 
@@ -288,7 +290,8 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     from tests.dist_helpers import gpu_recon
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     res = {}
-    for mode in ("off", "fast", "fallback", "nofold"):
+    modes = ("off", "fast", "fallback", "nofold") + (("hu2",) if name == "traj_n128_p6z6_ga1" else ())
+    for mode in modes:
         model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
         prof = _one_step(model, opt, loss_fn, batches[0], mode, store)
         plist = [p for g in opt.param_groups for p in g["params"] if p in opt.state]
@@ -299,7 +302,7 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     if name == "traj_c1_n128":   # (the mixed-state engine needs k_finalize before its adjoint)
         assert "k_finalize" not in res["fast"][3] and "k_finalize" in res["nofold"][3], res["fast"][3]
     assert "k_gather_adam" in res["nofold"][3]
-    for mode in ("fast", "fallback", "nofold"):
+    for mode in modes[1:]:
         for k in res["off"][0]:
             assert np.array_equal(res["off"][0][k], res[mode][0][k]), (mode, k)
         for a, b in zip(res["off"][1], res[mode][1]):
