@@ -245,6 +245,13 @@ int ptyx_slots_export(ptyx_plan *plan, void *stream, int32_t use_last, int32_t c
 int ptyx_obj_gather_slots(ptyx_plan *plan, void *stream, const float *blocks, int32_t n_ranks, int32_t cap,
                           int32_t self_rank, const float *obja, const float *objp, float *d_obja, float *d_objp,
                           int32_t sparse_n, float *d_shifts);
+/* ptyx_obj_gather_slots, then the optimizer step ptyx_plan_set_adam registered (consumed), as
+ * ptyx_adam_step[_store] would take it right after (ABI 210): the caller has made every other
+ * gradient final (the probe part all-reduced).  A k_fused3 plan with one slice folds the step into
+ * the gather's launch (k_gather_adam); otherwise a k_adam launch follows.  Bitwise either way. */
+int ptyx_obj_gather_slots_adam(ptyx_plan *plan, void *stream, const float *blocks, int32_t n_ranks, int32_t cap,
+                               int32_t self_rank, const float *obja, const float *objp, float *d_obja,
+                               float *d_objp, int32_t sparse_n, float *d_shifts);
 
 /* Adjoint for an external loss: given dLdI (n_idx,N,N) = dL/d(dp_fwd) for the patterns idx,
  * accumulate the object / probe / position gradients (autograd of PtychoAD.forward). */

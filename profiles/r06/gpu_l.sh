@@ -24,3 +24,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt_ar" -o kt --output-
 python tools/trace_gaps.py "$O/kt_ar/kt_kernel_trace.csv" --last 3000 > "$O/gaps_ar.txt" &&
 echo "always-reduce: $(python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(d['value'], d['ms_per_optimizer_step'])" "$O/refcad_ar.json")" &&
 head -20 "$O/gaps_ar.txt"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_split.py -x -v --timeout 180 --timeout-method thread -k "slot or rccl" > "$O/split.log" 2>&1 &&
+echo "split: $(tail -1 "$O/split.log")"

@@ -40,7 +40,8 @@ EXPORTS = ("ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forwar
            "ptyx_plan_register_capacity", "ptyx_abi_struct_sizes", "ptyx_build_id", "ptyx_raw_read", "ptyx_meas_stats_len", "ptyx_meas_ws_bytes", "ptyx_meas_stats", "ptyx_meas_finish",
            "ptyx_meas_mean", "ptyx_meas_mean_seq", "ptyx_meas_pad_background", "ptyx_meas_pad_resample",
            "ptyx_step_select", "ptyx_step_store", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_set_select", "ptyx_plan_check",
-           "ptyx_plan_slot_floats", "ptyx_slot_block_floats", "ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots")
+           "ptyx_plan_slot_floats", "ptyx_slot_block_floats", "ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots",
+           "ptyx_obj_gather_slots_adam")
 
 
 class PtyxError(RuntimeError):
@@ -190,7 +191,8 @@ def load(path: str | None = None):
     lib.ptyx_slot_block_floats.restype = ctypes.c_int64
     lib.ptyx_slots_export.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ptyx_obj_gather_slots.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, i32, vp]
-    for name in ("ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots", "ptyx_plan_check", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_set_select", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
+    lib.ptyx_obj_gather_slots_adam.argtypes = lib.ptyx_obj_gather_slots.argtypes
+    for name in ("ptyx_plan_slot_target", "ptyx_slots_export", "ptyx_obj_gather_slots", "ptyx_obj_gather_slots_adam", "ptyx_plan_check", "ptyx_adam_step", "ptyx_adam_step_store", "ptyx_plan_set_adam", "ptyx_plan_set_select", "ptyx_step_select", "ptyx_step_store", "ptyx_plan_create", "ptyx_plan_destroy", "ptyx_forward", "ptyx_forward_loss_grad",
                  "ptyx_forward_loss_grad_begin", "ptyx_forward_loss_grad_end", "ptyx_set_tuning",
                  "ptyx_adjoint_dldi", "ptyx_meas_gather", "ptyx_loss_pacbed", "ptyx_obj_rblur", "ptyx_blur_adjoint", "ptyx_patch_gather",
                  "ptyx_patch_scatter_add", "ptyx_obj_constrain", "ptyx_probe_fix_int",

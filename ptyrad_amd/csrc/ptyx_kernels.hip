@@ -1197,13 +1197,21 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
 // The Adam tensors that ARE obja / objp (parameter = the call's object, gradient = its d_obja /
 // d_objp) take their step in the tile blocks, the probe's in the probe-row blocks; every other
 // tensor must fit one k_adam launch and must not overlap what those blocks write.
-static bool fused_adam_setup(const ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_grads& gz,
-                             const GatherArgs& g, int tiles, FusedAdamArgs* f) {
+// (probe_rows: the probe gradient's row pass is part of the launch; else it is final before it)
+static bool fused_adam_setup(const ptyx_plan* pl, const float* obja, const float* objp, const float* probe,
+                             const ptyx_grads& gz, bool probe_rows, const GatherArgs& g, int tiles, FusedAdamArgs* f) {
   constexpr int N = 128;
   const ptyx_dims& d = pl->d;
   if (d.O != 1) return false;
   const int64_t nobj = (int64_t)d.Nz * d.Ny * d.Nx, nprobe = 2LL * N * N * d.P;
-  const bool probe_rows = gz.d_probe && a.shift;   // (else the probe gradient is final before the launch)
+  probe_rows = probe_rows && gz.d_probe;
+  struct {
+    const float *obja, *objp;
+  } a{obja, objp};
+  struct {
+    const float* probe;
+  } in_{probe};
+  const auto* in = &in_;
   *f = FusedAdamArgs{};
   f->ga = g;
   f->h = pl->fadam_h;
@@ -1311,7 +1319,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   FusedAdamArgs fz{};
   const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles &&
                     g_tuning[kTuneGatherRows] != 1 && g_tuning[kTuneFuseAdam] != 0 &&
-                    fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+                    fused_adam_setup(pl, a.obja, a.objp, in->probe, gz, a.shift, g, tiles, &fz);
   // k_finalize folded into the small call's tail launch when nothing between them needs the
   // coefficients (one data term; the object gather, if any, after the tail: k_gather_adam)
   const bool tail_small = !bins && (gz.d_probe || d_shifts);
@@ -1545,7 +1553,8 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   FusedAdamArgs fz{};
   const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && sparse_tiles && P <= kGatherMaxNp &&
                     g_tuning[kTuneGatherRows] != 0 && g_tuning[kTuneGatherSplit] < 1 && g_tuning[kTuneFuseAdam] != 0 &&
-                    (small_tail || !(gz.d_probe || d_shifts)) && fused_adam_setup(pl, in, a, gz, g, tiles, &fz);
+                    (small_tail || !(gz.d_probe || d_shifts)) &&
+                    fused_adam_setup(pl, a.obja, a.objp, in->probe, gz, a.shift, g, tiles, &fz);
   if (gather_here && !fuse) {
     ProfScope ps(pl, kKGather, st);
     launch_gather<N, true, true>(pl, g, tiles, Nz, sparse_tiles, st);
@@ -2440,10 +2449,32 @@ extern "C" int ptyx_slots_export(ptyx_plan* pl, void* stream, int32_t use_last, 
   return launch_status("k_slots_meta launch");
 }
 
+static int gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_t n_ranks, int32_t cap,
+                        int32_t self_rank, const float* obja, const float* objp, float* d_obja, float* d_objp,
+                        int32_t sparse_n, float* d_shifts, bool fadam);
+
 extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_t n_ranks, int32_t cap,
                                      int32_t self_rank, const float* obja, const float* objp, float* d_obja,
                                      float* d_objp, int32_t sparse_n, float* d_shifts) {
   g_err.clear();
+  return gather_slots(pl, stream, blocks, n_ranks, cap, self_rank, obja, objp, d_obja, d_objp, sparse_n, d_shifts,
+                      false);
+}
+
+extern "C" int ptyx_obj_gather_slots_adam(ptyx_plan* pl, void* stream, const float* blocks, int32_t n_ranks,
+                                          int32_t cap, int32_t self_rank, const float* obja, const float* objp,
+                                          float* d_obja, float* d_objp, int32_t sparse_n, float* d_shifts) {
+  g_err.clear();
+  if (pl && !pl->fadam_set) return fail(PTYX_EINVAL, "ptyx_obj_gather_slots_adam without ptyx_plan_set_adam");
+  const int rc = gather_slots(pl, stream, blocks, n_ranks, cap, self_rank, obja, objp, d_obja, d_objp, sparse_n,
+                              d_shifts, true);
+  if (pl) pl->fadam_set = pl->fadam_done = false;
+  return rc;
+}
+
+static int gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_t n_ranks, int32_t cap,
+                        int32_t self_rank, const float* obja, const float* objp, float* d_obja, float* d_objp,
+                        int32_t sparse_n, float* d_shifts, bool fadam) {
   if (!pl) return fail(PTYX_EINVAL, "plan is null");
   if (pl->pend) return fail(PTYX_EINVAL, "a ptyx_forward_loss_grad_begin call is waiting on this plan");
   const int64_t sf = ptyx_plan_slot_floats(pl);
@@ -2463,6 +2494,13 @@ extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* b
   int rc = launch_status("k_slots_unpack launch");
   if (rc) return rc;
   pl->slots_ready = false;
+  // (the other ranks' position rows first: with the fused step their Adam runs in the gather's launch)
+  if (d_shifts && n_ranks > 1) {
+    hipLaunchKernelGGL(k_slots_rows_add, dim3((n + 255) / 256), dim3(256), 0, st, blocks, n, cap, bfl, (long long)sf,
+                       self_rank, d_shifts);
+    if ((rc = launch_status("k_slots_rows_add launch"))) return rc;
+  }
+  bool done = false;
   if (d_obja || d_objp) {
 #if !defined(PTYX_ONLY_N) || PTYX_ONLY_N == 128
     constexpr int N = 128;
@@ -2476,17 +2514,27 @@ extern "C" int ptyx_obj_gather_slots(ptyx_plan* pl, void* stream, const float* b
     const bool sparse_tiles = (long long)n * BinReach<N>::n < 64LL * tiles;
     g.nz = pl->d.Nz;
     g.zgrid = 1;
-    ProfScope ps(pl, kKGather, st);
-    launch_gather<N, true, false>(pl, g, tiles, pl->d.Nz, sparse_tiles, st);
+    // ptyx_obj_gather_slots_adam: every other gradient is final (the caller all-reduced the probe
+    // part): the gather with the optimizer step in one launch (k_gather_adam, no probe-row blocks)
+    FusedAdamArgs fz{};
+    ptyx_grads gz{};
+    gz.d_obja = d_obja;
+    gz.d_objp = d_objp;
+    if (fadam && pl->d.Nz == 1 && sparse_tiles && g_tuning[kTuneGatherRows] != 1 && g_tuning[kTuneFuseAdam] != 0 &&
+        fused_adam_setup(pl, obja, objp, nullptr, gz, false, g, tiles, &fz)) {
+      ProfScope ps(pl, kKGatherAdam, st);
+      hipLaunchKernelGGL((k_gather_adam<N, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+      done = true;
+    } else {
+      ProfScope ps(pl, kKGather, st);
+      launch_gather<N, true, false>(pl, g, tiles, pl->d.Nz, sparse_tiles, st);
+    }
     if ((rc = launch_status("k_obj_gather (slots) launch"))) return rc;
 #endif
   }
-  if (d_shifts && n_ranks > 1) {
-    hipLaunchKernelGGL(k_slots_rows_add, dim3((n + 255) / 256), dim3(256), 0, st, blocks, n, cap, bfl, (long long)sf,
-                       self_rank, d_shifts);
-    if ((rc = launch_status("k_slots_rows_add launch"))) return rc;
-  }
-  return PTYX_OK;
+  if (fadam && !done)
+    rc = opt::adam_launch(st, pl->fadam_ts, pl->fadam_h, pl->fadam_store ? &pl->fadam_ss : nullptr);
+  return rc;
 }
 
 extern "C" int ptyx_adjoint_dldi(ptyx_plan* pl, void* stream, const ptyx_inputs* in, const int32_t* idx,

@@ -416,10 +416,12 @@ class Plan:
         _lib.check(self.lib.ptyx_slots_export(self._h, self._stream(), int(bool(use_last)), int(cap), _ptr(block),
                                               _ptr(d_shifts)))
 
-    def gather_slots(self, blocks, n_ranks: int, cap: int, rank: int, t: dict, grads: dict, sparse_n: int):
+    def gather_slots(self, blocks, n_ranks: int, cap: int, rank: int, t: dict, grads: dict, sparse_n: int,
+                     adam=False):
         """ptyx_obj_gather_slots: object gradient of every rank block's patterns (the all-gathered
         ``blocks``) into grads['obja'] / ['objp'], and the other ranks' position-gradient rows
-        into grads['shifts']."""
+        into grads['shifts'].  ``adam``: then the optimizer step set_adam registered
+        (ptyx_obj_gather_slots_adam; every other gradient must be final)."""
         _need(blocks, torch.float32, "blocks", self.device)
         if blocks.numel() != n_ranks * self.slot_block_floats(cap):
             raise ValueError("blocks must hold n_ranks x slot_block_floats(cap) floats")
@@ -427,9 +429,9 @@ class Plan:
         for k, v in g.items():
             if v is not None:
                 _need(v, torch.float32, f"grad {k}", self.device)
-        _lib.check(self.lib.ptyx_obj_gather_slots(self._h, self._stream(), _ptr(blocks), int(n_ranks), int(cap),
-                                                  int(rank), _ptr(t["obja"]), _ptr(t["objp"]), _ptr(g["obja"]),
-                                                  _ptr(g["objp"]), int(sparse_n), _ptr(g["shifts"])))
+        fn = self.lib.ptyx_obj_gather_slots_adam if adam else self.lib.ptyx_obj_gather_slots
+        _lib.check(fn(self._h, self._stream(), _ptr(blocks), int(n_ranks), int(cap), int(rank), _ptr(t["obja"]),
+                      _ptr(t["objp"]), _ptr(g["obja"]), _ptr(g["objp"]), int(sparse_n), _ptr(g["shifts"])))
 
     def adjoint_dldi(self, t: dict, idx, dLdI, grads: dict, grad_scale: float = 1.0):
         """ptyx_adjoint_dldi: accumulate gradients for an external dL/d(dp)."""

@@ -378,8 +378,11 @@ class SlotExchange:
     position-gradient rows added to its own.  Bytes a rank sends: its cap slots (128 KiB each at
     N = 128) and rows, against 2·(W−1)/W of the object and position gradients for the all-reduce."""
 
-    def __init__(self, ctx, cap):
+    def __init__(self, ctx, cap, defer=False):
         self.ctx, self.cap = ctx, int(cap)
+        # defer: the call only exports and all-gathers; finish() runs the gather later (after the
+        # caller's all-reduce of the other gradients, so the optimizer step can ride in it)
+        self.defer, self._pending = bool(defer), None
 
     def _block(self, plan):
         """(this rank's block, all blocks): with RCCL the rank's block IS its slice of the
@@ -399,7 +402,16 @@ class SlotExchange:
         mine, recv = self._block(plan)
         plan.export_slots(cap, mine, grads.get("shifts"), use_last=used)
         ctx.all_gather_into(recv, mine)
-        plan.gather_slots(recv, ctx.world, cap, ctx.rank, t, grads, cfg.sparse_n if cfg.sparse_on else 1)
+        self._pending = (plan, recv, t, grads, cfg.sparse_n if cfg.sparse_on else 1)
+        if not self.defer:
+            self.finish()
+
+    def finish(self, adam=False):
+        """The deferred gather over every rank's slots; ``adam``: with the optimizer step the plan has
+        registered (ptyx_obj_gather_slots_adam: the other gradients must be final by now)."""
+        plan, recv, t, grads, sn = self._pending
+        self._pending = None
+        plan.gather_slots(recv, self.ctx.world, self.cap, self.ctx.rank, t, grads, sn, adam=adam)
 
     def dense(self, tensors):
         """The same exchange for a loss without slots (the CPU test doubles): each tensor holds

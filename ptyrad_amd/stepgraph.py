@@ -222,11 +222,16 @@ class StepGraphs:
         t.update(model._base())
         cfg = LossConfig.from_loss_params(loss_fn.loss_params)
         terms = sterms
+        sx = None
         if split:
             from .reconstruction import SlotExchange
+            # with the slot exchange and one HIP Adam launch for the step, the gather waits for the
+            # probe / loss-term all-reduce below and takes the optimizer step in its launch
+            fargs = optimizer.fused_step_args() if (self.FUSE_ADAM and scap and extra and sp is not None and
+                                                    hasattr(optimizer, "fused_step_args")) else None
+            sx = SlotExchange(ctx, scap, defer=fargs is not None) if scap else None
             model.plan.forward_loss_grad(t, sidx, soff, cfg, grads, grad_scale=grad_scale, loss_terms=sterms,
-                                         batch_sums_reduce=ctx.allreduce_sums,
-                                         slot_exchange=SlotExchange(ctx, scap) if scap else None, _rows_checked=True)
+                                         batch_sums_reduce=ctx.allreduce_sums, slot_exchange=sx, _rows_checked=True)
         else:
             prep = _lib.PTYX_PREP_GRAD_STORE if self._store_from else 0
             if sel is not None:
@@ -252,6 +257,10 @@ class StepGraphs:
                 terms.index_copy_(0, mine_t, sterms)
             # (with the slot exchange the object / position gradients are already whole)
             ctx.allreduce(flat_grad[ar_skip:] if (split and scap) else flat_grad)
+            if sx is not None and sx.defer:
+                model.plan.set_adam(fargs, (_ptr(terms), int(G), _ptr(rstart), _ptr(cnt), _ptr(terms_all)))
+                sx.finish(adam=True)
+                return
         if sp is not None:
             optimizer._external_step_inc = True
         # the loss terms into the iteration's table, then the counter advances: inside the HIP

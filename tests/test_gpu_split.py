@@ -336,18 +336,24 @@ def _nccl_slot_worker(rank, port, path, out):
         from ptyrad_amd.reconstruction import DistContext
         from tests.dist_helpers import gpu_recon
         z = np.load(path, allow_pickle=False)
+        from ptyrad_amd.stepgraph import StepGraphs
         res = {}
-        for slots in (False, True):
-            for graphs in (False, True):
+        # (slots, graphs, the slot gather taking the optimizer step: ptyx_obj_gather_slots_adam)
+        for slots, graphs, fuse in ((False, False, True), (False, True, True), (True, False, True),
+                                    (True, True, True), (True, True, False)):
+            StepGraphs.FUSE_ADAM = fuse
+            try:
                 ctx = DistContext(split_batches=True, always_reduce=True, slot_exchange=slots)
                 model, _, _, _, last = gpu_recon(z, ctx, shard=True, graphs=graphs, ret_all=True)
-                tag = f"{'s' if slots else 'f'}{'g' if graphs else 'e'}"
-                res.update({f"{tag}_obja": model.opt_obja.detach().cpu().numpy(),
-                            f"{tag}_objp": model.opt_objp.detach().cpu().numpy(),
-                            f"{tag}_probe": model.opt_probe.detach().cpu().numpy(),
-                            f"{tag}_shifts": model.opt_probe_pos_shifts.detach().cpu().numpy(),
-                            f"{tag}_terms": np.array([np.asarray(v) for v in last.values()]),
-                            f"{tag}_bufs": np.array(len(ctx._slot_bufs))})
+            finally:
+                StepGraphs.FUSE_ADAM = True
+            tag = f"{'s' if slots else 'f'}{'g' if graphs else 'e'}{'' if fuse else 'n'}"
+            res.update({f"{tag}_obja": model.opt_obja.detach().cpu().numpy(),
+                        f"{tag}_objp": model.opt_objp.detach().cpu().numpy(),
+                        f"{tag}_probe": model.opt_probe.detach().cpu().numpy(),
+                        f"{tag}_shifts": model.opt_probe_pos_shifts.detach().cpu().numpy(),
+                        f"{tag}_terms": np.array([np.asarray(v) for v in last.values()]),
+                        f"{tag}_bufs": np.array(len(ctx._slot_bufs))})
         np.savez(out, **res)
     finally:
         torch.distributed.destroy_process_group()
@@ -360,7 +366,8 @@ def test_slot_exchange_under_rccl_equals_flat_allreduce(tmp_path):
     the probe gradient and the loss terms all-reduced.  At world size 1 under RCCL (always_reduce)
     the slot gather runs over the very patterns, in the very order, the engine's own gather takes:
     the trajectory is BITWISE the flat all-reduce's, eager and graph-replayed (the all-gathers
-    captured), and matches the reference's (RMS < 1e-5)."""
+    captured; the graph steps' slot gather taking the optimizer step, ptyx_obj_gather_slots_adam,
+    or not), and matches the reference's (RMS < 1e-5)."""
     dev()
     import torch.multiprocessing as mp
     path = os.path.join(GOLDEN, "traj_c1_n128.npz")
@@ -368,7 +375,7 @@ def test_slot_exchange_under_rccl_equals_flat_allreduce(tmp_path):
     mp.start_processes(_nccl_slot_worker, args=(_free_port(), path, out), nprocs=1, start_method="spawn")
     r = np.load(out)
     assert int(r["sg_bufs"]) >= 1 and int(r["fe_bufs"]) == 0          # the exchange really ran (and only there)
-    for tag in ("se", "sg", "fg"):
+    for tag in ("se", "sg", "sgn", "fg"):
         for k in ("obja", "objp", "probe", "shifts", "terms"):
             assert np.array_equal(r["fe_" + k], r[f"{tag}_" + k]), (tag, k)
     z = np.load(path, allow_pickle=False)
