@@ -1205,13 +1205,6 @@ static bool fused_adam_setup(const ptyx_plan* pl, const float* obja, const float
   if (d.O != 1) return false;
   const int64_t nobj = (int64_t)d.Nz * d.Ny * d.Nx, nprobe = 2LL * N * N * d.P;
   probe_rows = probe_rows && gz.d_probe;
-  struct {
-    const float *obja, *objp;
-  } a{obja, objp};
-  struct {
-    const float* probe;
-  } in_{probe};
-  const auto* in = &in_;
   *f = FusedAdamArgs{};
   f->ga = g;
   f->h = pl->fadam_h;
@@ -1226,16 +1219,16 @@ static bool fused_adam_setup(const ptyx_plan* pl, const float* obja, const float
     const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
     return Span{lo, lo + (uintptr_t)(4 * n)};
   };
-  owned.push_back(span(a.obja, nobj));
-  owned.push_back(span(a.objp, nobj));
+  owned.push_back(span(obja, nobj));
+  owned.push_back(span(objp, nobj));
   if (gz.d_obja) owned.push_back(span(gz.d_obja, nobj));
   if (gz.d_objp) owned.push_back(span(gz.d_objp, nobj));
   if (probe_rows) owned.push_back(span(gz.d_probe, nprobe));
   for (const opt::AdamTensor& t : pl->fadam_ts) {
     if (!t.numel) continue;
     int plane = -1;
-    if (t.numel == nobj && gz.d_obja && t.g == gz.d_obja && t.p == a.obja) plane = 0;
-    else if (t.numel == nobj && gz.d_objp && t.g == gz.d_objp && t.p == a.objp) plane = 1;
+    if (t.numel == nobj && gz.d_obja && t.g == gz.d_obja && t.p == obja) plane = 0;
+    else if (t.numel == nobj && gz.d_objp && t.g == gz.d_objp && t.p == objp) plane = 1;
     if (plane >= 0) {
       if (f->om[plane]) return false;   // (the same tensor twice)
       f->op[plane] = t.p; f->om[plane] = t.m; f->ov[plane] = t.v; f->ostep[plane] = t.step; f->olr[plane] = t.lr;
@@ -1243,7 +1236,7 @@ static bool fused_adam_setup(const ptyx_plan* pl, const float* obja, const float
       owned.push_back(span(t.v, nobj));
       continue;
     }
-    if (probe_rows && t.numel == nprobe && t.g == gz.d_probe && t.p == in->probe) {
+    if (probe_rows && t.numel == nprobe && t.g == gz.d_probe && t.p == probe) {
       if (f->pp) return false;
       f->pp = t.p; f->pm = t.m; f->pv = t.v; f->pstep = t.step; f->plr = t.lr;
       owned.push_back(span(t.p, nprobe));

@@ -36,12 +36,13 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def bench_problem(config, device, seed=1234):
-    """bench.py's inputs for one GPU: geometry, seeded random object, probe modes, uniform DPs."""
+def bench_problem(config, device, seed=1234, world=1, rank=0):
+    """bench.py's inputs for one GPU (rank `rank` of a `world`-GPU job's geometry): geometry, seeded
+    random object, probe modes, uniform DPs."""
     from ptyrad_amd import synthetic as syn
     cfg = syn.BENCH_CONFIGS[config]
     N, P, O, Nz = cfg["N"], cfg["P"], cfg["O"], cfg["Nz"]
-    crop_pos, shifts, (Ny, Nx), _, _ = syn.bench_geometry(config)
+    crop_pos, shifts, (Ny, Nx), _, _ = syn.bench_geometry(config, world, rank)
     n = crop_pos.shape[0]
     g = torch.Generator(device=device)
     g.manual_seed(seed)
@@ -134,13 +135,21 @@ SUBSET = {"c5": (512, "PTYX_STRIPE_MB", "512"),        # 4 MiB of stripe interme
           "c4": (512, "PTYX_OBJ_SCRATCH_MB", "256")}   # 16 slot planes = 2 MiB a pattern → 128 a call
 
 
-@pytest.mark.parametrize("config", ["c5", "c3", "c4"])
-def test_bench_geometry_subset_gradients_vs_oracle(config, monkeypatch):
+@pytest.mark.parametrize("config,world,rank", [("c5", 1, 0), ("c3", 1, 0), ("c4", 1, 0),
+                                               ("c5", 8, 7), ("c3", 8, 3), ("c4", 8, 7)],
+                         ids=["c5", "c3", "c4", "c5_rank7of8", "c3_rank3of8", "c4_rank7of8"])
+def test_bench_geometry_subset_gradients_vs_oracle(config, world, rank, monkeypatch):
+    """Also one rank's shard of the 8-GPU job (bench_geometry(config, 8, r): c4's rows split by rank,
+    c3 / c5's block starting at the rank's first scan row): the replicated object, of which the
+    shard's windows touch one band (the engines' bounding box / tile skips), the last rank's band
+    at the object's bottom edge."""
     device = dev()
     from ptyrad_amd.engine import LossConfig, Plan, batch_offsets
     n_sub, env, mb_cap = SUBSET[config]
     monkeypatch.setenv(env, mb_cap)
-    cfg, t, probe_c, H, crop_pos, shifts = bench_problem(config, device, seed=99)
+    cfg, t, probe_c, H, crop_pos, shifts = bench_problem(config, device, seed=99, world=world, rank=rank)
+    if world > 1:   # the shard's rows are its own band, away from the single-rank block's
+        assert int(crop_pos[:, 0].min()) > 0
     n = crop_pos.shape[0]
     O, Nz, Ny, Nx = t["obja"].shape
     rng = np.random.default_rng(11)
