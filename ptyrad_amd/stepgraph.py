@@ -343,7 +343,8 @@ class StepGraphs:
             for pieces, G, split, mine, scap in steps:
                 scap = scap if (split and slots) else 0
                 sizes = tuple(len(p) for p in pieces)
-                key = (sizes, G, split, mine, scap, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs())
+                key = (sizes, G, split, mine, scap, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs(),
+                       (self.STORE, self.FUSE_ADAM, self.SELECT))
                 if key not in self.static:
                     n, nb = sum(sizes), len(sizes)
                     self.static[key] = (torch.zeros(n, dtype=torch.int32, device=dev),
