@@ -347,3 +347,36 @@ def test_graphs_fused_adam_bitwise_unfused_and_reference(name):
             assert np.array_equal(base[k], out[v][k]), (v, k)
     for k, ref in (("opt_obja", z["final_obja"]), ("opt_objp", z["final_objp"])):
         assert float(np.sqrt(np.mean((out[(True, True, -1)][k].astype(np.float64) - ref) ** 2))) < 1e-5, k
+
+
+def test_graphs_fused_step_with_grad_accumulation():
+    """grad_accumulation = 2 on the k_fused3 geometry: a step's call holds two mini-batches, so the
+    folded k_finalize (k_small_tail_fin) computes two coefficients a workgroup and the fused Adam
+    follows a two-batch gradient.  Eager, graph-replayed with every fold, and graph-replayed with
+    none: bitwise the same parameters and optimizer state after three iterations."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    from ptyrad_amd.reconstruction import recon_step
+    from ptyrad_amd.stepgraph import StepGraphs
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    out = {}
+    for tag, graphs, fold in (("eager", False, True), ("fused", True, True), ("plain", True, False)):
+        StepGraphs.FUSE_ADAM = StepGraphs.SELECT = fold
+        try:
+            model, opt, loss_fn, batches, _ = gpu_recon(z, niter=0, ret_all=True)
+            flat = np.concatenate(batches)
+            quarters = np.array_split(flat, 4)           # 4 mini-batches, 2 optimizer steps an iteration
+            for it in (1, 2, 3):
+                recon_step(quarters, 2, model, opt, loss_fn, None, it, verbose=False, graphs=graphs)
+            if graphs:
+                assert model._step_graphs.replays >= 1
+        finally:
+            StepGraphs.FUSE_ADAM = StepGraphs.SELECT = True
+        plist = [p for g in opt.param_groups for p in g["params"] if p in opt.state]
+        out[tag] = (_params(model), [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist])
+    for tag in ("fused", "plain"):
+        for k in out["eager"][0]:
+            assert np.array_equal(out["eager"][0][k], out[tag][0][k]), (tag, k)
+        for se, sf in zip(out["eager"][1], out[tag][1]):
+            for k in se:
+                assert torch.equal(se[k], sf[k]), (tag, k)
