@@ -1115,8 +1115,12 @@ struct Ramp {
 // pattern's v formed right after the sums), 2 = the full pass with ∂ℓ/∂I = c_single u_single +
 // c_poissn u_poissn of the pattern's mini-batch (slots / slabs / position sums then carry the
 // coefficients; no partial sums written).  0 = one data term, unit coefficient (the c2 kernel).
-template <bool SHIFT, bool SINGLE, int QM, int MODE = 0>
-__global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
+// HOLD (small calls, at most one workgroup a CU; shifted probes): ψ⁰ stays in registers from the
+// first transform to the slot instead of the park round trip (one workgroup a CU leaves the
+// register file to it).
+template <bool SHIFT, bool SINGLE, int QM, int MODE = 0, bool HOLD = false>
+__global__ __launch_bounds__(256, HOLD ? 1 : 2) void k_fused3(F3Args a) {
+  static_assert(!HOLD || (SHIFT && MODE == 0), "HOLD: the shifted-probe ring path, one data term");
   using namespace rf;
   __shared__ float2 buf[kLdsElems];
   __shared__ float s_red[4 * 2];
@@ -1173,6 +1177,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
     const int fx = fixed_of(tid);
     const int l0 = tid & 1;
     const PatInfo p = p_nxt;
+    float2 hold[HOLD ? 64 : 1];   // HOLD: ψ⁰
     // slot (row-permuted): element (y = j + 64 l0, x = fx) at row 2j + l0 → offset 2048·j
     const Rsrc r_slot = rsrc(a.slots + (size_t)pat * kN2, kN2 * 8);
     const int vslot0 = 8 * (l0 * kN + fx);
@@ -1218,7 +1223,8 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
           const float2 O = sl[rb * 64 + io];
-          if constexpr (MODE != 1) st2(v[j], r_park, vpark, 2048 * j);
+          if constexpr (HOLD) hold[j] = v[j];
+          else if constexpr (MODE != 1) st2(v[j], r_park, vpark, 2048 * j);
           v[j] = pcm(v[j], O);
           pin(v[j]);
         }
@@ -1356,7 +1362,7 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
     // post3 ring: ψ⁰ park + object window, 8 register pairs ahead (A = 2, S = 2 slot stores)
     auto issue3 = [&](auto Q, int vpo, int voo) {
       constexpr int q = decltype(Q)::value;
-      dma_c<4096 * q>(s_park, vpo, m0w + (q % 8) * 2048);
+      if constexpr (!HOLD) dma_c<4096 * q>(s_park, vpo, m0w + (q % 8) * 2048);
       dma_m<2 * q>(s_obj, voo, m0w + (q % 8) * 2048 + 1024, os);
     };
     fft_inv(v, buf, lc, cd.wsign, [&] {
@@ -1373,12 +1379,14 @@ __global__ __launch_bounds__(256, 2) void k_fused3(F3Args a) {
       const int vslot = rf::opaque(vslot0);
       rf::sfor<0, 32>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        vm_wait<ring_wait_count(q, 2, 0, 8)>();
+        vm_wait<ring_wait_count(q, HOLD ? 1 : 2, 0, 8)>();
         const float2* sl = ringw + (q % 8) * 256;
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int j = 2 * q + rb;
-          const float2 ps = sl[rb * 64 + lam];
+          float2 ps;
+          if constexpr (HOLD) ps = hold[j];
+          else ps = sl[rb * 64 + lam];
           const float2 O = sl[128 + rb * 64 + io];
           const float2 gv = pscale(v[j], inv_n);
           st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)

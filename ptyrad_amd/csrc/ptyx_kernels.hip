@@ -284,12 +284,13 @@ struct DeviceGuard {
 // Engine-variant tuning (ptyx_set_tuning): -1 = the measured default.  Process-wide; the
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
-               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneRowsHu, kTuneCount };
+               kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneRowsHu, kTunePsiHold,
+               kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
-                                            "tail_fin", "small_spec", "sel_fold", "rows_hu"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                            "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -1179,8 +1180,13 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
     ProfScope ps(pl, kKFused, st);
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
+    // at most one workgroup a CU (the default cadence's small calls): ψ⁰ may stay in registers
+    const bool hold = G <= pl->n_cu && g_tuning[kTunePsiHold] == 1;
     if (a.shift) {
-      if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
+      if (half && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 0, 0, true>), gr, bl, 0, st, f);
+      else if (single && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 2, 0, true>), gr, bl, 0, st, f);
+      else if (hold) hipLaunchKernelGGL((f3::k_fused3<true, false, 2, 0, true>), gr, bl, 0, st, f);
+      else if (half) hipLaunchKernelGGL((f3::k_fused3<true, true, 0>), gr, bl, 0, st, f);
       else if (single) hipLaunchKernelGGL((f3::k_fused3<true, true, 2>), gr, bl, 0, st, f);
       else hipLaunchKernelGGL((f3::k_fused3<true, false, 2>), gr, bl, 0, st, f);
     } else {

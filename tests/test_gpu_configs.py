@@ -282,3 +282,32 @@ def test_small_call_probe_spectrum_variants_vs_oracle(tuning, spec, P, Nz):
     for k in ("obja", "objp", "probe"):
         assert rel(g[k], og[k]) < TOL_G, k
     assert rel(g["shifts"], og["shifts"]) < TOL_SH
+
+
+@pytest.mark.parametrize("q1", [0.5, 1.0])
+def test_small_call_psi_hold_bitwise(tuning, q1):
+    """k_fused3 with ψ⁰ held in registers instead of parked (tuning "psi_hold" 1: calls of at most one
+    workgroup a CU, 256 VGPRs + AGPRs): the park stores exactly the registers it reloads, so the
+    results are bitwise the parking kernel's, and at the oracle's."""
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(128, 5, 5, P=1, O=1, Nz=1, seed=23)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=json.loads(json.dumps(orc_default_loss())))
+    d["loss_params"]["loss_single"]["dp_pow"] = q1
+    batches = [np.array([0, 5, 9, 14, 3, 12, 22]), np.array([7, 18, 2, 24])]
+    out = []
+    for hold in (-1, 1):
+        tuning("psi_hold", hold)
+        ks = {}
+        out.append(run_fused(d, dev(), batches, meas_f16=False, kernels=ks))
+        assert "k_fused" in ks, ks
+    (t0, dp0, g0, _), (t1, dp1, g1, _) = out
+    np.testing.assert_array_equal(t0, t1)
+    np.testing.assert_array_equal(dp0, dp1)
+    for k in g0:
+        np.testing.assert_array_equal(g0[k], g1[k])
+    oterms, _, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                          d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(t1, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g1[k], og[k]) < TOL_G, k
