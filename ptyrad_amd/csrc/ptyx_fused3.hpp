@@ -1389,7 +1389,9 @@ __global__ __launch_bounds__(256, HOLD ? 1 : 2) void k_fused3(F3Args a) {
           else ps = sl[rb * 64 + lam];
           const float2 O = sl[128 + rb * 64 + io];
           const float2 gv = pscale(v[j], inv_n);
-          st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);   // g_O / c_m = g·conj(ψ⁰)
+          // g_O / c_m = g·conj(ψ⁰); HOLD (a small call: the gather reads the slots next) keeps them in L2
+          if constexpr (HOLD) st2(pcmc(gv, ps), r_slot, vslot, 2048 * j);
+          else st2_stream(pcmc(gv, ps), r_slot, vslot, 2048 * j);
           v[j] = pcmc(gv, O);                                                          // g·conj(O)
           pin(v[j]);
         }

@@ -1181,7 +1181,8 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
     const dim3 gr(G), bl(256);
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
     // at most one workgroup a CU (the default cadence's small calls): ψ⁰ may stay in registers
-    const bool hold = G <= pl->n_cu && g_tuning[kTunePsiHold] == 1;
+    // (measured: c2 at ga = 1 0.1099 → 0.1080 ms a step, profiles/r06/psi_hold/; tuning psi_hold 0 parks)
+    const bool hold = G <= pl->n_cu && g_tuning[kTunePsiHold] != 0;
     if (a.shift) {
       if (half && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 0, 0, true>), gr, bl, 0, st, f);
       else if (single && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 2, 0, true>), gr, bl, 0, st, f);

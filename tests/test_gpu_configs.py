@@ -286,9 +286,9 @@ def test_small_call_probe_spectrum_variants_vs_oracle(tuning, spec, P, Nz):
 
 @pytest.mark.parametrize("q1", [0.5, 1.0])
 def test_small_call_psi_hold_bitwise(tuning, q1):
-    """k_fused3 with ψ⁰ held in registers instead of parked (tuning "psi_hold" 1: calls of at most one
-    workgroup a CU, 256 VGPRs + AGPRs): the park stores exactly the registers it reloads, so the
-    results are bitwise the parking kernel's, and at the oracle's."""
+    """k_fused3 with ψ⁰ held in registers instead of parked (calls of at most one workgroup a CU,
+    256 VGPRs + AGPRs; the default there, tuning "psi_hold" 0 parks): the park stores exactly the
+    registers it reloads, so the results are bitwise the parking kernel's, and at the oracle's."""
     from ptyrad_amd import synthetic as syn
     pr = syn.random_problem(128, 5, 5, P=1, O=1, Nz=1, seed=23)
     d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
@@ -296,7 +296,7 @@ def test_small_call_psi_hold_bitwise(tuning, q1):
     d["loss_params"]["loss_single"]["dp_pow"] = q1
     batches = [np.array([0, 5, 9, 14, 3, 12, 22]), np.array([7, 18, 2, 24])]
     out = []
-    for hold in (-1, 1):
+    for hold in (0, 1):
         tuning("psi_hold", hold)
         ks = {}
         out.append(run_fused(d, dev(), batches, meas_f16=False, kernels=ks))
