@@ -115,6 +115,7 @@ class StepGraphs:
     STORE = True                  # whole-batch steps' calls overwrite the object gradient (A/B switch)
     FUSE_ADAM = True              # one-rank steps fold the optimizer step into the engine call (A/B switch)
     SELECT = True                 # whole-batch steps' calls pick their own indices (PTYX_PREP_SELECT; A/B switch)
+    CHUNK = 16                    # consecutive steps of one shape replayed as one graph (1: one step a graph)
 
     def __init__(self):
         self.graphs = {}          # key -> CUDAGraph
@@ -157,6 +158,18 @@ class StepGraphs:
                 b[:h.size].copy_(torch.from_numpy(h), non_blocking=False)
             self._host = tuple(h.copy() for h in host)
         return bufs
+
+    def _evict(self, gkey):
+        """Drop one captured graph; a single step's also takes its chunk graphs (they replay its
+        static buffers) and its static state."""
+        self.graphs.pop(gkey, None)
+        if gkey and gkey[0] == "chunk":
+            return
+        for k in [k for k in self.graphs if k and k[0] == "chunk" and k[2] == gkey]:
+            del self.graphs[k]
+        self.static.pop(gkey, None)
+        self._sptr.pop(gkey, None)
+        self._seen.discard(gkey)
 
     def _drop_graphs(self):
         self.graphs.clear()
@@ -339,8 +352,18 @@ class StepGraphs:
             return tuple(int(v.data_ptr()) for p in live for v in optimizer.state.get(p, {}).values()
                          if isinstance(v, torch.Tensor))
 
+        # consecutive steps of one shape: a run of CHUNK of them replays as ONE graph of CHUNK step
+        # bodies (the device counter picks each body's mini-batch), so the replay boundary's idle
+        # gap (≈ 8 µs at c2, more than a launch inside a graph) is paid once per CHUNK steps
+        shapes = [(tuple(len(p) for p in st[0]),) + tuple(st[1:]) for st in steps]
+        run_left = [0] * len(steps)
+        for i in range(len(steps) - 1, -1, -1):
+            run_left[i] = 1 + (run_left[i + 1] if i + 1 < len(steps) and shapes[i + 1] == shapes[i] else 0)
+        K = max(1, int(self.CHUNK))
         try:
-            for pieces, G, split, mine, scap in steps:
+            i = 0
+            while i < len(steps):
+                pieces, G, split, mine, scap = steps[i]
                 scap = scap if (split and slots) else 0
                 sizes = tuple(len(p) for p in pieces)
                 key = (sizes, G, split, mine, scap, live_ids, hyper, lcfg, tuning, ptrs, id(optimizer), state_ptrs(),
@@ -353,12 +376,14 @@ class StepGraphs:
                                         torch.as_tensor(mine, dtype=torch.long).to(dev) if (extra and mine) else None)
                 args = (model, optimizer, loss_fn, flat_grad, grads, key, 1.0 / ga, cnt, idx_all, istart, rstart,
                         terms_all, ctx, extra, G, split, scap, ar_skip)
-                gr = self.graphs.get(key)
+                n_body = K if (K > 1 and key in self._seen and run_left[i] >= K) else 1
+                gkey = key if n_body == 1 else ("chunk", n_body, key)
+                gr = self.graphs.get(gkey)
                 if gr is not None:
                     gr.replay()
-                    self.replays += 1
                 elif key in self._seen:
-                    # second step of this shape: capture it (the optimizer state exists by now)
+                    # second step of this shape (the optimizer state exists by now): capture it, or a
+                    # chunk of n_body of them
                     gr = torch.cuda.CUDAGraph()
                     if self.pool is None:
                         self.pool = torch.cuda.graph_pool_handle()
@@ -367,21 +392,21 @@ class StepGraphs:
                         self._step_ptrs(key, sts, dev)
                     torch.cuda.synchronize(dev)
                     with torch.cuda.graph(gr, pool=self.pool):
-                        self._body(*args)
-                    self.graphs[key] = gr
+                        for _ in range(n_body):
+                            self._body(*args)
+                    self.graphs[gkey] = gr
                     self.captures += 1
                     while len(self.graphs) > self.MAX_GRAPHS:   # oldest first (e.g. a learning-rate schedule)
-                        old = next(iter(self.graphs))
-                        del self.graphs[old]
-                        self.static.pop(old, None)
-                        self._sptr.pop(old, None)
-                        self._seen.discard(old)
+                        self._evict(next(iter(self.graphs)))
                     gr.replay()
-                    self.replays += 1
                 else:
                     self._body(*args)
                     self.eager += 1
                     self._seen.add(key)
+                    i += 1
+                    continue
+                self.replays += n_body
+                i += n_body
         finally:
             for g, c in zip(optimizer.param_groups, saved):
                 g["capturable"] = c

@@ -380,3 +380,45 @@ def test_graphs_fused_step_with_grad_accumulation():
         for se, sf in zip(out["eager"][1], out[tag][1]):
             for k in se:
                 assert torch.equal(se[k], sf[k]), (tag, k)
+
+
+@pytest.mark.parametrize("ga", [1, 2])
+def test_graphs_chunked_replay_bitwise_one_step_graphs(ga):
+    """StepGraphs.CHUNK: a run of consecutive same-shape steps replays as ONE graph of CHUNK step
+    bodies (the device counter picks each body's mini-batch), the run's remainder as one-step
+    graphs.  64 patterns in 10·ga mini-batches (ga 1: runs of 4 and 6 steps of one shape; ga 2: runs of
+    2 and 8), CHUNK 3, 16 (no run that long: one-step graphs only) and 1, against eager: bitwise the same
+    parameters, optimizer state and loss history after three iterations."""
+    need_gpu()
+    from tests.dist_helpers import gpu_recon
+    from ptyrad_amd.reconstruction import recon_step
+    from ptyrad_amd.stepgraph import StepGraphs
+    z = np.load(os.path.join(GOLDEN, "traj_c1_n128.npz"), allow_pickle=False)
+    out = {}
+    for tag, graphs, chunk in (("eager", False, 1), ("c1", True, 1), ("c3", True, 3), ("c16", True, 16)):
+        StepGraphs.CHUNK = chunk
+        try:
+            model, opt, loss_fn, batches, _ = gpu_recon(z, niter=0, ret_all=True)
+            flat = np.concatenate(batches)
+            parts = np.array_split(flat, 10 * ga)      # ragged: two step shapes, each a run of 5
+            hist = [recon_step(parts, ga, model, opt, loss_fn, None, it, verbose=False, graphs=graphs)
+                    for it in (1, 2, 3)]
+            sg = model._step_graphs if graphs else None
+        finally:
+            StepGraphs.CHUNK = 16
+        if chunk == 3:
+            assert any(k[0] == "chunk" for k in sg.graphs), list(sg.graphs)
+        if graphs:
+            assert sg.replays >= 1
+        plist = [p for g in opt.param_groups for p in g["params"] if p in opt.state]
+        out[tag] = (_params(model), [{k: v.detach().cpu().clone() for k, v in opt.state[p].items()} for p in plist],
+                    hist)
+    for tag in ("c1", "c3", "c16"):
+        for k in out["eager"][0]:
+            assert np.array_equal(out["eager"][0][k], out[tag][0][k]), (tag, k)
+        for se, sf in zip(out["eager"][1], out[tag][1]):
+            for k in se:
+                assert torch.equal(se[k], sf[k]), (tag, k)
+        for a, b in zip(out["eager"][2], out[tag][2]):
+            for k in a:
+                assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (tag, k)

@@ -40,7 +40,11 @@ def main():
                     help="init_process_group('nccl') at world size 1 with every collective of the data-parallel "
                          "step executed (DistContext(always_reduce=True)): mini-batches split over the ranks "
                          "(the default cadence on several GPUs) or dealt whole")
+    ap.add_argument("--chunk", type=int, default=None, help="StepGraphs.CHUNK: same-shape steps a graph (A/B)")
     a = ap.parse_args()
+    if a.chunk is not None:
+        from ptyrad_amd.stepgraph import StepGraphs
+        StepGraphs.CHUNK = a.chunk
     ctx = None
     if a.rccl != "off":
         import torch.distributed as dist
@@ -103,7 +107,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.iters
         steps = -(-len(batches) // ga)
         sg = getattr(model, "_step_graphs", None)
-        print(json.dumps({"ga": ga, "P": P, "O": O, "Nz": Nz, "simlar": a.simlar, "graphs": a.graphs, "rccl": a.rccl, "tune": a.tune, "replays": sg.replays if sg else 0,
+        print(json.dumps({"ga": ga, "P": P, "O": O, "Nz": Nz, "simlar": a.simlar, "graphs": a.graphs, "rccl": a.rccl, "tune": a.tune, "chunk": a.chunk, "replays": sg.replays if sg else 0,
                           "mini_batches": len(batches), "optimizer_steps": steps,
                           "s_per_iter": round(dt, 4), "patterns_per_s": round(n / dt, 1),
                           "ms_per_optimizer_step": round(1e3 * dt / steps, 4),
