@@ -12,7 +12,7 @@
 //              of four needs four exchanges, not eight).  Two exchange forms: "agent" (the memory
 //              model's agent-scope release / acquire: an L2 write-back per wave) and "xcd" (stores
 //              acknowledged, then the readers' L1 invalidated: enough when one L2 holds the pattern);
-//              A third, "xcd_l2", keeps the arrival counter in that L2 as well (workgroup-scope
+//              A third, "xcd_flags", keeps the arrival counter in that L2 as well (workgroup-scope
 //              atomics and polls) and invalidates only L1 on the acquire side;
 //   meet_only   — the four exchanges alone, nothing transformed (their sync cost).
 // Every variant multiplies by a point-wise factor between transforms (the object / loss stand-ins,
@@ -84,16 +84,20 @@ __device__ __forceinline__ void pattern_barrier_xcd(int* c, int target, int* err
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
-// XCD-local with the counter in that L2 too: workgroup-scope atomics and polls (performed in L2,
-// polls bypassing L1), and only L1 invalidated on the acquire side (no L2 invalidation).
-__device__ __forceinline__ void pattern_barrier_l2(int* c, int target, int* err) {
+// XCD-local with one flag a workgroup instead of a shared counter (no serialised atomics): each
+// workgroup stores its epoch to its own flag (agent-scope relaxed store after its data stores are
+// acknowledged), threads 0 … W−1 each poll one flag, then the readers' L1 is invalidated.
+// (A first form kept the counter in L2 with workgroup-scope atomics and polls: the polls hit the
+// poller's own L1 and never saw the other arrivals — barrier time-outs — and is gone.)
+__device__ __forceinline__ void pattern_barrier_flags(int* flags, int W, int target, int* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int sub = (int)(blockIdx.x >> 3) % W;
+  if (threadIdx.x == 0) __hip_atomic_store(flags + sub, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)threadIdx.x < W) {
     int it = 0;
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-      if (++it > (1 << 18)) {
+    while (__hip_atomic_load(flags + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it > (1 << 20)) {
         atomicAdd(err, 1);
         break;
       }
@@ -101,14 +105,16 @@ __device__ __forceinline__ void pattern_barrier_l2(int* c, int target, int* err)
     }
   }
   __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
-template <int MODE>
+// c: the pattern's counter (modes 0, 1) or its 8 flags (mode 2); target: arrivals (modes 0, 1) or
+// the exchange's epoch (mode 2)
+template <int MODE, int W>
 __device__ __forceinline__ void meet(int* c, int target, int* err) {
   if constexpr (MODE == 0) pattern_barrier(c, target, err);
   else if constexpr (MODE == 1) pattern_barrier_xcd(c, target, err);
-  else pattern_barrier_l2(c, target, err);
+  else pattern_barrier_flags(c, W, target / W, err);
 }
 
 // the four exchanges alone (the sync cost of a split chain, nothing transformed)
@@ -116,7 +122,7 @@ template <int W, int MODE>
 __global__ __launch_bounds__(256) void k_meet_only(int* cnt, int base, int* err) {
   const int b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int pat = (r / W) * 8 + xcd;
-  for (int k = 0; k < 4; ++k) meet<MODE>(cnt + pat, base + (k + 1) * W, err);
+  for (int k = 0; k < 4; ++k) meet<MODE, W>(cnt + (MODE == 2 ? 8 : 1) * pat, base + (k + 1) * W, err);
 }
 
 template <int W, int MODE = 0>
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(256) void k_lds_chain(float2* f, const float2* M, c
   };
   auto xchg = [&](int k) {
     if constexpr (W == 1) __syncthreads();
-    else meet<MODE>(cnt + pat, base + (k + 1) * W, err);
+    else meet<MODE, W>(cnt + (MODE == 2 ? 8 : 1) * pat, base + (k + 1) * W, err);
   };
   // F1 = F⁻¹ (rows, then columns) · M0 · F2 = F (columns, then rows) · M1 · F3 = F⁻¹ (rows, columns)
   // · M2 · F4 = F (columns, rows) · M3
@@ -265,7 +271,7 @@ static void run_lds(Bufs& d, const std::vector<float2>& f0, std::vector<float2>&
   const size_t fb = f0.size() * sizeof(float2);
   // one launch from f0 for the bitwise check, then the timing (the field keeps transforming)
   CK(hipMemcpy(d.f, f0.data(), fb, hipMemcpyHostToDevice));
-  CK(hipMemset(d.cnt, 0, kPat * sizeof(int)));
+  CK(hipMemset(d.cnt, 0, 8 * kPat * sizeof(int)));
   CK(hipMemset(d.err, 0, sizeof(int)));
   int launches = 0;
   auto launch = [&](int) {
@@ -286,9 +292,9 @@ static void run_lds(Bufs& d, const std::vector<float2>& f0, std::vector<float2>&
   ok = ok && same && err == 0;
   std::printf("{\"variant\": \"lds\", \"W\": %d, \"exchange\": \"%s\", \"workgroups\": %d, \"us_per_call\": %.2f, "
               "\"bitwise_w1\": %s, \"barrier_timeouts\": %d}\n",
-              W, W == 1 ? "none" : MODE == 0 ? "agent" : MODE == 1 ? "xcd" : "xcd_l2", kPat * W, us, same ? "true" : "false", err);
+              W, W == 1 ? "none" : MODE == 0 ? "agent" : MODE == 1 ? "xcd" : "xcd_flags", kPat * W, us, same ? "true" : "false", err);
   if (W > 1) {   // the exchanges alone
-    CK(hipMemset(d.cnt, 0, kPat * sizeof(int)));
+    CK(hipMemset(d.cnt, 0, 8 * kPat * sizeof(int)));
     int nl = 0;
     const double um = time_us([&](int) {
       hipLaunchKernelGGL((k_meet_only<W, MODE>), dim3(kPat * W), dim3(256), 0, 0, d.cnt, nl * 4 * W, d.err);
@@ -297,7 +303,7 @@ static void run_lds(Bufs& d, const std::vector<float2>& f0, std::vector<float2>&
     CK(hipMemcpy(&err, d.err, sizeof(int), hipMemcpyDeviceToHost));
     ok = ok && err == 0;
     std::printf("{\"variant\": \"meet_only\", \"W\": %d, \"exchange\": \"%s\", \"us_per_call\": %.2f, "
-                "\"barrier_timeouts\": %d}\n", W, MODE == 0 ? "agent" : MODE == 1 ? "xcd" : "xcd_l2", um, err);
+                "\"barrier_timeouts\": %d}\n", W, MODE == 0 ? "agent" : MODE == 1 ? "xcd" : "xcd_flags", um, err);
   }
 }
 
@@ -320,7 +326,7 @@ int main() {
   CK(hipMalloc(&d.f, n * sizeof(float2)));
   CK(hipMalloc(&d.M, M.size() * sizeof(float2)));
   CK(hipMalloc(&d.twg, N * sizeof(float2)));
-  CK(hipMalloc(&d.cnt, kPat * sizeof(int)));
+  CK(hipMalloc(&d.cnt, 8 * kPat * sizeof(int)));
   CK(hipMalloc(&d.err, sizeof(int)));
   CK(hipMemcpy(d.M, M.data(), M.size() * sizeof(float2), hipMemcpyHostToDevice));
   CK(hipMemcpy(d.twg, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice));
