@@ -231,7 +231,7 @@ def set_tuning(key: str, value: int) -> None:
     check(load().ptyx_set_tuning(key.encode(), int(value)))
 
 
-TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam", "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold")   # ptyx_set_tuning's keys
+TUNING_KEYS = ("s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split", "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam", "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold", "gadam_lead")   # ptyx_set_tuning's keys
 
 
 def get_tuning(key: str) -> int:

@@ -285,12 +285,13 @@ struct DeviceGuard {
 // variants all compute the same results (tests/test_gpu_configs.py checks each against the oracle).
 enum TuneKey { kTuneHold = 0, kTunePsi0, kTuneGather, kTuneDeferGroups, kTuneGatherSplit, kTuneGenWg, kTuneGatherRows,
                kTuneFmmHoldH, kTuneFuseAdam, kTuneTailFin, kTuneSmallSpec, kTuneSelFold, kTuneRowsHu, kTunePsiHold,
-               kTuneCount };
+               kTuneGadamLead, kTuneCount };
 const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_defer_groups", "gather_split",
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
-                                            "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2, 1};
-long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                            "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold",
+                                            "gadam_lead"};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2, 2, 1};
+long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
 extern "C" int ptyx_set_tuning(const char* key, int64_t value) {
@@ -1151,11 +1152,21 @@ static void launch_fused3_both(const ptyx_plan* pl, const f3::F3Args& f, bool sh
 #undef PTYX_F3B
 }
 
+// k_fused3's workgroups for a call: nwg3 (two a CU) — or, with tuning psi_hold 2 (an A/B switch for
+// large calls), one a CU so that every call runs the register-held ψ⁰ variant
+static bool fused3_force_hold(const ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg) {
+  return g_tuning[kTunePsiHold] == 2 && pl->d.Nz == 1 && a.shift && !(cfg->single_on && cfg->poissn_on);
+}
+static int fused3_groups(const ptyx_plan* pl, const KArgs& a, const ptyx_loss_cfg* cfg) {
+  const int cap = fused3_force_hold(pl, a, cfg) ? std::min(pl->nwg3, pl->n_cu) : pl->nwg3;
+  return std::max(1, std::min(cap, a.n_idx));
+}
+
 // Preparation, pattern table and the k_fused3 / k_fused3ms pass (everything before k_finalize).
 static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const ptyx_loss_cfg* cfg,
                        const ptyx_grads& gz, hipStream_t st) {
   const int Nz = pl->d.Nz;                 // > 1: k_fused3ms (multislice)
-  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int G = fused3_groups(pl, a, cfg);
   const int nseg = a.n_batches + G;
   int rc = register_prep(pl, in, a, cfg, st, nseg);
   if (rc) return rc;
@@ -1182,7 +1193,7 @@ static int fused3_pass(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, con
     const bool half = single && f.q == 0.5f;   // dp_pow 1/2 (the schema default): sqrt / rsqrt form
     // at most one workgroup a CU (the default cadence's small calls): ψ⁰ may stay in registers
     // (measured: c2 at ga = 1 0.1099 → 0.1080 ms a step, profiles/r06/psi_hold/; tuning psi_hold 0 parks)
-    const bool hold = G <= pl->n_cu && g_tuning[kTunePsiHold] != 0;
+    const bool hold = (G <= pl->n_cu && g_tuning[kTunePsiHold] != 0) || fused3_force_hold(pl, a, cfg);
     if (a.shift) {
       if (half && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 0, 0, true>), gr, bl, 0, st, f);
       else if (single && hold) hipLaunchKernelGGL((f3::k_fused3<true, true, 2, 0, true>), gr, bl, 0, st, f);
@@ -1268,6 +1279,7 @@ static bool fused_adam_setup(const ptyx_plan* pl, const float* obja, const float
     f->rest.h = f->h;
   }
   if (pl->fadam_store) opt::adam_set_store(f->rest, pl->fadam_ss);
+  f->lead = g_tuning[kTuneGadamLead] != 0 ? 1 : 0;
   if (probe_rows) {
     f->pblocks = N / f3::kPrLinesT * d.P;
     f->ptmp = pl->slab;
@@ -1286,7 +1298,7 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   const bool single = cfg->single_on != 0;
   const bool both = single && cfg->poissn_on;               // k_fused3 / k_fused3ms MODE 1 / 2
   const int ci = both ? 2 : single ? 0 : 1;                // (2: the kernel applies the coefficients)
-  const int G = std::max(1, std::min(pl->nwg3, a.n_idx));
+  const int G = fused3_groups(pl, a, cfg);
   const int nseg = a.n_batches + G;
   int rc = PTYX_OK;
   if (ph != kPhaseEnd && (rc = fused3_pass(pl, in, a, cfg, gz, st))) return rc;

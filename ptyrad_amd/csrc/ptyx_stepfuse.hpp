@@ -14,6 +14,7 @@
 //                                        Adam step of those probe elements;
 //   the rest                             k_adam's chunks over every other tensor (positions ...),
 //                                        whose gradients are complete before the launch.
+// (Role order; with f.lead the probe-row and rest blocks take the first block indices.)
 // Same arithmetic as the unfused path (gather_apply's expressions, ptyx_adam.hpp's element update),
 // so the trajectory is bitwise the gather + rows + k_adam one (tests/test_gpu_stepgraph.py).
 
@@ -38,6 +39,9 @@ struct FusedAdamArgs {
   double plr;
   opt::AdamArgs rest;      // every other tensor (and the step bookkeeping in rest.scnt)
   int rblocks;
+  int lead;                // 1: the probe-row and rest blocks take the launch's first block indices
+                           // (dispatched first: their chains overlap the tile rounds instead of
+                           // trailing them); 0: tiles first
 };
 
 // One object tile: the gather's sums, then gradient + Adam per pixel (thread e, e + 256, ...).
@@ -229,8 +233,12 @@ __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, in
 // else gather_adam_tile's.
 template <int N, bool ROWPERM, bool ROWS = false, int HU = 1>
 __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
-  const int b = blockIdx.x;
-  if (b == 0 && f.rest.scnt) {   // as k_step_store: every thread reads *scnt before it advances
+  int b = blockIdx.x;   // the block's role index: tiles, then probe rows, then rest
+  if (f.lead) {
+    const int nl = f.pblocks + f.rblocks;
+    b = b < nl ? f.tiles + b : b - nl;
+  }
+  if (blockIdx.x == 0 && f.rest.scnt) {   // as k_step_store: every thread reads *scnt before it advances
     const int64_t c = *f.rest.scnt;
     const int64_t r0 = f.rest.srstart[c];
     for (int i = threadIdx.x; i < f.rest.snb * 5; i += blockDim.x) f.rest.sterms_all[r0 * 5 + i] = f.rest.sterms[i];

@@ -311,3 +311,32 @@ def test_small_call_psi_hold_bitwise(tuning, q1):
     np.testing.assert_allclose(t1, oterms, rtol=TOL_TERMS, atol=1e-7)
     for k in ("obja", "objp", "probe"):
         assert rel(g1[k], og[k]) < TOL_G, k
+
+
+def test_large_call_psi_hold_forced_vs_parking_and_oracle(tuning):
+    """tuning psi_hold 2 (an A/B switch for large calls): one k_fused3 workgroup a CU, each running
+    several patterns with ψ⁰ held in registers, instead of two a CU parking it.  400 patterns in
+    two mini-batches (more than the CUs): both forms at the oracle's; their probe-gradient segments
+    differ (another workgroup count), so they agree to fp32 summation order, not bitwise."""
+    from ptyrad_amd import synthetic as syn
+    pr = syn.random_problem(128, 20, 20, P=1, O=1, Nz=1, seed=29)
+    d = dict(obja=pr.obja, objp=pr.objp, probe=pr.probe * np.float32(30.0), shifts=pr.shifts, crop_pos=pr.crop_pos,
+             H=pr.H, occu=pr.occu, meas=pr.meas, shift_probes=True, loss_params=json.loads(json.dumps(orc_default_loss())))
+    perm = np.random.default_rng(4).permutation(400)
+    batches = [perm[:200], perm[200:]]
+    out = []
+    for hold in (0, 2):
+        tuning("psi_hold", hold)
+        ks = {}
+        out.append(run_fused(d, dev(), batches, meas_f16=False, kernels=ks))
+        assert "k_fused" in ks, ks
+    (t0, dp0, g0, _), (t2, dp2, g2, _) = out
+    np.testing.assert_array_equal(dp0, dp2)          # the forward model is per pattern: same bits
+    np.testing.assert_allclose(t2, t0, rtol=1e-6, atol=1e-9)
+    for k in g0:
+        assert rel(g2[k], g0[k]) < 1e-6, k
+    oterms, _, og = orc.forward_loss_grad(d["obja"], d["objp"], d["probe"], d["shifts"], d["crop_pos"], d["H"],
+                                          d["occu"], d["meas"], batches, d["loss_params"])
+    np.testing.assert_allclose(t2, oterms, rtol=TOL_TERMS, atol=1e-7)
+    for k in ("obja", "objp", "probe"):
+        assert rel(g2[k], og[k]) < TOL_G, k

@@ -256,6 +256,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
     _lib.set_tuning("fuse_adam", 0 if mode == "fallback" else -1)
     _lib.set_tuning("tail_fin", 0 if mode == "nofold" else -1)
     _lib.set_tuning("rows_hu", 2 if mode == "hu2" else -1)
+    _lib.set_tuning("gadam_lead", 0 if mode == "nolead" else -1)
     model.plan.profile_begin()
     try:
         if mode == "off":
@@ -270,6 +271,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
         _lib.set_tuning("fuse_adam", -1)
         _lib.set_tuning("tail_fin", -1)
         _lib.set_tuning("rows_hu", -1)
+        _lib.set_tuning("gadam_lead", -1)
     torch.cuda.synchronize()
     return prof
 
@@ -281,7 +283,9 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     its last launch (k_gather_adam: object gather + Adam of obja / objp per tile, the probe
     gradient's rows + its Adam, k_adam's chunks for the positions) leaves parameters, gradients and
     optimizer state BITWISE what the call followed by the HIP Adam leaves; so does the fallback
-    (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue).  The fused
+    (fuse_adam 0: the registered step as a k_adam launch after the ordinary epilogue); so does the
+    fused launch with its tile blocks first (gadam_lead 0, "nolead") instead of its probe-row and rest
+    blocks.  The fused
     call also folds k_finalize into its tail launch (k_small_tail_fin: every workgroup recomputes
     the mini-batch coefficients); tail_fin 0 ("nofold") keeps the k_finalize launch: the same bits.
     traj_n128_p6z6_ga1 (the tBL demo's 6 probe modes, 6 slices): the mixed-state engine, whose fused
@@ -290,7 +294,7 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     from tests.dist_helpers import gpu_recon
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     res = {}
-    modes = ("off", "fast", "fallback", "nofold") + (("hu2",) if name == "traj_n128_p6z6_ga1" else ())
+    modes = ("off", "fast", "fallback", "nofold", "nolead") + (("hu2",) if name == "traj_n128_p6z6_ga1" else ())
     for mode in modes:
         model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
         prof = _one_step(model, opt, loss_fn, batches[0], mode, store)
