@@ -224,8 +224,10 @@ __device__ __forceinline__ void small_tail_body(int bx, const float2* segslab, c
     return;
   }
   // the kSegSplit partial chains are independent: each round issues the loads of all of them, then
-  // adds (a missing segment adds 0·0 = +0 to a partial that is never −0: unchanged), so the sums
-  // and their order are k_segslab_reduce + k_segslab_final's
+  // adds (a missing segment leaves its partial unchanged, as k_segslab_reduce skips it), so the
+  // sums and their order are k_segslab_reduce + k_segslab_final's.  The slab loads do not wait for
+  // the segment ids: every g < nseg is inside the slab buffer, and an unused segment's value (never
+  // written: anything, NaN included) is dropped by the select, never multiplied.
   const int e = bx * 256 + threadIdx.x;
   float2 part[kSegSplit];
 #pragma unroll
@@ -237,15 +239,16 @@ __device__ __forceinline__ void small_tail_body(int bx, const float2* segslab, c
     for (int y = 0; y < kSegSplit; ++y) {
       const int g = g0 + y;
       mm[y] = g < nseg ? segbid[g] : -1;
-      u[y] = make_float2(0.f, 0.f);
-      if (mm[y] >= 0) u[y] = segslab[(size_t)g * kN2 + e];
+      u[y] = g < nseg ? segslab[(size_t)g * kN2 + e] : make_float2(0.f, 0.f);
     }
     if (g0 == 0) pre();
 #pragma unroll
     for (int y = 0; y < kSegSplit; ++y) {
-      const float c = mm[y] >= 0 ? coef_of(mm[y]) : 0.f;
-      part[y].x = fmaf(c, u[y].x, part[y].x);
-      part[y].y = fmaf(c, u[y].y, part[y].y);
+      if (mm[y] >= 0) {
+        const float c = coef_of(mm[y]);
+        part[y].x = fmaf(c, u[y].x, part[y].x);
+        part[y].y = fmaf(c, u[y].y, part[y].y);
+      }
     }
   }
   if (nseg <= 0) pre();
