@@ -460,3 +460,53 @@ def test_invalid_inputs_are_reported_through_the_c_abi(geom, bad):
     torch.cuda.synchronize()
     with pytest.raises(IndexError, match="scan index"):
         plan.forward_loss_grad(t, good[0], batch_offsets(good), cfg, zero_grads(t))
+
+
+def _nccl_chunk_worker(rank, port, path, out, split):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from ptyrad_amd.reconstruction import DistContext
+        from ptyrad_amd.stepgraph import StepGraphs
+        from tests.dist_helpers import gpu_recon
+        z = dict(np.load(path, allow_pickle=False))
+        z["batch_sizes"] = np.full(8, z["batches"].size // 8)     # 8 steps of one shape an iteration
+        res = {}
+        for tag, graphs, chunk in (("e", False, 1), ("g1", True, 1), ("g3", True, 3)):
+            StepGraphs.CHUNK = chunk
+            try:
+                ctx = DistContext(split_batches=split, always_reduce=True, slot_exchange=split)
+                model, _, _, _, last = gpu_recon(z, ctx, shard=True, graphs=graphs, ret_all=True, niter=3)
+            finally:
+                StepGraphs.CHUNK = 16
+            sg = getattr(model, "_step_graphs", None)
+            res.update({f"{tag}_obja": model.opt_obja.detach().cpu().numpy(),
+                        f"{tag}_objp": model.opt_objp.detach().cpu().numpy(),
+                        f"{tag}_probe": model.opt_probe.detach().cpu().numpy(),
+                        f"{tag}_shifts": model.opt_probe_pos_shifts.detach().cpu().numpy(),
+                        f"{tag}_terms": np.array([np.asarray(v) for v in last.values()]),
+                        f"{tag}_chunks": np.array(sum(1 for k in (sg.graphs if sg else {}) if k[0] == "chunk"))})
+        np.savez(out, **res)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["split_slots", "whole_batches"])
+def test_chunked_step_graphs_with_rccl_collectives_bitwise_eager(tmp_path, split):
+    """StepGraphs.CHUNK with the collectives captured (RCCL at world size 1, every collective
+    forced): 8 same-shape steps an iteration replayed as graphs of 3 step bodies (plus one-step
+    graphs for the remainder) — with split mini-batches, each body holds its loss-sum all-reduce,
+    the slot all-gather and the fused slot gather; with whole ones, the gradient all-reduce.
+    Bitwise the eager trajectory and the one-step graphs' after three iterations."""
+    dev()
+    import torch.multiprocessing as mp
+    path = os.path.join(GOLDEN, "traj_c1_n128.npz")
+    out = str(tmp_path / "nccl_chunk.npz")
+    mp.start_processes(_nccl_chunk_worker, args=(_free_port(), path, out, split), nprocs=1, start_method="spawn")
+    r = np.load(out)
+    assert int(r["g3_chunks"]) >= 1, int(r["g3_chunks"])
+    for tag in ("g1", "g3"):
+        for k in ("obja", "objp", "probe", "shifts", "terms"):
+            assert np.array_equal(r["e_" + k], r[f"{tag}_" + k]), (tag, k)
