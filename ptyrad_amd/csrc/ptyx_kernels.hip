@@ -1329,8 +1329,10 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   // step in one launch after the probe / position sums (ptyx_stepfuse.hpp)
   float* d_shifts = a.shift ? gz.d_shifts : nullptr;
   FusedAdamArgs fz{};
+  // (gather_rows 1: the row-split gather's order, as launch_gather then runs it unfused)
+  const bool rows_fuse = g_tuning[kTuneGatherRows] == 1;
   const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles &&
-                    g_tuning[kTuneGatherRows] != 1 && g_tuning[kTuneFuseAdam] != 0 &&
+                    g_tuning[kTuneFuseAdam] != 0 &&
                     fused_adam_setup(pl, a.obja, a.objp, in->probe, gz, a.shift, g, tiles, &fz);
   // k_finalize folded into the small call's tail launch when nothing between them needs the
   // coefficients (one data term; the object gather, if any, after the tail: k_gather_adam)
@@ -1414,7 +1416,9 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   }
   if (fuse) {
     ProfScope ps(pl, kKGatherAdam, st);
-    hipLaunchKernelGGL((k_gather_adam<N, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+    const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
+    if (rows_fuse) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
+    else hipLaunchKernelGGL((k_gather_adam<N, true>), gr, dim3(256), 0, st, fz);
     pl->fadam_done = true;
     return launch_status("k_gather_adam launch");
   }

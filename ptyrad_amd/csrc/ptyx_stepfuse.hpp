@@ -229,9 +229,9 @@ __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, in
   }
 }
 
-// ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine; HU hits in flight a wave),
-// else gather_adam_tile's.
-template <int N, bool ROWPERM, bool ROWS = false, int HU = 1>
+// ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine; HU hits in flight a wave;
+// MP false: one slot plane a hit, the single-state engine's row-split gather), else gather_adam_tile's.
+template <int N, bool ROWPERM, bool ROWS = false, int HU = 1, bool MP = true>
 __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
   int b = blockIdx.x;   // the block's role index: tiles, then probe rows, then rest
   if (f.lead) {
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
     if (threadIdx.x == 0) *f.rest.scnt = c + 1;
   }
   if (b < f.tiles) {
-    if constexpr (ROWS) gather_rows_adam_tile<N, ROWPERM, true, HU>(f, b);
+    if constexpr (ROWS) gather_rows_adam_tile<N, ROWPERM, MP, HU>(f, b);
     else gather_adam_tile<N, ROWPERM>(f, b);
     return;
   }

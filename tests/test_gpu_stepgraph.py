@@ -276,9 +276,9 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
     return prof
 
 
-@pytest.mark.parametrize("name,store", [("traj_c1_n128", False), ("traj_c1_n128", True),
-                                        ("traj_n128_p6z6_ga1", True)])
-def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
+@pytest.mark.parametrize("name,store,rows", [("traj_c1_n128", False, -1), ("traj_c1_n128", True, -1),
+                                             ("traj_c1_n128", True, 1), ("traj_n128_p6z6_ga1", True, -1)])
+def test_fused_adam_call_bitwise_the_call_then_adam(name, store, rows):
     """PTYX_PREP_FUSED_ADAM (ABI 209): the k_fused3 small call with the optimizer step folded into
     its last launch (k_gather_adam: object gather + Adam of obja / objp per tile, the probe
     gradient's rows + its Adam, k_adam's chunks for the positions) leaves parameters, gradients and
@@ -289,11 +289,23 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store):
     call also folds k_finalize into its tail launch (k_small_tail_fin: every workgroup recomputes
     the mini-batch coefficients); tail_fin 0 ("nofold") keeps the k_finalize launch: the same bits.
     traj_n128_p6z6_ga1 (the tBL demo's 6 probe modes, 6 slices): the mixed-state engine, whose fused
-    launch runs the row-split gather over the slices and the probe rows of every mode."""
+    launch runs the row-split gather over the slices and the probe rows of every mode.  rows 1
+    (tuning gather_rows): the single-state call's gather row-split too, fused (k_gather_adam's
+    one-plane row tiles) and unfused (k_obj_gather_rows) alike."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
+    from ptyrad_amd import _lib
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     res = {}
+    _lib.set_tuning("gather_rows", rows)
+    try:
+        _fused_adam_modes(name, store, z, res)
+    finally:
+        _lib.set_tuning("gather_rows", -1)
+
+
+def _fused_adam_modes(name, store, z, res):
+    from tests.dist_helpers import gpu_recon
     modes = ("off", "fast", "fallback", "nofold", "nolead") + (("hu2",) if name == "traj_n128_p6z6_ga1" else ())
     for mode in modes:
         model, opt, loss_fn, batches, _ = gpu_recon(z, niter=1, ret_all=True)   # (Adam state exists)
