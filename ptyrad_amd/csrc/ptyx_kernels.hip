@@ -290,7 +290,7 @@ const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
                                             "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold",
                                             "gadam_lead"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 1, 1, 1, 1, 1, 1, 2, 2, 1};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 2, 1, 1, 1, 1, 1, 2, 2, 1};
 long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
@@ -537,6 +537,20 @@ static int alloc_bins(ptyx_plan* pl) {
 // k_obj_gather over `tiles` × `nzg` tile planes.  A grid that cannot fill the GPU (a small object:
 // the tBL demo's 370² has 144 tiles a slice) splits every tile's candidates over S workgroups whose
 // partial sums k_obj_gather_fin adds in split order (deterministic for a given call shape).
+// The small gathers' form: 0 = tiles (k_obj_gather; fused: gather_adam_tile), 1 = row-split
+// (k_obj_gather_rows; fused: the row tiles), 2 = row-split with the fused single-plane launch held
+// to 128 VGPRs (k_gather_adam_r4: four workgroups a CU; mixed-state calls: as 1).  Tuning
+// gather_rows overrides for every unsplit gather; by default calls of at most kSmallCall patterns
+// run row-split — single-state ones in form 2 (c2 at ga = 1: the fused launch 22.2 → 20.4 µs,
+// profiles/r06/rows_r4/) — and larger ones in tiles.  One decision for the fused and the unfused
+// launches, so both sum every pixel's hits in the same order (bitwise the same gradients).
+static int gather_form(bool mp, long long n) {
+  const long long tr = g_tuning[kTuneGatherRows];
+  if (tr >= 0) return (int)tr;
+  if (n > f3::kSmallCall) return 0;
+  return mp ? 1 : 2;
+}
+
 template <int N, bool ROWPERM, bool MP>
 static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg, bool sparse_tiles, hipStream_t st) {
   const int parts = tiles * nzg;
@@ -548,10 +562,8 @@ static void launch_gather(const ptyx_plan* pl, GatherArgs g, int tiles, int nzg,
     S = std::max(1, std::min<int>((int)g_tuning[kTuneGatherSplit], pl->gpart_cap / parts));
   g.part = pl->gpart;
   g.pcnt = pl->gpcnt;
-  // rows over waves (k_obj_gather_rows): mixed-state small calls by default; gather_rows 1 / 0
-  // forces it on / off for every unsplit gather
-  const long long tr = g_tuning[kTuneGatherRows];
-  if (S == 1 && (tr == 1 || (tr < 0 && MP && g.n <= f3::kSmallCall))) {
+  // rows over waves (k_obj_gather_rows): gather_form
+  if (S == 1 && gather_form(MP, g.n) >= 1) {
     if (sparse_tiles) hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, 4, MP>), dim3(tiles, nzg), dim3(64 * 4), 0, st, g);
     else hipLaunchKernelGGL((k_obj_gather_rows<N, ROWPERM, kGWaves, MP>), dim3(tiles, nzg), dim3(64 * kGWaves), 0, st, g);
     return;
@@ -1329,8 +1341,9 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   // step in one launch after the probe / position sums (ptyx_stepfuse.hpp)
   float* d_shifts = a.shift ? gz.d_shifts : nullptr;
   FusedAdamArgs fz{};
-  // (gather_rows 1: the row-split gather's order, as launch_gather then runs it unfused)
-  const bool rows_fuse = g_tuning[kTuneGatherRows] == 1;
+  // (the gather's form and order as launch_gather would run it unfused)
+  const int gform = gather_form(false, a.n_idx);
+  const bool rows_fuse = gform >= 1;
   const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && Nz == 1 && sparse_tiles &&
                     g_tuning[kTuneFuseAdam] != 0 &&
                     fused_adam_setup(pl, a.obja, a.objp, in->probe, gz, a.shift, g, tiles, &fz);
@@ -1417,7 +1430,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   if (fuse) {
     ProfScope ps(pl, kKGatherAdam, st);
     const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
-    if (rows_fuse) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
+    if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
+    else if (rows_fuse) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
     else hipLaunchKernelGGL((k_gather_adam<N, true>), gr, dim3(256), 0, st, fz);
     pl->fadam_done = true;
     return launch_status("k_gather_adam launch");
@@ -1568,7 +1582,7 @@ static int run_fmm(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, const p
   // probe rows and the optimizer step in one launch after the probe / position sums
   FusedAdamArgs fz{};
   const bool fuse = ph == kPhaseAll && pl->fadam_on && gather_here && !bins && sparse_tiles && P <= kGatherMaxNp &&
-                    g_tuning[kTuneGatherRows] != 0 && g_tuning[kTuneGatherSplit] < 1 && g_tuning[kTuneFuseAdam] != 0 &&
+                    gather_form(true, g.n) >= 1 && g_tuning[kTuneGatherSplit] < 1 && g_tuning[kTuneFuseAdam] != 0 &&
                     (small_tail || !(gz.d_probe || d_shifts)) &&
                     fused_adam_setup(pl, a.obja, a.objp, in->probe, gz, a.shift, g, tiles, &fz);
   if (gather_here && !fuse) {
@@ -2536,10 +2550,14 @@ static int gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_
     ptyx_grads gz{};
     gz.d_obja = d_obja;
     gz.d_objp = d_objp;
-    if (fadam && pl->d.Nz == 1 && sparse_tiles && g_tuning[kTuneGatherRows] != 1 && g_tuning[kTuneFuseAdam] != 0 &&
+    const int gform = gather_form(false, n);
+    if (fadam && pl->d.Nz == 1 && sparse_tiles && g_tuning[kTuneFuseAdam] != 0 &&
         fused_adam_setup(pl, obja, objp, nullptr, gz, false, g, tiles, &fz)) {
       ProfScope ps(pl, kKGatherAdam, st);
-      hipLaunchKernelGGL((k_gather_adam<N, true>), dim3(fz.tiles + fz.pblocks + fz.rblocks), dim3(256), 0, st, fz);
+      const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
+      if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
+      else if (gform == 1) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
+      else hipLaunchKernelGGL((k_gather_adam<N, true>), gr, dim3(256), 0, st, fz);
       done = true;
     } else {
       ProfScope ps(pl, kKGather, st);

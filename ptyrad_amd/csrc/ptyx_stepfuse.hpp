@@ -231,8 +231,8 @@ __device__ __forceinline__ void gather_rows_adam_tile(const FusedAdamArgs& f, in
 
 // ROWS: the tile blocks are gather_rows_adam_tile's (mixed-state engine; HU hits in flight a wave;
 // MP false: one slot plane a hit, the single-state engine's row-split gather), else gather_adam_tile's.
-template <int N, bool ROWPERM, bool ROWS = false, int HU = 1, bool MP = true>
-__global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
+template <int N, bool ROWPERM, bool ROWS, int HU, bool MP>
+__device__ __forceinline__ void gather_adam_body(const FusedAdamArgs& f) {
   int b = blockIdx.x;   // the block's role index: tiles, then probe rows, then rest
   if (f.lead) {
     const int nl = f.pblocks + f.rblocks;
@@ -283,4 +283,14 @@ __global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
                            &s_bc2s[threadIdx.x]);
   __syncthreads();
   opt::adam_chunks(f.rest, s_nstep, s_bc2s, b - f.tiles - f.pblocks, f.rblocks);
+}
+template <int N, bool ROWPERM, bool ROWS = false, int HU = 1, bool MP = true>
+__global__ __launch_bounds__(256) void k_gather_adam(FusedAdamArgs f) {
+  gather_adam_body<N, ROWPERM, ROWS, HU, MP>(f);
+}
+// The one-plane row form held to 128 VGPRs: four workgroups a CU instead of three (tuning
+// gather_rows 2; 131 VGPRs unconstrained)
+template <int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_adam_r4(FusedAdamArgs f) {
+  gather_adam_body<N, true, true, 1, false>(f);
 }
