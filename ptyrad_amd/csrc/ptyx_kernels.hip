@@ -290,7 +290,7 @@ const char* const kTuneNames[kTuneCount] = {"s3_hold", "s_psi0", "s_gather", "s_
                                             "gen_wg_per_cu", "gather_rows", "fmm_hold_h", "fuse_adam",
                                             "tail_fin", "small_spec", "sel_fold", "rows_hu", "psi_hold",
                                             "gadam_lead"};
-const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 2, 1, 1, 1, 1, 1, 2, 2, 1};
+const long long kTuneMax[kTuneCount] = {4, 1, 1, 4096, 16, 16, 3, 1, 1, 1, 1, 1, 2, 2, 1};
 long long g_tuning[kTuneCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 
@@ -539,16 +539,17 @@ static int alloc_bins(ptyx_plan* pl) {
 // partial sums k_obj_gather_fin adds in split order (deterministic for a given call shape).
 // The small gathers' form: 0 = tiles (k_obj_gather; fused: gather_adam_tile), 1 = row-split
 // (k_obj_gather_rows; fused: the row tiles), 2 = row-split with the fused single-plane launch held
-// to 128 VGPRs (k_gather_adam_r4: four workgroups a CU; mixed-state calls: as 1).  Tuning
-// gather_rows overrides for every unsplit gather; by default calls of at most kSmallCall patterns
-// run row-split — single-state ones in form 2 (c2 at ga = 1: the fused launch 22.2 → 20.4 µs,
-// profiles/r06/rows_r4/) — and larger ones in tiles.  One decision for the fused and the unfused
+// to 128 VGPRs (k_gather_adam_r4: four workgroups a CU; mixed-state calls: as 1), 3 = the same at
+// 96 VGPRs (k_gather_adam_r5: five a CU, 20 B of spill; every tile of a c2 call in one round).
+// Tuning gather_rows overrides for every unsplit gather; by default calls of at most kSmallCall
+// patterns run row-split — single-state ones in form 3 (c2 at ga = 1: the fused launch 22.2 →
+// 20.4 (form 2) → 19.0 µs, profiles/r06/rows_r4/, rows_r5/) — and larger ones in tiles.  One decision for the fused and the unfused
 // launches, so both sum every pixel's hits in the same order (bitwise the same gradients).
 static int gather_form(bool mp, long long n) {
   const long long tr = g_tuning[kTuneGatherRows];
   if (tr >= 0) return (int)tr;
   if (n > f3::kSmallCall) return 0;
-  return mp ? 1 : 2;
+  return mp ? 1 : 3;
 }
 
 template <int N, bool ROWPERM, bool MP>
@@ -1430,7 +1431,8 @@ static int run_fused3(ptyx_plan* pl, const ptyx_inputs* in, const KArgs& a, cons
   if (fuse) {
     ProfScope ps(pl, kKGatherAdam, st);
     const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
-    if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
+    if (gform == 3) hipLaunchKernelGGL((k_gather_adam_r5<N>), gr, dim3(256), 0, st, fz);
+    else if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
     else if (rows_fuse) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
     else hipLaunchKernelGGL((k_gather_adam<N, true>), gr, dim3(256), 0, st, fz);
     pl->fadam_done = true;
@@ -2555,7 +2557,8 @@ static int gather_slots(ptyx_plan* pl, void* stream, const float* blocks, int32_
         fused_adam_setup(pl, obja, objp, nullptr, gz, false, g, tiles, &fz)) {
       ProfScope ps(pl, kKGatherAdam, st);
       const dim3 gr(fz.tiles + fz.pblocks + fz.rblocks);
-      if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
+      if (gform == 3) hipLaunchKernelGGL((k_gather_adam_r5<N>), gr, dim3(256), 0, st, fz);
+      else if (gform == 2) hipLaunchKernelGGL((k_gather_adam_r4<N>), gr, dim3(256), 0, st, fz);
       else if (gform == 1) hipLaunchKernelGGL((k_gather_adam<N, true, true, 1, false>), gr, dim3(256), 0, st, fz);
       else hipLaunchKernelGGL((k_gather_adam<N, true>), gr, dim3(256), 0, st, fz);
       done = true;

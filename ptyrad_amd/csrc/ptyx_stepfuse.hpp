@@ -294,3 +294,8 @@ template <int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_adam_r4(FusedAdamArgs f) {
   gather_adam_body<N, true, true, 1, false>(f);
 }
+// ... and to 96 VGPRs: five workgroups a CU, every tile of a c2 call in one round (gather_rows 3)
+template <int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_gather_adam_r5(FusedAdamArgs f) {
+  gather_adam_body<N, true, true, 1, false>(f);
+}

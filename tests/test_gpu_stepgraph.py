@@ -278,6 +278,7 @@ def _one_step(model, opt, loss_fn, idx, mode, store):
 
 @pytest.mark.parametrize("name,store,rows", [("traj_c1_n128", False, -1), ("traj_c1_n128", True, -1),
                                              ("traj_c1_n128", True, 1), ("traj_c1_n128", True, 2),
+                                             ("traj_c1_n128", True, 3),
                                              ("traj_n128_p6z6_ga1", True, -1)])
 def test_fused_adam_call_bitwise_the_call_then_adam(name, store, rows):
     """PTYX_PREP_FUSED_ADAM (ABI 209): the k_fused3 small call with the optimizer step folded into
@@ -292,8 +293,8 @@ def test_fused_adam_call_bitwise_the_call_then_adam(name, store, rows):
     traj_n128_p6z6_ga1 (the tBL demo's 6 probe modes, 6 slices): the mixed-state engine, whose fused
     launch runs the row-split gather over the slices and the probe rows of every mode.  rows 1
     (tuning gather_rows): the single-state call's gather row-split too, fused (k_gather_adam's
-    one-plane row tiles; 2: k_gather_adam_r4, the same held to 128 VGPRs) and unfused
-    (k_obj_gather_rows) alike."""
+    one-plane row tiles; 2 / 3: k_gather_adam_r4 / _r5, the same held to 128 / 96 VGPRs; −1: the
+    default, form 3 for these small single-state calls) and unfused (k_obj_gather_rows) alike."""
     need_gpu()
     from tests.dist_helpers import gpu_recon
     from ptyrad_amd import _lib
